@@ -1,0 +1,301 @@
+#!/usr/bin/env python3
+"""bench.py — device-resident Internet checksum throughput (BASELINE.json metric).
+
+One "step" = one pass of the hot path (nsx_csum_fixed_dev → gfx950 kernel) over
+one device-resident batch. Default workload = BASELINE.json configs[1]
+(config 2): 1,048,576 × 1500 B fixed-stride TCP segments per GPU, splitmix64
+bytes (seed 0x1071 + rank) generated on the device. N GPUs = N ranks, one per
+GPU (torchrun), each checksumming its own batch: the path shards with no
+exchange, so there is no data-path collective and scaling is
+weak. value = Σ bytes over all ranks ÷ max over ranks of the timed region.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Printed by rank 0: one JSON line with the contract fields plus
+  roofline     — dominant kernel: algorithmic bytes per launch ÷ its mean
+                 duration (HIP events on the launch stream) vs 8 TB/s HBM;
+                 traffic = PMC-measured HBM bytes per launch from the committed
+                 rocprofv3 summary (profiles/), or null;
+  cpu_baseline — the Go-faithful CPU restatement (oracle, 1 thread) timed on a
+                 bounded sample of the same workload (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "network-stack_amd"))
+
+METRIC = "GiB/s device-resident Internet checksum, 1M×1500B segments, 1/2/4/8 GPU"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md §Chip-level parameters
+GIB = float(1 << 30)
+
+# Workloads (BASELINE.json configs; per GPU). "kind" picks the entry point.
+WORKLOADS = {
+    2: dict(kind="fixed", n=1 << 20, seg_len=1500, stride=1500, seed=0x1071,
+            name="config2: 1M x 1500B fixed-stride TCP segments per GPU, device-resident"),
+    3: dict(kind="ragged", n=1 << 20, lo=64, hi=9000, seed=0x1072,
+            name="config3: 1M ragged 64-9000B segments per GPU, densely packed (odd starts), device-resident"),
+    4: dict(kind="fixed", n=1 << 18, seg_len=65536, stride=65536, seed=0x1073,
+            name="config4: 256K x 64KiB TSO-size segments per GPU, device-resident"),
+    5: dict(kind="fixed", n=1 << 24, seg_len=1500, stride=1500, seed=0x1071,
+            name="config5: 16M x 1500B per GPU (128M x 1500B over 8 GPUs), device-resident"),
+}
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", type=int, default=2, choices=sorted(WORKLOADS))
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0 = skip)")
+    ap.add_argument("--param", action="append", default=[], metavar="NAME=V",
+                    help="kernel knob: blocks_per_cu, segs_per_wave, nontemporal, block_mode, xcd_map")
+    return ap.parse_args(argv)
+
+
+# ---------------------------------------------------------------------------
+# distributed plumbing (shared with the gloo CPU tests)
+# ---------------------------------------------------------------------------
+class Dist:
+    def __init__(self, backend: str | None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.on = self.world > 1
+        if self.on and not dist.is_initialized():
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group(backend=backend)
+
+    def barrier(self, device=None):
+        if self.on:
+            if device is not None and self.dist.get_backend() == "nccl":
+                self.dist.barrier(device_ids=[device])
+            else:
+                self.dist.barrier()
+
+    def max(self, x: float, device=None) -> float:
+        if not self.on:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64, device=device if device is not None else "cpu")
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, x: float, device=None) -> float:
+        if not self.on:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64, device=device if device is not None else "cpu")
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def close(self):
+        if self.on and self.dist.is_initialized():
+            self.dist.destroy_process_group()
+
+
+def timed_loop(step, sync, barrier, steps: int, warmup: int, ev_pair=None):
+    """W untimed steps; then EXACTLY K steps bracketed by barrier + sync on both
+    sides. ev_pair() → (start, end) events recorded around each launch on the
+    launch stream (per-launch kernel duration). Returns (wall_s, [launch_ms])."""
+    for _ in range(warmup):
+        step()
+    sync()
+    barrier()
+    sync()
+    evs = [ev_pair() for _ in range(steps)] if ev_pair else None
+    t0 = time.perf_counter()
+    for i in range(steps):
+        if evs:
+            evs[i][0].record()
+        step()
+        if evs:
+            evs[i][1].record()
+    sync()
+    barrier()
+    sync()
+    wall = time.perf_counter() - t0
+    launch_ms = [a.elapsed_time(b) for a, b in evs] if evs else []
+    return wall, launch_ms
+
+
+def result_line(*, world, steps, warmup, wall_max, bytes_per_rank_step, units_total, workload, cfg, launch_ms,
+                alg_bytes_per_launch, cpu_baseline, traffic, dtype="u16") -> dict:
+    total_bytes = bytes_per_rank_step * world * steps
+    mean_launch_ms = sum(launch_ms) / len(launch_ms) if launch_ms else None
+    achieved = alg_bytes_per_launch / (mean_launch_ms * 1e-3) / 1e9 if mean_launch_ms else None
+    return {
+        "metric": METRIC,
+        "value": round(total_bytes / wall_max / GIB, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": round(wall_max / steps * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": dtype,
+        "data": "synthetic: splitmix64 bytes (seed %#x + rank) generated on device" % cfg["seed"],
+        "config": {"workload": workload, "segments_per_gpu": cfg["n"], "bytes_per_gpu": bytes_per_rank_step,
+                   "units_per_step_all_gpus": units_total,
+                   "parallelism": f"shard{world} (independent per-GPU batches, no collective)"},
+        "kernel_ms_mean": None if mean_launch_ms is None else round(mean_launch_ms, 5),
+        "roofline": None if achieved is None else {
+            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4),
+            "traffic": None if traffic is None else traffic.get("bytes_per_launch"),
+            "traffic_source": None if traffic is None else traffic.get("source"),
+            "alg_bytes_per_launch": alg_bytes_per_launch},
+        "cpu_baseline": cpu_baseline,
+    }
+
+
+# ---------------------------------------------------------------------------
+# GPU workload
+# ---------------------------------------------------------------------------
+PARAMS = {"blocks_per_cu": 1, "segs_per_wave": 2, "nontemporal": 3, "block_mode": 4, "xcd_map": 5}
+
+
+def build_workload(cfg, rank, device):
+    import numpy as np
+    import torch
+    import nsx
+    seed = cfg["seed"] + rank
+    w = {"seed": seed}
+    if cfg["kind"] == "fixed":
+        n, L, S = cfg["n"], cfg["seg_len"], cfg["stride"]
+        buf = torch.empty((n - 1) * S + L, dtype=torch.uint8, device=device)
+        nsx.fill_splitmix64_dev(buf, seed)
+        out = torch.empty(n, dtype=torch.int16, device=device)
+        w.update(buf=buf, out=out, bytes=n * L, alg=n * L + 2 * n,
+                 step=lambda: nsx.fixed_dev(buf, S, L, n, out=out))
+    else:
+        rng = np.random.default_rng(cfg["seed"])  # same lengths on every rank, bytes differ by seed
+        n = cfg["n"]
+        lens = rng.integers(cfg["lo"], cfg["hi"] + 1, n).astype(np.uint64)
+        offs = np.zeros(n + 1, np.uint64)
+        offs[1:] = np.cumsum(lens)
+        total = int(offs[-1])
+        buf = torch.empty(total, dtype=torch.uint8, device=device)
+        nsx.fill_splitmix64_dev(buf, seed)
+        d_offs = torch.from_numpy(offs.view(np.int64)).to(device)
+        out = torch.empty(n, dtype=torch.int16, device=device)
+        w.update(buf=buf, out=out, offsets=offs, bytes=total, alg=total + 2 * n + 8 * (n + 1),
+                 step=lambda: nsx.ragged_dev(buf, d_offs, out=out))
+    return w
+
+
+def cpu_baseline(cfg, w, seconds: float) -> dict:
+    """Go-faithful CPU restatement (oracle_go_batch_fixed / oracle_batch_ragged:
+    allocate + concatenate + serial compare-carry loop per segment, tcp.go:72-95),
+    one thread, over a bounded sample of this rank's own batch; its results are
+    also compared with the GPU's for the same segments (the checker role)."""
+    import ctypes
+    import numpy as np
+    import torch
+    sys.path.insert(0, ROOT)
+    from oracle import csum_oracle as O
+    lib = O.c_oracle()
+    torch.cuda.synchronize()
+    if cfg["kind"] == "fixed":
+        n, L, S = cfg["n"], cfg["seg_len"], cfg["stride"]
+        m = min(n, max(1, (256 << 20) // S))  # sample: the first m segments (≤ 256 MiB)
+        sample = w["buf"][: (m - 1) * S + L].cpu().numpy()
+        gpu = w["out"][:m].cpu().numpy().view(np.uint16)
+        out = np.empty(m, np.uint16)
+        t0, reps = time.perf_counter(), 0
+        while True:
+            lib.oracle_go_batch_fixed(sample.ctypes.data_as(ctypes.c_void_p), S, L, m, None, 0,
+                                      out.ctypes.data_as(ctypes.c_void_p))
+            reps += 1
+            if time.perf_counter() - t0 >= seconds:
+                break
+        dt = time.perf_counter() - t0
+        nbytes = reps * m * L
+        desc = f"first {m} segments x {L}B of rank 0's batch, {reps} pass(es), Go-faithful serial loop"
+    else:
+        offs = w["offsets"]
+        m = int(min(len(offs) - 1, 50000))
+        hi = int(offs[m])
+        sample = w["buf"][:hi].cpu().numpy()
+        gpu = w["out"][:m].cpu().numpy().view(np.uint16)
+        out = np.empty(m, np.uint16)
+        so = np.ascontiguousarray(offs[: m + 1])
+        t0, reps = time.perf_counter(), 0
+        while True:
+            for i in range(m):
+                out[i] = lib.oracle_go_checksum(None, 0, sample[int(so[i]):].ctypes.data_as(ctypes.c_void_p),
+                                                int(so[i + 1] - so[i]))
+            reps += 1
+            if time.perf_counter() - t0 >= seconds:
+                break
+        dt = time.perf_counter() - t0
+        nbytes = reps * hi
+        desc = f"first {m} ragged segments of rank 0's batch, {reps} pass(es), Go-faithful serial loop"
+    return {"value": round(nbytes / dt / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": desc, "seconds": round(dt, 2), "sample_parity_vs_gpu": bool(np.array_equal(out, gpu)),
+            "host_cpus": os.cpu_count()}
+
+
+def load_traffic(config_id: int):
+    p = os.path.join(ROOT, "profiles", f"traffic_config{config_id}.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        d = json.load(f)
+    d["source"] = os.path.relpath(p, ROOT)
+    return d
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    import torch
+    import nsx
+    dist = Dist("nccl")
+    if dist.world != args.gpus and dist.on:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {dist.world}; using WORLD_SIZE", file=sys.stderr)
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a GPU: the checksum path is HIP-only (no CPU fallback)")
+    dev_id = dist.local_rank if dist.on else 0
+    torch.cuda.set_device(dev_id)
+    device = torch.device("cuda", dev_id)
+    for kv in args.param:
+        k, v = kv.split("=")
+        nsx.set_param(PARAMS[k], int(v))
+
+    cfg = WORKLOADS[args.config]
+    w = build_workload(cfg, dist.rank, device)
+    torch.cuda.synchronize()
+
+    def ev_pair():
+        return torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+    wall, launch_ms = timed_loop(w["step"], torch.cuda.synchronize, lambda: dist.barrier(dev_id),
+                                 args.steps, args.warmup, ev_pair)
+    wall_max = dist.max(wall, device)
+    cpu = None
+    if dist.world == 1 and args.cpu_seconds > 0:
+        cpu = cpu_baseline(cfg, w, args.cpu_seconds)
+    line = result_line(world=dist.world, steps=args.steps, warmup=args.warmup, wall_max=wall_max,
+                       bytes_per_rank_step=w["bytes"], units_total=cfg["n"] * dist.world, workload=cfg["name"],
+                       cfg=cfg, launch_ms=launch_ms, alg_bytes_per_launch=w["alg"], cpu_baseline=cpu,
+                       traffic=load_traffic(args.config))
+    if args.param:
+        line["config"]["params"] = args.param
+    if dist.rank == 0:
+        print(json.dumps(line), flush=True)
+    dist.close()
+
+
+if __name__ == "__main__":
+    main()

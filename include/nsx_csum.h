@@ -1,0 +1,160 @@
+/*
+ * nsx_csum.h — C ABI of the MI355X-native Internet checksum (RFC 1071) path.
+ *
+ * This is the drop-in boundary for the reference's one checksum function,
+ *   transport/tcp/tcp.go:72-95  func (s segment) computeChecksum(ipPseudoHeader []byte) uint16
+ * (reference: oneee-playground/network-stack, pure Go). A Go caller reaches it
+ * through the cgo shim in network-stack_amd/go/transport/tcp/ (INTEGRATION.md).
+ *
+ * Semantics shared by every entry point (tcp.go:68-95):
+ *   - the checksummed stream is prefix ‖ segment (tcp.go:73); an odd total is
+ *     zero-padded (tcp.go:74-77);
+ *   - 16-bit big-endian words are added with end-around carry (tcp.go:79-92);
+ *   - the RAW one's-complement sum is returned, NOT complemented (tcp.go:94).
+ *     0x0000 only for an all-zero input; a nonzero input whose sum is
+ *     ≡ 0 mod 0xFFFF gives 0xFFFF. The sender stores nsx_field(raw) = ~raw
+ *     (tcp_test.go:28); a receiver accepts iff raw == 0xFFFF (tcp.go:70).
+ *
+ * Conventions:
+ *   - Return 0 (NSX_OK) or a negative errno-style code; never abort or print.
+ *   - The caller owns every buffer. No pointer is retained after the stream
+ *     work completes (device calls) or after return (host calls).
+ *   - Device calls are asynchronous on `stream` (a hipStream_t; NULL = the
+ *     default stream of the current device). Device pointers must belong to the
+ *     device current on the calling thread. No host synchronisation, no
+ *     allocation inside device calls (hipGraph-capturable).
+ *   - Re-entrant; no global mutable state on the data path.
+ *   - A device call on a host with no usable GPU returns NSX_ENODEV. There is no
+ *     CPU fallback for the batch/device entry points.
+ */
+#ifndef NSX_CSUM_H
+#define NSX_CSUM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NSX_OK      0
+#define NSX_EIO    (-5)   /* a HIP runtime call or kernel launch failed */
+#define NSX_ENOMEM (-12)  /* host or device allocation failed */
+#define NSX_ENODEV (-19)  /* no usable GPU / bad device ordinal */
+#define NSX_EINVAL (-22)  /* null pointer with nonzero length, bad sizes */
+
+#define NSX_ABI_VERSION 1
+
+typedef void* nsx_stream_t; /* hipStream_t, opaque to C/Go callers */
+
+/* ----------------------------------------------------------------------------
+ * Single segment, host CPU.
+ * Replaces: transport/tcp/tcp.go:72-95 computeChecksum (called from
+ * tcp_test.go:28,30). Exactly its semantics over prefix ‖ seg, without the
+ * reference's allocation/copy of the concatenation (tcp.go:73) and without
+ * writing into the prefix's spare capacity. For per-segment cgo calls; never
+ * touches the GPU (a per-segment cgo call must not drive the device).
+ * prefix may be NULL iff prefix_len == 0; likewise seg.
+ */
+int nsx_csum16(const uint8_t* prefix, size_t prefix_len,
+               const uint8_t* seg, size_t seg_len, uint16_t* out_raw_sum);
+
+/* ----------------------------------------------------------------------------
+ * Device-resident batches (the hot path). One result (raw sum) per segment.
+ *
+ * d_prefix_partial (nullable): per-segment integer sum of the prefix's
+ * big-endian 16-bit words (e.g. an IPv4/IPv6 TCP pseudo-header, whose length is
+ * even), folded or not; result[i] = raw sum over prefix_i ‖ segment_i.
+ * Produce it with nsx_pseudo_ipv4_partial_dev or nsx_csum_fixed_dev on the
+ * pseudo-headers themselves.
+ */
+
+/* Fixed stride: segment i occupies d_base[i*stride, i*stride + seg_len).
+ * The span [d_base, d_base + (n-1)*stride + seg_len) must be readable.
+ * Replaces a Go loop of computeChecksum over equal-size segments (tcp.go:72). */
+int nsx_csum_fixed_dev(const void* d_base, uint64_t stride, uint32_t seg_len, uint64_t n,
+                       const uint32_t* d_prefix_partial, uint16_t* d_out, nsx_stream_t stream);
+
+/* Ragged: segment i occupies d_base[d_offsets[i], d_offsets[i+1]); d_offsets
+ * has n+1 non-decreasing entries; segments may start at any byte (dense packing,
+ * odd starts). The span [d_base + d_offsets[0], d_base + d_offsets[n]) must be
+ * readable. */
+int nsx_csum_ragged_dev(const void* d_base, const uint64_t* d_offsets, uint64_t n,
+                        const uint32_t* d_prefix_partial, uint16_t* d_out, nsx_stream_t stream);
+
+/* Receive-side verify (tcp.go:70): d_ok[i] = (raw_i == 0xFFFF), where raw_i is
+ * the ragged-batch raw sum with the optional prefix partial. d_raw (nullable)
+ * also receives the raw sums. */
+int nsx_verify_ragged_dev(const void* d_base, const uint64_t* d_offsets, uint64_t n,
+                          const uint32_t* d_prefix_partial, uint8_t* d_ok, uint16_t* d_raw,
+                          nsx_stream_t stream);
+
+/* IPv4 TCP pseudo-header partials (RFC 9293 §3.1: src(4) dst(4) 0 proto len(2))
+ * for n segments: d_src/d_dst are n×4 address bytes as ip.Addr.Raw()
+ * (network/ip/v4/ipv4.go:15), d_len the TCP length of each segment, proto e.g.
+ * ip.NextProtoTCP = 6 (network/ip/protocols.go:8). Writes the integer BE-word
+ * sum to d_partial[i] (the d_prefix_partial convention above). */
+int nsx_pseudo_ipv4_partial_dev(const uint8_t* d_src, const uint8_t* d_dst,
+                                const uint32_t* d_len, uint8_t proto, uint64_t n,
+                                uint32_t* d_partial, nsx_stream_t stream);
+
+/* ----------------------------------------------------------------------------
+ * Host-resident batches: pinned staging, H2D → kernel → D2H double-buffered
+ * over two streams per GPU, segments sharded contiguously across num_gpus
+ * devices (0 = all visible). No collective: shards are independent.
+ * h_prefix_partial nullable.
+ */
+int nsx_csum_fixed_host(const uint8_t* h_base, uint64_t stride, uint32_t seg_len, uint64_t n,
+                        const uint32_t* h_prefix_partial, uint16_t* h_out, int num_gpus);
+
+int nsx_csum_ragged_host(const uint8_t* h_base, const uint64_t* h_offsets, uint64_t n,
+                         const uint32_t* h_prefix_partial, uint16_t* h_out, int num_gpus);
+
+/* Pinned (DMA-registered) host memory for zero-copy staging from Go via
+ * unsafe.Slice (cgo forbids C retaining Go pointers; runtime.Pinner does not
+ * DMA-register). */
+int nsx_alloc_pinned(size_t bytes, void** out);
+int nsx_free_pinned(void* p);
+
+/* ----------------------------------------------------------------------------
+ * Sharding plan (host logic, no GPU): split n segments over `parts` shards.
+ * Fixed stride (h_offsets NULL): contiguous index ranges of near-equal count.
+ * Ragged: contiguous index ranges of near-equal BYTE count using the prefix-sum
+ * offsets. Writes parts+1 boundaries to out_bounds (out_bounds[0]=0,
+ * out_bounds[parts]=n).
+ */
+int nsx_shard_plan(const uint64_t* h_offsets, uint64_t n, int parts, uint64_t* out_bounds);
+
+/* ----------------------------------------------------------------------------
+ * Synthetic batches (bench/test data): byte j of the stream is
+ * byte j%8 of the little-endian word splitmix64(seed, j/8); writes stream bytes
+ * [byte_off, byte_off + nbytes) to d_buf. Counter-based, so any range can be
+ * regenerated on the host. */
+int nsx_fill_splitmix64_dev(void* d_buf, uint64_t byte_off, uint64_t nbytes, uint64_t seed,
+                            nsx_stream_t stream);
+
+/* ----------------------------------------------------------------------------
+ * Introspection / tuning.
+ */
+int nsx_abi_version(void);
+int nsx_device_count(int* out_count);        /* NSX_OK with 0 when no GPU */
+const char* nsx_strerror(int code);
+
+/* Kernel-variant knobs for benchmarking (process-wide; 0 restores the default).
+ * Not needed for correctness; every variant is bit-exact. */
+#define NSX_PARAM_BLOCKS_PER_CU   1  /* persistent-grid occupancy, 1..8  */
+#define NSX_PARAM_SEGS_PER_WAVE   2  /* fixed path: 1, 2 or 4 segments per wave pass */
+#define NSX_PARAM_NONTEMPORAL     3  /* 1 = nt loads (read-once stream) */
+#define NSX_PARAM_BLOCK_MODE      4  /* 0 auto (a block per segment when n < resident waves), 1 wave per segment, 2 block per segment */
+#define NSX_PARAM_XCD_MAP         5  /* 1 (default) deal each XCD a contiguous region of the batch; 2 plain grid-stride */
+int nsx_set_param(int param, int64_t value);
+int nsx_get_param(int param, int64_t* value);
+
+/* Receiver/sender helpers (tcp.go:68-71, tcp_test.go:28-31). */
+static inline uint16_t nsx_field(uint16_t raw_sum) { return (uint16_t)~raw_sum; }
+static inline int nsx_verify(uint16_t raw_sum) { return raw_sum == 0xFFFF; }
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NSX_CSUM_H */

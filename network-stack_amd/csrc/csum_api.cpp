@@ -1,0 +1,238 @@
+// csum_api.cpp — C ABI (include/nsx_csum.h) over the gfx950 checksum kernels.
+//
+// Boundary for transport/tcp/tcp.go:72-95 (computeChecksum). Device entry points
+// validate arguments, pick the kernel variant and launch asynchronously on the
+// caller's stream; host entry points shard a host-resident batch over GPUs and
+// pipeline pinned H2D → kernel → D2H per GPU. Nothing here computes a batch
+// checksum on the CPU: with no GPU the batch calls return NSX_ENODEV.
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../../include/nsx_csum.h"
+#include "csum_kernels.h"
+#include "host_csum.h"
+
+namespace {
+
+// ---------------------------------------------------------------- params
+std::atomic<int64_t> g_blocks_per_cu{0}, g_segs_per_wave{0}, g_nontemporal{0}, g_block_mode{0},
+    g_xcd_map{0};
+
+constexpr int kDefaultBlocksPerCU = 8;  // 8 × 4 waves = 32 waves/CU (kernels fit 64 VGPRs)
+constexpr int kDefaultSegsPerWave = 2;
+constexpr int kMaxDevices = 64;
+
+struct DevInfo {
+    int cus = 0;
+    bool ok = false;
+};
+DevInfo g_dev[kMaxDevices];
+std::once_flag g_dev_once[kMaxDevices];
+
+int device_count_raw() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return n;
+}
+
+const DevInfo* dev_info(int dev) {
+    if (dev < 0 || dev >= kMaxDevices) return nullptr;
+    std::call_once(g_dev_once[dev], [dev] {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0) {
+            g_dev[dev].cus = cus;
+            g_dev[dev].ok = true;
+        } else {
+            (void)hipGetLastError();
+        }
+    });
+    return g_dev[dev].ok ? &g_dev[dev] : nullptr;
+}
+
+// Current device of the calling thread, or -1 when there is no usable GPU.
+int current_device() {
+    if (device_count_raw() <= 0) return -1;
+    int d = -1;
+    if (hipGetDevice(&d) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    return dev_info(d) ? d : -1;
+}
+
+nsx::LaunchCfg make_cfg(int dev, uint64_t n, bool segs_can_split) {
+    const DevInfo* di = dev_info(dev);
+    int64_t bpc = g_blocks_per_cu.load();
+    if (bpc <= 0 || bpc > 8) bpc = kDefaultBlocksPerCU;
+    int64_t spw = g_segs_per_wave.load();
+    if (spw != 1 && spw != 2 && spw != 4) spw = kDefaultSegsPerWave;
+    nsx::LaunchCfg c;
+    c.max_blocks = (uint32_t)(di->cus * bpc);
+    c.segs_per_wave = (int)spw;
+    c.nontemporal = g_nontemporal.load() == 1 ? 1 : 0;
+    c.xcd_map = g_xcd_map.load() == 2 ? 0 : 1;
+    const int64_t bm = g_block_mode.load();
+    const uint64_t resident_waves = (uint64_t)di->cus * 32;
+    c.block_mode = segs_can_split && (bm == 2 || (bm == 0 && n < resident_waves));
+    return c;
+}
+
+int map_err(hipError_t e) {
+    if (e == hipSuccess) return NSX_OK;
+    (void)hipGetLastError();
+    if (e == hipErrorOutOfMemory) return NSX_ENOMEM;
+    if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return NSX_ENODEV;
+    return NSX_EIO;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nsx_abi_version(void) { return NSX_ABI_VERSION; }
+
+int nsx_device_count(int* out_count) {
+    if (!out_count) return NSX_EINVAL;
+    *out_count = device_count_raw();
+    return NSX_OK;
+}
+
+const char* nsx_strerror(int code) {
+    switch (code) {
+        case NSX_OK: return "ok";
+        case NSX_EIO: return "HIP runtime or kernel launch failure";
+        case NSX_ENOMEM: return "out of memory";
+        case NSX_ENODEV: return "no usable GPU";
+        case NSX_EINVAL: return "invalid argument";
+        default: return "unknown error";
+    }
+}
+
+int nsx_set_param(int param, int64_t value) {
+    switch (param) {
+        case NSX_PARAM_BLOCKS_PER_CU: g_blocks_per_cu = value; return NSX_OK;
+        case NSX_PARAM_SEGS_PER_WAVE: g_segs_per_wave = value; return NSX_OK;
+        case NSX_PARAM_NONTEMPORAL: g_nontemporal = value; return NSX_OK;
+        case NSX_PARAM_BLOCK_MODE: g_block_mode = value; return NSX_OK;
+        case NSX_PARAM_XCD_MAP: g_xcd_map = value; return NSX_OK;
+        default: return NSX_EINVAL;
+    }
+}
+
+int nsx_get_param(int param, int64_t* value) {
+    if (!value) return NSX_EINVAL;
+    switch (param) {
+        case NSX_PARAM_BLOCKS_PER_CU: *value = g_blocks_per_cu; return NSX_OK;
+        case NSX_PARAM_SEGS_PER_WAVE: *value = g_segs_per_wave; return NSX_OK;
+        case NSX_PARAM_NONTEMPORAL: *value = g_nontemporal; return NSX_OK;
+        case NSX_PARAM_BLOCK_MODE: *value = g_block_mode; return NSX_OK;
+        case NSX_PARAM_XCD_MAP: *value = g_xcd_map; return NSX_OK;
+        default: return NSX_EINVAL;
+    }
+}
+
+// ------------------------------------------------------------ single segment
+int nsx_csum16(const uint8_t* prefix, size_t prefix_len, const uint8_t* seg, size_t seg_len,
+               uint16_t* out_raw_sum) {
+    if (!out_raw_sum || (prefix_len && !prefix) || (seg_len && !seg)) return NSX_EINVAL;
+    *out_raw_sum = nsx::host_csum16(prefix, prefix_len, seg, seg_len);
+    return NSX_OK;
+}
+
+// ------------------------------------------------------------ device batches
+int nsx_csum_fixed_dev(const void* d_base, uint64_t stride, uint32_t seg_len, uint64_t n,
+                       const uint32_t* d_prefix_partial, uint16_t* d_out, nsx_stream_t stream) {
+    if (n == 0) return NSX_OK;
+    if (!d_out || (seg_len && !d_base)) return NSX_EINVAL;
+    if (n > 1 && stride == 0 && seg_len) { /* every segment aliases the first: allowed */ }
+    if (n > ((uint64_t)1 << 40)) return NSX_EINVAL;
+    const int dev = current_device();
+    if (dev < 0) return NSX_ENODEV;
+    nsx::LaunchCfg c = make_cfg(dev, n, true);
+    return map_err(nsx::launch_fixed(c, d_base, stride, seg_len, n, d_prefix_partial, d_out,
+                                     static_cast<hipStream_t>(stream)));
+}
+
+int nsx_csum_ragged_dev(const void* d_base, const uint64_t* d_offsets, uint64_t n,
+                        const uint32_t* d_prefix_partial, uint16_t* d_out, nsx_stream_t stream) {
+    if (n == 0) return NSX_OK;
+    if (!d_out || !d_offsets || !d_base) return NSX_EINVAL;
+    if (n > ((uint64_t)1 << 40)) return NSX_EINVAL;
+    const int dev = current_device();
+    if (dev < 0) return NSX_ENODEV;
+    nsx::LaunchCfg c = make_cfg(dev, n, true);
+    return map_err(nsx::launch_ragged(c, d_base, d_offsets, n, d_prefix_partial, d_out, nullptr,
+                                      static_cast<hipStream_t>(stream)));
+}
+
+int nsx_verify_ragged_dev(const void* d_base, const uint64_t* d_offsets, uint64_t n,
+                          const uint32_t* d_prefix_partial, uint8_t* d_ok, uint16_t* d_raw,
+                          nsx_stream_t stream) {
+    if (n == 0) return NSX_OK;
+    if (!d_ok || !d_offsets || !d_base) return NSX_EINVAL;
+    if (n > ((uint64_t)1 << 40)) return NSX_EINVAL;
+    const int dev = current_device();
+    if (dev < 0) return NSX_ENODEV;
+    nsx::LaunchCfg c = make_cfg(dev, n, true);
+    return map_err(nsx::launch_ragged(c, d_base, d_offsets, n, d_prefix_partial, d_raw, d_ok,
+                                      static_cast<hipStream_t>(stream)));
+}
+
+int nsx_pseudo_ipv4_partial_dev(const uint8_t* d_src, const uint8_t* d_dst, const uint32_t* d_len,
+                                uint8_t proto, uint64_t n, uint32_t* d_partial, nsx_stream_t stream) {
+    if (n == 0) return NSX_OK;
+    if (!d_src || !d_dst || !d_len || !d_partial) return NSX_EINVAL;
+    const int dev = current_device();
+    if (dev < 0) return NSX_ENODEV;
+    const DevInfo* di = dev_info(dev);
+    return map_err(nsx::launch_pseudo_ipv4(d_src, d_dst, d_len, proto, n, d_partial, (uint32_t)di->cus * 8,
+                                           static_cast<hipStream_t>(stream)));
+}
+
+int nsx_fill_splitmix64_dev(void* d_buf, uint64_t byte_off, uint64_t nbytes, uint64_t seed,
+                            nsx_stream_t stream) {
+    if (nbytes == 0) return NSX_OK;
+    if (!d_buf) return NSX_EINVAL;
+    const int dev = current_device();
+    if (dev < 0) return NSX_ENODEV;
+    const DevInfo* di = dev_info(dev);
+    return map_err(nsx::launch_fill_splitmix64(d_buf, byte_off, nbytes, seed, (uint32_t)di->cus * 8,
+                                               static_cast<hipStream_t>(stream)));
+}
+
+// ------------------------------------------------------------ sharding plan
+int nsx_shard_plan(const uint64_t* h_offsets, uint64_t n, int parts, uint64_t* out_bounds) {
+    if (parts < 1 || !out_bounds) return NSX_EINVAL;
+    nsx::shard_plan(h_offsets, n, parts, out_bounds);
+    return NSX_OK;
+}
+
+// ------------------------------------------------------------ pinned memory
+int nsx_alloc_pinned(size_t bytes, void** out) {
+    if (!out) return NSX_EINVAL;
+    *out = nullptr;
+    if (bytes == 0) return NSX_OK;
+    if (device_count_raw() <= 0) return NSX_ENODEV;
+    hipError_t e = hipHostMalloc(out, bytes, hipHostMallocPortable);
+    if (e != hipSuccess) {
+        *out = nullptr;
+        return map_err(e);
+    }
+    return NSX_OK;
+}
+
+int nsx_free_pinned(void* p) {
+    if (!p) return NSX_OK;
+    return map_err(hipHostFree(p));
+}
+
+}  // extern "C"

@@ -1,0 +1,260 @@
+// host_batch.cpp — host-resident batches: shard over GPUs, pipeline per GPU.
+//
+// The reference's checksum input lives in transport buffers in host memory
+// (transport/pipe/pipe.go:73-124 hands []byte slices between goroutines), so the
+// end-to-end path is host → HBM → kernel → host. Each GPU gets a contiguous
+// shard (no collective: segments are independent) and a host thread that
+// double-buffers fixed-size chunks over two HIP streams: chunk k+1's H2D copy
+// overlaps chunk k's kernel and D2H. Caller memory that is already pinned
+// (nsx_alloc_pinned) is DMA'd directly; pageable memory is bounced through
+// pinned staging buffers.
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "../../include/nsx_csum.h"
+#include "csum_kernels.h"
+#include "host_csum.h"
+
+namespace {
+
+constexpr uint64_t kChunkBytes = 64ull << 20;
+
+bool is_pinned(const void* p) {
+    if (!p) return false;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+int map_err(hipError_t e) {
+    if (e == hipSuccess) return NSX_OK;
+    (void)hipGetLastError();
+    return e == hipErrorOutOfMemory ? NSX_ENOMEM : NSX_EIO;
+}
+
+#define NSX_TRY(expr)                          \
+    do {                                       \
+        hipError_t e_ = (expr);                \
+        if (e_ != hipSuccess) {                \
+            rc = map_err(e_);                  \
+            goto done;                         \
+        }                                      \
+    } while (0)
+
+nsx::LaunchCfg default_cfg(int dev, uint64_t n) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    int64_t bpc = 0, spw = 0, nt = 0, bm = 0, xm = 0;
+    nsx_get_param(NSX_PARAM_BLOCKS_PER_CU, &bpc);
+    nsx_get_param(NSX_PARAM_SEGS_PER_WAVE, &spw);
+    nsx_get_param(NSX_PARAM_NONTEMPORAL, &nt);
+    nsx_get_param(NSX_PARAM_BLOCK_MODE, &bm);
+    nsx_get_param(NSX_PARAM_XCD_MAP, &xm);
+    if (bpc <= 0 || bpc > 8) bpc = 8;
+    if (spw != 1 && spw != 2 && spw != 4) spw = 2;
+    nsx::LaunchCfg c;
+    c.max_blocks = (uint32_t)(cus * bpc);
+    c.segs_per_wave = (int)spw;
+    c.nontemporal = nt == 1;
+    c.xcd_map = xm == 2 ? 0 : 1;
+    c.block_mode = bm == 2 || (bm == 0 && n < (uint64_t)cus * 32);
+    return c;
+}
+
+// One chunk = segments [c0, c1) of the shard.
+struct Chunk {
+    uint64_t c0, c1;
+    uint64_t byte_lo, byte_hi;  // host span copied for the chunk
+};
+
+struct Job {
+    // inputs (shard-relative views)
+    const uint8_t* h_base;
+    uint64_t stride;
+    uint32_t seg_len;
+    const uint64_t* h_offsets;  // null → fixed stride; else absolute offsets into h_base
+    uint64_t lo, hi;            // segment index range of the shard
+    const uint32_t* h_partial;
+    uint16_t* h_out;
+    int dev;
+    int rc;
+};
+
+std::vector<Chunk> plan_chunks(const Job& j) {
+    std::vector<Chunk> v;
+    if (!j.h_offsets) {
+        const uint64_t span = std::max<uint64_t>(std::max<uint64_t>(j.stride, j.seg_len), 1);
+        const uint64_t per = std::max<uint64_t>(1, kChunkBytes / span);
+        for (uint64_t c0 = j.lo; c0 < j.hi; c0 += per) {
+            const uint64_t c1 = std::min(j.hi, c0 + per);
+            v.push_back({c0, c1, c0 * j.stride, (c1 - 1) * j.stride + j.seg_len});
+        }
+    } else {
+        uint64_t c0 = j.lo;
+        while (c0 < j.hi) {
+            uint64_t c1 = c0 + 1;
+            while (c1 < j.hi && j.h_offsets[c1 + 1] - j.h_offsets[c0] <= kChunkBytes) ++c1;
+            v.push_back({c0, c1, j.h_offsets[c0], j.h_offsets[c1]});
+            c0 = c1;
+        }
+    }
+    return v;
+}
+
+void run_job(Job* j) {
+    int rc = NSX_OK;
+    const std::vector<Chunk> chunks = plan_chunks(*j);
+    uint64_t max_span = 0, max_segs = 0;
+    for (const Chunk& c : chunks) {
+        max_span = std::max(max_span, c.byte_hi - c.byte_lo);
+        max_segs = std::max(max_segs, c.c1 - c.c0);
+    }
+    const bool in_pinned = is_pinned(j->h_base);
+    const bool out_pinned = is_pinned(j->h_out);
+    const bool ragged = j->h_offsets != nullptr;
+    hipStream_t st[2] = {nullptr, nullptr};
+    uint8_t* d_data[2] = {nullptr, nullptr};
+    uint16_t* d_out[2] = {nullptr, nullptr};
+    uint32_t* d_part[2] = {nullptr, nullptr};
+    uint64_t* d_off[2] = {nullptr, nullptr};
+    uint8_t* h_stage[2] = {nullptr, nullptr};
+    uint16_t* h_ostage[2] = {nullptr, nullptr};
+    uint32_t* h_pstage[2] = {nullptr, nullptr};
+    uint64_t* h_offstage[2] = {nullptr, nullptr};
+    nsx::LaunchCfg cfg;
+    const Chunk* pending[2] = {nullptr, nullptr};
+
+    NSX_TRY(hipSetDevice(j->dev));
+    cfg = default_cfg(j->dev, max_segs);
+    for (int s = 0; s < 2; ++s) {
+        NSX_TRY(hipStreamCreateWithFlags(&st[s], hipStreamNonBlocking));
+        NSX_TRY(hipMalloc(&d_data[s], std::max<uint64_t>(max_span, 16)));
+        NSX_TRY(hipMalloc(&d_out[s], max_segs * sizeof(uint16_t)));
+        if (j->h_partial) {
+            NSX_TRY(hipMalloc(&d_part[s], max_segs * sizeof(uint32_t)));
+            NSX_TRY(hipHostMalloc(&h_pstage[s], max_segs * sizeof(uint32_t), hipHostMallocPortable));
+        }
+        if (ragged) {
+            NSX_TRY(hipMalloc(&d_off[s], (max_segs + 1) * sizeof(uint64_t)));
+            NSX_TRY(hipHostMalloc(&h_offstage[s], (max_segs + 1) * sizeof(uint64_t), hipHostMallocPortable));
+        }
+        if (!in_pinned) NSX_TRY(hipHostMalloc(&h_stage[s], std::max<uint64_t>(max_span, 16), hipHostMallocPortable));
+        if (!out_pinned) NSX_TRY(hipHostMalloc(&h_ostage[s], max_segs * sizeof(uint16_t), hipHostMallocPortable));
+    }
+
+    for (size_t k = 0; k < chunks.size(); ++k) {
+        const int s = (int)(k & 1);
+        const Chunk& c = chunks[k];
+        const uint64_t cn = c.c1 - c.c0, span = c.byte_hi - c.byte_lo;
+        if (pending[s]) {  // slot reuse: finish chunk k-2
+            NSX_TRY(hipStreamSynchronize(st[s]));
+            if (!out_pinned)
+                std::memcpy(j->h_out + pending[s]->c0, h_ostage[s],
+                            (pending[s]->c1 - pending[s]->c0) * sizeof(uint16_t));
+            pending[s] = nullptr;
+        }
+        const uint8_t* src = j->h_base + c.byte_lo;
+        if (!in_pinned) {
+            std::memcpy(h_stage[s], src, span);
+            src = h_stage[s];
+        }
+        if (span) NSX_TRY(hipMemcpyAsync(d_data[s], src, span, hipMemcpyHostToDevice, st[s]));
+        if (j->h_partial) {
+            std::memcpy(h_pstage[s], j->h_partial + c.c0, cn * sizeof(uint32_t));
+            NSX_TRY(hipMemcpyAsync(d_part[s], h_pstage[s], cn * sizeof(uint32_t), hipMemcpyHostToDevice, st[s]));
+        }
+        uint16_t* out_dst = out_pinned ? j->h_out + c.c0 : h_ostage[s];
+        hipError_t e;
+        if (ragged) {
+            for (uint64_t i = 0; i <= cn; ++i) h_offstage[s][i] = j->h_offsets[c.c0 + i] - c.byte_lo;
+            NSX_TRY(hipMemcpyAsync(d_off[s], h_offstage[s], (cn + 1) * sizeof(uint64_t), hipMemcpyHostToDevice,
+                                   st[s]));
+            e = nsx::launch_ragged(cfg, d_data[s], d_off[s], cn, d_part[s], d_out[s], nullptr, st[s]);
+        } else {
+            e = nsx::launch_fixed(cfg, d_data[s], j->stride, j->seg_len, cn, d_part[s], d_out[s], st[s]);
+        }
+        NSX_TRY(e);
+        NSX_TRY(hipMemcpyAsync(out_dst, d_out[s], cn * sizeof(uint16_t), hipMemcpyDeviceToHost, st[s]));
+        pending[s] = &c;
+    }
+    for (int s = 0; s < 2; ++s) {
+        if (!st[s]) continue;
+        NSX_TRY(hipStreamSynchronize(st[s]));
+        if (pending[s] && !out_pinned)
+            std::memcpy(j->h_out + pending[s]->c0, h_ostage[s], (pending[s]->c1 - pending[s]->c0) * sizeof(uint16_t));
+        pending[s] = nullptr;
+    }
+
+done:
+    for (int s = 0; s < 2; ++s) {
+        if (st[s]) (void)hipStreamSynchronize(st[s]);
+        if (d_data[s]) (void)hipFree(d_data[s]);
+        if (d_out[s]) (void)hipFree(d_out[s]);
+        if (d_part[s]) (void)hipFree(d_part[s]);
+        if (d_off[s]) (void)hipFree(d_off[s]);
+        if (h_stage[s]) (void)hipHostFree(h_stage[s]);
+        if (h_ostage[s]) (void)hipHostFree(h_ostage[s]);
+        if (h_pstage[s]) (void)hipHostFree(h_pstage[s]);
+        if (h_offstage[s]) (void)hipHostFree(h_offstage[s]);
+        if (st[s]) (void)hipStreamDestroy(st[s]);
+    }
+    j->rc = rc;
+}
+
+int run_sharded(const uint8_t* h_base, uint64_t stride, uint32_t seg_len, const uint64_t* h_offsets, uint64_t n,
+                const uint32_t* h_partial, uint16_t* h_out, int num_gpus) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess) {
+        (void)hipGetLastError();
+        count = 0;
+    }
+    if (count <= 0) return NSX_ENODEV;
+    if (num_gpus <= 0) num_gpus = count;
+    if (num_gpus > count) return NSX_ENODEV;
+    int caller_dev = 0;
+    (void)hipGetDevice(&caller_dev);
+    if ((uint64_t)num_gpus > n) num_gpus = (int)n;
+    std::vector<uint64_t> bounds(num_gpus + 1);
+    nsx::shard_plan(h_offsets, n, num_gpus, bounds.data());
+    std::vector<Job> jobs(num_gpus);
+    for (int g = 0; g < num_gpus; ++g)
+        jobs[g] = Job{h_base, stride, seg_len, h_offsets, bounds[g], bounds[g + 1], h_partial, h_out, g, NSX_OK};
+    std::vector<std::thread> th;
+    for (int g = 1; g < num_gpus; ++g)
+        if (jobs[g].hi > jobs[g].lo) th.emplace_back(run_job, &jobs[g]);
+    if (jobs[0].hi > jobs[0].lo) run_job(&jobs[0]);
+    for (auto& t : th) t.join();
+    (void)hipSetDevice(caller_dev);
+    for (const Job& j : jobs)
+        if (j.rc != NSX_OK) return j.rc;
+    return NSX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nsx_csum_fixed_host(const uint8_t* h_base, uint64_t stride, uint32_t seg_len, uint64_t n,
+                        const uint32_t* h_prefix_partial, uint16_t* h_out, int num_gpus) {
+    if (n == 0) return NSX_OK;
+    if (!h_out || (seg_len && !h_base)) return NSX_EINVAL;
+    return run_sharded(h_base, stride, seg_len, nullptr, n, h_prefix_partial, h_out, num_gpus);
+}
+
+int nsx_csum_ragged_host(const uint8_t* h_base, const uint64_t* h_offsets, uint64_t n,
+                         const uint32_t* h_prefix_partial, uint16_t* h_out, int num_gpus) {
+    if (n == 0) return NSX_OK;
+    if (!h_out || !h_offsets || !h_base) return NSX_EINVAL;
+    for (uint64_t i = 0; i < n; ++i)
+        if (h_offsets[i + 1] < h_offsets[i]) return NSX_EINVAL;
+    return run_sharded(h_base, 0, 0, h_offsets, n, h_prefix_partial, h_out, num_gpus);
+}
+
+}  // extern "C"

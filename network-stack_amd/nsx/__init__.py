@@ -1,0 +1,227 @@
+"""nsx — Python binding of libnsx_csum.so (include/nsx_csum.h) for tests and bench.
+
+The product is the C ABI + gfx950 kernels in ../csrc; this module is plumbing:
+ctypes calls with torch tensors as device buffers. There is no fallback of any
+kind: if the library is missing, importing a device call raises, and on a host
+without a GPU the device calls return NSX_ENODEV, raised here as NsxError.
+
+Reference interface mirrored (transport/tcp/tcp.go:72-95):
+    computeChecksum(ipPseudoHeader []byte) uint16  → csum16(prefix, seg) -> int
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libnsx_csum.so")
+HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "nsx_csum.h")
+
+NSX_OK, NSX_EIO, NSX_ENOMEM, NSX_ENODEV, NSX_EINVAL = 0, -5, -12, -19, -22
+PARAM_BLOCKS_PER_CU, PARAM_SEGS_PER_WAVE, PARAM_NONTEMPORAL, PARAM_BLOCK_MODE, PARAM_XCD_MAP = 1, 2, 3, 4, 5
+
+
+class NsxError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        self.code = code
+        super().__init__(f"{what}: {lib().nsx_strerror(code).decode()} ({code})")
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load the in-tree product library; fail loudly if it was not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"libnsx_csum.so not built at {LIB_PATH}: run `make -C network-stack_amd` "
+                              "or __graft_entry__.build()")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, sz, u64, u32, i32, u8 = (ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint32,
+                                     ctypes.c_int, ctypes.c_uint8)
+        sig = {
+            "nsx_csum16": [vp, sz, vp, sz, vp],
+            "nsx_csum_fixed_dev": [vp, u64, u32, u64, vp, vp, vp],
+            "nsx_csum_ragged_dev": [vp, vp, u64, vp, vp, vp],
+            "nsx_verify_ragged_dev": [vp, vp, u64, vp, vp, vp, vp],
+            "nsx_pseudo_ipv4_partial_dev": [vp, vp, vp, u8, u64, vp, vp],
+            "nsx_csum_fixed_host": [vp, u64, u32, u64, vp, vp, i32],
+            "nsx_csum_ragged_host": [vp, vp, u64, vp, vp, i32],
+            "nsx_alloc_pinned": [sz, ctypes.POINTER(vp)],
+            "nsx_free_pinned": [vp],
+            "nsx_shard_plan": [vp, u64, i32, vp],
+            "nsx_fill_splitmix64_dev": [vp, u64, u64, u64, vp],
+            "nsx_abi_version": [],
+            "nsx_device_count": [ctypes.POINTER(i32)],
+            "nsx_set_param": [i32, ctypes.c_int64],
+            "nsx_get_param": [i32, ctypes.POINTER(ctypes.c_int64)],
+        }
+        for name, args in sig.items():
+            f = getattr(L, name)
+            f.argtypes = args
+            f.restype = ctypes.c_int
+        L.nsx_strerror.argtypes = [i32]
+        L.nsx_strerror.restype = ctypes.c_char_p
+        _lib = L
+    return _lib
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != NSX_OK:
+        raise NsxError(rc, what)
+
+
+def _np_ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _dev_ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(stream):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+# ---------------------------------------------------------------------------
+# host-side API
+# ---------------------------------------------------------------------------
+def abi_version() -> int:
+    return lib().nsx_abi_version()
+
+
+def device_count() -> int:
+    c = ctypes.c_int(0)
+    _check(lib().nsx_device_count(ctypes.byref(c)), "nsx_device_count")
+    return c.value
+
+
+def csum16(prefix: bytes, seg: bytes) -> int:
+    """computeChecksum (tcp.go:72-95): raw one's-complement sum over prefix ‖ seg."""
+    p = np.frombuffer(bytes(prefix), np.uint8) if prefix else None
+    s = np.frombuffer(bytes(seg), np.uint8) if seg else None
+    out = ctypes.c_uint16(0)
+    _check(lib().nsx_csum16(_np_ptr(p), len(prefix), _np_ptr(s), len(seg), ctypes.byref(out)), "nsx_csum16")
+    return out.value
+
+
+def field(raw: int) -> int:
+    return (~raw) & 0xFFFF
+
+
+def verify(raw: int) -> bool:
+    return raw == 0xFFFF
+
+
+def shard_plan(n: int, parts: int, offsets: np.ndarray | None = None) -> np.ndarray:
+    b = np.zeros(parts + 1, np.uint64)
+    off = None if offsets is None else np.ascontiguousarray(offsets, np.uint64)
+    _check(lib().nsx_shard_plan(_np_ptr(off), n, parts, _np_ptr(b)), "nsx_shard_plan")
+    return b
+
+
+def set_param(param: int, value: int) -> None:
+    _check(lib().nsx_set_param(param, value), "nsx_set_param")
+
+
+def get_param(param: int) -> int:
+    v = ctypes.c_int64(0)
+    _check(lib().nsx_get_param(param, ctypes.byref(v)), "nsx_get_param")
+    return v.value
+
+
+def fixed_host(buf: np.ndarray, stride: int, seg_len: int, n: int, partial: np.ndarray | None = None,
+               num_gpus: int = 0) -> np.ndarray:
+    buf = np.ascontiguousarray(buf, np.uint8)
+    out = np.empty(n, np.uint16)
+    part = None if partial is None else np.ascontiguousarray(partial, np.uint32)
+    _check(lib().nsx_csum_fixed_host(_np_ptr(buf), stride, seg_len, n, _np_ptr(part), _np_ptr(out), num_gpus),
+           "nsx_csum_fixed_host")
+    return out
+
+
+def ragged_host(buf: np.ndarray, offsets: np.ndarray, partial: np.ndarray | None = None,
+                num_gpus: int = 0) -> np.ndarray:
+    buf = np.ascontiguousarray(buf, np.uint8)
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    n = offsets.size - 1
+    out = np.empty(max(n, 0), np.uint16)
+    part = None if partial is None else np.ascontiguousarray(partial, np.uint32)
+    _check(lib().nsx_csum_ragged_host(_np_ptr(buf), _np_ptr(offsets), n, _np_ptr(part), _np_ptr(out), num_gpus),
+           "nsx_csum_ragged_host")
+    return out
+
+
+class PinnedBuffer:
+    """nsx_alloc_pinned-backed numpy view (DMA-registered host memory)."""
+
+    def __init__(self, nbytes: int):
+        p = ctypes.c_void_p()
+        _check(lib().nsx_alloc_pinned(nbytes, ctypes.byref(p)), "nsx_alloc_pinned")
+        self._p = p
+        self.nbytes = nbytes
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p.value)) if nbytes else \
+            np.zeros(0, np.uint8)
+
+    def free(self):
+        if self._p:
+            _check(lib().nsx_free_pinned(self._p), "nsx_free_pinned")
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+# ---------------------------------------------------------------------------
+# device-side API (torch tensors as HBM buffers)
+# ---------------------------------------------------------------------------
+def fixed_dev(buf, stride: int, seg_len: int, n: int, partial=None, out=None, stream=None):
+    import torch
+    if out is None:
+        out = torch.empty(n, dtype=torch.int16, device=buf.device)  # u16 bits
+    _check(lib().nsx_csum_fixed_dev(_dev_ptr(buf), stride, seg_len, n, _dev_ptr(partial), _dev_ptr(out),
+                                    _stream(stream)), "nsx_csum_fixed_dev")
+    return out
+
+
+def ragged_dev(buf, offsets, partial=None, out=None, stream=None):
+    import torch
+    n = offsets.numel() - 1
+    if out is None:
+        out = torch.empty(max(n, 0), dtype=torch.int16, device=offsets.device)  # u16 bits
+    _check(lib().nsx_csum_ragged_dev(_dev_ptr(buf), _dev_ptr(offsets), n, _dev_ptr(partial), _dev_ptr(out),
+                                     _stream(stream)), "nsx_csum_ragged_dev")
+    return out
+
+
+def verify_ragged_dev(buf, offsets, partial=None, raw=None, stream=None):
+    import torch
+    n = offsets.numel() - 1
+    ok = torch.empty(max(n, 0), dtype=torch.uint8, device=offsets.device)
+    _check(lib().nsx_verify_ragged_dev(_dev_ptr(buf), _dev_ptr(offsets), n, _dev_ptr(partial), _dev_ptr(ok),
+                                       _dev_ptr(raw), _stream(stream)), "nsx_verify_ragged_dev")
+    return ok
+
+
+def pseudo_ipv4_partial_dev(src, dst, length, proto: int = 6, out=None, stream=None):
+    import torch
+    n = length.numel()
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=length.device)  # u32 bits
+    _check(lib().nsx_pseudo_ipv4_partial_dev(_dev_ptr(src), _dev_ptr(dst), _dev_ptr(length), proto, n,
+                                             _dev_ptr(out), _stream(stream)), "nsx_pseudo_ipv4_partial_dev")
+    return out
+
+
+def fill_splitmix64_dev(buf, seed: int, byte_off: int = 0, stream=None):
+    _check(lib().nsx_fill_splitmix64_dev(_dev_ptr(buf), byte_off, buf.numel() * buf.element_size(), seed,
+                                         _stream(stream)), "nsx_fill_splitmix64_dev")
+    return buf

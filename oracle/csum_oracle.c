@@ -1,0 +1,231 @@
+/*
+ * csum_oracle.c — TEST INFRASTRUCTURE ONLY. NOT PART OF THE PRODUCT.
+ *
+ * CPU restatement of the reference's Internet checksum path, used solely as the
+ * checker by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg.
+ * Nothing under network-stack_amd/ links, loads or calls this file.
+ *
+ * Reference (oneee-playground/network-stack @ 2025-06-29, pure Go, no cgo):
+ *   transport/tcp/tcp.go:72-95   func (s segment) computeChecksum(ipPseudoHeader []byte) uint16
+ *   transport/tcp/tcp.go:98-128  func (s segment) bytes() []byte
+ *   transport/tcp/tcp.go:59-66   func (s segment) computeOffset() uint8
+ *   transport/tcp/tcp.go:188-216 ctl.byte / ctlFromByte
+ *   transport/tcp/tcp.go:225-231 option.bytes
+ *
+ * Parity pinning: the reference is Go and no Go toolchain exists in this
+ * container or on the GPU box, so the reference cannot be built or run here
+ * (SURVEY.md §8c). This restatement is pinned by (1) the reference's only
+ * checksum test, transport/tcp/tcp_test.go:26-32 (store ^sum over the
+ * segment{data:"hello"} serialization, the re-sum must be 0xFFFF), reproduced in
+ * tests/test_oracle.py, and (2) the RFC 1071 §3 numerical example plus the
+ * hand-derived KATs of SURVEY.md §8c (tests/golden/kat.json).
+ *
+ * Two formulations that must agree bit for bit:
+ *   oracle_go_checksum   — literal restatement: allocate + concatenate prefix and
+ *                          segment (tcp.go:73), zero-pad an odd total (tcp.go:74-77),
+ *                          16-bit big-endian words with the compare-carry end-around
+ *                          add (tcp.go:79-92), return the raw sum (tcp.go:94).
+ *   oracle_fold_checksum — wide form: integer sum of BE words over the virtual
+ *                          concatenation into a u64, then fold to 16 bits.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <pthread.h>
+
+#define ORACLE_EXPORT __attribute__((visibility("default")))
+
+/* tcp.go:72-95, statement for statement. Returns 0xFFFFFFFF on allocation
+ * failure (the Go code would panic). */
+ORACLE_EXPORT uint32_t oracle_go_checksum(const uint8_t* prefix, size_t prefix_len,
+                                          const uint8_t* seg, size_t seg_len) {
+    /* input := append(ipPseudoHeader, s.bytes()...)  (tcp.go:73) */
+    size_t n = prefix_len + seg_len;
+    uint8_t* input = (uint8_t*)malloc(n + 1);
+    if (!input) return 0xFFFFFFFFu;
+    if (prefix_len) memcpy(input, prefix, prefix_len);
+    if (seg_len) memcpy(input + prefix_len, seg, seg_len);
+    /* if len(input)%2 == 1 { input = append(input, byte(0)) }  (tcp.go:74-77) */
+    if (n % 2 == 1) input[n++] = 0;
+    /* the serial end-around-carry loop (tcp.go:79-92) */
+    uint16_t sum = 0;
+    for (size_t idx = 0; idx < n; idx += 2) {
+        uint16_t v = (uint16_t)(((uint16_t)input[idx] << 8) + (uint16_t)input[idx + 1]);
+        v = (uint16_t)(v + sum);
+        if (sum > v) v++;
+        sum = v;
+    }
+    free(input);
+    return sum; /* raw sum, not complemented (tcp.go:94) */
+}
+
+static inline uint16_t fold64(uint64_t s) {
+    while (s >> 16) s = (s & 0xFFFFu) + (s >> 16);
+    return (uint16_t)s;
+}
+
+/* Integer sum of the big-endian 16-bit words of bytes that begin at logical
+ * position `pos` of the concatenated stream (pos parity decides pairing). */
+static uint64_t be_word_sum(const uint8_t* p, size_t len, size_t pos) {
+    uint64_t s = 0;
+    for (size_t i = 0; i < len; i++) {
+        uint64_t b = p[i];
+        s += ((pos + i) & 1) ? b : (b << 8);
+    }
+    return s;
+}
+
+/* Wide formulation over the virtual concatenation prefix||seg (no copy). */
+ORACLE_EXPORT uint32_t oracle_fold_checksum(const uint8_t* prefix, size_t prefix_len,
+                                            const uint8_t* seg, size_t seg_len) {
+    uint64_t s = be_word_sum(prefix, prefix_len, 0) + be_word_sum(seg, seg_len, prefix_len);
+    return fold64(s);
+}
+
+/* Raw sum of one segment with a pre-summed prefix partial (the device API's
+ * d_prefix_partial convention: any integer sum, folded or not, of the prefix's
+ * BE words; the prefix length is even). */
+static uint16_t seg_with_partial(const uint8_t* seg, size_t len, uint32_t partial) {
+    return fold64((uint64_t)partial + be_word_sum(seg, len, 0));
+}
+
+/* Batch forms used as the checker of the device kernels. */
+ORACLE_EXPORT void oracle_batch_fixed(const uint8_t* base, uint64_t stride, uint32_t seg_len,
+                                      uint64_t n, const uint32_t* prefix_partial,
+                                      uint16_t* out) {
+    for (uint64_t i = 0; i < n; i++)
+        out[i] = seg_with_partial(base + i * stride, seg_len, prefix_partial ? prefix_partial[i] : 0);
+}
+
+ORACLE_EXPORT void oracle_batch_ragged(const uint8_t* base, const uint64_t* offsets, uint64_t n,
+                                       const uint32_t* prefix_partial, uint16_t* out) {
+    for (uint64_t i = 0; i < n; i++)
+        out[i] = seg_with_partial(base + offsets[i], (size_t)(offsets[i + 1] - offsets[i]),
+                                  prefix_partial ? prefix_partial[i] : 0);
+}
+
+/* The Go-faithful form over a fixed-stride batch: one oracle_go_checksum call
+ * (allocate, concatenate, pad, serial loop) per segment, exactly as a Go caller
+ * looping over computeChecksum would pay it. This is bench.py's cpu_baseline leg. */
+ORACLE_EXPORT void oracle_go_batch_fixed(const uint8_t* base, uint64_t stride, uint32_t seg_len,
+                                         uint64_t n, const uint8_t* prefix, size_t prefix_len,
+                                         uint16_t* out) {
+    for (uint64_t i = 0; i < n; i++)
+        out[i] = (uint16_t)oracle_go_checksum(prefix, prefix_len, base + i * stride, seg_len);
+}
+
+/* Multi-threaded variant of oracle_batch_fixed / _ragged for full-size checks
+ * in the GPU tests (contiguous index shards, one pthread each). */
+typedef struct {
+    const uint8_t* base; uint64_t stride; uint32_t seg_len; const uint64_t* offsets;
+    uint64_t lo, hi; const uint32_t* partial; uint16_t* out;
+} shard_arg;
+
+static void* shard_run(void* a_) {
+    shard_arg* a = (shard_arg*)a_;
+    for (uint64_t i = a->lo; i < a->hi; i++) {
+        const uint8_t* p; size_t len;
+        if (a->offsets) { p = a->base + a->offsets[i]; len = (size_t)(a->offsets[i + 1] - a->offsets[i]); }
+        else { p = a->base + i * a->stride; len = a->seg_len; }
+        a->out[i] = seg_with_partial(p, len, a->partial ? a->partial[i] : 0);
+    }
+    return NULL;
+}
+
+ORACLE_EXPORT void oracle_batch_mt(const uint8_t* base, uint64_t stride, uint32_t seg_len,
+                                   const uint64_t* offsets, uint64_t n,
+                                   const uint32_t* prefix_partial, uint16_t* out, int threads) {
+    if (threads < 1) threads = 1;
+    if (threads > 64) threads = 64;
+    pthread_t th[64];
+    shard_arg args[64];
+    for (int t = 0; t < threads; t++) {
+        args[t] = (shard_arg){base, stride, seg_len, offsets, n * t / threads, n * (t + 1) / threads,
+                              prefix_partial, out};
+        pthread_create(&th[t], NULL, shard_run, &args[t]);
+    }
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+}
+
+/* ---- tcp.go:98-128 segment serialization (for struct-level parity) ---- */
+
+typedef struct {
+    uint8_t kind, length;
+    const uint8_t* data; size_t data_len;
+} oracle_option;
+
+typedef struct {
+    uint16_t src_port, dst_port;
+    uint32_t seq_num, ack_num;
+    uint8_t offset, control; /* control: already-encoded ctl byte (tcp.go:197-206) */
+    uint16_t window, checksum, urgent_ptr;
+    const oracle_option* options; size_t n_options;
+    const uint8_t* data; size_t data_len;
+} oracle_segment;
+
+/* option.bytes (tcp.go:225-231): MSS → kind,length,data...; every other kind → kind. */
+static size_t option_bytes(const oracle_option* o, uint8_t* out) {
+    if (o->kind == 2) {
+        out[0] = o->kind; out[1] = o->length;
+        if (o->data_len) memcpy(out + 2, o->data, o->data_len);
+        return 2 + o->data_len;
+    }
+    out[0] = o->kind;
+    return 1;
+}
+
+/* Returns the serialized length; writes at most `cap` bytes (call with cap=0 to
+ * size). Reproduces the reference's option padding exactly: it appends
+ * `remainder` zero bytes, not 4-remainder (tcp.go:118-121). */
+ORACLE_EXPORT size_t oracle_segment_bytes(const oracle_segment* s, uint8_t* out, size_t cap) {
+    size_t optlen = 0;
+    for (size_t i = 0; i < s->n_options; i++)
+        optlen += (s->options[i].kind == 2) ? 2 + s->options[i].data_len : 1;
+    size_t total = 20 + optlen;
+    if (s->n_options > 0) total += total % 4;
+    total += s->data_len;
+    if (cap < total) return total;
+    uint8_t* b = out;
+    b[0] = s->src_port >> 8; b[1] = s->src_port & 0xFF;
+    b[2] = s->dst_port >> 8; b[3] = s->dst_port & 0xFF;
+    for (int i = 0; i < 4; i++) b[4 + i] = (uint8_t)(s->seq_num >> (24 - 8 * i));
+    for (int i = 0; i < 4; i++) b[8 + i] = (uint8_t)(s->ack_num >> (24 - 8 * i));
+    b[12] = s->offset; b[13] = s->control;
+    b[14] = s->window >> 8; b[15] = s->window & 0xFF;
+    b[16] = s->checksum >> 8; b[17] = s->checksum & 0xFF;
+    b[18] = s->urgent_ptr >> 8; b[19] = s->urgent_ptr & 0xFF;
+    size_t at = 20;
+    if (s->n_options > 0) {
+        for (size_t i = 0; i < s->n_options; i++) at += option_bytes(&s->options[i], b + at);
+        size_t rem = at % 4;
+        memset(b + at, 0, rem);
+        at += rem;
+    }
+    if (s->data_len) memcpy(b + at, s->data, s->data_len);
+    return at + s->data_len;
+}
+
+/* computeOffset (tcp.go:59-66): ceil((20 + Σ len(option.bytes())) / 4). */
+ORACLE_EXPORT uint8_t oracle_compute_offset(const oracle_segment* s) {
+    size_t off = 20;
+    for (size_t i = 0; i < s->n_options; i++)
+        off += (s->options[i].kind == 2) ? 2 + s->options[i].data_len : 1;
+    return (uint8_t)((off + 3) / 4);
+}
+
+/* ---- synthetic data: splitmix64 stream, counter-based ---- */
+static inline uint64_t splitmix64_at(uint64_t seed, uint64_t i) {
+    uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+/* Byte j of the stream is byte (j % 8) of little-endian word j / 8. */
+ORACLE_EXPORT void oracle_splitmix64_fill(uint8_t* buf, uint64_t byte_off, uint64_t nbytes,
+                                          uint64_t seed) {
+    for (uint64_t j = 0; j < nbytes; j++) {
+        uint64_t pos = byte_off + j;
+        buf[j] = (uint8_t)(splitmix64_at(seed, pos >> 3) >> (8 * (pos & 7)));
+    }
+}

@@ -1,0 +1,287 @@
+"""TEST INFRASTRUCTURE ONLY — not part of the product.
+
+Python/numpy restatement of the reference's Internet checksum, used to generate
+and check the committed golden fixtures (tests/golden/) and as a second,
+independent formulation beside oracle/csum_oracle.c. Only tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module.
+
+Reference (pure Go; cannot be built or run here):
+  transport/tcp/tcp.go:72-95   computeChecksum — concat prefix‖segment, zero-pad an
+                               odd total, 16-bit BE words, compare-carry end-around
+                               add, return the RAW sum (not complemented)
+  transport/tcp/tcp.go:98-128  segment.bytes — BE header, options, (buggy) padding, data
+  transport/tcp/tcp.go:59-66   computeOffset
+  transport/tcp/tcp.go:188-216 ctl.byte / ctlFromByte
+Pinned by transport/tcp/tcp_test.go:26-32 and RFC 1071 §3 (see tests/test_oracle.py).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from dataclasses import dataclass, field
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "libnsx_oracle.so")
+
+
+# ---------------------------------------------------------------------------
+# Pure-Python restatements (small inputs only)
+# ---------------------------------------------------------------------------
+def go_checksum(prefix: bytes, seg: bytes) -> int:
+    """Literal restatement of tcp.go:72-95 (serial compare-carry loop)."""
+    data = bytearray(prefix) + bytearray(seg)          # tcp.go:73
+    if len(data) % 2 == 1:                              # tcp.go:74-77
+        data.append(0)
+    s = 0
+    for idx in range(0, len(data), 2):                  # tcp.go:80-92
+        v = ((data[idx] << 8) + data[idx + 1]) & 0xFFFF
+        v = (v + s) & 0xFFFF
+        if s > v:
+            v += 1
+        s = v
+    return s                                            # tcp.go:94
+
+
+def fold(s: int) -> int:
+    while s >> 16:
+        s = (s & 0xFFFF) + (s >> 16)
+    return s
+
+
+def be_word_sum(b: bytes, pos: int = 0) -> int:
+    """Integer sum of BE 16-bit words for bytes starting at stream position pos."""
+    a = np.frombuffer(bytes(b), dtype=np.uint8).astype(np.uint64)
+    if a.size == 0:
+        return 0
+    w = np.where((np.arange(a.size) + pos) % 2 == 0, a << np.uint64(8), a)
+    return int(w.sum(dtype=np.uint64))
+
+
+def fold_checksum(prefix: bytes, seg: bytes) -> int:
+    """Wide formulation: integer BE-word sum of the virtual concatenation, folded."""
+    return fold(be_word_sum(prefix, 0) + be_word_sum(seg, len(prefix)))
+
+
+def field_value(raw: int) -> int:
+    """What the sender stores in the checksum field (tcp_test.go:28)."""
+    return (~raw) & 0xFFFF
+
+
+def verify(raw: int) -> bool:
+    """Receiver acceptance rule (tcp.go:70)."""
+    return raw == 0xFFFF
+
+
+# ---------------------------------------------------------------------------
+# numpy batch forms (fixture generation, full-size spot checks)
+# ---------------------------------------------------------------------------
+def batch_fixed(buf: np.ndarray, stride: int, seg_len: int, n: int,
+                partial: np.ndarray | None = None) -> np.ndarray:
+    buf = np.asarray(buf, dtype=np.uint8)
+    out = np.empty(n, dtype=np.uint16)
+    if n == 0:
+        return out
+    idx = (np.arange(n, dtype=np.int64) * stride)[:, None] + np.arange(seg_len, dtype=np.int64)[None, :]
+    seg = buf[idx].astype(np.uint64) if seg_len else np.zeros((n, 0), np.uint64)
+    wts = np.where(np.arange(seg_len) % 2 == 0, 256, 1).astype(np.uint64)
+    s = (seg * wts[None, :]).sum(axis=1, dtype=np.uint64)
+    if partial is not None:
+        s = s + np.asarray(partial, dtype=np.uint64)
+    for _ in range(4):
+        s = (s & np.uint64(0xFFFF)) + (s >> np.uint64(16))
+    out[:] = s.astype(np.uint16)
+    return out
+
+
+def batch_ragged(buf: np.ndarray, offsets: np.ndarray, partial: np.ndarray | None = None) -> np.ndarray:
+    buf = np.asarray(buf, dtype=np.uint8)
+    offsets = np.asarray(offsets, dtype=np.uint64)
+    n = offsets.size - 1
+    out = np.empty(n, dtype=np.uint16)
+    for i in range(n):
+        lo, hi = int(offsets[i]), int(offsets[i + 1])
+        s = be_word_sum(buf[lo:hi].tobytes(), 0)
+        if partial is not None:
+            s += int(partial[i])
+        out[i] = fold(s)
+    return out
+
+
+def splitmix64_bytes(seed: int, byte_off: int, nbytes: int) -> np.ndarray:
+    """Byte j of the stream = byte j%8 of LE word j//8, word i = splitmix64(seed, i)."""
+    w0 = byte_off // 8
+    w1 = (byte_off + nbytes + 7) // 8
+    i = np.arange(w0, w1, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + (i + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    b = z.astype("<u8").view(np.uint8)
+    s = byte_off - w0 * 8
+    return b[s:s + nbytes].copy()
+
+
+# ---------------------------------------------------------------------------
+# tcp.go segment model (struct-level parity)
+# ---------------------------------------------------------------------------
+@dataclass
+class Ctl:
+    """tcp.go:188-216 — flags in order cwr, ece, urg, ack, psh, rst, syn, fin (MSB first)."""
+    cwr: bool = False
+    ece: bool = False
+    urg: bool = False
+    ack: bool = False
+    psh: bool = False
+    rst: bool = False
+    syn: bool = False
+    fin: bool = False
+
+    def byte(self) -> int:
+        flags = [self.cwr, self.ece, self.urg, self.ack, self.psh, self.rst, self.syn, self.fin]
+        b = 0
+        for idx, f in enumerate(flags):
+            if f:
+                b |= 1 << (7 - idx)
+        return b
+
+    @staticmethod
+    def from_byte(b: int) -> "Ctl":
+        names = ["cwr", "ece", "urg", "ack", "psh", "rst", "syn", "fin"]
+        return Ctl(**{n: bool(b & (1 << (7 - i))) for i, n in enumerate(names)})
+
+
+@dataclass
+class Option:
+    kind: int = 0
+    length: int = 0
+    data: bytes = b""
+
+    def bytes(self) -> bytes:  # tcp.go:225-231
+        if self.kind == 2:
+            return bytes([self.kind, self.length]) + self.data
+        return bytes([self.kind])
+
+
+@dataclass
+class Segment:
+    src_port: int = 0
+    dst_port: int = 0
+    seq_num: int = 0
+    ack_num: int = 0
+    offset: int = 0
+    control: Ctl = field(default_factory=Ctl)
+    window: int = 0
+    checksum: int = 0
+    urgent_ptr: int = 0
+    options: list = field(default_factory=list)
+    data: bytes = b""
+
+    def compute_offset(self) -> int:  # tcp.go:59-66
+        off = 20 + sum(len(o.bytes()) for o in self.options)
+        return (off + 3) // 4
+
+    def bytes(self) -> bytes:  # tcp.go:98-128
+        b = bytearray()
+        b += self.src_port.to_bytes(2, "big") + self.dst_port.to_bytes(2, "big")
+        b += self.seq_num.to_bytes(4, "big") + self.ack_num.to_bytes(4, "big")
+        b += bytes([self.offset & 0xFF, self.control.byte()])
+        b += self.window.to_bytes(2, "big")
+        b += self.checksum.to_bytes(2, "big") + self.urgent_ptr.to_bytes(2, "big")
+        if self.options:
+            for o in self.options:
+                b += o.bytes()
+            rem = len(b) % 4
+            if rem > 0:
+                b += bytes(rem)  # reference pads `remainder`, not 4-remainder (tcp.go:118-121)
+        b += self.data
+        return bytes(b)
+
+    def compute_checksum(self, pseudo: bytes = b"") -> int:  # tcp.go:72-95
+        return go_checksum(pseudo, self.bytes())
+
+
+def ipv4_pseudo_header(src: bytes, dst: bytes, proto: int, length: int) -> bytes:
+    """RFC 9293 §3.1 IPv4 pseudo-header: src(4) dst(4) zero(1) proto(1) len(2).
+    Inputs as ip.Addr.Raw() (ipv4.go:15) and ip.NextProtoTCP = 6 (protocols.go:8)."""
+    return bytes(src) + bytes(dst) + bytes([0, proto & 0xFF]) + (length & 0xFFFF).to_bytes(2, "big")
+
+
+def ipv6_pseudo_header(src: bytes, dst: bytes, next_header: int, length: int) -> bytes:
+    """RFC 8200 §8.1 IPv6 pseudo-header: src(16) dst(16) len(4) zero(3) nh(1)."""
+    return bytes(src) + bytes(dst) + (length & 0xFFFFFFFF).to_bytes(4, "big") + bytes(3) + bytes([next_header & 0xFF])
+
+
+# ---------------------------------------------------------------------------
+# C restatement (oracle/csum_oracle.c) via ctypes
+# ---------------------------------------------------------------------------
+def build_c_oracle(force: bool = False) -> str:
+    src = os.path.join(HERE, "csum_oracle.c")
+    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", HERE])
+    return LIB_PATH
+
+
+_c = None
+
+
+def c_oracle():
+    global _c
+    if _c is None:
+        if not os.path.exists(LIB_PATH):
+            build_c_oracle()
+        lib = ctypes.CDLL(LIB_PATH)
+        u8p = ctypes.c_void_p
+        lib.oracle_go_checksum.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.c_size_t]
+        lib.oracle_go_checksum.restype = ctypes.c_uint32
+        lib.oracle_fold_checksum.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.c_size_t]
+        lib.oracle_fold_checksum.restype = ctypes.c_uint32
+        lib.oracle_batch_fixed.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, u8p, u8p]
+        lib.oracle_batch_ragged.argtypes = [u8p, u8p, ctypes.c_uint64, u8p, u8p]
+        lib.oracle_batch_mt.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint32, u8p, ctypes.c_uint64,
+                                        u8p, u8p, ctypes.c_int]
+        lib.oracle_go_batch_fixed.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+                                              u8p, ctypes.c_size_t, u8p]
+        lib.oracle_splitmix64_fill.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]
+        _c = lib
+    return _c
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def c_go_checksum(prefix: bytes, seg: bytes) -> int:
+    p = np.frombuffer(bytes(prefix), np.uint8) if prefix else None
+    s = np.frombuffer(bytes(seg), np.uint8) if seg else None
+    return c_oracle().oracle_go_checksum(_ptr(p), len(prefix), _ptr(s), len(seg))
+
+
+def c_fold_checksum(prefix: bytes, seg: bytes) -> int:
+    p = np.frombuffer(bytes(prefix), np.uint8) if prefix else None
+    s = np.frombuffer(bytes(seg), np.uint8) if seg else None
+    return c_oracle().oracle_fold_checksum(_ptr(p), len(prefix), _ptr(s), len(seg))
+
+
+def c_batch(buf: np.ndarray, n: int, stride: int = 0, seg_len: int = 0, offsets: np.ndarray | None = None,
+            partial: np.ndarray | None = None, threads: int = 8) -> np.ndarray:
+    """Multi-threaded C oracle over a fixed-stride (offsets None) or ragged batch."""
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    out = np.empty(n, dtype=np.uint16)
+    if offsets is not None:
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    if partial is not None:
+        partial = np.ascontiguousarray(partial, dtype=np.uint32)
+    c_oracle().oracle_batch_mt(_ptr(buf), stride, seg_len, _ptr(offsets), n, _ptr(partial), _ptr(out), threads)
+    return out
+
+
+def c_splitmix64(seed: int, nbytes: int, byte_off: int = 0) -> np.ndarray:
+    out = np.empty(nbytes, dtype=np.uint8)
+    c_oracle().oracle_splitmix64_fill(_ptr(out), byte_off, nbytes, seed)
+    return out

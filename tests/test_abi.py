@@ -1,0 +1,199 @@
+"""C-ABI boundary tests that need no GPU: the library loads, exports every
+function include/nsx_csum.h declares, the single-segment host entry point
+(computeChecksum, tcp.go:72-95) matches the oracle, host logic (shard plan,
+params) behaves, and device entry points refuse loudly without a GPU."""
+import ctypes
+import json
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import nsx
+from conftest import GOLDEN, ROOT
+from oracle import csum_oracle as O
+
+HEADER = os.path.join(ROOT, "include", "nsx_csum.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(nsx_[a-z_0-9]+)\s*\(", src, flags=re.M)
+    inline = set(re.findall(r"static inline [a-z_0-9]+ (nsx_[a-z_0-9]+)\(", src))
+    return sorted(set(names) - inline)
+
+
+def test_header_declares_the_boundary():
+    names = declared_functions()
+    for must in ("nsx_csum16", "nsx_csum_fixed_dev", "nsx_csum_ragged_dev", "nsx_csum_fixed_host",
+                 "nsx_csum_ragged_host", "nsx_verify_ragged_dev", "nsx_pseudo_ipv4_partial_dev"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    L = nsx.lib()
+    missing = [n for n in declared_functions() if not hasattr(L, n)]
+    assert not missing, missing
+    out = subprocess.run(["nm", "-D", "--defined-only", nsx.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (nsx_\w+)", out))
+    assert set(declared_functions()) <= exported
+
+
+def test_library_has_gfx950_code_object():
+    out = subprocess.run(["/opt/rocm/bin/roc-obj-ls", nsx.LIB_PATH], capture_output=True, text=True)
+    if out.returncode != 0:
+        pytest.skip("roc-obj-ls unavailable")
+    assert "gfx950" in out.stdout
+
+
+def test_abi_version():
+    assert nsx.abi_version() == 1
+
+
+@pytest.mark.parametrize("case", json.load(open(os.path.join(GOLDEN, "kat.json"))), ids=lambda c: c["name"])
+def test_csum16_kat(case):
+    assert nsx.csum16(bytes.fromhex(case["prefix"]), bytes.fromhex(case["segment"])) == case["raw"]
+
+
+def test_csum16_golden_vectors():
+    idx = json.load(open(os.path.join(GOLDEN, "vectors.json")))
+    blob = np.fromfile(os.path.join(GOLDEN, "vectors.bin"), np.uint8)
+    for c in idx:
+        seg = blob[c["offset"]:c["offset"] + c["length"]].tobytes()
+        assert nsx.csum16(bytes.fromhex(c["prefix"]), seg) == c["raw"], c
+
+
+def test_csum16_reference_TestSegmentComputeChecksum():
+    """tcp_test.go:26-32 through the C ABI."""
+    s = O.Segment(data=b"hello")
+    s.checksum = nsx.field(nsx.csum16(b"", s.bytes()))
+    assert nsx.verify(nsx.csum16(b"", s.bytes()))
+
+
+def test_csum16_random_vs_oracle():
+    rng = np.random.default_rng(11)
+    for _ in range(1500):
+        n = int(rng.integers(0, 3000))
+        pl = int(rng.integers(0, 45))
+        seg = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        if rng.integers(0, 8) == 0:
+            seg = b"\xff" * n
+        pre = rng.integers(0, 256, pl, dtype=np.uint8).tobytes()
+        assert nsx.csum16(pre, seg) == O.c_go_checksum(pre, seg), (n, pl)
+
+
+def test_csum16_unaligned_views():
+    """Misaligned host pointers (computeChecksum takes any []byte)."""
+    buf = O.c_splitmix64(0x1071, 70000)
+    for start in range(8):
+        for n in (0, 1, 2, 7, 8, 9, 1499, 1500, 65536):
+            seg = buf[start:start + n]
+            out = ctypes.c_uint16()
+            rc = nsx.lib().nsx_csum16(None, 0, seg.ctypes.data_as(ctypes.c_void_p), n, ctypes.byref(out))
+            assert rc == 0 and out.value == O.c_go_checksum(b"", seg.tobytes())
+
+
+def test_csum16_errors():
+    L = nsx.lib()
+    out = ctypes.c_uint16()
+    assert L.nsx_csum16(None, 4, None, 0, ctypes.byref(out)) == nsx.NSX_EINVAL
+    assert L.nsx_csum16(None, 0, None, 3, ctypes.byref(out)) == nsx.NSX_EINVAL
+    assert L.nsx_csum16(None, 0, None, 0, None) == nsx.NSX_EINVAL
+    assert L.nsx_csum16(None, 0, None, 0, ctypes.byref(out)) == 0 and out.value == 0
+
+
+def test_shard_plan_fixed():
+    for n, parts in ((0, 1), (10, 3), (1 << 20, 8), (5, 8)):
+        b = nsx.shard_plan(n, parts)
+        assert b[0] == 0 and b[-1] == n and np.all(np.diff(b.astype(np.int64)) >= 0)
+        sizes = np.diff(b.astype(np.int64))
+        assert sizes.max() - sizes.min() <= 1
+
+
+def test_shard_plan_ragged_byte_balanced():
+    rng = np.random.default_rng(0x1072)
+    lens = rng.integers(64, 9001, 100000).astype(np.uint64)
+    offs = np.zeros(lens.size + 1, np.uint64)
+    offs[1:] = np.cumsum(lens)
+    b = nsx.shard_plan(lens.size, 8, offs)
+    assert b[0] == 0 and b[-1] == lens.size
+    per = [int(offs[b[g + 1]] - offs[b[g]]) for g in range(8)]
+    assert max(per) - min(per) <= 2 * 9000
+    assert sum(per) == int(offs[-1])
+
+
+def test_params_roundtrip():
+    for p in (nsx.PARAM_BLOCKS_PER_CU, nsx.PARAM_SEGS_PER_WAVE, nsx.PARAM_NONTEMPORAL, nsx.PARAM_BLOCK_MODE,
+              nsx.PARAM_XCD_MAP):
+        old = nsx.get_param(p)
+        nsx.set_param(p, 1)
+        assert nsx.get_param(p) == 1
+        nsx.set_param(p, old)
+    with pytest.raises(nsx.NsxError):
+        nsx.set_param(99, 1)
+
+
+def test_device_calls_fail_loudly_without_gpu():
+    """No CPU fallback: on a GPU-less host every device/batch entry point reports
+    NSX_ENODEV (never a silently computed result)."""
+    if nsx.device_count() > 0:
+        pytest.skip("GPU present")
+    L = nsx.lib()
+    fake = ctypes.c_void_p(0x1000)
+    assert L.nsx_csum_fixed_dev(fake, 1500, 1500, 4, None, fake, None) == nsx.NSX_ENODEV
+    assert L.nsx_csum_ragged_dev(fake, fake, 4, None, fake, None) == nsx.NSX_ENODEV
+    assert L.nsx_verify_ragged_dev(fake, fake, 4, None, fake, None, None) == nsx.NSX_ENODEV
+    assert L.nsx_pseudo_ipv4_partial_dev(fake, fake, fake, 6, 4, fake, None) == nsx.NSX_ENODEV
+    assert L.nsx_fill_splitmix64_dev(fake, 0, 16, 1, None) == nsx.NSX_ENODEV
+    buf = np.zeros(3000, np.uint8)
+    with pytest.raises(nsx.NsxError) as e:
+        nsx.fixed_host(buf, 1500, 1500, 2)
+    assert e.value.code == nsx.NSX_ENODEV
+    with pytest.raises(nsx.NsxError):
+        nsx.ragged_host(buf, np.array([0, 10, 3000], np.uint64))
+    p = ctypes.c_void_p()
+    assert L.nsx_alloc_pinned(64, ctypes.byref(p)) == nsx.NSX_ENODEV
+
+
+def test_device_calls_validate_before_device():
+    L = nsx.lib()
+    fake = ctypes.c_void_p(0x1000)
+    assert L.nsx_csum_fixed_dev(fake, 1500, 1500, 0, None, None, None) == 0   # n == 0 is a no-op
+    assert L.nsx_csum_fixed_dev(None, 1500, 1500, 4, None, fake, None) == nsx.NSX_EINVAL
+    assert L.nsx_csum_fixed_dev(fake, 1500, 1500, 4, None, None, None) == nsx.NSX_EINVAL
+    assert L.nsx_csum_ragged_dev(fake, None, 4, None, fake, None) == nsx.NSX_EINVAL
+    bad = np.array([0, 10, 5], np.uint64)
+    assert L.nsx_csum_ragged_host(np.zeros(16, np.uint8).ctypes.data_as(ctypes.c_void_p),
+                                  bad.ctypes.data_as(ctypes.c_void_p), 2, None,
+                                  np.zeros(2, np.uint16).ctypes.data_as(ctypes.c_void_p), 0) == nsx.NSX_EINVAL
+
+
+def test_c_caller_compiles_and_links(tmp_path):
+    """A plain C program (what cgo compiles) includes the header and links the library."""
+    src = tmp_path / "caller.c"
+    src.write_text(r'''
+#include <stdio.h>
+#include <string.h>
+#include "nsx_csum.h"
+int main(void) {
+    unsigned char seg[25] = {0};
+    memcpy(seg + 20, "hello", 5);
+    uint16_t raw = 0;
+    if (nsx_csum16(NULL, 0, seg, sizeof seg, &raw) != NSX_OK) return 2;
+    uint16_t f = nsx_field(raw);
+    seg[16] = f >> 8; seg[17] = f & 0xFF;           /* tcp.go:110 */
+    uint16_t again = 0;
+    nsx_csum16(NULL, 0, seg, sizeof seg, &again);
+    printf("%04x %04x %d\n", raw, again, nsx_verify(again));
+    return nsx_verify(again) ? 0 : 1;
+}
+''')
+    exe = tmp_path / "caller"
+    libdir = os.path.dirname(nsx.LIB_PATH)
+    subprocess.check_call(["gcc", "-std=c11", "-Wall", "-Werror", str(src), "-I", os.path.join(ROOT, "include"),
+                           "-L", libdir, "-lnsx_csum", f"-Wl,-rpath,{libdir}", "-o", str(exe)])
+    out = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert out.returncode == 0 and out.stdout.split() == ["43d2", "ffff", "1"]

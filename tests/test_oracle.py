@@ -1,0 +1,156 @@
+"""Oracle pinning (CPU): the restatement against the reference's own test, RFC
+1071 and the committed golden fixtures; the four formulations against each
+other. Mirrors transport/tcp/tcp_test.go for the segment model."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from oracle import csum_oracle as O
+
+
+def load(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+# --- transport/tcp/tcp_test.go, restated against the oracle segment model ---
+
+def test_reference_TestSegmentComputeChecksum():
+    """tcp_test.go:26-32: field = ^sum; the re-sum over the same segment is 0xFFFF."""
+    s = O.Segment(data=b"hello")
+    s.checksum = (~s.compute_checksum(b"")) & 0xFFFF
+    assert s.compute_checksum(b"") == 0xFFFF, f"{s.checksum:b}"
+    # and with the C restatements
+    assert O.c_go_checksum(b"", s.bytes()) == 0xFFFF
+    assert O.c_fold_checksum(b"", s.bytes()) == 0xFFFF
+
+
+def test_reference_TestSegmentComputeOffset():
+    """tcp_test.go:11-24."""
+    s = O.Segment()
+    assert s.compute_offset() == 20 // 4
+    s.options.append(O.Option())
+    assert s.compute_offset() == 20 // 4 + 1
+
+
+def test_reference_TestSegmentCodec_bytes():
+    """tcp_test.go:34-55 builds this segment; its bytes() layout (tcp.go:98-128)."""
+    s = O.Segment(src_port=1, dst_port=2, seq_num=3, ack_num=4, offset=5, window=6, checksum=7,
+                  urgent_ptr=8, data=bytes([9]))
+    s.offset = s.compute_offset()
+    assert s.bytes().hex() == "00010002" "00000003" "00000004" "05" "00" "0006" "0007" "0008" "09"
+
+
+def test_reference_TestCTLCodec():
+    """tcp_test.go:57-67."""
+    c = O.Ctl(urg=True, rst=True)
+    assert O.Ctl.from_byte(c.byte()) == c
+    assert c.byte() == 0b00100100
+
+
+# --- KATs and formulation agreement ---
+
+@pytest.mark.parametrize("case", load("kat.json"), ids=lambda c: c["name"])
+def test_kat(case):
+    p, s = bytes.fromhex(case["prefix"]), bytes.fromhex(case["segment"])
+    for f in (O.go_checksum, O.fold_checksum, O.c_go_checksum, O.c_fold_checksum):
+        assert f(p, s) == case["raw"], f.__name__
+    assert case["field"] == (~case["raw"]) & 0xFFFF
+
+
+def test_kat_sender_receiver_roundtrip():
+    """Storing field=^raw at bytes 16-17 (tcp.go:110) makes the receiver's sum 0xFFFF."""
+    rng = np.random.default_rng(7)
+    for n in (0, 1, 5, 100, 1480):
+        seg = O.Segment(src_port=int(rng.integers(65536)), dst_port=443, seq_num=int(rng.integers(1 << 32)),
+                        data=rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+        seg.offset = seg.compute_offset()
+        pseudo = O.ipv4_pseudo_header(b"\x0a\x00\x00\x01", b"\x0a\x00\x00\x02", 6, len(seg.bytes()))
+        seg.checksum = O.field_value(seg.compute_checksum(pseudo))
+        assert O.verify(seg.compute_checksum(pseudo))
+
+
+def test_random_agreement_all_formulations():
+    rng = np.random.default_rng(0xC0FFEE)
+    for _ in range(400):
+        n = int(rng.integers(0, 700))
+        pl = int(rng.integers(0, 45))
+        kind = rng.integers(0, 4)
+        if kind == 0:
+            seg = bytes(n)
+        elif kind == 1:
+            seg = b"\xff" * n
+        else:
+            seg = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        pre = rng.integers(0, 256, pl, dtype=np.uint8).tobytes()
+        want = O.go_checksum(pre, seg)
+        assert O.fold_checksum(pre, seg) == want
+        assert O.c_go_checksum(pre, seg) == want
+        assert O.c_fold_checksum(pre, seg) == want
+
+
+def test_zero_only_for_all_zero_input():
+    rng = np.random.default_rng(3)
+    for _ in range(200):
+        n = int(rng.integers(1, 64))
+        seg = bytearray(n)
+        seg[int(rng.integers(n))] = int(rng.integers(1, 256))
+        assert O.c_go_checksum(b"", bytes(seg)) != 0
+
+
+# --- golden fixtures ---
+
+def test_golden_vectors():
+    idx = load("vectors.json")
+    blob = np.fromfile(os.path.join(GOLDEN, "vectors.bin"), np.uint8)
+    for c in idx:
+        seg = blob[c["offset"]:c["offset"] + c["length"]].tobytes()
+        pre = bytes.fromhex(c["prefix"])
+        assert O.c_go_checksum(pre, seg) == c["raw"]
+        assert O.c_fold_checksum(b"", seg) == c["raw_no_prefix"]
+        assert O.fold(O.be_word_sum(seg) + c["prefix_partial"]) == c["raw"]
+
+
+def test_golden_ragged():
+    meta = load("ragged.json")
+    blob = np.fromfile(os.path.join(GOLDEN, "ragged.bin"), np.uint8)
+    offs = np.array(meta["offsets"], np.uint64)
+    part = np.array(meta["partial"], np.uint32)
+    assert O.c_batch(blob, offs.size - 1, offsets=offs).tolist() == meta["raw"]
+    assert O.c_batch(blob, offs.size - 1, offsets=offs, partial=part).tolist() == meta["raw_with_partial"]
+    assert O.batch_ragged(blob, offs).tolist() == meta["raw"]
+
+
+def test_golden_segments():
+    for c in load("segments.json"):
+        b = bytes.fromhex(c["bytes"])
+        assert O.go_checksum(b"", b) == c["raw"]
+        assert O.go_checksum(bytes.fromhex(c["pseudo_ipv4"]), b) == c["raw_with_pseudo"]
+
+
+def test_reference_option_padding_quirk():
+    """tcp.go:118-121 pads `remainder` zero bytes, not 4-remainder: 20 B + MSS(6)
+    = 26 → remainder 2 → 28 B (aligned by luck); NOOP: 21 → +1 → 22 (not 24)."""
+    s = O.Segment(options=[O.Option(kind=1)])
+    assert len(s.bytes()) == 22
+    s = O.Segment(options=[O.Option(kind=2, length=4, data=b"\x05\xb4\x00\x00")])
+    assert len(s.bytes()) == 28
+
+
+# --- synthetic data generator ---
+
+def test_splitmix64_py_vs_c():
+    for off, n in ((0, 64), (3, 61), (8, 1000), (12345, 777)):
+        assert np.array_equal(O.splitmix64_bytes(0x1071, off, n), O.c_splitmix64(0x1071, n, off))
+
+
+def test_batch_fixed_numpy_vs_c():
+    buf = O.c_splitmix64(0x1071, 1500 * 64)
+    a = O.batch_fixed(buf, 1500, 1500, 64)
+    b = O.c_batch(buf, 64, stride=1500, seg_len=1500)
+    assert np.array_equal(a, b)
+    for i in (0, 17, 63):
+        assert a[i] == O.go_checksum(b"", buf[i * 1500:(i + 1) * 1500].tobytes())

@@ -1,0 +1,92 @@
+#!/usr/bin/env python3
+"""Kernel-variant sweep: interleaved rounds in ONE process (cdna_hip_programming.md
+§5.4 rule 24), per-launch HIP-event time on the launch stream, median per variant.
+
+    python tools/sweep.py [--configs 2,3,4] [--rounds 5] [--iters 20]
+"""
+import argparse
+import itertools
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "network-stack_amd"))
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+import nsx  # noqa: E402
+
+
+def variants(kind):
+    out = []
+    for bpc, spw, nt, xcd in itertools.product((8, 4, 2), (1, 2, 4), (0, 1), (1, 2)):
+        if kind != "fixed2" and spw != 1:
+            continue
+        out.append(dict(blocks_per_cu=bpc, segs_per_wave=spw, nontemporal=nt, xcd_map=xcd))
+    return out
+
+
+def apply(v):
+    for k, val in v.items():
+        nsx.set_param(bench.PARAMS[k], val)
+
+
+def time_variant(w, iters):
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
+    for i in range(iters):
+        evs[i][0].record()
+        w["step"]()
+        evs[i][1].record()
+    torch.cuda.synchronize()
+    return statistics.median(a.elapsed_time(b) for a, b in evs)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="2,3,4")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "sweep.json"))
+    a = ap.parse_args()
+    torch.cuda.set_device(0)
+    results = {}
+    for cid in [int(c) for c in a.configs.split(",")]:
+        cfg = bench.WORKLOADS[cid]
+        w = bench.build_workload(cfg, 0, torch.device("cuda", 0))
+        kind = "fixed2" if cfg["kind"] == "fixed" and cfg["seg_len"] <= 4093 else cfg["kind"]
+        vs = variants(kind)
+        if cid in (3, 4):
+            vs += [dict(v, block_mode=2) for v in vs if v["blocks_per_cu"] == 8]
+        times = {i: [] for i in range(len(vs))}
+        for i, v in enumerate(vs):  # warm each once
+            apply(v)
+            time_variant(w, 3)
+        for r in range(a.rounds):
+            for i, v in enumerate(vs):
+                apply(v)
+                times[i].append(time_variant(w, a.iters))
+            print(f"config{cid} round {r} done", flush=True)
+        rows = []
+        for i, v in enumerate(vs):
+            med = statistics.median(times[i])
+            rows.append(dict(v, ms=round(med, 4), GBps=round(w["alg"] / med / 1e6, 1),
+                             frac=round(w["alg"] / med / 1e6 / 8000, 4), ms_min=round(min(times[i]), 4)))
+            nsx.set_param(nsx.PARAM_BLOCK_MODE, 0)
+        rows.sort(key=lambda r: r["ms"])
+        results[f"config{cid}"] = rows
+        for r in rows[:8]:
+            print(f"config{cid}", json.dumps(r), flush=True)
+        print(f"config{cid} worst", json.dumps(rows[-1]), flush=True)
+        del w
+        torch.cuda.empty_cache()
+    os.makedirs(os.path.dirname(a.out), exist_ok=True)
+    with open(a.out, "w") as f:
+        json.dump(results, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
