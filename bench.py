@@ -55,8 +55,11 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", type=int, default=2, choices=sorted(WORKLOADS))
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0 = skip)")
+    ap.add_argument("--settle-s", type=float, default=0.5, help="device clock settle time before warmup (setup)")
     ap.add_argument("--param", action="append", default=[], metavar="NAME=V",
-                    help="kernel knob: blocks_per_cu, segs_per_wave, nontemporal, block_mode, xcd_map")
+                    help="kernel knob (include/nsx_csum.h NSX_PARAM_*): " + ", ".join(
+                        ["blocks_per_cu", "segs_per_wave", "nontemporal", "block_mode", "xcd_map", "kernel",
+                         "stream_rows"]))
     return ap.parse_args(argv)
 
 
@@ -163,7 +166,8 @@ def result_line(*, world, steps, warmup, wall_max, bytes_per_rank_step, units_to
 # ---------------------------------------------------------------------------
 # GPU workload
 # ---------------------------------------------------------------------------
-PARAMS = {"blocks_per_cu": 1, "segs_per_wave": 2, "nontemporal": 3, "block_mode": 4, "xcd_map": 5}
+PARAMS = {"blocks_per_cu": 1, "segs_per_wave": 2, "nontemporal": 3, "block_mode": 4, "xcd_map": 5, "kernel": 6,
+          "stream_rows": 7}
 
 
 def build_workload(cfg, rank, device):
@@ -276,6 +280,16 @@ def main(argv=None):
     cfg = WORKLOADS[args.config]
     w = build_workload(cfg, dist.rank, device)
     torch.cuda.synchronize()
+    # Setup, not measurement: after data generation the GPU's clocks sit in an
+    # idle state and the first ~50 launches run up to 20 % slow (tools/drift.py).
+    # Run the workload's own kernel for --settle-s seconds so the W warmup and
+    # K timed steps that follow see the steady state a long-running transport
+    # loop would.
+    settle_until = time.perf_counter() + args.settle_s
+    while time.perf_counter() < settle_until:
+        for _ in range(10):
+            w["step"]()
+        torch.cuda.synchronize()
 
     def ev_pair():
         return torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -140,13 +140,15 @@ int nsx_abi_version(void);
 int nsx_device_count(int* out_count);        /* NSX_OK with 0 when no GPU */
 const char* nsx_strerror(int code);
 
-/* Kernel-variant knobs for benchmarking (process-wide; 0 restores the default).
+/* Kernel-variant knobs for benchmarking (process-wide; 0 = the default).
  * Not needed for correctness; every variant is bit-exact. */
-#define NSX_PARAM_BLOCKS_PER_CU   1  /* persistent-grid occupancy, 1..8  */
-#define NSX_PARAM_SEGS_PER_WAVE   2  /* fixed path: 1, 2 or 4 segments per wave pass */
-#define NSX_PARAM_NONTEMPORAL     3  /* 1 = nt loads (read-once stream) */
-#define NSX_PARAM_BLOCK_MODE      4  /* 0 auto (a block per segment when n < resident waves), 1 wave per segment, 2 block per segment */
-#define NSX_PARAM_XCD_MAP         5  /* 1 (default) deal each XCD a contiguous region of the batch; 2 plain grid-stride */
+#define NSX_PARAM_BLOCKS_PER_CU   1  /* persistent grid, 1..8 blocks of 256 threads per CU (default per path) */
+#define NSX_PARAM_SEGS_PER_WAVE   2  /* per-segment kernels: 1, 2, 4 or 8 segments per wave pass */
+#define NSX_PARAM_NONTEMPORAL     3  /* 1 nt loads (default), 2 default-policy loads */
+#define NSX_PARAM_BLOCK_MODE      4  /* 0 auto (a block per segment when n < 4*CUs), 1 never, 2 always */
+#define NSX_PARAM_XCD_MAP         5  /* task deal: 1 XCD-contiguous regions (default), 2 grid-stride, 3 one contiguous range per wave */
+#define NSX_PARAM_KERNEL          6  /* 1 row-stream, 2 per-segment, 3 buffer-load per-segment (fixed ≤4 KiB segments) */
+#define NSX_PARAM_STREAM_ROWS     7  /* row-stream: 4, 8 (default) or 16 KiB in flight per wave */
 int nsx_set_param(int param, int64_t value);
 int nsx_get_param(int param, int64_t* value);
 

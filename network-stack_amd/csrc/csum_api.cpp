@@ -21,11 +21,9 @@
 namespace {
 
 // ---------------------------------------------------------------- params
-std::atomic<int64_t> g_blocks_per_cu{0}, g_segs_per_wave{0}, g_nontemporal{0}, g_block_mode{0},
-    g_xcd_map{0};
+constexpr int kNumParams = 8;
+std::atomic<int64_t> g_param[kNumParams];  // index = NSX_PARAM_*; 0 = default
 
-constexpr int kDefaultBlocksPerCU = 8;  // 8 × 4 waves = 32 waves/CU (kernels fit 64 VGPRs)
-constexpr int kDefaultSegsPerWave = 2;
 constexpr int kMaxDevices = 64;
 
 struct DevInfo {
@@ -69,21 +67,8 @@ int current_device() {
     return dev_info(d) ? d : -1;
 }
 
-nsx::LaunchCfg make_cfg(int dev, uint64_t n, bool segs_can_split) {
-    const DevInfo* di = dev_info(dev);
-    int64_t bpc = g_blocks_per_cu.load();
-    if (bpc <= 0 || bpc > 8) bpc = kDefaultBlocksPerCU;
-    int64_t spw = g_segs_per_wave.load();
-    if (spw != 1 && spw != 2 && spw != 4) spw = kDefaultSegsPerWave;
-    nsx::LaunchCfg c;
-    c.max_blocks = (uint32_t)(di->cus * bpc);
-    c.segs_per_wave = (int)spw;
-    c.nontemporal = g_nontemporal.load() == 1 ? 1 : 0;
-    c.xcd_map = g_xcd_map.load() == 2 ? 0 : 1;
-    const int64_t bm = g_block_mode.load();
-    const uint64_t resident_waves = (uint64_t)di->cus * 32;
-    c.block_mode = segs_can_split && (bm == 2 || (bm == 0 && n < resident_waves));
-    return c;
+nsx::LaunchCfg make_cfg(int dev, uint64_t n, bool /*segs_can_split*/) {
+    return nsx::default_launch_cfg(dev_info(dev)->cus, n);
 }
 
 int map_err(hipError_t e) {
@@ -95,6 +80,24 @@ int map_err(hipError_t e) {
 }
 
 }  // namespace
+
+namespace nsx {
+
+LaunchCfg default_launch_cfg(int cus, uint64_t /*n*/) {
+    auto get = [](int p) { return (int)g_param[p].load(); };
+    LaunchCfg c;
+    c.cus = cus;
+    c.blocks_per_cu = get(NSX_PARAM_BLOCKS_PER_CU);
+    c.segs_per_wave = get(NSX_PARAM_SEGS_PER_WAVE);
+    c.nontemporal = get(NSX_PARAM_NONTEMPORAL);
+    c.block_mode = get(NSX_PARAM_BLOCK_MODE);
+    c.xcd_map = get(NSX_PARAM_XCD_MAP);
+    c.kernel = get(NSX_PARAM_KERNEL);
+    c.rows = get(NSX_PARAM_STREAM_ROWS);
+    return c;
+}
+
+}  // namespace nsx
 
 extern "C" {
 
@@ -118,26 +121,15 @@ const char* nsx_strerror(int code) {
 }
 
 int nsx_set_param(int param, int64_t value) {
-    switch (param) {
-        case NSX_PARAM_BLOCKS_PER_CU: g_blocks_per_cu = value; return NSX_OK;
-        case NSX_PARAM_SEGS_PER_WAVE: g_segs_per_wave = value; return NSX_OK;
-        case NSX_PARAM_NONTEMPORAL: g_nontemporal = value; return NSX_OK;
-        case NSX_PARAM_BLOCK_MODE: g_block_mode = value; return NSX_OK;
-        case NSX_PARAM_XCD_MAP: g_xcd_map = value; return NSX_OK;
-        default: return NSX_EINVAL;
-    }
+    if (param < 1 || param >= kNumParams) return NSX_EINVAL;
+    g_param[param] = value;
+    return NSX_OK;
 }
 
 int nsx_get_param(int param, int64_t* value) {
-    if (!value) return NSX_EINVAL;
-    switch (param) {
-        case NSX_PARAM_BLOCKS_PER_CU: *value = g_blocks_per_cu; return NSX_OK;
-        case NSX_PARAM_SEGS_PER_WAVE: *value = g_segs_per_wave; return NSX_OK;
-        case NSX_PARAM_NONTEMPORAL: *value = g_nontemporal; return NSX_OK;
-        case NSX_PARAM_BLOCK_MODE: *value = g_block_mode; return NSX_OK;
-        case NSX_PARAM_XCD_MAP: *value = g_xcd_map; return NSX_OK;
-        default: return NSX_EINVAL;
-    }
+    if (!value || param < 1 || param >= kNumParams) return NSX_EINVAL;
+    *value = g_param[param];
+    return NSX_OK;
 }
 
 // ------------------------------------------------------------ single segment

@@ -6,13 +6,26 @@
 
 namespace nsx {
 
+constexpr int kKernelRowStream = 1;  // csum_stream_kernel
+constexpr int kKernelPerSegment = 2; // csum_fixed_kernel / csum_wave_kernel
+constexpr int kKernelPipelined = 3;  // csum_fixed_buf_kernel (fixed stride, ≤4 rows; the default there)
+
+// Raw NSX_PARAM_* values (0 = "default for this path"); the launchers resolve
+// them per path (fixed short / fixed long / ragged) to the defaults measured
+// best on MI355X by tools/sweep.py.
 struct LaunchCfg {
-    uint32_t max_blocks;  // persistent grid cap = CUs × blocks per CU
-    int segs_per_wave;    // fixed path: segments per wave pass (1, 2, 4)
-    int nontemporal;      // 1 = nt loads
-    int xcd_map;          // 1 = XCD-contiguous task deal
-    bool block_mode;      // one segment per 256-thread block (few long segments)
+    int cus;             // compute units of the device
+    int blocks_per_cu;   // persistent grid = cus × blocks_per_cu blocks of 256 threads
+    int segs_per_wave;   // per-segment fixed kernel: 1, 2, 4
+    int nontemporal;     // 1 nt loads, 2 default policy
+    int block_mode;      // 1 never, 2 always, 0 auto (n < 4·cus)
+    int xcd_map;         // 1 XCD-contiguous deal, 2 grid-stride, 3 contiguous range per wave
+    int kernel;          // kKernelRowStream / kKernelPerSegment
+    int rows;            // row-stream rows per batch: 4, 8, 16
 };
+
+// Launch configuration from the process-wide NSX_PARAM_* knobs (csum_api.cpp).
+LaunchCfg default_launch_cfg(int cus, uint64_t n);
 
 hipError_t launch_fixed(const LaunchCfg& c, const void* d_base, uint64_t stride, uint32_t seg_len,
                         uint64_t n, const uint32_t* partial, uint16_t* out, hipStream_t st);

@@ -114,10 +114,18 @@ struct TaskIter {
     uint64_t next, end, step;
 };
 
+// xcd_map: 1 = each XCD's blocks stream one contiguous eighth of the batch,
+// dealt round-robin inside it; 0 = plain grid-stride; 2 = every wave owns one
+// contiguous range of tasks and walks it in order (a sequential stream per wave).
 __device__ __forceinline__ TaskIter task_iter(uint64_t ntasks, uint32_t wave, int xcd_map) {
     const uint32_t nb = gridDim.x, b = blockIdx.x;
     TaskIter it;
-    if (xcd_map && nb >= 16 && (nb & 7) == 0) {
+    if (xcd_map == 2) {
+        const uint64_t waves = (uint64_t)nb * kWavesPerBlock, g = (uint64_t)b * kWavesPerBlock + wave;
+        it.next = ntasks * g / waves;
+        it.end = ntasks * (g + 1) / waves;
+        it.step = 1;
+    } else if (xcd_map == 1 && nb >= 16 && (nb & 7) == 0) {
         // blocks b, b+8, ... share an XCD (observed round-robin dispatch; speed only).
         const uint32_t x = b & 7, slot = b >> 3, per = nb >> 3;
         const uint64_t lo = ntasks * x / 8, hi = ntasks * (x + 1) / 8;
@@ -197,6 +205,181 @@ __global__ __launch_bounds__(kBlock) void csum_fixed_kernel(
             const uint32_t pp = partial ? partial[my_seg] : 0u;
             out[my_seg] = (uint16_t)finish(mine, mine_even, pp);
         }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Software-pipelined fixed-stride kernel on buffer loads. Same work split as
+// csum_fixed_kernel (U segments × NROWS rows per wave task), but task t+1's
+// loads are issued before task t is reduced, so every wave keeps a task's worth
+// of loads in flight while it computes. All memory operations are
+// unconditional buffer ops: a lane that must not load gets an out-of-range
+// offset (the hardware returns 0 and moves no data), so hipcc can count
+// vmcnt exactly across the two register buffers instead of draining to 0.
+// Range checking on gfx950 is per dword (tools/probes/buffer_oob.hip): with
+// num_records ending at the 4-aligned end of the batch, a 16-byte load that
+// straddles the end returns exactly its in-range dwords, so no tail path.
+// ---------------------------------------------------------------------------
+// Mask for the chunk of lane byte offset ql inside a row whose segment bytes are
+// [lo_r, hi_r) relative to the row start (both clamped, 32-bit).
+__device__ __forceinline__ uint32_t keep_mask(int32_t lo_r, int32_t hi_r, int32_t d) {
+    const int32_t e = min(max(hi_r - d, 0), 4), s = min(max(lo_r - d, 0), 4);
+    const uint32_t me = e >= 4 ? 0xFFFFFFFFu : ((1u << (8 * e)) - 1u);
+    const uint32_t ms = s >= 4 ? 0xFFFFFFFFu : ((1u << (8 * s)) - 1u);
+    return me & ~ms;
+}
+
+constexpr uint32_t kOOB = 0x80000000u;  // voffset that is always out of range (num_records < 2^31)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint64_t bytes) {
+    // Wave-uniform inputs only, so no waterfall loop (guide T20); clamp without a
+    // 64-bit unsigned compare (SALU has none: hipcc would borrow VGPRs for it).
+    const uint32_t nr = (bytes >> 31) ? kOOB - 1 : (uint32_t)bytes;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)nr, 0x00020000);
+}
+
+template <bool NT>
+__device__ __forceinline__ u32x4 bld16(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    v4u x = __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, NT ? 2 : 0);
+    return u32x4{x.x, x.y, x.z, x.w};
+}
+
+// Byte mask keeping the low `keep` bytes of a dword (keep in 1..3).
+__device__ __forceinline__ uint32_t low_keep(uint32_t keep) { return (1u << (8 * keep)) - 1u; }
+
+// Segment window descriptor: base = the segment start rounded down to 4 B,
+// num_records = head + len rounded UP to 4 B. The per-dword range check then
+// returns 0 for every dword outside the segment's window (and moves no data
+// for them), so only the partial first dword (head bytes of the previous
+// segment) and the partial last dword (bytes past the end) need a byte mask.
+struct SegWin {
+    __amdgpu_buffer_rsrc_t r;
+    uint32_t head;  // 0..3 bytes before the segment in its first dword
+    uint32_t end;   // head + len: window bytes that belong to the segment
+    bool even;      // segment starts at an even address (byte-swap rule)
+};
+
+__device__ __forceinline__ SegWin seg_win(const uint8_t* p, uint32_t len, bool live) {
+    SegWin w;
+    w.head = (uint32_t)((uintptr_t)p & 3u);
+    w.end = w.head + len;
+    w.even = ((uintptr_t)p & 1u) == 0;
+    w.r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p - w.head), 0,
+                                            live ? (int)((w.end + 3u) & ~3u) : 0, 0x00020000);
+    return w;
+}
+
+// Apply the two partial-dword masks to row k's chunk of this lane.
+__device__ __forceinline__ u32x4 edge_mask(u32x4 x, const SegWin& w, uint32_t k, uint32_t lane) {
+    if (w.head && k == 0 && lane == 0) x.x &= ~low_keep(w.head);
+    const uint32_t keep = w.end & 3u;
+    if (keep) {
+        const uint32_t ld = (w.end - 1u) >> 2;  // dword holding the last byte
+        if ((ld >> 8) == k && ((ld & 255u) >> 2) == lane) {
+            const uint32_t m = low_keep(keep), c = ld & 3u;
+            x.x &= c == 0 ? m : 0xFFFFFFFFu;
+            x.y &= c == 1 ? m : 0xFFFFFFFFu;
+            x.z &= c == 2 ? m : 0xFFFFFFFFu;
+            x.w &= c == 3 ? m : 0xFFFFFFFFu;
+        }
+    }
+    return x;
+}
+
+template <int U>
+__device__ __forceinline__ void fixed_flush(uint32_t res, uint32_t first, uint32_t step, uint32_t count, uint32_t n,
+                                            __amdgpu_buffer_rsrc_t ors, uint32_t lane) {
+    const uint32_t j = lane / U;
+    const uint32_t seg = (first + j * step) * U + lane % U;
+    const uint32_t off = (j < count && seg < n) ? seg * 2 : kOOB;
+    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, off, 0, 0);
+}
+
+// Fixed stride on buffer loads: a wave task = U consecutive segments × NROWS
+// rows, every load unconditional (lanes past a segment's window read 0 and
+// move no data). Results are parked one per lane and flushed with a single
+// scattered 2-byte store per 64/U tasks.
+//
+// ALIGNED (base, stride and seg_len all ≡ 0 mod 4 — e.g. config 2, 1500 B):
+// every segment starts 4-aligned and even, so there are no edge masks, the
+// descriptor size is a constant and the finish (byte swap + prefix partial) is
+// done vector-wide for the whole group at flush time; the group's partials are
+// loaded when the group starts, so their latency hides under 64/U tasks.
+template <int U, int NROWS, bool NT, bool ALIGNED>
+__global__ __launch_bounds__(kBlock) void csum_fixed_buf_kernel(
+    const uint8_t* __restrict__ base, uint64_t stride, uint32_t seg_len, uint32_t n,
+    const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, int xcd_map) {
+    constexpr uint32_t G = kWave / U;
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const uint32_t ntasks = (n + U - 1) / U;
+    const TaskIter it = task_iter(ntasks, wave, xcd_map);
+    const uint32_t end = (uint32_t)it.end, step = (uint32_t)it.step;
+    const __amdgpu_buffer_rsrc_t ors = make_rsrc(out, (uint64_t)n * 2);
+    const __amdgpu_buffer_rsrc_t prs = make_rsrc(partial, partial ? (uint64_t)n * 4 : 0);
+    // Lane l's segment within a group that starts at task `first`.
+    auto group_seg = [&](uint32_t first) { return (first + (lane / U) * step) * U + lane % U; };
+    uint32_t res = 0, k = 0, first = (uint32_t)it.next;
+    uint32_t gpart = 0;
+    if constexpr (ALIGNED) {
+        const uint32_t sg = group_seg(first);
+        gpart = __builtin_amdgcn_raw_buffer_load_b32(prs, sg < n ? sg * 4 : kOOB, 0, 0);
+    }
+    for (uint32_t t = (uint32_t)it.next; t < end; t += step) {
+        const uint32_t s0 = t * U;
+        u32x4 v[U][NROWS];
+        SegWin w[U];
+        const uint8_t* p = base + (uint64_t)s0 * stride;
+#pragma unroll
+        for (int u = 0; u < U; ++u, p += stride) {
+            if constexpr (ALIGNED) {
+                w[u].r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p), 0,
+                                                           s0 + u < n ? (int)seg_len : 0, 0x00020000);
+            } else {
+                w[u] = seg_win(p, seg_len, s0 + u < n);
+            }
+#pragma unroll
+            for (int r = 0; r < NROWS; ++r) v[u][r] = bld16<NT>(w[u].r, r * kRow + lane * 16);
+        }
+        uint32_t part = 0;
+        if constexpr (!ALIGNED)
+            part = __builtin_amdgcn_raw_buffer_load_b32(prs, lane < (uint32_t)U ? (s0 + lane) * 4 : kOOB, 0, 0);
+        // All U*NROWS loads are issued before the first use: LLVM would otherwise
+        // sink each (invariant) load next to its consumer and serialise the wave
+        // on memory. An in/out operand pins each load above this point.
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int r = 0; r < NROWS; ++r) asm volatile("" : "+v"(v[u][r]));
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            uint32_t acc = 0;
+#pragma unroll
+            for (int r = 0; r < NROWS; ++r) {
+                if constexpr (ALIGNED) acc = sad4(v[u][r], acc);
+                else acc = sad4(edge_mask(v[u][r], w[u], r, lane), acc);
+            }
+            const uint32_t tot = wave_sum(fold32(acc));
+            uint32_t rr;
+            if constexpr (ALIGNED) rr = tot;
+            else rr = finish(tot, w[u].even, __builtin_amdgcn_readlane(part, u));
+            res = lane == k * U + u ? rr : res;
+        }
+        if (++k == G) {
+            if constexpr (ALIGNED) res = finish(res, true, gpart);
+            fixed_flush<U>(res, first, step, k, n, ors, lane);
+            k = 0;
+            first = t + step;
+            if constexpr (ALIGNED) {
+                const uint32_t sg = group_seg(first);
+                gpart = __builtin_amdgcn_raw_buffer_load_b32(prs, (first < end && sg < n) ? sg * 4 : kOOB, 0, 0);
+            }
+        }
+    }
+    if (k) {
+        if constexpr (ALIGNED) res = finish(res, true, gpart);
+        fixed_flush<U>(res, first, step, k, n, ors, lane);
     }
 }
 
@@ -304,6 +487,159 @@ __global__ __launch_bounds__(kBlock) void csum_block_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Row-stream kernel. A wave owns a run of kRun consecutive segments and streams
+// their rows in batches of R wave-wide loads that cross segment boundaries, so
+// each batch keeps R KiB in flight whatever the segment lengths (short ragged
+// segments no longer cost a full latency round trip each). The run's offsets
+// sit one per lane in a VGPR (prefetched one run ahead) and are read with
+// v_readlane; per-segment wave totals are parked in lane (s - a) of a VGPR and
+// finished in parallel (byte-swap rule + prefix partial) at the end of the run,
+// which then stores 2·kRun contiguous bytes of results.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kRun = 32;
+
+struct SegMeta {        // wave-uniform description of one segment's window
+    const uint8_t* wb;  // 4-byte-aligned window base (segment start rounded down)
+    int64_t lo, hi;     // segment bytes are [lo, hi) of the window (lo = head <= 3)
+    uint32_t rows;      // 1 KiB rows covering [0, hi); 0 for an empty segment
+};
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t k) {
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, k);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), k);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+template <bool RAGGED>
+__device__ __forceinline__ SegMeta seg_meta(const uint8_t* base, uint64_t my_off, uint64_t a, uint64_t s,
+                                            uint64_t stride, uint32_t seg_len) {
+    uint64_t o0, len;
+    if constexpr (RAGGED) {
+        o0 = readlane64(my_off, (uint32_t)(s - a));
+        const uint64_t o1 = readlane64(my_off, (uint32_t)(s - a + 1));
+        len = o1 > o0 ? o1 - o0 : 0;
+    } else {
+        o0 = s * stride;
+        len = seg_len;
+    }
+    const uint8_t* p = base + o0;
+    const uint32_t head = (uint32_t)((uintptr_t)p & 3u);
+    SegMeta m;
+    m.wb = p - head;
+    m.lo = head;
+    m.hi = (int64_t)head + (int64_t)len;
+    m.rows = len ? (uint32_t)((m.hi + kRow - 1) / kRow) : 0u;
+    return m;
+}
+
+template <bool RAGGED, int R, bool NT, bool VERIFY>
+__global__ __launch_bounds__(kBlock) void csum_stream_kernel(
+    const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, uint64_t stride,
+    uint32_t seg_len, uint64_t n, const uint32_t* __restrict__ partial, uint16_t* __restrict__ out,
+    uint8_t* __restrict__ ok, const uint8_t* safe_end, int xcd_map) {
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    if constexpr (RAGGED) safe_end = align_up4(base + offsets[n]);
+    const uint64_t ntasks = (n + kRun - 1) / kRun;
+    TaskIter it = task_iter(ntasks, wave, xcd_map);
+
+    uint64_t nxt_off = 0;
+    if constexpr (RAGGED) {
+        if (it.next < it.end) {
+            const uint64_t a = it.next * kRun, cnt = min((uint64_t)kRun, n - a);
+            if (lane <= cnt) nxt_off = offsets[a + lane];
+        }
+    }
+    for (uint64_t t = it.next; t < it.end; t += it.step) {
+        const uint64_t a = t * kRun, b = min(a + kRun, n);
+        const uint64_t my_off = nxt_off;
+        if constexpr (RAGGED) {  // prefetch the next run's offsets
+            const uint64_t tn = t + it.step;
+            if (tn < it.end) {
+                const uint64_t an = tn * kRun, cnt = min((uint64_t)kRun, n - an);
+                nxt_off = lane <= cnt ? offsets[an + lane] : 0;
+            }
+        }
+        const uint32_t my_part = (partial && a + lane < b) ? partial[a + lane] : 0u;
+
+        uint32_t sums = 0;  // lane k: LE half-sum total of segment a+k
+        uint32_t acc = 0;   // this lane's share of segment `cur`
+        uint64_t cur = a;
+        uint64_t ps = a;    // planning cursor: segment ps, row pr
+        uint32_t pr = 0;
+        SegMeta pm = seg_meta<RAGGED>(base, my_off, a, ps, stride, seg_len);
+        for (;;) {
+            // Plan R slots (scalar): row start address, the segment's bytes as
+            // [lo_r, hi_r) relative to that row (clamped to 32 bits), and the
+            // segment as an offset in the run (kRun = no slot).
+            const uint8_t* sra[R];
+            int32_t slo[R], shi[R];
+            uint32_t sd[R];
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                while (ps < b && pr >= pm.rows) {
+                    ++ps;
+                    pr = 0;
+                    if (ps < b) pm = seg_meta<RAGGED>(base, my_off, a, ps, stride, seg_len);
+                }
+                const int64_t rb = (int64_t)pr * kRow;
+                sd[j] = ps < b ? (uint32_t)(ps - a) : kRun;
+                sra[j] = pm.wb + rb;
+                slo[j] = (int32_t)max(min(pm.lo - rb, (int64_t)kRow + 16), (int64_t)-16);
+                shi[j] = (int32_t)max(min(pm.hi - rb, (int64_t)kRow + 16), (int64_t)-16);
+                ++pr;
+            }
+            if (sd[0] == kRun) break;
+            // Issue all R loads.
+            u32x4 v[R];
+            const int32_t d = (int32_t)lane * 16;
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                v[j] = u32x4{0u, 0u, 0u, 0u};
+                if (sd[j] != kRun && d < shi[j]) {
+                    const uint8_t* ad = sra[j] + d;
+                    if (sra[j] + kRow <= safe_end || ad + 16 <= safe_end) v[j] = ld16<NT>(ad);
+                    else v[j] = ld16_guarded(ad, safe_end);
+                }
+            }
+            // Consume in order; a segment change parks the finished total.
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                if (sd[j] != kRun) {
+                    if (a + sd[j] != cur) {
+                        const uint32_t tot = wave_sum(fold32(acc));
+                        sums = lane == (uint32_t)(cur - a) ? tot : sums;
+                        acc = 0;
+                        cur = a + sd[j];
+                    }
+                    u32x4 x = v[j];
+                    if (slo[j] > 0 || shi[j] < (int32_t)kRow) {
+                        x.x &= keep_mask(slo[j], shi[j], d);
+                        x.y &= keep_mask(slo[j], shi[j], d + 4);
+                        x.z &= keep_mask(slo[j], shi[j], d + 8);
+                        x.w &= keep_mask(slo[j], shi[j], d + 12);
+                    }
+                    acc = sad4(x, acc);
+                }
+            }
+            acc = fold32(acc);
+        }
+        if (cur < b) {
+            const uint32_t tot = wave_sum(fold32(acc));
+            sums = lane == (uint32_t)(cur - a) ? tot : sums;
+        }
+        // Finish every segment of the run in parallel, one per lane.
+        if (a + lane < b) {
+            const uint64_t o = RAGGED ? my_off : (a + lane) * stride;
+            const bool even = (((uintptr_t)base + o) & 1u) == 0;
+            const uint32_t res = finish(sums, even, my_part);
+            if (out) out[a + lane] = (uint16_t)res;
+            if constexpr (VERIFY) ok[a + lane] = res == 0xFFFFu;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // IPv4 pseudo-header partials: src(4) dst(4) 0 proto len16 (RFC 9293 §3.1).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void pseudo_ipv4_kernel(const uint8_t* __restrict__ src,
@@ -353,21 +689,52 @@ __global__ __launch_bounds__(kBlock) void fill_bytes_kernel(uint8_t* __restrict_
 // ---------------------------------------------------------------------------
 // Launchers (host side of this translation unit).
 // ---------------------------------------------------------------------------
-static hipError_t launch_fixed_rows(const LaunchCfg& c, const uint8_t* base, uint64_t stride,
-                                    uint32_t seg_len, uint64_t n, const uint32_t* partial,
-                                    uint16_t* out, const uint8_t* safe_end, int nrows, int u,
-                                    hipStream_t st) {
+// Resolved launch parameters for one call.
+struct Plan {
+    uint32_t max_blocks;
+    int spw, rows, xcd;
+    bool nt;
+};
+
+enum class Path { kFixedShort, kFixedLong, kRagged, kBlock };
+
+// Per-path defaults (tools/sweep.py, MI355X):
+//   fixed ≤4 rows : buffer-load kernel, 4 segments/wave, 2 blocks/CU (8 waves/CU)
+//   fixed long    : per-segment wave kernel, 2 blocks/CU (8 waves/CU, 4 KiB in flight each)
+//   ragged        : row-stream kernel, 8 rows/batch, 4 blocks/CU
+// nt loads and the XCD-contiguous deal everywhere.
+static Plan resolve(const LaunchCfg& c, Path p) {
+    Plan r;
+    int bpc = c.blocks_per_cu;
+    if (bpc < 1 || bpc > 8)
+        bpc = (p == Path::kFixedLong || p == Path::kFixedShort) ? 2 : (p == Path::kBlock ? 8 : 4);
+    r.max_blocks = (uint32_t)(c.cus * bpc);
+    r.spw = (c.segs_per_wave == 1 || c.segs_per_wave == 2 || c.segs_per_wave == 4 || c.segs_per_wave == 8)
+                ? c.segs_per_wave : 4;
+    r.rows = (c.rows == 4 || c.rows == 8 || c.rows == 16) ? c.rows : 8;
+    r.xcd = c.xcd_map == 2 ? 0 : (c.xcd_map == 3 ? 2 : 1);
+    r.nt = c.nontemporal != 2;
+    return r;
+}
+
+static bool use_block_mode(const LaunchCfg& c, uint64_t n) {
+    return c.block_mode == 2 || (c.block_mode == 0 && n < (uint64_t)c.cus * 4);
+}
+
+static hipError_t launch_fixed_rows(const Plan& c, const uint8_t* base, uint64_t stride, uint32_t seg_len,
+                                    uint64_t n, const uint32_t* partial, uint16_t* out, const uint8_t* safe_end,
+                                    int nrows, int u, hipStream_t st) {
     const uint64_t ntasks = (n + u - 1) / u;
     const uint64_t want = (ntasks + kWavesPerBlock - 1) / kWavesPerBlock;
     const uint32_t grid = (uint32_t)(want < c.max_blocks ? want : c.max_blocks);
 #define NSX_FIXED(U_, NR_)                                                                          \
     if (u == U_ && nrows == NR_) {                                                                   \
-        if (c.nontemporal)                                                                           \
+        if (c.nt)                                                                                    \
             hipLaunchKernelGGL((csum_fixed_kernel<U_, NR_, true>), dim3(grid), dim3(kBlock), 0, st,  \
-                               base, stride, seg_len, n, partial, out, safe_end, c.xcd_map);         \
+                               base, stride, seg_len, n, partial, out, safe_end, c.xcd);             \
         else                                                                                         \
             hipLaunchKernelGGL((csum_fixed_kernel<U_, NR_, false>), dim3(grid), dim3(kBlock), 0, st, \
-                               base, stride, seg_len, n, partial, out, safe_end, c.xcd_map);         \
+                               base, stride, seg_len, n, partial, out, safe_end, c.xcd);             \
         return hipGetLastError();                                                                    \
     }
     NSX_FIXED(1, 1) NSX_FIXED(2, 1) NSX_FIXED(4, 1)
@@ -377,31 +744,84 @@ static hipError_t launch_fixed_rows(const LaunchCfg& c, const uint8_t* base, uin
     return hipErrorInvalidValue;
 }
 
+static hipError_t launch_fixed_pipe(const Plan& c, const uint8_t* base, uint64_t stride, uint32_t seg_len,
+                                    uint64_t n, const uint32_t* partial, uint16_t* out, const uint8_t* safe_end,
+                                    int nrows, int u, hipStream_t st) {
+    const uint64_t ntasks = (n + u - 1) / u;
+    const uint64_t want = (ntasks + kWavesPerBlock - 1) / kWavesPerBlock;
+    const uint32_t grid = (uint32_t)(want < c.max_blocks ? want : c.max_blocks);
+    const bool aligned = ((uintptr_t)base & 3u) == 0 && (stride & 3u) == 0 && (seg_len & 3u) == 0;
+#define NSX_PIPE(U_, NR_)                                                                                  \
+    if (u == U_ && nrows == NR_) {                                                                          \
+        if (aligned) {                                                                                      \
+            if (c.nt)                                                                                       \
+                hipLaunchKernelGGL((csum_fixed_buf_kernel<U_, NR_, true, true>), dim3(grid), dim3(kBlock), 0, st, \
+                                   base, stride, seg_len, (uint32_t)n, partial, out, c.xcd);                \
+            else                                                                                            \
+                hipLaunchKernelGGL((csum_fixed_buf_kernel<U_, NR_, false, true>), dim3(grid), dim3(kBlock), 0, \
+                                   st, base, stride, seg_len, (uint32_t)n, partial, out, c.xcd);            \
+        } else {                                                                                            \
+            if (c.nt)                                                                                       \
+                hipLaunchKernelGGL((csum_fixed_buf_kernel<U_, NR_, true, false>), dim3(grid), dim3(kBlock), 0, \
+                                   st, base, stride, seg_len, (uint32_t)n, partial, out, c.xcd);            \
+            else                                                                                            \
+                hipLaunchKernelGGL((csum_fixed_buf_kernel<U_, NR_, false, false>), dim3(grid), dim3(kBlock), 0, \
+                                   st, base, stride, seg_len, (uint32_t)n, partial, out, c.xcd);            \
+        }                                                                                                   \
+        return hipGetLastError();                                                                           \
+    }
+    NSX_PIPE(1, 1) NSX_PIPE(2, 1) NSX_PIPE(4, 1) NSX_PIPE(8, 1)
+    NSX_PIPE(1, 2) NSX_PIPE(2, 2) NSX_PIPE(4, 2) NSX_PIPE(8, 2)
+    NSX_PIPE(1, 4) NSX_PIPE(2, 4) NSX_PIPE(4, 4)
+#undef NSX_PIPE
+    return hipErrorInvalidValue;
+}
+
 template <bool RAGGED, bool VERIFY>
-static hipError_t launch_seg(const LaunchCfg& c, const uint8_t* base, const uint64_t* offsets,
-                             uint64_t stride, uint32_t seg_len, uint64_t n, const uint32_t* partial,
-                             uint16_t* out, uint8_t* ok, const uint8_t* safe_end, bool block_mode,
-                             hipStream_t st) {
+static hipError_t launch_seg(const Plan& c, const uint8_t* base, const uint64_t* offsets, uint64_t stride,
+                             uint32_t seg_len, uint64_t n, const uint32_t* partial, uint16_t* out, uint8_t* ok,
+                             const uint8_t* safe_end, bool block_mode, hipStream_t st) {
     if (block_mode) {
         const uint32_t grid = (uint32_t)(n < c.max_blocks ? n : c.max_blocks);
-        if (c.nontemporal)
-            hipLaunchKernelGGL((csum_block_kernel<RAGGED, 4, true, VERIFY>), dim3(grid), dim3(kBlock), 0,
-                               st, base, offsets, stride, seg_len, n, partial, out, ok, safe_end);
+        if (c.nt)
+            hipLaunchKernelGGL((csum_block_kernel<RAGGED, 4, true, VERIFY>), dim3(grid), dim3(kBlock), 0, st, base,
+                               offsets, stride, seg_len, n, partial, out, ok, safe_end);
         else
-            hipLaunchKernelGGL((csum_block_kernel<RAGGED, 4, false, VERIFY>), dim3(grid), dim3(kBlock), 0,
-                               st, base, offsets, stride, seg_len, n, partial, out, ok, safe_end);
+            hipLaunchKernelGGL((csum_block_kernel<RAGGED, 4, false, VERIFY>), dim3(grid), dim3(kBlock), 0, st, base,
+                               offsets, stride, seg_len, n, partial, out, ok, safe_end);
     } else {
         const uint64_t want = (n + kWavesPerBlock - 1) / kWavesPerBlock;
         const uint32_t grid = (uint32_t)(want < c.max_blocks ? want : c.max_blocks);
-        if (c.nontemporal)
-            hipLaunchKernelGGL((csum_wave_kernel<RAGGED, 4, true, VERIFY>), dim3(grid), dim3(kBlock), 0, st,
-                               base, offsets, stride, seg_len, n, partial, out, ok, safe_end, c.xcd_map);
+        if (c.nt)
+            hipLaunchKernelGGL((csum_wave_kernel<RAGGED, 4, true, VERIFY>), dim3(grid), dim3(kBlock), 0, st, base,
+                               offsets, stride, seg_len, n, partial, out, ok, safe_end, c.xcd);
         else
-            hipLaunchKernelGGL((csum_wave_kernel<RAGGED, 4, false, VERIFY>), dim3(grid), dim3(kBlock), 0,
-                               st, base, offsets, stride, seg_len, n, partial, out, ok, safe_end,
-                               c.xcd_map);
+            hipLaunchKernelGGL((csum_wave_kernel<RAGGED, 4, false, VERIFY>), dim3(grid), dim3(kBlock), 0, st, base,
+                               offsets, stride, seg_len, n, partial, out, ok, safe_end, c.xcd);
     }
     return hipGetLastError();
+}
+
+template <bool RAGGED, bool VERIFY>
+static hipError_t launch_stream(const Plan& c, const uint8_t* base, const uint64_t* offsets, uint64_t stride,
+                                uint32_t seg_len, uint64_t n, const uint32_t* partial, uint16_t* out, uint8_t* ok,
+                                const uint8_t* safe_end, hipStream_t st) {
+    const uint64_t ntasks = (n + kRun - 1) / kRun;
+    const uint64_t want = (ntasks + kWavesPerBlock - 1) / kWavesPerBlock;
+    const uint32_t grid = (uint32_t)(want < c.max_blocks ? want : c.max_blocks);
+#define NSX_STREAM(R_)                                                                                      \
+    if (c.rows == R_) {                                                                                      \
+        if (c.nt)                                                                                            \
+            hipLaunchKernelGGL((csum_stream_kernel<RAGGED, R_, true, VERIFY>), dim3(grid), dim3(kBlock), 0, st, \
+                               base, offsets, stride, seg_len, n, partial, out, ok, safe_end, c.xcd);        \
+        else                                                                                                 \
+            hipLaunchKernelGGL((csum_stream_kernel<RAGGED, R_, false, VERIFY>), dim3(grid), dim3(kBlock), 0,  \
+                               st, base, offsets, stride, seg_len, n, partial, out, ok, safe_end, c.xcd);     \
+        return hipGetLastError();                                                                            \
+    }
+    NSX_STREAM(4) NSX_STREAM(8) NSX_STREAM(16)
+#undef NSX_STREAM
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch_fixed(const LaunchCfg& c, const void* d_base, uint64_t stride, uint32_t seg_len,
@@ -409,26 +829,50 @@ hipError_t launch_fixed(const LaunchCfg& c, const void* d_base, uint64_t stride,
     const uint8_t* base = static_cast<const uint8_t*>(d_base);
     const uint8_t* end = base + (n - 1) * stride + seg_len;
     const uint8_t* safe_end = reinterpret_cast<const uint8_t*>(((uintptr_t)end + 3) & ~(uintptr_t)3);
+    if (use_block_mode(c, n))
+        return launch_seg<false, false>(resolve(c, Path::kBlock), base, nullptr, stride, seg_len, n, partial, out,
+                                        nullptr, safe_end, true, st);
     // Rows a segment window can span (the window starts up to 3 bytes early).
     const uint64_t rows = ((uint64_t)seg_len + 3 + kRow - 1) / kRow;
-    if (rows <= 4 && !c.block_mode) {
-        int nrows = rows <= 1 ? 1 : (rows <= 2 ? 2 : 4);
-        int u = c.segs_per_wave;
-        if (nrows == 4 && u > 2) u = 2;
-        return launch_fixed_rows(c, base, stride, seg_len, n, partial, out, safe_end, nrows, u, st);
+    const Path path = rows <= 4 ? Path::kFixedShort : Path::kFixedLong;
+    const Plan p = resolve(c, path);
+    if (c.kernel == kKernelRowStream)
+        return launch_stream<false, false>(p, base, nullptr, stride, seg_len, n, partial, out, nullptr, safe_end, st);
+    if (path == Path::kFixedShort) {
+        const int nrows = rows <= 1 ? 1 : (rows <= 2 ? 2 : 4);
+        if (c.kernel == kKernelPipelined || c.kernel == 0) {
+            const int u = (nrows == 4 && p.spw > 4) ? 4 : p.spw;
+            // Buffer descriptors address ≤ 2^31 bytes of results/partials: chunk huge batches.
+            constexpr uint64_t kChunk = 1ull << 28;
+            for (uint64_t c0 = 0; c0 < n; c0 += kChunk) {
+                const uint64_t cn = n - c0 < kChunk ? n - c0 : kChunk;
+                hipError_t e = launch_fixed_pipe(p, base + c0 * stride, stride, seg_len, cn,
+                                                 partial ? partial + c0 : nullptr, out + c0, safe_end, nrows, u, st);
+                if (e != hipSuccess) return e;
+            }
+            return hipSuccess;
+        }
+        const int u = (nrows == 4 && p.spw > 2) ? 2 : (p.spw > 4 ? 4 : p.spw);
+        return launch_fixed_rows(p, base, stride, seg_len, n, partial, out, safe_end, nrows, u, st);
     }
-    return launch_seg<false, false>(c, base, nullptr, stride, seg_len, n, partial, out, nullptr, safe_end,
-                                    c.block_mode, st);
+    return launch_seg<false, false>(p, base, nullptr, stride, seg_len, n, partial, out, nullptr, safe_end, false, st);
 }
 
 hipError_t launch_ragged(const LaunchCfg& c, const void* d_base, const uint64_t* d_offsets, uint64_t n,
                          const uint32_t* partial, uint16_t* out, uint8_t* ok, hipStream_t st) {
     const uint8_t* base = static_cast<const uint8_t*>(d_base);
-    if (ok)
-        return launch_seg<true, true>(c, base, d_offsets, 0, 0, n, partial, out, ok, nullptr, c.block_mode,
-                                      st);
-    return launch_seg<true, false>(c, base, d_offsets, 0, 0, n, partial, out, nullptr, nullptr, c.block_mode,
-                                   st);
+    if (use_block_mode(c, n)) {
+        const Plan p = resolve(c, Path::kBlock);
+        if (ok) return launch_seg<true, true>(p, base, d_offsets, 0, 0, n, partial, out, ok, nullptr, true, st);
+        return launch_seg<true, false>(p, base, d_offsets, 0, 0, n, partial, out, nullptr, nullptr, true, st);
+    }
+    const Plan p = resolve(c, Path::kRagged);
+    if (c.kernel != kKernelPerSegment) {
+        if (ok) return launch_stream<true, true>(p, base, d_offsets, 0, 0, n, partial, out, ok, nullptr, st);
+        return launch_stream<true, false>(p, base, d_offsets, 0, 0, n, partial, out, nullptr, nullptr, st);
+    }
+    if (ok) return launch_seg<true, true>(p, base, d_offsets, 0, 0, n, partial, out, ok, nullptr, false, st);
+    return launch_seg<true, false>(p, base, d_offsets, 0, 0, n, partial, out, nullptr, nullptr, false, st);
 }
 
 hipError_t launch_pseudo_ipv4(const uint8_t* src, const uint8_t* dst, const uint32_t* len, uint8_t proto,

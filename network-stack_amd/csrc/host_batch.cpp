@@ -50,22 +50,11 @@ int map_err(hipError_t e) {
 
 nsx::LaunchCfg default_cfg(int dev, uint64_t n) {
     int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    int64_t bpc = 0, spw = 0, nt = 0, bm = 0, xm = 0;
-    nsx_get_param(NSX_PARAM_BLOCKS_PER_CU, &bpc);
-    nsx_get_param(NSX_PARAM_SEGS_PER_WAVE, &spw);
-    nsx_get_param(NSX_PARAM_NONTEMPORAL, &nt);
-    nsx_get_param(NSX_PARAM_BLOCK_MODE, &bm);
-    nsx_get_param(NSX_PARAM_XCD_MAP, &xm);
-    if (bpc <= 0 || bpc > 8) bpc = 8;
-    if (spw != 1 && spw != 2 && spw != 4) spw = 2;
-    nsx::LaunchCfg c;
-    c.max_blocks = (uint32_t)(cus * bpc);
-    c.segs_per_wave = (int)spw;
-    c.nontemporal = nt == 1;
-    c.xcd_map = xm == 2 ? 0 : 1;
-    c.block_mode = bm == 2 || (bm == 0 && n < (uint64_t)cus * 32);
-    return c;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) {
+        (void)hipGetLastError();
+        cus = 256;
+    }
+    return nsx::default_launch_cfg(cus, n);
 }
 
 // One chunk = segments [c0, c1) of the shard.

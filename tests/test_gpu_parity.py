@@ -25,8 +25,7 @@ def gpu():
     assert nsx.device_count() > 0
     torch.cuda.set_device(0)
     yield
-    for p in (nsx.PARAM_BLOCKS_PER_CU, nsx.PARAM_SEGS_PER_WAVE, nsx.PARAM_NONTEMPORAL, nsx.PARAM_BLOCK_MODE,
-              nsx.PARAM_XCD_MAP):
+    for p in nsx.ALL_PARAMS:
         nsx.set_param(p, 0)
 
 
@@ -175,10 +174,17 @@ def test_zero_segments_is_noop():
 
 # ------------------------------------------------------------------ variants
 
-VARIANTS = [dict(spw=s, nt=nt, xcd=x, bpc=b) for s in (1, 2, 4) for nt in (0, 1) for x in (1, 2) for b in (8, 3)]
+VARIANTS = ([dict(kernel=2, spw=s, nt=nt, xcd=x, bpc=b, rows=0) for s in (1, 2, 4) for nt in (1, 2) for x in (1, 2)
+             for b in (8, 3)] +
+            [dict(kernel=1, spw=0, nt=nt, xcd=x, bpc=b, rows=r) for r in (4, 8, 16) for nt in (1, 2) for x in (1, 2)
+             for b in (8, 3)] +
+            [dict(kernel=3, spw=s, nt=nt, xcd=x, bpc=b, rows=0) for s in (1, 2, 4, 8) for nt in (1, 2)
+             for x in (1, 2, 3) for b in (8, 3)])
 
 
 def set_variant(v, block_mode=0):
+    nsx.set_param(nsx.PARAM_KERNEL, v["kernel"])
+    nsx.set_param(nsx.PARAM_STREAM_ROWS, v["rows"])
     nsx.set_param(nsx.PARAM_SEGS_PER_WAVE, v["spw"])
     nsx.set_param(nsx.PARAM_NONTEMPORAL, v["nt"])
     nsx.set_param(nsx.PARAM_XCD_MAP, v["xcd"])
@@ -202,7 +208,7 @@ def test_all_variants_bit_exact():
                     nsx.fixed_dev(d, stride, L, n, out=out)
                     assert np.array_equal(u16(out), w), (v, bm, L, stride, n)
     finally:
-        set_variant(dict(spw=0, nt=0, xcd=0, bpc=0), 0)
+        set_variant(dict(kernel=0, rows=0, spw=0, nt=0, xcd=0, bpc=0), 0)
 
 
 # ------------------------------------------------------------------ verify / pseudo-header

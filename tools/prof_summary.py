@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile.sh run into profiles/ (committed evidence).
+
+Reads gpurun_out/prof_<tag>_c<cfg>/{kt,fetch,write,sq}/run_*.csv and writes
+  profiles/<tag>_config<cfg>.md          — kernel stats + per-launch counters
+  profiles/<tag>_config<cfg>_kernel_stats.csv (rocprofv3 --stats, verbatim)
+  profiles/traffic_config<cfg>.json      — HBM bytes per launch for bench.py
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE (KiB) reads exactly half
+the bytes of a wide coalesced stream on gfx950 → ×2; WRITE_SIZE (KiB) as is.
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main(tag, cfg, kernel_substr="csum"):
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}_c{cfg}")
+    dst = os.path.join(ROOT, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    stats = os.path.join(src, "kt", "run_kernel_stats.csv")
+    shutil.copy(stats, os.path.join(dst, f"{tag}_config{cfg}_kernel_stats.csv"))
+    rows = list(csv.DictReader(open(stats)))
+    trace = [r for r in csv.DictReader(open(os.path.join(src, "kt", "run_kernel_trace.csv")))
+             if kernel_substr in r["Kernel_Name"]]
+    dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in trace]
+    kname = trace[0]["Kernel_Name"]
+    counters = collections.defaultdict(list)
+    for grp in ("fetch", "write", "sq"):
+        p = os.path.join(src, grp, "run_counter_collection.csv")
+        if not os.path.exists(p):
+            continue
+        for r in csv.DictReader(open(p)):
+            if kernel_substr in r["Kernel_Name"]:
+                counters[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    mean = {k: statistics.mean(v) for k, v in counters.items()}
+    fetch_b = mean.get("FETCH_SIZE", 0) * 1024 * 2
+    write_b = mean.get("WRITE_SIZE", 0) * 1024
+    traffic = {"bytes_per_launch": int(fetch_b + write_b), "fetch_bytes_corrected": int(fetch_b),
+               "write_bytes": int(write_b), "fetch_size_kib_raw": mean.get("FETCH_SIZE"),
+               "write_size_kib_raw": mean.get("WRITE_SIZE"), "kernel": kname, "launches": len(counters["FETCH_SIZE"]),
+               "note": "FETCH_SIZE x2 (gfx950 wide-stream calibration, MI355X_MICROARCH.md HBM section)",
+               "profile": f"profiles/{tag}_config{cfg}.md"}
+    with open(os.path.join(dst, f"traffic_config{cfg}.json"), "w") as f:
+        json.dump(traffic, f, indent=1)
+    lines = [f"# rocprofv3 summary — {tag}, bench.py --config {cfg}", "",
+             f"Command: `tools/profile.sh {cfg} {tag}` (bench.py --config {cfg} --steps 50 --warmup 5 under "
+             "`rocprofv3 --kernel-trace --stats`, then one `--pmc` pass per counter group).", "",
+             "## Kernel stats (rocprofv3 --stats)", "", "| kernel | calls | avg µs | min µs | max µs |",
+             "|---|---|---|---|---|"]
+    for r in rows:
+        lines.append(f"| `{r['Name'][:110]}` | {r['Calls']} | {float(r['AverageNs'])/1e3:.1f} | "
+                     f"{float(r['MinNs'])/1e3:.1f} | {float(r['MaxNs'])/1e3:.1f} |")
+    lines += ["", f"Checksum kernel per-launch durations (µs, trace order): "
+              f"median {statistics.median(dur):.1f}, mean {statistics.mean(dur):.1f}, min {min(dur):.1f}, "
+              f"max {max(dur):.1f}", "", "## Counters per launch (mean over launches)", "",
+              "| counter | value |", "|---|---|"]
+    for k in sorted(mean):
+        lines.append(f"| {k} | {mean[k]:.6g} |")
+    lines += ["", "## HBM traffic per launch", "",
+              f"- FETCH_SIZE ×2 ×1024 = {fetch_b/1e9:.4f} GB (gfx950: FETCH_SIZE counts half of a wide stream)",
+              f"- WRITE_SIZE ×1024 = {write_b/1e6:.3f} MB",
+              f"- total = {(fetch_b + write_b)/1e9:.4f} GB per launch"]
+    if "GRBM_GUI_ACTIVE" in mean:
+        clk = mean["GRBM_GUI_ACTIVE"] / 8 / (statistics.mean(dur) * 1e-6) / 1e9
+        lines.append(f"- effective clock ≈ GRBM_GUI_ACTIVE/8/duration ≈ {clk:.2f} GHz")
+    with open(os.path.join(dst, f"{tag}_config{cfg}.md"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], int(sys.argv[2]), *(sys.argv[3:4]))

@@ -1,0 +1,22 @@
+#!/bin/bash
+# rocprofv3 evidence for one bench workload: kernel-trace stats, then each PMC
+# group in its own pass (never combined with other trace domains).
+# usage: tools/profile.sh <config> [tag]
+set -u
+cfg=${1:-2}; tag=${2:-r01}
+out=gpurun_out/prof_${tag}_c${cfg}
+mkdir -p "$out"
+export TMPDIR=/tmp
+B="bench.py --config $cfg --steps 50 --warmup 5 --cpu-seconds 0"
+run() {  # run <name> <timeout> rocprofv3-args...
+  local name=$1 t=$2; shift 2
+  echo "=== $name"
+  timeout -k 10 "$t" rocprofv3 "$@" -d "$out/$name" -o run -f csv -- python3 $B > "$out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"; tail -2 "$out/$name.log"
+  if [ $rc -ge 124 ]; then echo "fatal rc=$rc"; exit $rc; fi
+}
+run kt 300 --kernel-trace --stats
+run fetch 300 --kernel-trace --pmc FETCH_SIZE
+run write 300 --kernel-trace --pmc WRITE_SIZE
+run sq 300 --kernel-trace --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE

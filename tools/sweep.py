@@ -23,14 +23,22 @@ import nsx  # noqa: E402
 
 def variants(kind):
     out = []
-    for bpc, spw, nt, xcd in itertools.product((8, 4, 2), (1, 2, 4), (0, 1), (1, 2)):
+    for bpc, rows, nt, xcd in itertools.product((8, 4, 2), (4, 8, 16), (1,), (1, 3)):
+        out.append(dict(kernel=1, blocks_per_cu=bpc, stream_rows=rows, nontemporal=nt, xcd_map=xcd))
+    for bpc, spw, nt in itertools.product((8, 4, 2), (1, 2, 4), (1,)):
         if kind != "fixed2" and spw != 1:
             continue
-        out.append(dict(blocks_per_cu=bpc, segs_per_wave=spw, nontemporal=nt, xcd_map=xcd))
+        for xcd in (1, 3):
+            out.append(dict(kernel=2, blocks_per_cu=bpc, segs_per_wave=spw, nontemporal=nt, xcd_map=xcd))
+    if kind == "fixed2":
+        for bpc, spw, xcd in itertools.product((8, 4, 2, 1), (1, 2, 4, 8), (1, 3)):
+            out.append(dict(kernel=3, blocks_per_cu=bpc, segs_per_wave=spw, nontemporal=1, xcd_map=xcd))
     return out
 
 
 def apply(v):
+    for p in nsx.ALL_PARAMS:
+        nsx.set_param(p, 0)
     for k, val in v.items():
         nsx.set_param(bench.PARAMS[k], val)
 
@@ -60,7 +68,7 @@ def main():
         kind = "fixed2" if cfg["kind"] == "fixed" and cfg["seg_len"] <= 4093 else cfg["kind"]
         vs = variants(kind)
         if cid in (3, 4):
-            vs += [dict(v, block_mode=2) for v in vs if v["blocks_per_cu"] == 8]
+            vs += [dict(v, block_mode=2) for v in vs if v["kernel"] == 2 and v["blocks_per_cu"] == 8]
         times = {i: [] for i in range(len(vs))}
         for i, v in enumerate(vs):  # warm each once
             apply(v)
@@ -75,7 +83,8 @@ def main():
             med = statistics.median(times[i])
             rows.append(dict(v, ms=round(med, 4), GBps=round(w["alg"] / med / 1e6, 1),
                              frac=round(w["alg"] / med / 1e6 / 8000, 4), ms_min=round(min(times[i]), 4)))
-            nsx.set_param(nsx.PARAM_BLOCK_MODE, 0)
+            for p in nsx.ALL_PARAMS:
+                nsx.set_param(p, 0)
         rows.sort(key=lambda r: r["ms"])
         results[f"config{cid}"] = rows
         for r in rows[:8]:
