@@ -640,6 +640,261 @@ __global__ __launch_bounds__(kBlock) void csum_stream_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Ragged row-stream on buffer loads (the default ragged kernel). Same schedule
+// as csum_stream_kernel — a wave owns kRun consecutive segments and streams
+// their 1 KiB rows in batches of R loads that cross segment boundaries — but
+// every load goes through a segment-window descriptor (csum_fixed_buf_kernel's
+// SegWin rule), so it is unconditional, pinned ahead of its use, and only the
+// partial first / last dword of a segment needs a byte mask. Per-slot state is
+// two scalars (segment slot in the run, row); descriptors are rebuilt from the
+// lane-resident offsets at issue. Segment lengths must be < 2^31 bytes.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ u32x4 edge_mask2(u32x4 x, uint32_t head, uint32_t end, uint32_t k, uint32_t lane) {
+    SegWin w;
+    w.head = head;
+    w.end = end;
+    return edge_mask(x, w, k, lane);
+}
+
+struct RunSeg {  // wave-uniform view of segment slot j of the current run
+    const uint8_t* wb;
+    uint32_t head, end, rows;
+};
+
+__device__ __forceinline__ RunSeg run_seg(const uint8_t* base, uint64_t my_off, uint32_t j) {
+    const uint64_t o0 = readlane64(my_off, j), o1 = readlane64(my_off, j + 1);
+    const uint32_t len = o1 > o0 ? (uint32_t)(o1 - o0) : 0u;
+    const uint8_t* p = base + o0;
+    RunSeg s;
+    s.head = (uint32_t)((uintptr_t)p & 3u);
+    s.wb = p - s.head;
+    s.end = s.head + len;
+    s.rows = len ? (s.end + kRow - 1) / kRow : 0u;
+    return s;
+}
+
+template <int R, bool NT, bool VERIFY>
+__global__ __launch_bounds__(kBlock) void csum_ragged_buf_kernel(
+    const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, uint32_t n,
+    const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, uint8_t* __restrict__ ok, int xcd_map) {
+    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const uint32_t ntasks = (n + kRun - 1) / kRun;
+    const TaskIter it = task_iter(ntasks, wave, xcd_map);
+    const uint32_t end = (uint32_t)it.end, step = (uint32_t)it.step;
+    const __amdgpu_buffer_rsrc_t ofs = make_rsrc(offsets, ((uint64_t)n + 1) * 8);
+    const __amdgpu_buffer_rsrc_t prs = make_rsrc(partial, partial ? (uint64_t)n * 4 : 0);
+    const __amdgpu_buffer_rsrc_t ors = make_rsrc(out, out ? (uint64_t)n * 2 : 0);
+    const __amdgpu_buffer_rsrc_t oks = make_rsrc(ok, VERIFY ? (uint64_t)n : 0);
+    auto load_offs = [&](uint32_t t) -> uint64_t {  // lane l: offsets[t*kRun + l], l <= run length
+        const uint32_t a = t * kRun;
+        const uint32_t voff = (t < end && lane <= kRun && a + lane <= n) ? (a + lane) * 8 : kOOB;
+        const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, voff, 0, 0);
+        return ((uint64_t)x.y << 32) | x.x;
+    };
+    uint64_t nxt_off = load_offs((uint32_t)it.next);
+    for (uint32_t t = (uint32_t)it.next; t < end; t += step) {
+        const uint32_t a = t * kRun, cnt = min(kRun, n - a);
+        const uint64_t my_off = nxt_off;
+        nxt_off = load_offs(t + step);  // prefetch the next run's offsets
+        const uint32_t my_part =
+            __builtin_amdgcn_raw_buffer_load_b32(prs, lane < cnt ? (a + lane) * 4 : kOOB, 0, 0);
+        uint32_t sums = 0, acc = 0;
+        uint32_t cur = 0;                                   // slot being accumulated
+        RunSeg cs = run_seg(base, my_off, 0);               // its window
+        uint32_t ps = 0, pr = 0, prows = cs.rows;           // planning cursor
+        for (;;) {
+            uint32_t sd[R], srow[R];
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                while (ps < cnt && pr >= prows) {
+                    ++ps;
+                    pr = 0;
+                    if (ps < cnt) prows = run_seg(base, my_off, ps).rows;
+                }
+                sd[j] = ps < cnt ? ps : kRun;
+                srow[j] = pr++;
+            }
+            if (sd[0] == kRun) break;
+            u32x4 v[R];
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                const bool live = sd[j] != kRun;
+                const RunSeg g = run_seg(base, my_off, live ? sd[j] : 0);
+                const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+                    const_cast<uint8_t*>(g.wb), 0, live ? (int)((g.end + 3u) & ~3u) : 0, 0x00020000);
+                v[j] = bld16<NT>(r, srow[j] * kRow + lane * 16);
+            }
+#pragma unroll
+            for (int j = 0; j < R; ++j) asm volatile("" : "+v"(v[j]));
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                if (sd[j] != kRun) {
+                    if (sd[j] != cur) {
+                        const uint32_t tot = wave_sum(fold32(acc));
+                        sums = lane == cur ? tot : sums;
+                        acc = 0;
+                        cur = sd[j];
+                        cs = run_seg(base, my_off, cur);
+                    }
+                    acc = sad4(edge_mask2(v[j], cs.head, cs.end, srow[j], lane), acc);
+                }
+            }
+            acc = fold32(acc);
+        }
+        if (cur < cnt) {
+            const uint32_t tot = wave_sum(fold32(acc));
+            sums = lane == cur ? tot : sums;
+        }
+        const bool even = (((uintptr_t)base + my_off) & 1u) == 0;
+        const uint32_t res = finish(sums, even, my_part);
+        const bool mine = lane < cnt;
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, mine ? (a + lane) * 2 : kOOB, 0, 0);
+        if constexpr (VERIFY)
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(res == 0xFFFFu), oks, mine ? a + lane : kOOB, 0, 0);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Ragged prefix-scan kernel (the default ragged kernel).
+//
+// With byte weights w(a) = 1 at even and 256 at odd addresses, let
+// S(x) = Σ_{a<x} b_a·w(a). For a segment [s, e) the raw checksum is
+// fold(S(e) − S(s)), byte-swapped iff s is even (the rule of finish()); the
+// difference is an exact integer, 0 iff every byte is 0. So a densely packed
+// run of segments is one contiguous byte range, and its checksums are the
+// differences of S sampled at the segment boundaries.
+//
+// A wave owns a run of kScanRun consecutive segments (kScanRun+1 boundaries,
+// one per lane). It streams the run's bytes as 1 KiB rows
+// through one buffer descriptor (full rows aligned to 128-byte lines, no
+// per-segment windows, R rows in flight), and per row does: lane half-sums (v_sad_u16), an inclusive wave
+// scan (DPP), and — only in rows that hold a boundary — each boundary lane
+// fetches the chunk and exclusive prefix of the lane its boundary falls in
+// (ds_bpermute) and adds the partial chunk below the boundary. Work per byte
+// no longer depends on how many segments the bytes are cut into.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kScanRun = 63;
+
+// Keep bytes [lo, hi) (0 ≤ lo ≤ hi ≤ 16) of a 16-byte chunk.
+__device__ __forceinline__ u32x4 keep_bytes(u32x4 x, int32_t lo, int32_t hi) {
+    x.x &= keep_mask(lo, hi, 0);
+    x.y &= keep_mask(lo, hi, 4);
+    x.z &= keep_mask(lo, hi, 8);
+    x.w &= keep_mask(lo, hi, 12);
+    return x;
+}
+
+// Inclusive prefix sum over the 64 lanes (DPP row shifts, then row broadcasts).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return v;
+}
+
+__device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t src_lane) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane * 4), (int)v);
+}
+
+template <int R, bool NT, bool VERIFY>
+__global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
+    const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, uint32_t n,
+    const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, uint8_t* __restrict__ ok, int xcd_map) {
+    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const uint32_t ntasks = (n + kScanRun - 1) / kScanRun;
+    const TaskIter it = task_iter(ntasks, wave, xcd_map);
+    const uint32_t end = (uint32_t)it.end, step = (uint32_t)it.step;
+    const __amdgpu_buffer_rsrc_t ofs = make_rsrc(offsets, ((uint64_t)n + 1) * 8);
+    const __amdgpu_buffer_rsrc_t prs = make_rsrc(partial, partial ? (uint64_t)n * 4 : 0);
+    const __amdgpu_buffer_rsrc_t ors = make_rsrc(out, out ? (uint64_t)n * 2 : 0);
+    const __amdgpu_buffer_rsrc_t oks = make_rsrc(ok, VERIFY ? (uint64_t)n : 0);
+    auto load_offs = [&](uint32_t t) -> uint64_t {  // lane l ≤ run length: offsets[t*kScanRun + l]
+        const uint32_t a = t * kScanRun;
+        const uint32_t voff = (t < end && lane <= kScanRun && a + lane <= n) ? (a + lane) * 8 : kOOB;
+        const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, voff, 0, 0);
+        return ((uint64_t)x.y << 32) | x.x;
+    };
+    uint64_t nxt_off = load_offs((uint32_t)it.next);
+    for (uint32_t t = (uint32_t)it.next; t < end; t += step) {
+        const uint32_t a = t * kScanRun, cnt = min(kScanRun, n - a);
+        const uint64_t my_off = nxt_off;  // boundary `lane` of the run (lanes 0..cnt)
+        nxt_off = load_offs(t + step);
+        const uint32_t my_part = __builtin_amdgcn_raw_buffer_load_b32(prs, lane < cnt ? (a + lane) * 4 : kOOB, 0, 0);
+        const uint64_t lo = readlane64(my_off, 0), hi = readlane64(my_off, cnt);
+        // Rows start on a 128-byte line so a 1 KiB row touches exactly 8 lines.
+        const uint8_t* rbase = reinterpret_cast<const uint8_t*>(((uintptr_t)(base + lo)) & ~(uintptr_t)127);
+        const uint64_t span = (uint64_t)((base + hi) - rbase);           // bytes from rbase to the run's end
+        const uint32_t head = (uint32_t)((uintptr_t)(base + lo) & 127u);  // bytes before the run in row 0
+        const uint64_t nrows = (span + kRow - 1) / kRow;
+        // Boundary lane state: its position relative to rbase, and S there.
+        const int64_t brel = lane <= cnt ? (int64_t)((base + my_off) - rbase) : -1;
+        uint64_t bval = 0;
+        uint64_t carry = 0;  // S over all rows before the current one
+        for (uint64_t r0 = 0; r0 < nrows; r0 += R) {
+            // One descriptor per batch, based at the batch's first row.
+            const uint8_t* bb = rbase + r0 * kRow;
+            const uint64_t rem = span - r0 * kRow;
+            const __amdgpu_buffer_rsrc_t rs = make_rsrc(bb, (rem + 3) & ~3ull);
+            u32x4 v[R];
+#pragma unroll
+            for (int j = 0; j < R; ++j) v[j] = bld16<NT>(rs, j * kRow + lane * 16);
+#pragma unroll
+            for (int j = 0; j < R; ++j) asm volatile("" : "+v"(v[j]));
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                const uint64_t r = r0 + j;
+                if (r >= nrows) break;
+                u32x4 x = v[j];
+                const int64_t rowrel = (int64_t)(r * kRow);
+                if (r == 0 && head) {  // bytes before the run's first segment
+                    const int32_t h = (int32_t)head - (int32_t)lane * 16;
+                    x = keep_bytes(x, min(max(h, 0), 16), 16);
+                }
+                if (rowrel + (int64_t)kRow > (int64_t)span) {  // bytes past the run's end
+                    const int32_t e = (int32_t)((int64_t)span - rowrel) - (int32_t)lane * 16;
+                    x = keep_bytes(x, 0, min(max(e, 0), 16));
+                }
+                const uint32_t sl = sad4(x, 0u);
+                const uint32_t incl = wave_incl_scan(sl);
+                const uint32_t row_total = __builtin_amdgcn_readlane(incl, 63);
+                const int64_t q = brel - rowrel;  // boundary position inside this row
+                const bool here = q >= 0 && q < (int64_t)kRow;
+                if (__builtin_amdgcn_ballot_w64(here)) {
+                    const uint32_t src = here ? (uint32_t)(q >> 4) : lane;
+                    const uint32_t pre = bperm(incl - sl, src);
+                    u32x4 y;
+                    y.x = bperm(x.x, src);
+                    y.y = bperm(x.y, src);
+                    y.z = bperm(x.z, src);
+                    y.w = bperm(x.w, src);
+                    const uint32_t part = sad4(keep_bytes(y, 0, (int32_t)(q & 15)), 0u);
+                    if (here) bval = carry + pre + part;
+                }
+                carry += row_total;
+            }
+        }
+        if (brel >= (int64_t)(nrows * kRow)) bval = carry;  // boundary at the very end of the rows
+        // Segment `lane` = [boundary lane, boundary lane+1).
+        const uint64_t nb = ((uint64_t)__shfl_down((unsigned long long)bval, 1));
+        const uint64_t d = nb - bval;
+        const uint32_t le = fold32((uint32_t)(d & 0xFFFFFFFFu)) + fold32((uint32_t)(d >> 32));
+        const bool even = (((uintptr_t)base + my_off) & 1u) == 0;
+        const uint32_t res = finish(le, even, my_part);
+        const bool mine = lane < cnt;
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, mine ? (a + lane) * 2 : kOOB, 0, 0);
+        if constexpr (VERIFY)
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(res == 0xFFFFu), oks, mine ? a + lane : kOOB, 0, 0);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // IPv4 pseudo-header partials: src(4) dst(4) 0 proto len16 (RFC 9293 §3.1).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void pseudo_ipv4_kernel(const uint8_t* __restrict__ src,
@@ -701,13 +956,13 @@ enum class Path { kFixedShort, kFixedLong, kRagged, kBlock };
 // Per-path defaults (tools/sweep.py, MI355X):
 //   fixed ≤4 rows : buffer-load kernel, 4 segments/wave, 2 blocks/CU (8 waves/CU)
 //   fixed long    : per-segment wave kernel, 2 blocks/CU (8 waves/CU, 4 KiB in flight each)
-//   ragged        : row-stream kernel, 8 rows/batch, 4 blocks/CU
+//   ragged        : prefix-scan kernel, 8 rows/batch, 8 blocks/CU (occupancy-capped at 5 waves/SIMD)
 // nt loads and the XCD-contiguous deal everywhere.
 static Plan resolve(const LaunchCfg& c, Path p) {
     Plan r;
     int bpc = c.blocks_per_cu;
     if (bpc < 1 || bpc > 8)
-        bpc = (p == Path::kFixedLong || p == Path::kFixedShort) ? 2 : (p == Path::kBlock ? 8 : 4);
+        bpc = (p == Path::kFixedLong || p == Path::kFixedShort) ? 2 : (p == Path::kRagged ? 8 : 8);
     r.max_blocks = (uint32_t)(c.cus * bpc);
     r.spw = (c.segs_per_wave == 1 || c.segs_per_wave == 2 || c.segs_per_wave == 4 || c.segs_per_wave == 8)
                 ? c.segs_per_wave : 4;
@@ -858,6 +1113,65 @@ hipError_t launch_fixed(const LaunchCfg& c, const void* d_base, uint64_t stride,
     return launch_seg<false, false>(p, base, nullptr, stride, seg_len, n, partial, out, nullptr, safe_end, false, st);
 }
 
+template <bool VERIFY>
+static hipError_t launch_ragged_buf(const Plan& c, const uint8_t* base, const uint64_t* offsets, uint64_t n,
+                                    const uint32_t* partial, uint16_t* out, uint8_t* ok, hipStream_t st) {
+    // Buffer descriptors address ≤ 2^31 bytes of offsets/results: chunk huge batches.
+    constexpr uint64_t kChunk = 1ull << 27;
+    for (uint64_t c0 = 0; c0 < n; c0 += kChunk) {
+        const uint32_t cn = (uint32_t)(n - c0 < kChunk ? n - c0 : kChunk);
+        const uint64_t ntasks = (cn + kRun - 1) / kRun;
+        const uint64_t want = (ntasks + kWavesPerBlock - 1) / kWavesPerBlock;
+        const uint32_t grid = (uint32_t)(want < c.max_blocks ? want : c.max_blocks);
+        const uint32_t* pc = partial ? partial + c0 : nullptr;
+        uint16_t* oc = out ? out + c0 : nullptr;
+        uint8_t* kc = ok ? ok + c0 : nullptr;
+#define NSX_RBUF(R_)                                                                                             \
+        if (c.rows == R_) {                                                                                       \
+            if (c.nt)                                                                                             \
+                hipLaunchKernelGGL((csum_ragged_buf_kernel<R_, true, VERIFY>), dim3(grid), dim3(kBlock), 0, st,   \
+                                   base, offsets + c0, cn, pc, oc, kc, c.xcd);                                    \
+            else                                                                                                  \
+                hipLaunchKernelGGL((csum_ragged_buf_kernel<R_, false, VERIFY>), dim3(grid), dim3(kBlock), 0, st,  \
+                                   base, offsets + c0, cn, pc, oc, kc, c.xcd);                                    \
+        }
+        NSX_RBUF(4) NSX_RBUF(8) NSX_RBUF(16)
+#undef NSX_RBUF
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+template <bool VERIFY>
+static hipError_t launch_ragged_scan(const Plan& c, const uint8_t* base, const uint64_t* offsets, uint64_t n,
+                                     const uint32_t* partial, uint16_t* out, uint8_t* ok, hipStream_t st) {
+    constexpr uint64_t kChunk = 1ull << 27;
+    for (uint64_t c0 = 0; c0 < n; c0 += kChunk) {
+        const uint32_t cn = (uint32_t)(n - c0 < kChunk ? n - c0 : kChunk);
+        const uint64_t ntasks = (cn + kScanRun - 1) / kScanRun;
+        const uint64_t want = (ntasks + kWavesPerBlock - 1) / kWavesPerBlock;
+        const uint32_t grid = (uint32_t)(want < c.max_blocks ? want : c.max_blocks);
+        const uint32_t* pc = partial ? partial + c0 : nullptr;
+        uint16_t* oc = out ? out + c0 : nullptr;
+        uint8_t* kc = ok ? ok + c0 : nullptr;
+#define NSX_RSCAN(R_)                                                                                             \
+        if (c.rows == R_) {                                                                                        \
+            if (c.nt)                                                                                              \
+                hipLaunchKernelGGL((csum_ragged_scan_kernel<R_, true, VERIFY>), dim3(grid), dim3(kBlock), 0, st,   \
+                                   base, offsets + c0, cn, pc, oc, kc, c.xcd);                                     \
+            else                                                                                                   \
+                hipLaunchKernelGGL((csum_ragged_scan_kernel<R_, false, VERIFY>), dim3(grid), dim3(kBlock), 0, st,  \
+                                   base, offsets + c0, cn, pc, oc, kc, c.xcd);                                     \
+        }
+        NSX_RSCAN(4) NSX_RSCAN(8) NSX_RSCAN(16)
+#undef NSX_RSCAN
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
 hipError_t launch_ragged(const LaunchCfg& c, const void* d_base, const uint64_t* d_offsets, uint64_t n,
                          const uint32_t* partial, uint16_t* out, uint8_t* ok, hipStream_t st) {
     const uint8_t* base = static_cast<const uint8_t*>(d_base);
@@ -867,7 +1181,15 @@ hipError_t launch_ragged(const LaunchCfg& c, const void* d_base, const uint64_t*
         return launch_seg<true, false>(p, base, d_offsets, 0, 0, n, partial, out, nullptr, nullptr, true, st);
     }
     const Plan p = resolve(c, Path::kRagged);
-    if (c.kernel != kKernelPerSegment) {
+    if (c.kernel == 0 || c.kernel == kKernelScan) {
+        if (ok) return launch_ragged_scan<true>(p, base, d_offsets, n, partial, out, ok, st);
+        return launch_ragged_scan<false>(p, base, d_offsets, n, partial, out, nullptr, st);
+    }
+    if (c.kernel == kKernelPipelined) {
+        if (ok) return launch_ragged_buf<true>(p, base, d_offsets, n, partial, out, ok, st);
+        return launch_ragged_buf<false>(p, base, d_offsets, n, partial, out, nullptr, st);
+    }
+    if (c.kernel == kKernelRowStream) {
         if (ok) return launch_stream<true, true>(p, base, d_offsets, 0, 0, n, partial, out, ok, nullptr, st);
         return launch_stream<true, false>(p, base, d_offsets, 0, 0, n, partial, out, nullptr, nullptr, st);
     }

@@ -211,6 +211,41 @@ def test_all_variants_bit_exact():
         set_variant(dict(kernel=0, rows=0, spw=0, nt=0, xcd=0, bpc=0), 0)
 
 
+RAGGED_VARIANTS = ([dict(kernel=k, rows=r, nt=nt, xcd=x, bpc=b, spw=0) for k in (3, 4) for r in (4, 8, 16)
+                    for nt in (1, 2) for x in (1, 2, 3) for b in (8, 2)] +
+                   [dict(kernel=1, rows=r, nt=1, xcd=1, bpc=4, spw=0) for r in (4, 8, 16)] +
+                   [dict(kernel=2, rows=0, nt=1, xcd=x, bpc=4, spw=0) for x in (1, 3)])
+
+
+def test_ragged_variants_bit_exact():
+    rng = np.random.default_rng(1234)
+    lens = rng.integers(0, 9001, 20000).astype(np.uint64)
+    lens[rng.integers(0, 20000, 300)] = 0
+    lens[rng.integers(0, 20000, 40)] = rng.integers(1, 4, 40)
+    lens[rng.integers(0, 20000, 10)] = rng.integers(100000, 300000, 10)
+    offs = np.zeros(lens.size + 1, np.uint64)
+    offs[1:] = np.cumsum(lens)
+    offs += np.uint64(5)
+    buf = O.c_splitmix64(0x1072, int(offs[-1]) + 3)
+    part = rng.integers(0, 1 << 31, lens.size, dtype=np.uint32)
+    want = O.c_batch(buf, lens.size, offsets=offs)
+    want_p = O.c_batch(buf, lens.size, offsets=offs, partial=part)
+    d, o, p = dev(buf), dev(offs.view(np.int64)), dev(part.view(np.int32))
+    try:
+        for v in RAGGED_VARIANTS:
+            for bm in (0, 1):
+                set_variant(v, bm)
+                out = torch.empty(lens.size, dtype=torch.int16, device="cuda")
+                nsx.ragged_dev(d, o, out=out)
+                assert np.array_equal(u16(out), want), (v, bm)
+                nsx.ragged_dev(d, o, partial=p, out=out)
+                assert np.array_equal(u16(out), want_p), (v, bm)
+                okv = host(nsx.verify_ragged_dev(d, o, partial=p))
+                assert np.array_equal(okv.astype(bool), want_p == 0xFFFF), (v, bm)
+    finally:
+        set_variant(dict(kernel=0, rows=0, spw=0, nt=0, xcd=0, bpc=0), 0)
+
+
 # ------------------------------------------------------------------ verify / pseudo-header
 
 def test_pseudo_ipv4_partial_and_verify_roundtrip():

@@ -31,7 +31,7 @@ def main(tag, cfg, kernel_substr="csum"):
     dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in trace]
     kname = trace[0]["Kernel_Name"]
     counters = collections.defaultdict(list)
-    for grp in ("fetch", "write", "sq"):
+    for grp in ("fetch", "write", "sq", "sq2", "tcc", "ta"):
         p = os.path.join(src, grp, "run_counter_collection.csv")
         if not os.path.exists(p):
             continue

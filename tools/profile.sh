@@ -13,10 +13,12 @@ run() {  # run <name> <timeout> rocprofv3-args...
   echo "=== $name"
   timeout -k 10 "$t" rocprofv3 "$@" -d "$out/$name" -o run -f csv -- python3 $B > "$out/$name.log" 2>&1
   local rc=$?
-  echo "=== $name rc=$rc"; tail -2 "$out/$name.log"
+  echo "=== $name rc=$rc"; tail -1 "$out/$name.log" | cut -c1-200
   if [ $rc -ge 124 ]; then echo "fatal rc=$rc"; exit $rc; fi
 }
 run kt 300 --kernel-trace --stats
 run fetch 300 --kernel-trace --pmc FETCH_SIZE
 run write 300 --kernel-trace --pmc WRITE_SIZE
 run sq 300 --kernel-trace --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE
+run sq2 300 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA SQ_INST_LEVEL_VMEM SQ_WAVE_CYCLES SQ_ACTIVE_INST_VMEM SQ_INSTS_VMEM_WR
+run tcc 300 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum

@@ -30,6 +30,9 @@ def variants(kind):
             continue
         for xcd in (1, 3):
             out.append(dict(kernel=2, blocks_per_cu=bpc, segs_per_wave=spw, nontemporal=nt, xcd_map=xcd))
+    if kind == "ragged":
+        for k, bpc, rows, xcd in itertools.product((3, 4), (8, 4, 2, 1), (4, 8, 16), (1, 3)):
+            out.append(dict(kernel=k, blocks_per_cu=bpc, stream_rows=rows, nontemporal=1, xcd_map=xcd))
     if kind == "fixed2":
         for bpc, spw, xcd in itertools.product((8, 4, 2, 1), (1, 2, 4, 8), (1, 3)):
             out.append(dict(kernel=3, blocks_per_cu=bpc, segs_per_wave=spw, nontemporal=1, xcd_map=xcd))
