@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""End-to-end host-memory rate of the checksum path (north_star: segments come
+from and return to the transport's host buffers). Times nsx_csum_fixed_host /
+nsx_csum_ragged_host — pinned H2D → kernel → D2H, double-buffered over two
+streams per GPU — on config 2 (1M x 1500 B) and config 3 (1M ragged) batches
+held in pinned memory (nsx_alloc_pinned) and in pageable numpy memory.
+Results are spot-checked against the oracle (tools are test infrastructure).
+
+    python tools/e2e_host.py [--reps 5] [--gpus 0]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "network-stack_amd"))
+
+import numpy as np  # noqa: E402
+
+import nsx  # noqa: E402
+from oracle import csum_oracle as O  # noqa: E402
+
+
+def timed(fn, reps):
+    fn()  # warm (allocations, first touch)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        out = fn()
+        ts.append(time.perf_counter() - t0)
+    return statistics.median(ts), out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--gpus", type=int, default=0)
+    a = ap.parse_args()
+    res = {"gpus_visible": nsx.device_count()}
+    n, L = 1 << 20, 1500
+    nbytes = n * L
+    page = O.c_splitmix64(0x1071, nbytes)
+    pin = nsx.PinnedBuffer(nbytes)
+    pin.array[:] = page
+    for name, arr in (("fixed_pinned", pin.array), ("fixed_pageable", page)):
+        t, out = timed(lambda: nsx.fixed_host(arr, L, L, n, num_gpus=a.gpus), a.reps)
+        idx = np.arange(0, n, 4099)
+        want = O.batch_fixed(page[: (idx[-1] + 1) * L], L, L, int(idx[-1]) + 1)[idx]
+        assert np.array_equal(out[idx], want), name
+        res[name] = {"seconds": t, "GB_per_s": nbytes / t / 1e9, "GiB_per_s": nbytes / t / (1 << 30)}
+        print(name, json.dumps(res[name]), flush=True)
+    pin.free()
+    rng = np.random.default_rng(0x1072)
+    lens = rng.integers(64, 9001, n).astype(np.uint64)
+    offs = np.zeros(n + 1, np.uint64)
+    offs[1:] = np.cumsum(lens)
+    total = int(offs[-1])
+    rpage = O.c_splitmix64(0x1072, total)
+    rpin = nsx.PinnedBuffer(total)
+    rpin.array[:] = rpage
+    for name, arr in (("ragged_pinned", rpin.array), ("ragged_pageable", rpage)):
+        t, out = timed(lambda: nsx.ragged_host(arr, offs, num_gpus=a.gpus), a.reps)
+        sel = np.arange(0, n, 4099)
+        for i in sel[:64]:
+            assert out[i] == O.c_fold_checksum(b"", rpage[int(offs[i]):int(offs[i + 1])].tobytes()), (name, i)
+        res[name] = {"seconds": t, "GB_per_s": total / t / 1e9, "GiB_per_s": total / t / (1 << 30)}
+        print(name, json.dumps(res[name]), flush=True)
+    rpin.free()
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "e2e_host.json"), "w") as f:
+        json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
