@@ -59,7 +59,7 @@ def parse_args(argv=None):
     ap.add_argument("--param", action="append", default=[], metavar="NAME=V",
                     help="kernel knob (include/nsx_csum.h NSX_PARAM_*): " + ", ".join(
                         ["blocks_per_cu", "segs_per_wave", "nontemporal", "block_mode", "xcd_map", "kernel",
-                         "stream_rows"]))
+                         "stream_rows", "run_segs"]))
     return ap.parse_args(argv)
 
 
@@ -167,7 +167,7 @@ def result_line(*, world, steps, warmup, wall_max, bytes_per_rank_step, units_to
 # GPU workload
 # ---------------------------------------------------------------------------
 PARAMS = {"blocks_per_cu": 1, "segs_per_wave": 2, "nontemporal": 3, "block_mode": 4, "xcd_map": 5, "kernel": 6,
-          "stream_rows": 7}
+          "stream_rows": 7, "run_segs": 8}
 
 
 def build_workload(cfg, rank, device):

@@ -148,7 +148,8 @@ const char* nsx_strerror(int code);
 #define NSX_PARAM_BLOCK_MODE      4  /* 0 auto (a block per segment when n < 4*CUs), 1 never, 2 always */
 #define NSX_PARAM_XCD_MAP         5  /* task deal: 1 XCD-contiguous regions (default), 2 grid-stride, 3 one contiguous range per wave */
 #define NSX_PARAM_KERNEL          6  /* 1 row-stream, 2 per-segment, 3 buffer-load, 4 prefix-scan (ragged); 0 = per-path default */
-#define NSX_PARAM_STREAM_ROWS     7  /* row-stream: 4, 8 (default) or 16 KiB in flight per wave */
+#define NSX_PARAM_STREAM_ROWS     7  /* row-stream / scan: 4, 8 (default) or 16 KiB in flight per wave */
+#define NSX_PARAM_RUN_SEGS        8  /* ragged scan kernel: segments per wave task, 1..63 (default 16) */
 int nsx_set_param(int param, int64_t value);
 int nsx_get_param(int param, int64_t* value);
 

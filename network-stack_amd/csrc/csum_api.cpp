@@ -21,7 +21,7 @@
 namespace {
 
 // ---------------------------------------------------------------- params
-constexpr int kNumParams = 8;
+constexpr int kNumParams = 9;
 std::atomic<int64_t> g_param[kNumParams];  // index = NSX_PARAM_*; 0 = default
 
 constexpr int kMaxDevices = 64;
@@ -94,6 +94,7 @@ LaunchCfg default_launch_cfg(int cus, uint64_t /*n*/) {
     c.xcd_map = get(NSX_PARAM_XCD_MAP);
     c.kernel = get(NSX_PARAM_KERNEL);
     c.rows = get(NSX_PARAM_STREAM_ROWS);
+    c.run_segs = get(NSX_PARAM_RUN_SEGS);
     return c;
 }
 

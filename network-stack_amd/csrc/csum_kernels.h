@@ -23,6 +23,7 @@ struct LaunchCfg {
     int xcd_map;         // 1 XCD-contiguous deal, 2 grid-stride, 3 contiguous range per wave
     int kernel;          // kKernelRowStream / kKernelPerSegment
     int rows;            // row-stream rows per batch: 4, 8, 16
+    int run_segs;        // ragged scan kernel: segments per wave task, 1..63
 };
 
 // Launch configuration from the process-wide NSX_PARAM_* knobs (csum_api.cpp).

@@ -766,7 +766,7 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_buf_kernel(
 // run of segments is one contiguous byte range, and its checksums are the
 // differences of S sampled at the segment boundaries.
 //
-// A wave owns a run of kScanRun consecutive segments (kScanRun+1 boundaries,
+// A wave owns a run of up to kScanRun consecutive segments (run+1 boundaries,
 // one per lane). It streams the run's bytes as 1 KiB rows
 // through one buffer descriptor (full rows aligned to 128-byte lines, no
 // per-segment windows, R rows in flight), and per row does: lane half-sums (v_sad_u16), an inclusive wave
@@ -804,26 +804,27 @@ __device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t src_lane) {
 template <int R, bool NT, bool VERIFY>
 __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, uint32_t n,
-    const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, uint8_t* __restrict__ ok, int xcd_map) {
+    const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, uint8_t* __restrict__ ok, int xcd_map,
+    uint32_t run) {
     typedef uint32_t v2u __attribute__((ext_vector_type(2)));
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const uint32_t ntasks = (n + kScanRun - 1) / kScanRun;
+    const uint32_t ntasks = (n + run - 1) / run;  // run ≤ kScanRun segments per wave task
     const TaskIter it = task_iter(ntasks, wave, xcd_map);
     const uint32_t end = (uint32_t)it.end, step = (uint32_t)it.step;
     const __amdgpu_buffer_rsrc_t ofs = make_rsrc(offsets, ((uint64_t)n + 1) * 8);
     const __amdgpu_buffer_rsrc_t prs = make_rsrc(partial, partial ? (uint64_t)n * 4 : 0);
     const __amdgpu_buffer_rsrc_t ors = make_rsrc(out, out ? (uint64_t)n * 2 : 0);
     const __amdgpu_buffer_rsrc_t oks = make_rsrc(ok, VERIFY ? (uint64_t)n : 0);
-    auto load_offs = [&](uint32_t t) -> uint64_t {  // lane l ≤ run length: offsets[t*kScanRun + l]
-        const uint32_t a = t * kScanRun;
-        const uint32_t voff = (t < end && lane <= kScanRun && a + lane <= n) ? (a + lane) * 8 : kOOB;
+    auto load_offs = [&](uint32_t t) -> uint64_t {  // lane l ≤ run length: offsets[t*run + l]
+        const uint32_t a = t * run;
+        const uint32_t voff = (t < end && lane <= run && a + lane <= n) ? (a + lane) * 8 : kOOB;
         const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, voff, 0, 0);
         return ((uint64_t)x.y << 32) | x.x;
     };
     uint64_t nxt_off = load_offs((uint32_t)it.next);
     for (uint32_t t = (uint32_t)it.next; t < end; t += step) {
-        const uint32_t a = t * kScanRun, cnt = min(kScanRun, n - a);
+        const uint32_t a = t * run, cnt = min(run, n - a);
         const uint64_t my_off = nxt_off;  // boundary `lane` of the run (lanes 0..cnt)
         nxt_off = load_offs(t + step);
         const uint32_t my_part = __builtin_amdgcn_raw_buffer_load_b32(prs, lane < cnt ? (a + lane) * 4 : kOOB, 0, 0);
@@ -847,38 +848,50 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
             for (int j = 0; j < R; ++j) v[j] = bld16<NT>(rs, j * kRow + lane * 16);
 #pragma unroll
             for (int j = 0; j < R; ++j) asm volatile("" : "+v"(v[j]));
+            // Phase 1: edge masks (first/last row of the run only), lane half-sums
+            // and the R row scans as independent chains (ILP across rows).
+            uint32_t sl[R], incl[R];
 #pragma unroll
             for (int j = 0; j < R; ++j) {
                 const uint64_t r = r0 + j;
-                if (r >= nrows) break;
-                u32x4 x = v[j];
                 const int64_t rowrel = (int64_t)(r * kRow);
                 if (r == 0 && head) {  // bytes before the run's first segment
                     const int32_t h = (int32_t)head - (int32_t)lane * 16;
-                    x = keep_bytes(x, min(max(h, 0), 16), 16);
+                    v[j] = keep_bytes(v[j], min(max(h, 0), 16), 16);
                 }
-                if (rowrel + (int64_t)kRow > (int64_t)span) {  // bytes past the run's end
+                if (r < nrows && rowrel + (int64_t)kRow > (int64_t)span) {  // bytes past the run's end
                     const int32_t e = (int32_t)((int64_t)span - rowrel) - (int32_t)lane * 16;
-                    x = keep_bytes(x, 0, min(max(e, 0), 16));
+                    v[j] = keep_bytes(v[j], 0, min(max(e, 0), 16));
                 }
-                const uint32_t sl = sad4(x, 0u);
-                const uint32_t incl = wave_incl_scan(sl);
-                const uint32_t row_total = __builtin_amdgcn_readlane(incl, 63);
-                const int64_t q = brel - rowrel;  // boundary position inside this row
-                const bool here = q >= 0 && q < (int64_t)kRow;
-                if (__builtin_amdgcn_ballot_w64(here)) {
-                    const uint32_t src = here ? (uint32_t)(q >> 4) : lane;
-                    const uint32_t pre = bperm(incl - sl, src);
-                    u32x4 y;
-                    y.x = bperm(x.x, src);
-                    y.y = bperm(x.y, src);
-                    y.z = bperm(x.z, src);
-                    y.w = bperm(x.w, src);
-                    const uint32_t part = sad4(keep_bytes(y, 0, (int32_t)(q & 15)), 0u);
-                    if (here) bval = carry + pre + part;
-                }
-                carry += row_total;
+                sl[j] = sad4(v[j], 0u);
             }
+#pragma unroll
+            for (int j = 0; j < R; ++j) incl[j] = wave_incl_scan(sl[j]);
+            // Phase 2: boundaries that fall in this batch (rows past nrows hold zeros).
+            const int64_t qb = brel - (int64_t)(r0 * kRow);
+            const bool in_batch = qb >= 0 && qb < (int64_t)R * kRow;
+            if (__builtin_amdgcn_ballot_w64(in_batch)) {
+                uint64_t c = carry;
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    const int64_t q = qb - (int64_t)j * kRow;  // boundary position inside row j
+                    const bool here = q >= 0 && q < (int64_t)kRow;
+                    if (__builtin_amdgcn_ballot_w64(here)) {
+                        const uint32_t src = here ? (uint32_t)(q >> 4) : lane;
+                        const uint32_t pre = bperm(incl[j] - sl[j], src);
+                        u32x4 y;
+                        y.x = bperm(v[j].x, src);
+                        y.y = bperm(v[j].y, src);
+                        y.z = bperm(v[j].z, src);
+                        y.w = bperm(v[j].w, src);
+                        const uint32_t part = sad4(keep_bytes(y, 0, (int32_t)(q & 15)), 0u);
+                        if (here) bval = c + pre + part;
+                    }
+                    c += __builtin_amdgcn_readlane(incl[j], 63);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < R; ++j) carry += __builtin_amdgcn_readlane(incl[j], 63);
         }
         if (brel >= (int64_t)(nrows * kRow)) bval = carry;  // boundary at the very end of the rows
         // Segment `lane` = [boundary lane, boundary lane+1).
@@ -949,6 +962,7 @@ struct Plan {
     uint32_t max_blocks;
     int spw, rows, xcd;
     bool nt;
+    uint32_t run;  // ragged scan kernel: segments per wave task (1..kScanRun)
 };
 
 enum class Path { kFixedShort, kFixedLong, kRagged, kBlock };
@@ -956,19 +970,19 @@ enum class Path { kFixedShort, kFixedLong, kRagged, kBlock };
 // Per-path defaults (tools/sweep.py, MI355X):
 //   fixed ≤4 rows : buffer-load kernel, 4 segments/wave, 2 blocks/CU (8 waves/CU)
 //   fixed long    : per-segment wave kernel, 2 blocks/CU (8 waves/CU, 4 KiB in flight each)
-//   ragged        : prefix-scan kernel, 8 rows/batch, 8 blocks/CU (occupancy-capped at 5 waves/SIMD)
+//   ragged        : prefix-scan kernel, 16-segment runs, 8 rows/batch, 2 blocks/CU
 // nt loads and the XCD-contiguous deal everywhere.
 static Plan resolve(const LaunchCfg& c, Path p) {
     Plan r;
     int bpc = c.blocks_per_cu;
-    if (bpc < 1 || bpc > 8)
-        bpc = (p == Path::kFixedLong || p == Path::kFixedShort) ? 2 : (p == Path::kRagged ? 8 : 8);
+    if (bpc < 1 || bpc > 8) bpc = p == Path::kBlock ? 8 : 2;
     r.max_blocks = (uint32_t)(c.cus * bpc);
     r.spw = (c.segs_per_wave == 1 || c.segs_per_wave == 2 || c.segs_per_wave == 4 || c.segs_per_wave == 8)
                 ? c.segs_per_wave : 4;
     r.rows = (c.rows == 4 || c.rows == 8 || c.rows == 16) ? c.rows : 8;
     r.xcd = c.xcd_map == 2 ? 0 : (c.xcd_map == 3 ? 2 : 1);
     r.nt = c.nontemporal != 2;
+    r.run = (c.run_segs >= 1 && c.run_segs <= (int)kScanRun) ? (uint32_t)c.run_segs : 16u;
     return r;
 }
 
@@ -1149,7 +1163,7 @@ static hipError_t launch_ragged_scan(const Plan& c, const uint8_t* base, const u
     constexpr uint64_t kChunk = 1ull << 27;
     for (uint64_t c0 = 0; c0 < n; c0 += kChunk) {
         const uint32_t cn = (uint32_t)(n - c0 < kChunk ? n - c0 : kChunk);
-        const uint64_t ntasks = (cn + kScanRun - 1) / kScanRun;
+        const uint64_t ntasks = (cn + c.run - 1) / c.run;
         const uint64_t want = (ntasks + kWavesPerBlock - 1) / kWavesPerBlock;
         const uint32_t grid = (uint32_t)(want < c.max_blocks ? want : c.max_blocks);
         const uint32_t* pc = partial ? partial + c0 : nullptr;
@@ -1159,10 +1173,10 @@ static hipError_t launch_ragged_scan(const Plan& c, const uint8_t* base, const u
         if (c.rows == R_) {                                                                                        \
             if (c.nt)                                                                                              \
                 hipLaunchKernelGGL((csum_ragged_scan_kernel<R_, true, VERIFY>), dim3(grid), dim3(kBlock), 0, st,   \
-                                   base, offsets + c0, cn, pc, oc, kc, c.xcd);                                     \
+                                   base, offsets + c0, cn, pc, oc, kc, c.xcd, c.run);                              \
             else                                                                                                   \
                 hipLaunchKernelGGL((csum_ragged_scan_kernel<R_, false, VERIFY>), dim3(grid), dim3(kBlock), 0, st,  \
-                                   base, offsets + c0, cn, pc, oc, kc, c.xcd);                                     \
+                                   base, offsets + c0, cn, pc, oc, kc, c.xcd, c.run);                              \
         }
         NSX_RSCAN(4) NSX_RSCAN(8) NSX_RSCAN(16)
 #undef NSX_RSCAN

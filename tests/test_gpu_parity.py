@@ -183,6 +183,7 @@ VARIANTS = ([dict(kernel=2, spw=s, nt=nt, xcd=x, bpc=b, rows=0) for s in (1, 2, 
 
 
 def set_variant(v, block_mode=0):
+    nsx.set_param(nsx.PARAM_RUN_SEGS, v.get("run", 0))
     nsx.set_param(nsx.PARAM_KERNEL, v["kernel"])
     nsx.set_param(nsx.PARAM_STREAM_ROWS, v["rows"])
     nsx.set_param(nsx.PARAM_SEGS_PER_WAVE, v["spw"])
@@ -214,6 +215,7 @@ def test_all_variants_bit_exact():
 RAGGED_VARIANTS = ([dict(kernel=k, rows=r, nt=nt, xcd=x, bpc=b, spw=0) for k in (3, 4) for r in (4, 8, 16)
                     for nt in (1, 2) for x in (1, 2, 3) for b in (8, 2)] +
                    [dict(kernel=1, rows=r, nt=1, xcd=1, bpc=4, spw=0) for r in (4, 8, 16)] +
+                   [dict(kernel=4, rows=8, nt=1, xcd=1, bpc=8, spw=0, run=rs) for rs in (1, 2, 7, 16, 33, 63)] +
                    [dict(kernel=2, rows=0, nt=1, xcd=x, bpc=4, spw=0) for x in (1, 3)])
 
 

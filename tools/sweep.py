@@ -31,8 +31,10 @@ def variants(kind):
         for xcd in (1, 3):
             out.append(dict(kernel=2, blocks_per_cu=bpc, segs_per_wave=spw, nontemporal=nt, xcd_map=xcd))
     if kind == "ragged":
-        for k, bpc, rows, xcd in itertools.product((3, 4), (8, 4, 2, 1), (4, 8, 16), (1, 3)):
-            out.append(dict(kernel=k, blocks_per_cu=bpc, stream_rows=rows, nontemporal=1, xcd_map=xcd))
+        for bpc, rows, run in itertools.product((8, 4, 2), (4, 8, 16), (4, 8, 16, 32, 63)):
+            out.append(dict(kernel=4, blocks_per_cu=bpc, stream_rows=rows, nontemporal=1, xcd_map=1, run_segs=run))
+        for bpc, rows in itertools.product((8, 4), (8, 16)):
+            out.append(dict(kernel=3, blocks_per_cu=bpc, stream_rows=rows, nontemporal=1, xcd_map=1))
     if kind == "fixed2":
         for bpc, spw, xcd in itertools.product((8, 4, 2, 1), (1, 2, 4, 8), (1, 3)):
             out.append(dict(kernel=3, blocks_per_cu=bpc, segs_per_wave=spw, nontemporal=1, xcd_map=xcd))
