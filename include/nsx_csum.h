@@ -98,6 +98,55 @@ int nsx_pseudo_ipv4_partial_dev(const uint8_t* d_src, const uint8_t* d_dst,
                                 const uint32_t* d_len, uint8_t proto, uint64_t n,
                                 uint32_t* d_partial, nsx_stream_t stream);
 
+/* Fused sender path: segment.bytes() + computeChecksum +
+ * field write in one GPU pass (transport/tcp/tcp.go:98-128, :68-71). For each
+ * segment i it writes the wire image — the 20-byte big-endian header built from
+ * the fields below (checksum field = ~raw), the option bytes
+ * d_opts[d_opt_off[i], d_opt_off[i+1]) followed by the reference's padding of
+ * `remainder` zero bytes (tcp.go:118-121), then the payload
+ * d_data[d_data_off[i], d_data_off[i+1]) — to d_out + d_out_off[i], where raw is
+ * the sum over prefix_i ‖ image with the field zero. d_out_off[i] must be a
+ * multiple of 4 and leave room for nsx_tcp_wire_len bytes; up to 3 bytes after
+ * each image are zero-filled (use nsx_tcp_layout_host). d_opt_off nullable (no
+ * options); data_bytes = size of the d_data buffer. d_raw (nullable) receives
+ * the raw sums. All nsx_tcp_hdr_soa members are device arrays of n entries;
+ * `offset` is the whole byte 12, as the reference stores it (tcp.go:106). */
+typedef struct {
+    const uint16_t* src_port;
+    const uint16_t* dst_port;
+    const uint32_t* seq_num;
+    const uint32_t* ack_num;
+    const uint8_t* offset;
+    const uint8_t* control;  /* ctl.byte() (tcp.go:192-203) */
+    const uint16_t* window;
+    const uint16_t* urgent_ptr;
+} nsx_tcp_hdr_soa;
+
+int nsx_tcp_build_dev(const nsx_tcp_hdr_soa* hdr, const uint8_t* d_opts, const uint64_t* d_opt_off,
+                      const uint8_t* d_data, const uint64_t* d_data_off, uint64_t data_bytes,
+                      const uint32_t* d_prefix_partial, uint64_t n, uint8_t* d_out, const uint64_t* d_out_off,
+                      uint16_t* d_raw, nsx_stream_t stream);
+
+/* Wire length of segment.bytes() with opt_len option bytes (tcp.go:98-128). */
+uint64_t nsx_tcp_wire_len(uint64_t opt_len, uint64_t data_len);
+
+/* 4-byte-aligned output offsets for nsx_tcp_build_dev (host arrays; h_opt_off
+ * nullable): h_out_off[i] = Σ_{j<i} round_up4(wire_len_j), h_out_off[n] = total. */
+int nsx_tcp_layout_host(const uint64_t* h_opt_off, const uint64_t* h_data_off, uint64_t n, uint64_t* h_out_off);
+
+/* IPv4 header checksums (RFC 791 §3.1; SURVEY.md §8 f3 — the reference has no
+ * IPv4 header codec, network/ip/v4/ipv4.go holds addresses only). Packet i's
+ * header starts at d_base + i*stride + hdr_off (any alignment) and is IHL*4
+ * bytes, IHL = low nibble of its first byte.
+ *   mode 0 (receive): d_out_raw[i] = raw sum over the header as it stands;
+ *          the header is valid iff it is 0xFFFF.
+ *   mode 1 (send):    d_out_raw[i] (nullable) = raw sum with bytes 10-11 taken
+ *          as zero, and ~raw is written big-endian into bytes 10-11 in place.
+ * A malformed header (IHL < 5, or hdr_off + IHL*4 > stride) yields 0 and is
+ * left untouched. */
+int nsx_ipv4_hdr_csum_dev(void* d_base, uint64_t stride, uint32_t hdr_off, uint64_t n, int mode,
+                          uint16_t* d_out_raw, nsx_stream_t stream);
+
 /* ----------------------------------------------------------------------------
  * Host-resident batches: pinned staging, H2D → kernel → D2H double-buffered
  * over two streams per GPU, segments sharded contiguously across num_gpus

@@ -191,6 +191,53 @@ int nsx_pseudo_ipv4_partial_dev(const uint8_t* d_src, const uint8_t* d_dst, cons
                                            static_cast<hipStream_t>(stream)));
 }
 
+uint64_t nsx_tcp_wire_len(uint64_t opt_len, uint64_t data_len) {
+    return 20u + opt_len + (opt_len ? (20u + opt_len) % 4u : 0u) + data_len;
+}
+
+int nsx_tcp_layout_host(const uint64_t* h_opt_off, const uint64_t* h_data_off, uint64_t n, uint64_t* h_out_off) {
+    if (!h_out_off || (n && !h_data_off)) return NSX_EINVAL;
+    uint64_t at = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        h_out_off[i] = at;
+        const uint64_t ol = h_opt_off ? h_opt_off[i + 1] - h_opt_off[i] : 0;
+        at += (nsx_tcp_wire_len(ol, h_data_off[i + 1] - h_data_off[i]) + 3) & ~3ull;
+    }
+    h_out_off[n] = at;
+    return NSX_OK;
+}
+
+int nsx_tcp_build_dev(const nsx_tcp_hdr_soa* hdr, const uint8_t* d_opts, const uint64_t* d_opt_off,
+                      const uint8_t* d_data, const uint64_t* d_data_off, uint64_t data_bytes,
+                      const uint32_t* d_prefix_partial, uint64_t n, uint8_t* d_out, const uint64_t* d_out_off,
+                      uint16_t* d_raw, nsx_stream_t stream) {
+    if (n == 0) return NSX_OK;
+    if (!hdr || !hdr->src_port || !hdr->dst_port || !hdr->seq_num || !hdr->ack_num || !hdr->offset ||
+        !hdr->control || !hdr->window || !hdr->urgent_ptr || !d_data_off || !d_out || !d_out_off ||
+        (d_opt_off && !d_opts) || (data_bytes && !d_data))
+        return NSX_EINVAL;
+    const int dev = current_device();
+    if (dev < 0) return NSX_ENODEV;
+    const DevInfo* di = dev_info(dev);
+    const nsx::TcpHdrSoA h{hdr->src_port, hdr->dst_port, hdr->seq_num, hdr->ack_num,
+                           hdr->offset,   hdr->control,  hdr->window,  hdr->urgent_ptr};
+    return map_err(nsx::launch_tcp_build(h, d_opts, d_opt_off, d_data, d_data_off, data_bytes, d_prefix_partial, n,
+                                         d_out, d_out_off, d_raw, (uint32_t)di->cus * 2,
+                                         static_cast<hipStream_t>(stream)));
+}
+
+int nsx_ipv4_hdr_csum_dev(void* d_base, uint64_t stride, uint32_t hdr_off, uint64_t n, int mode,
+                          uint16_t* d_out_raw, nsx_stream_t stream) {
+    if (n == 0) return NSX_OK;
+    if (!d_base || (mode != 0 && mode != 1) || (mode == 0 && !d_out_raw)) return NSX_EINVAL;
+    if (n > 1 && stride == 0) return NSX_EINVAL;
+    const int dev = current_device();
+    if (dev < 0) return NSX_ENODEV;
+    const DevInfo* di = dev_info(dev);
+    return map_err(nsx::launch_ipv4_hdr(static_cast<uint8_t*>(d_base), stride, hdr_off, n, mode, d_out_raw,
+                                        (uint32_t)di->cus * 8, static_cast<hipStream_t>(stream)));
+}
+
 int nsx_fill_splitmix64_dev(void* d_buf, uint64_t byte_off, uint64_t nbytes, uint64_t seed,
                             nsx_stream_t stream) {
     if (nbytes == 0) return NSX_OK;

@@ -35,6 +35,21 @@ hipError_t launch_ragged(const LaunchCfg& c, const void* d_base, const uint64_t*
                          const uint32_t* partial, uint16_t* out, uint8_t* ok, hipStream_t st);
 hipError_t launch_pseudo_ipv4(const uint8_t* src, const uint8_t* dst, const uint32_t* len, uint8_t proto,
                               uint64_t n, uint32_t* partial, uint32_t max_blocks, hipStream_t st);
+struct TcpHdrSoA {  // device arrays, one entry per segment (tcp.go:39-54 field order)
+    const uint16_t* src_port;
+    const uint16_t* dst_port;
+    const uint32_t* seq;
+    const uint32_t* ack;
+    const uint8_t* offset;
+    const uint8_t* ctl;
+    const uint16_t* window;
+    const uint16_t* urgent;
+};
+hipError_t launch_tcp_build(const TcpHdrSoA& h, const uint8_t* opts, const uint64_t* opt_off, const uint8_t* data,
+                            const uint64_t* data_off, uint64_t data_bytes, const uint32_t* partial, uint64_t n,
+                            uint8_t* out, const uint64_t* out_off, uint16_t* raw, uint32_t max_blocks, hipStream_t st);
+hipError_t launch_ipv4_hdr(uint8_t* base, uint64_t stride, uint32_t hdr_off, uint64_t n, int mode, uint16_t* out,
+                           uint32_t max_blocks, hipStream_t st);
 hipError_t launch_fill_splitmix64(void* d_buf, uint64_t byte_off, uint64_t nbytes, uint64_t seed,
                                   uint32_t max_blocks, hipStream_t st);
 

@@ -908,6 +908,149 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Fused sender path: segment.bytes() + computeChecksum +
+// field write in one pass (transport/tcp/tcp.go:98-128 and :68-71). One wave
+// per segment writes the wire image — 20-byte BE header from SoA fields,
+// options, the reference's `remainder` padding (tcp.go:118-121), payload — as
+// whole dwords at out + out_off[i] (4-aligned; up to 3 slack bytes after the
+// image are zero-filled), summing the dwords it writes (checksum field = 0),
+// then stores ~raw into bytes 16-17 with the last header dword. Payload bytes
+// at any source alignment are realigned with v_alignbyte_b32.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t bswap16u(uint32_t v) { return ((v & 0xFFu) << 8) | ((v >> 8) & 0xFFu); }
+__device__ __forceinline__ uint32_t bswap32u(uint32_t v) {
+    return (v >> 24) | ((v >> 8) & 0xFF00u) | ((v << 8) & 0xFF0000u) | (v << 24);
+}
+
+__global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const uint8_t* __restrict__ opts,
+                                                           const uint64_t* __restrict__ opt_off,
+                                                           const uint8_t* __restrict__ data,
+                                                           const uint64_t* __restrict__ data_off, uint64_t data_bytes,
+                                                           const uint32_t* __restrict__ partial, uint64_t n,
+                                                           uint8_t* __restrict__ out,
+                                                           const uint64_t* __restrict__ out_off,
+                                                           uint16_t* __restrict__ raw_out) {
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const uint64_t data_end4 = (data_bytes + 3) & ~3ull;  // last payload dword reads whole
+    const TaskIter it = task_iter(n, wave, 1);
+    for (uint64_t i = it.next; i < it.end; i += it.step) {
+        const uint32_t D0 = bswap16u(h.src_port[i]) | (bswap16u(h.dst_port[i]) << 16);
+        const uint32_t D1 = bswap32u(h.seq[i]), D2 = bswap32u(h.ack[i]);
+        const uint32_t D3 = (uint32_t)h.offset[i] | ((uint32_t)h.ctl[i] << 8) | (bswap16u(h.window[i]) << 16);
+        const uint32_t D4 = bswap16u(h.urgent[i]) << 16;  // checksum field (bytes 16-17) = 0 for the sum
+        const uint64_t ob = opt_off ? opt_off[i] : 0;
+        const uint32_t optlen = opt_off ? (uint32_t)(opt_off[i + 1] - ob) : 0u;
+        const uint32_t hdr_end = 20u + optlen + (optlen ? (20u + optlen) % 4u : 0u);
+        const uint64_t db = data_off[i];
+        const uint64_t dlen = data_off[i + 1] - db;
+        const uint64_t wire = hdr_end + dlen;
+        uint8_t* o = out + out_off[i];
+        const uint64_t nbytes4 = (wire + 3) & ~3ull;  // whole dwords this segment owns
+        // Payload descriptor based at the segment's first payload dword.
+        const uint64_t dbase = db & ~3ull;
+        const __amdgpu_buffer_rsrc_t drs = make_rsrc(data + dbase, data_end4 - dbase);
+        auto hdr_byte = [&](uint32_t pos) -> uint32_t {  // pos < 20
+            const uint32_t k = pos >> 2, sh = 8 * (pos & 3);
+            const uint32_t w = k == 0 ? D0 : k == 1 ? D1 : k == 2 ? D2 : k == 3 ? D3 : D4;
+            return (w >> sh) & 0xFFu;
+        };
+        uint32_t acc = 0;
+        for (uint64_t r0 = 0; r0 * kRow < nbytes4; ++r0) {
+            const uint64_t pos0 = r0 * kRow + lane * 16;
+            if (pos0 >= nbytes4) continue;
+            u32x4 x;
+            if (pos0 >= hdr_end && pos0 + 16 <= wire) {
+                // Payload fast path: 16 source bytes at any alignment.
+                const uint64_t s = (db & 3u) + (pos0 - hdr_end);  // relative to dbase (< 2^31)
+                const uint32_t a = (uint32_t)(s & ~3ull), sh = (uint32_t)(s & 3u);
+                typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+                const v4u w = __builtin_amdgcn_raw_buffer_load_b128(drs, a, 0, 2);
+                const uint32_t w4 = __builtin_amdgcn_raw_buffer_load_b32(drs, a + 16, 0, 2);
+                x.x = __builtin_amdgcn_alignbyte(w.y, w.x, sh);
+                x.y = __builtin_amdgcn_alignbyte(w.z, w.y, sh);
+                x.z = __builtin_amdgcn_alignbyte(w.w, w.z, sh);
+                x.w = __builtin_amdgcn_alignbyte(w4, w.w, sh);
+            } else {
+                // Header / options / padding / payload edges / slack: byte by byte.
+                uint32_t b[16];
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const uint64_t pos = pos0 + j;
+                    uint32_t v = 0;
+                    if (pos < 20) v = hdr_byte((uint32_t)pos);
+                    else if (pos < 20u + optlen) v = opts[ob + (pos - 20)];
+                    else if (pos >= hdr_end && pos < wire) v = data[db + (pos - hdr_end)];
+                    b[j] = v;
+                }
+                x.x = b[0] | b[1] << 8 | b[2] << 16 | b[3] << 24;
+                x.y = b[4] | b[5] << 8 | b[6] << 16 | b[7] << 24;
+                x.z = b[8] | b[9] << 8 | b[10] << 16 | b[11] << 24;
+                x.w = b[12] | b[13] << 8 | b[14] << 16 | b[15] << 24;
+            }
+            acc = sad4(x, acc);
+            uint32_t* od = reinterpret_cast<uint32_t*>(o + pos0);
+            const uint64_t left = nbytes4 - pos0;  // ≥ 4, multiple of 4
+            if (pos0 != 16 || r0 != 0) od[0] = x.x;  // dword 4 (bytes 16-19) is stored last
+            if (left > 4) od[1] = x.y;
+            if (left > 8) od[2] = x.z;
+            if (left > 12) od[3] = x.w;
+        }
+        const uint32_t tot = wave_sum(fold32(acc));
+        if (lane == 0) {
+            const uint32_t raw = finish(tot, true, partial ? partial[i] : 0u);  // o is 4-aligned (even)
+            *reinterpret_cast<uint32_t*>(o + 16) = D4 | bswap16u(~raw & 0xFFFFu);
+            if (raw_out) raw_out[i] = (uint16_t)raw;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// IPv4 header checksum (RFC 791 §3.1 with the RFC 1071 sum), one thread per
+// packet: headers are 20-60 bytes, too short for a wave each. Packet i's header
+// starts at base + i*stride + hdr_off (any alignment, e.g. 14 behind an
+// Ethernet header) and is IHL*4 bytes (IHL = low nibble of byte 0). The thread
+// loads the ≤ 16 aligned dwords covering it with all loads in flight, masks to
+// the header (and, in fill mode, the checksum field at bytes 10-11), and applies
+// the same LE-half-sum / byte-swap rule as the segment kernels.
+// mode 0: out = raw sum over the header as it stands (valid iff 0xFFFF).
+// mode 1: out = raw sum with bytes 10-11 taken as zero; writes ~raw there.
+// A malformed header (IHL < 5, or longer than the stride) gets out = 0 and is
+// not written.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void ipv4_hdr_kernel(uint8_t* __restrict__ base, uint64_t stride,
+                                                          uint32_t hdr_off, uint64_t n, int mode,
+                                                          uint16_t* __restrict__ out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint8_t* p = base + i * stride + hdr_off;
+        const uint32_t len = (uint32_t)(p[0] & 15u) * 4u;
+        const bool ok = len >= 20 && (stride == 0 || hdr_off + len <= stride);
+        const uint32_t head = (uint32_t)((uintptr_t)p & 3u);
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(p - head);
+        const uint32_t nd = ok ? (head + len + 3u) >> 2 : 0u;
+        uint32_t d[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) d[k] = (uint32_t)k < nd ? __builtin_nontemporal_load(w + k) : 0u;
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            // keep window bytes [head, head+len), minus the field in fill mode
+            uint32_t m = keep_mask((int32_t)head, (int32_t)(head + len), 4 * k);
+            if (mode == 1) m &= ~keep_mask((int32_t)head + 10, (int32_t)head + 12, 4 * k);
+            acc = __builtin_amdgcn_sad_u16(d[k] & m, 0u, acc);
+        }
+        const uint32_t raw = ok ? finish(acc, ((uintptr_t)p & 1u) == 0, 0u) : 0u;
+        if (out) out[i] = (uint16_t)raw;
+        if (mode == 1 && ok) {
+            const uint16_t f = (uint16_t)~raw;
+            p[10] = (uint8_t)(f >> 8);
+            p[11] = (uint8_t)f;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // IPv4 pseudo-header partials: src(4) dst(4) 0 proto len16 (RFC 9293 §3.1).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void pseudo_ipv4_kernel(const uint8_t* __restrict__ src,
@@ -1217,6 +1360,24 @@ hipError_t launch_pseudo_ipv4(const uint8_t* src, const uint8_t* dst, const uint
     const uint32_t grid = (uint32_t)(want < max_blocks ? want : max_blocks);
     hipLaunchKernelGGL(pseudo_ipv4_kernel, dim3(grid), dim3(kBlock), 0, st, src, dst, len, (uint32_t)proto, n,
                        partial);
+    return hipGetLastError();
+}
+
+hipError_t launch_tcp_build(const TcpHdrSoA& h, const uint8_t* opts, const uint64_t* opt_off, const uint8_t* data,
+                            const uint64_t* data_off, uint64_t data_bytes, const uint32_t* partial, uint64_t n,
+                            uint8_t* out, const uint64_t* out_off, uint16_t* raw, uint32_t max_blocks, hipStream_t st) {
+    const uint64_t want = (n + kWavesPerBlock - 1) / kWavesPerBlock;
+    const uint32_t grid = (uint32_t)(want < max_blocks ? want : max_blocks);
+    hipLaunchKernelGGL(tcp_build_kernel, dim3(grid), dim3(kBlock), 0, st, h, opts, opt_off, data, data_off, data_bytes,
+                       partial, n, out, out_off, raw);
+    return hipGetLastError();
+}
+
+hipError_t launch_ipv4_hdr(uint8_t* base, uint64_t stride, uint32_t hdr_off, uint64_t n, int mode, uint16_t* out,
+                           uint32_t max_blocks, hipStream_t st) {
+    const uint64_t want = (n + kBlock - 1) / kBlock;
+    const uint32_t grid = (uint32_t)(want < max_blocks ? want : max_blocks);
+    hipLaunchKernelGGL(ipv4_hdr_kernel, dim3(grid), dim3(kBlock), 0, st, base, stride, hdr_off, n, mode, out);
     return hipGetLastError();
 }
 

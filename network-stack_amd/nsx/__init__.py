@@ -56,6 +56,9 @@ def lib() -> ctypes.CDLL:
             "nsx_free_pinned": [vp],
             "nsx_shard_plan": [vp, u64, i32, vp],
             "nsx_fill_splitmix64_dev": [vp, u64, u64, u64, vp],
+            "nsx_ipv4_hdr_csum_dev": [vp, u64, u32, u64, i32, vp, vp],
+            "nsx_tcp_build_dev": [vp, vp, vp, vp, vp, u64, vp, u64, vp, vp, vp, vp],
+            "nsx_tcp_layout_host": [vp, vp, u64, vp],
             "nsx_abi_version": [],
             "nsx_device_count": [ctypes.POINTER(i32)],
             "nsx_set_param": [i32, ctypes.c_int64],
@@ -65,6 +68,8 @@ def lib() -> ctypes.CDLL:
             f = getattr(L, name)
             f.argtypes = args
             f.restype = ctypes.c_int
+        L.nsx_tcp_wire_len.argtypes = [u64, u64]
+        L.nsx_tcp_wire_len.restype = ctypes.c_uint64
         L.nsx_strerror.argtypes = [i32]
         L.nsx_strerror.restype = ctypes.c_char_p
         _lib = L
@@ -220,6 +225,46 @@ def pseudo_ipv4_partial_dev(src, dst, length, proto: int = 6, out=None, stream=N
         out = torch.empty(n, dtype=torch.int32, device=length.device)  # u32 bits
     _check(lib().nsx_pseudo_ipv4_partial_dev(_dev_ptr(src), _dev_ptr(dst), _dev_ptr(length), proto, n,
                                              _dev_ptr(out), _stream(stream)), "nsx_pseudo_ipv4_partial_dev")
+    return out
+
+
+def ipv4_hdr_csum_dev(buf, stride: int, n: int, hdr_off: int = 0, mode: int = 0, out=None, stream=None):
+    """RFC 791 header checksums of n packets at a fixed stride (mode 0 verify, 1 fill in place)."""
+    import torch
+    if out is None and mode == 0:
+        out = torch.empty(n, dtype=torch.int16, device=buf.device)  # u16 bits
+    _check(lib().nsx_ipv4_hdr_csum_dev(_dev_ptr(buf), stride, hdr_off, n, mode, _dev_ptr(out), _stream(stream)),
+           "nsx_ipv4_hdr_csum_dev")
+    return out
+
+
+class TcpHdrSoA(ctypes.Structure):
+    _fields_ = [(name, ctypes.c_void_p) for name in
+                ("src_port", "dst_port", "seq_num", "ack_num", "offset", "control", "window", "urgent_ptr")]
+
+
+def tcp_wire_len(opt_len: int, data_len: int) -> int:
+    return lib().nsx_tcp_wire_len(opt_len, data_len)
+
+
+def tcp_layout_host(data_off: np.ndarray, opt_off: np.ndarray | None = None) -> np.ndarray:
+    data_off = np.ascontiguousarray(data_off, np.uint64)
+    n = data_off.size - 1
+    out = np.zeros(n + 1, np.uint64)
+    oo = None if opt_off is None else np.ascontiguousarray(opt_off, np.uint64)
+    _check(lib().nsx_tcp_layout_host(_np_ptr(oo), _np_ptr(data_off), n, _np_ptr(out)), "nsx_tcp_layout_host")
+    return out
+
+
+def tcp_build_dev(fields: dict, data, data_off, out, out_off, opts=None, opt_off=None, partial=None, raw=None,
+                  stream=None):
+    """Fused segment.bytes() + checksum + field write (fields: dict of device tensors)."""
+    soa = TcpHdrSoA(*[fields[k].data_ptr() for k in
+                      ("src_port", "dst_port", "seq_num", "ack_num", "offset", "control", "window", "urgent_ptr")])
+    n = data_off.numel() - 1
+    _check(lib().nsx_tcp_build_dev(ctypes.byref(soa), _dev_ptr(opts), _dev_ptr(opt_off), _dev_ptr(data),
+                                   _dev_ptr(data_off), data.numel(), _dev_ptr(partial), n, _dev_ptr(out),
+                                   _dev_ptr(out_off), _dev_ptr(raw), _stream(stream)), "nsx_tcp_build_dev")
     return out
 
 

@@ -49,6 +49,10 @@ def kat() -> list:
         ("prefix_odd_shifts_pairing", "aa", "bbcc", 0xAABB + 0xCC00 - 0xFFFF, "odd prefix: segment pairs shift"),
         ("hello_with_ipv4_pseudo", O.ipv4_pseudo_header(bytes([10, 0, 0, 1]), bytes([10, 0, 0, 2]), 6, 25).hex(),
          (bytes(20) + b"hello").hex(), None, "IPv4 pseudo-header (RFC 9293 §3.1) + hello segment"),
+        ("ipv4_header_valid", "", "45000073000040004011b861c0a80001c0a800c7", 0xFFFF,
+         "IPv4 header with its checksum field b861 (RFC 791 §3.1; widely published example): re-sum 0xFFFF"),
+        ("ipv4_header_field_zeroed", "", "450000730000400040110000c0a80001c0a800c7", 0x479E,
+         "same header, field zeroed: raw 0x479e, field = ~raw = 0xb861"),
     ]
     out = []
     for name, p, s, expect, src in cases:

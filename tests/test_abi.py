@@ -148,6 +148,10 @@ def test_device_calls_fail_loudly_without_gpu():
     assert L.nsx_verify_ragged_dev(fake, fake, 4, None, fake, None, None) == nsx.NSX_ENODEV
     assert L.nsx_pseudo_ipv4_partial_dev(fake, fake, fake, 6, 4, fake, None) == nsx.NSX_ENODEV
     assert L.nsx_fill_splitmix64_dev(fake, 0, 16, 1, None) == nsx.NSX_ENODEV
+    assert L.nsx_ipv4_hdr_csum_dev(fake, 64, 0, 4, 0, fake, None) == nsx.NSX_ENODEV
+    soa = nsx.TcpHdrSoA(*([0x1000] * 8))
+    assert L.nsx_tcp_build_dev(ctypes.byref(soa), None, None, fake, fake, 16, None, 4, fake, fake, None,
+                               None) == nsx.NSX_ENODEV
     buf = np.zeros(3000, np.uint8)
     with pytest.raises(nsx.NsxError) as e:
         nsx.fixed_host(buf, 1500, 1500, 2)
@@ -197,3 +201,26 @@ int main(void) {
                            "-L", libdir, "-lnsx_csum", f"-Wl,-rpath,{libdir}", "-o", str(exe)])
     out = subprocess.run([str(exe)], capture_output=True, text=True)
     assert out.returncode == 0 and out.stdout.split() == ["43d2", "ffff", "1"]
+
+
+def test_tcp_wire_len_and_layout_match_reference_bytes():
+    """nsx_tcp_wire_len / nsx_tcp_layout_host agree with len(segment.bytes()) (tcp.go:98-128)."""
+    rng = np.random.default_rng(21)
+    opt_sets = [[], [O.Option(kind=1)], [O.Option(kind=2, length=4, data=b"\x05\xb4\0\0")],
+                [O.Option(kind=1), O.Option(kind=1), O.Option(kind=0)],
+                [O.Option(kind=2, length=4, data=b"abcd"), O.Option(kind=1)]]
+    segs = []
+    for i in range(200):
+        opts = opt_sets[i % len(opt_sets)]
+        segs.append(O.Segment(options=opts, data=bytes(int(rng.integers(0, 300)))))
+    for s in segs:
+        ol = sum(len(o.bytes()) for o in s.options)
+        assert nsx.tcp_wire_len(ol, len(s.data)) == len(s.bytes())
+    opt_off = np.zeros(len(segs) + 1, np.uint64)
+    opt_off[1:] = np.cumsum([sum(len(o.bytes()) for o in s.options) for s in segs])
+    data_off = np.zeros(len(segs) + 1, np.uint64)
+    data_off[1:] = np.cumsum([len(s.data) for s in segs])
+    out_off = nsx.tcp_layout_host(data_off, opt_off)
+    want = np.zeros(len(segs) + 1, np.uint64)
+    want[1:] = np.cumsum([(len(s.bytes()) + 3) & ~3 for s in segs])
+    assert np.array_equal(out_off, want)

@@ -364,3 +364,111 @@ def test_config4_256K_x_64KiB_sampled_and_roundtrip():
     v[:, 17] = (fld & 0xFF).to(torch.uint8)
     ok = u16(nsx.fixed_dev(t, L, L, n, out=torch.empty(n, dtype=torch.int16, device="cuda")))
     assert (ok == 0xFFFF).all()
+
+
+# ------------------------------------------------------------------ IPv4 header checksum
+
+def _ipv4_headers(rng, n, stride, hdr_off):
+    buf = rng.integers(0, 256, n * stride + 8, dtype=np.uint8)
+    ihl = rng.integers(5, 16, n)
+    ihl[::97] = rng.integers(0, 5, len(ihl[::97]))  # some malformed
+    for i in range(n):
+        b0 = i * stride + hdr_off
+        buf[b0] = 0x40 | int(ihl[i])
+    return buf, ihl
+
+
+@pytest.mark.parametrize("stride,hdr_off", [(64, 0), (61, 1), (1514, 14), (1500, 0), (60, 0)])
+def test_ipv4_header_checksum_verify_and_fill(stride, hdr_off):
+    rng = np.random.default_rng(stride * 31 + hdr_off)
+    n = 3000
+    buf, ihl = _ipv4_headers(rng, n, stride, hdr_off)
+    d = dev(buf)
+    raw = u16(nsx.ipv4_hdr_csum_dev(d, stride, n, hdr_off=hdr_off, mode=0))
+    for i in range(n):
+        L = int(ihl[i]) * 4
+        ok = L >= 20 and hdr_off + L <= stride
+        h = buf[i * stride + hdr_off:i * stride + hdr_off + L].tobytes()
+        assert raw[i] == (O.go_checksum(b"", h) if ok else 0), i
+    # fill mode: field written in place, then every valid header verifies
+    out = torch.empty(n, dtype=torch.int16, device="cuda")
+    nsx.ipv4_hdr_csum_dev(d, stride, n, hdr_off=hdr_off, mode=1, out=out)
+    filled = host(d)
+    raw_fill = u16(out)
+    for i in range(0, n, 7):
+        L = int(ihl[i]) * 4
+        b0 = i * stride + hdr_off
+        if L >= 20 and hdr_off + L <= stride:
+            h = bytearray(buf[b0:b0 + L].tobytes())
+            h[10:12] = b"\0\0"
+            assert raw_fill[i] == O.go_checksum(b"", bytes(h))
+            assert (int(filled[b0 + 10]) << 8 | int(filled[b0 + 11])) == (~raw_fill[i]) & 0xFFFF
+        else:
+            assert np.array_equal(filled[b0:b0 + 12], buf[b0:b0 + 12])  # malformed: untouched
+    again = u16(nsx.ipv4_hdr_csum_dev(d, stride, n, hdr_off=hdr_off, mode=0))
+    valid = np.array([int(ihl[i]) * 4 >= 20 and hdr_off + int(ihl[i]) * 4 <= stride for i in range(n)])
+    assert (again[valid] == 0xFFFF).all()
+
+
+def test_ipv4_header_kat():
+    h = np.frombuffer(bytes.fromhex("450000730000400040110000c0a80001c0a800c7"), np.uint8).copy()
+    d = dev(h)
+    out = torch.empty(1, dtype=torch.int16, device="cuda")
+    nsx.ipv4_hdr_csum_dev(d, 20, 1, mode=1, out=out)
+    assert u16(out)[0] == 0x479E
+    assert host(d)[10:12].tobytes() == bytes.fromhex("b861")
+    assert u16(nsx.ipv4_hdr_csum_dev(d, 20, 1, mode=0))[0] == 0xFFFF
+
+
+# ------------------------------------------------------------------ fused serialize + checksum
+
+def test_tcp_build_matches_reference_bytes_and_checksum():
+    rng = np.random.default_rng(77)
+    n = 3000
+    opt_sets = [[], [O.Option(kind=1)], [O.Option(kind=2, length=4, data=b"\x05\xb4\0\0")],
+                [O.Option(kind=1), O.Option(kind=1), O.Option(kind=0)],
+                [O.Option(kind=2, length=4, data=b"wxyz"), O.Option(kind=1)], [O.Option(kind=1)] * 3]
+    segs, pseudos = [], []
+    for i in range(n):
+        L = int(rng.integers(0, 3000)) if i % 10 else int(rng.integers(0, 8))
+        s = O.Segment(src_port=int(rng.integers(1 << 16)), dst_port=int(rng.integers(1 << 16)),
+                      seq_num=int(rng.integers(1 << 32)), ack_num=int(rng.integers(1 << 32)),
+                      control=O.Ctl.from_byte(int(rng.integers(256))), window=int(rng.integers(1 << 16)),
+                      urgent_ptr=int(rng.integers(1 << 16)), options=list(opt_sets[i % len(opt_sets)]),
+                      data=rng.integers(0, 256, L, dtype=np.uint8).tobytes())
+        s.offset = s.compute_offset()
+        segs.append(s)
+        pseudos.append(O.ipv4_pseudo_header(rng.integers(0, 256, 4, dtype=np.uint8).tobytes(),
+                                            rng.integers(0, 256, 4, dtype=np.uint8).tobytes(), 6,
+                                            len(s.bytes())))
+    # payloads densely packed behind a 1-byte lead (odd source alignment)
+    data = b"\x99" + b"".join(s.data for s in segs)
+    data_off = np.zeros(n + 1, np.uint64)
+    data_off[1:] = np.cumsum([len(s.data) for s in segs])
+    data_off += np.uint64(1)
+    opts = b"".join(o.bytes() for s in segs for o in s.options) or b"\0"
+    opt_off = np.zeros(n + 1, np.uint64)
+    opt_off[1:] = np.cumsum([sum(len(o.bytes()) for o in s.options) for s in segs])
+    out_off = nsx.tcp_layout_host(data_off - np.uint64(1), opt_off)
+    u = lambda a, dt: dev(np.asarray(a, dt).view({np.uint16: np.int16, np.uint32: np.int32, np.uint8: np.uint8}[dt]))
+    fields = {"src_port": u([s.src_port for s in segs], np.uint16), "dst_port": u([s.dst_port for s in segs], np.uint16),
+              "seq_num": u([s.seq_num for s in segs], np.uint32), "ack_num": u([s.ack_num for s in segs], np.uint32),
+              "offset": u([s.offset for s in segs], np.uint8), "control": u([s.control.byte() for s in segs], np.uint8),
+              "window": u([s.window for s in segs], np.uint16), "urgent_ptr": u([s.urgent_ptr for s in segs], np.uint16)}
+    part = np.array([O.be_word_sum(p) for p in pseudos], np.uint32)
+    out = torch.full((int(out_off[-1]),), 0xAB, dtype=torch.uint8, device="cuda")
+    raw = torch.empty(n, dtype=torch.int16, device="cuda")
+    nsx.tcp_build_dev(fields, dev(np.frombuffer(data, np.uint8)), dev(data_off.view(np.int64)), out,
+                      dev(out_off.view(np.int64)), opts=dev(np.frombuffer(opts, np.uint8)),
+                      opt_off=dev(opt_off.view(np.int64)), partial=dev(part.view(np.int32)), raw=raw)
+    got, raw_h = host(out), u16(raw)
+    for i, s in enumerate(segs):
+        s.checksum = 0
+        r = s.compute_checksum(pseudos[i])
+        assert raw_h[i] == r, i
+        s.checksum = O.field_value(r)
+        wire = s.bytes()
+        o = int(out_off[i])
+        assert got[o:o + len(wire)].tobytes() == wire, i
+        assert not got[o + len(wire):int(out_off[i + 1])].any()   # slack zero-filled
+        assert O.verify(O.go_checksum(pseudos[i], wire))          # receiver accepts (tcp.go:70)
