@@ -1,0 +1,82 @@
+"""f4: the loopback transport feeding checksum batches.
+tests/cpp/test_pipe.cpp mirrors the reference's transport conformance suite
+(transport/test/conn.go) against nsx/pipe.hpp (a restatement of
+transport/pipe/pipe.go); the config-1 harness (network-stack_amd/tools/
+loopback.cpp) sends 64 x 1500 B TCP segments through it and verifies every
+checksum on arrival — per segment on the host (CPU) or as one GPU batch (gpu)."""
+import json
+import os
+import subprocess
+
+import pytest
+
+import nsx
+from conftest import ROOT
+
+INC = os.path.join(ROOT, "network-stack_amd", "include")
+LOOPBACK = os.path.join(ROOT, "network-stack_amd", "build", "nsx_loopback")
+
+
+def _build_pipe_test(tmp_path, extra=()):
+    exe = tmp_path / "test_pipe"
+    subprocess.check_call(["g++", "-std=c++17", "-O1", "-Wall", "-Wextra", "-Werror", "-pthread", *extra,
+                           os.path.join(ROOT, "tests", "cpp", "test_pipe.cpp"), "-I", INC, "-o", str(exe)])
+    return exe
+
+
+def test_pipe_conformance(tmp_path):
+    out = subprocess.run([str(_build_pipe_test(tmp_path))], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.startswith("pipe: 12 tests")
+
+
+def test_pipe_conformance_tsan(tmp_path):
+    """The race tests (conn.go TestWriteRace/TestReadRace) under ThreadSanitizer."""
+    try:
+        exe = _build_pipe_test(tmp_path, ("-fsanitize=thread",))
+    except subprocess.CalledProcessError:
+        pytest.skip("ThreadSanitizer unavailable")
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0 and "WARNING: ThreadSanitizer" not in out.stderr, out.stderr
+
+
+def _loopback(*args):
+    if not os.path.exists(LOOPBACK):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "network-stack_amd")])
+    out = subprocess.run([LOOPBACK, *args], capture_output=True, text=True, timeout=300)
+    return out.returncode, json.loads(out.stdout.strip().splitlines()[-1])
+
+
+def test_loopback_config1_host_verifies_every_segment():
+    rc, r = _loopback("--mode", "host", "--reps", "20")
+    assert rc == 0 and r["bad"] == 0 and r["reps"] == 20
+
+
+def test_loopback_detects_corruption_host():
+    rc, r = _loopback("--mode", "host", "--reps", "3", "--corrupt", "17")
+    assert rc == 0 and r["bad"] == 3
+
+
+def test_loopback_odd_lengths_host():
+    for L in ("20", "21", "1501", "9001"):
+        rc, r = _loopback("--mode", "host", "--reps", "2", "--seg-len", L, "--segments", "9")
+        assert rc == 0 and r["bad"] == 0, L
+
+
+def test_loopback_batch_refuses_without_gpu():
+    if nsx.device_count() > 0:
+        pytest.skip("GPU present")
+    rc, r = _loopback("--mode", "batch", "--reps", "1")
+    assert rc == 1 and "error" in r
+
+
+@pytest.mark.gpu
+def test_loopback_config1_gpu_batch():
+    rc, r = _loopback("--mode", "batch", "--reps", "50")
+    assert rc == 0 and r["bad"] == 0
+    rc, r = _loopback("--mode", "batch", "--reps", "3", "--corrupt", "63")
+    assert rc == 0 and r["bad"] == 3
+    for L in ("21", "1501", "9001"):
+        rc, r = _loopback("--mode", "batch", "--reps", "2", "--seg-len", L, "--segments", "9")
+        assert rc == 0 and r["bad"] == 0, L
+
