@@ -7,6 +7,11 @@
 //   --mode host   per-segment nsx_csum16 on arrival (computeChecksum's path)
 //   --mode batch  frames land in pinned memory; one nsx_csum_fixed_host call
 //                 (GPU) verifies the whole batch — the transport feeding batches.
+//   --mode ring-host / ring-gpu
+//                 buffered pipe (transport/pipe/buffered.go) whose receive
+//                 buffer is the batch (pinned for ring-gpu); the receiver
+//                 verifies the frames in place — per segment on the host, or
+//                 one GPU batch straight from the pipe's buffer (no copy).
 // Prints one JSON line.
 #include <chrono>
 #include <cstdio>
@@ -29,10 +34,10 @@ int main(int argc, char** argv) {
         else if (k == "--seg-len") seg_len = std::atoi(argv[i + 1]);
         else if (k == "--reps") reps = std::atoi(argv[i + 1]);
         else if (k == "--mode") mode = argv[i + 1];
-        else if (k == "--corrupt") corrupt = std::atoi(argv[i + 1]);  // flip a bit of segment K in transit
+        else if (k == "--corrupt") corrupt = std::atoi(argv[i + 1]);  // flip a bit of segment K
     }
-    if (seg_len < 20 || corrupt >= nseg || nseg < 1 || reps < 1 || (mode != "host" && mode != "batch")) {
-        std::fprintf(stderr, "usage: nsx_loopback [--segments N] [--seg-len L>=20] [--reps R] [--mode host|batch]\n");
+    if (seg_len < 20 || corrupt >= nseg || nseg < 1 || reps < 1 || (mode != "host" && mode != "batch" && mode != "ring-host" && mode != "ring-gpu")) {
+        std::fprintf(stderr, "usage: nsx_loopback [--segments N] [--seg-len L>=20] [--reps R] [--mode host|batch|ring-host|ring-gpu] [--corrupt K]\n");
         return 2;
     }
     // Build the segments once (sender side of tcp.go: field zero, sum, store ~sum).
@@ -56,55 +61,81 @@ int main(int argc, char** argv) {
         s.checksum = nsx_field(s.compute_checksum(pseudo[i]));
         wire[i] = s.bytes();
     }
-    uint8_t* frames = nullptr;
-    if (mode == "batch") {
+    if (corrupt >= 0) wire[corrupt][seg_len / 2] ^= 0x10;  // damaged in transit: the receiver must notice
+    const size_t batch = (size_t)nseg * seg_len;
+    const bool gpu = mode == "batch" || mode == "ring-gpu";
+    uint8_t* pinned = nullptr;
+    if (gpu) {
         void* p = nullptr;
-        const int rc = nsx_alloc_pinned((size_t)nseg * seg_len, &p);
+        const int rc = nsx_alloc_pinned(batch, &p);
         if (rc != NSX_OK) {
             std::printf("{\"error\": \"%s\"}\n", nsx_strerror(rc));
             return 1;
         }
-        frames = static_cast<uint8_t*>(p);
+        pinned = static_cast<uint8_t*>(p);
     }
     std::vector<uint8_t> frame(seg_len);
     std::vector<uint16_t> raw(nseg);
     long bad = 0;
-    double best = 1e30, total = 0;
-    for (int r = 0; r < reps; ++r) {
-        auto ends = nsx::pipe::make_pipe("client", "server");
-        nsx::pipe::End& c1 = ends.first;
-        nsx::pipe::End& c2 = ends.second;
-        const auto t0 = std::chrono::steady_clock::now();
-        std::thread writer([&] {
-            for (int i = 0; i < nseg; ++i) {
-                size_t n = 0;
-                if (c1.write(wire[i].data(), wire[i].size(), &n) != nsx::pipe::Err::kOk) return;
-            }
-        });
+    int rc = NSX_OK;
+    auto host_verify = [&](int i, const uint8_t* seg) {
+        uint16_t sum = 0;
+        nsx_csum16(pseudo[i].data(), pseudo[i].size(), seg, seg_len, &sum);
+        bad += !nsx_verify(sum);
+    };
+    auto gpu_verify = [&](const uint8_t* frames) {  // one batch call; raw sums come back per segment
+        rc = nsx_csum_fixed_host(frames, seg_len, seg_len, nseg, partial.data(), raw.data(), 1);
+        for (int i = 0; i < nseg && rc == NSX_OK; ++i) bad += !nsx_verify(raw[i]);
+    };
+    auto send_all = [&](auto& c1) {
         for (int i = 0; i < nseg; ++i) {
-            uint8_t* dst = frames ? frames + (size_t)i * seg_len : frame.data();
-            if (c2.read_full(dst, seg_len) != nsx::pipe::Err::kOk) { ++bad; break; }
-            if (i == corrupt) dst[seg_len / 2] ^= 0x10;
-            if (!frames) {
-                uint16_t sum = 0;
-                nsx_csum16(pseudo[i].data(), pseudo[i].size(), dst, seg_len, &sum);
-                if (!nsx_verify(sum)) ++bad;
-            }
+            size_t n = 0;
+            if (c1.write(wire[i].data(), wire[i].size(), &n) != nsx::pipe::Err::kOk) return;
         }
-        if (frames) {
-            const int rc = nsx_csum_fixed_host(frames, seg_len, seg_len, nseg, partial.data(), raw.data(), 1);
-            if (rc != NSX_OK) {
-                std::printf("{\"error\": \"%s\"}\n", nsx_strerror(rc));
-                return 1;
+    };
+    double best = 1e30, total = 0;
+    for (int r = 0; r < reps && rc == NSX_OK; ++r) {
+        auto t0 = std::chrono::steady_clock::now();
+        if (mode == "host" || mode == "batch") {
+            // unbuffered rendezvous pipe (pipe.go): frame with read_full
+            auto ends = nsx::pipe::make_pipe("client", "server");
+            t0 = std::chrono::steady_clock::now();
+            std::thread writer([&] { send_all(ends.first); });
+            for (int i = 0; i < nseg; ++i) {
+                uint8_t* dst = pinned ? pinned + (size_t)i * seg_len : frame.data();
+                if (ends.second.read_full(dst, seg_len) != nsx::pipe::Err::kOk) { ++bad; break; }
+                if (!pinned) host_verify(i, dst);
             }
-            for (int i = 0; i < nseg; ++i) bad += !nsx_verify(raw[i]);
+            if (pinned) gpu_verify(pinned);
+            writer.join();
+        } else {
+            // buffered pipe (buffered.go) whose receive buffer holds one batch;
+            // the receiver verifies the frames in place (peek/consume, no copy)
+            auto ends = nsx::pipe::make_buffered_pipe("client", "server", batch, nullptr, pinned);
+            t0 = std::chrono::steady_clock::now();
+            std::thread writer([&] { send_all(ends.first); });
+            const uint8_t* view = nullptr;
+            size_t avail = 0;
+            if (ends.second.peek(batch, &view, &avail) != nsx::pipe::Err::kOk || avail != batch) {
+                ++bad;
+            } else if (pinned) {
+                gpu_verify(view);
+            } else {
+                for (int i = 0; i < nseg; ++i) host_verify(i, view + (size_t)i * seg_len);
+            }
+            ends.second.consume(avail);
+            writer.join();
         }
-        writer.join();
         const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         best = dt < best ? dt : best;
         total += dt;
     }
-    if (frames) nsx_free_pinned(frames);
+    if (rc != NSX_OK) {
+        std::printf("{\"error\": \"%s\"}\n", nsx_strerror(rc));
+        if (pinned) nsx_free_pinned(pinned);
+        return 1;
+    }
+    if (pinned) nsx_free_pinned(pinned);
     const double bytes = (double)nseg * seg_len;
     std::printf("{\"config\": \"config1: %d x %dB TCP segments over nsx::pipe loopback\", \"mode\": \"%s\", "
                 "\"reps\": %d, \"bad\": %ld, \"corrupt\": %d, \"best_us_per_batch\": %.2f, \"mean_us_per_batch\": %.2f, "

@@ -1,7 +1,8 @@
 // C++ mirror of the reference's transport conformance suite
-// (transport/test/conn.go: ConnTestSuite) run against nsx::pipe, which restates
-// transport/pipe/pipe.go. Each test names the Go test it follows. A watchdog
-// fails the run if any test blocks for more than a second (conn.go:23-33).
+// (transport/test/conn.go: ConnTestSuite, buffered_conn.go: BufferedConnTestSuite)
+// run against nsx::pipe, which restates transport/pipe/pipe.go and buffered.go.
+// Each test names the Go test it follows. A watchdog fails the run if any test
+// blocks for more than a second (conn.go:23-33).
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -46,7 +47,8 @@ struct Watchdog {  // SetupTest's one-second timer
     ~Watchdog() { done = true; t.join(); }
 };
 
-static void TestReadWrite(End& c1, End& c2) {  // conn.go:41-68: partial reads
+template <class E>
+static void TestReadWrite(E& c1, E& c2) {  // conn.go:41-68: partial reads
     const auto data = bytes_of("Hello, World!");
     std::thread w([&] {
         size_t n = 0;
@@ -62,7 +64,8 @@ static void TestReadWrite(End& c1, End& c2) {  // conn.go:41-68: partial reads
     w.join();
 }
 
-static void TestWriteRace(End& c1, End& c2) {  // conn.go:70-107: writes never interleave
+template <class E>
+static void TestWriteRace(E& c1, E& c2) {  // conn.go:70-107: writes never interleave
     const auto data = bytes_of("ABCD");
     const int N = 10;
     std::vector<std::thread> ws;
@@ -85,7 +88,8 @@ static void TestWriteRace(End& c1, End& c2) {  // conn.go:70-107: writes never i
     CHECK(result == want);
 }
 
-static void TestReadRace(End& c1, End& c2) {  // conn.go:109-149
+template <class E>
+static void TestReadRace(E& c1, E& c2) {  // conn.go:109-149
     const auto data = bytes_of("ABCD");
     const int N = 10;
     std::thread w([&] {
@@ -114,7 +118,8 @@ static void TestReadRace(End& c1, End& c2) {  // conn.go:109-149
     CHECK(result == want);
 }
 
-static void try_read_write(End& c) {
+template <class E>
+static void try_read_write(E& c) {
     uint8_t buf[10] = {0};
     size_t n = 7;
     CHECK(c.read(buf, sizeof buf, &n) == Err::kClosed);
@@ -124,14 +129,16 @@ static void try_read_write(End& c) {
     CHECK(n == 0);
 }
 
-static void TestClose(End& c1, End& c2) {  // conn.go:151-184: both ends see ErrConnClosed
+template <class E>
+static void TestClose(E& c1, E& c2) {  // conn.go:151-184: both ends see ErrConnClosed
     CHECK(c1.close() == Err::kOk);
     CHECK(c1.close() == Err::kOk);  // once.Do: idempotent
     try_read_write(c1);
     try_read_write(c2);
 }
 
-static void TestReadBeforeClose(End& c1, End&) {  // conn.go:186-200: Close wakes a blocked Read
+template <class E>
+static void TestReadBeforeClose(E& c1, E&) {  // conn.go:186-200: Close wakes a blocked Read
     std::thread r([&] {
         size_t n = 0;
         CHECK(c1.read(nullptr, 0, &n) == Err::kClosed);
@@ -141,7 +148,8 @@ static void TestReadBeforeClose(End& c1, End&) {  // conn.go:186-200: Close wake
     r.join();
 }
 
-static void TestWriteBeforeClose(End& c1, End&) {  // conn.go:202-220: Close wakes a blocked Write
+template <class E>
+static void TestWriteBeforeClose(E& c1, E&) {  // conn.go:202-220: Close wakes a blocked Write
     const auto in = bytes_of("hey");
     std::thread w([&] {
         size_t n = 0;
@@ -152,7 +160,8 @@ static void TestWriteBeforeClose(End& c1, End&) {  // conn.go:202-220: Close wak
     w.join();
 }
 
-static void TestReadDeadLine(End& c1, End& c2) {  // conn.go:222-253
+template <class E>
+static void TestReadDeadLine(E& c1, E& c2) {  // conn.go:222-253
     c1.set_read_deadline(Clock::now() - std::chrono::seconds(1));
     uint8_t b[1];
     size_t n = 9;
@@ -169,7 +178,8 @@ static void TestReadDeadLine(End& c1, End& c2) {  // conn.go:222-253
     w.join();
 }
 
-static void TestWriteDeadLine(End& c1, End&) {  // conn.go:255-279
+template <class E>
+static void TestWriteDeadLine(E& c1, E&) {  // conn.go:255-279
     c1.set_write_deadline(Clock::now() - std::chrono::seconds(1));
     const uint8_t a = 'a';
     size_t n = 9;
@@ -177,7 +187,8 @@ static void TestWriteDeadLine(End& c1, End&) {  // conn.go:255-279
     CHECK(n == 0);
 }
 
-static void TestDeadLineWakesBlockedRead(End& c1, End&) {  // chanDeadLine firing mid-Read
+template <class E>
+static void TestDeadLineWakesBlockedRead(E& c1, E&) {  // chanDeadLine firing mid-Read
     c1.set_read_deadline(Clock::now() + std::chrono::milliseconds(30));
     uint8_t b[1];
     size_t n = 0;
@@ -186,18 +197,21 @@ static void TestDeadLineWakesBlockedRead(End& c1, End&) {  // chanDeadLine firin
     CHECK(Clock::now() - t0 >= std::chrono::milliseconds(25));
 }
 
-static void TestAddr(End& c1, End& c2) {  // conn.go:281-287
+template <class E>
+static void TestAddr(E& c1, E& c2) {  // conn.go:281-287
     CHECK(c1.local_addr() == c2.remote_addr());
     CHECK(c2.local_addr() == c1.remote_addr());
     CHECK(c1.local_addr() == "c1" && c2.local_addr() == "c2");
 }
 
-static void TestEmptyWrite(End& c1, End&) {  // pipe.go:97-99
+template <class E>
+static void TestEmptyWrite(E& c1, E&) {  // pipe.go:97-99
     size_t n = 5;
     CHECK(c1.write(nullptr, 0, &n) == Err::kOk && n == 0);
 }
 
-static void TestFramedStream(End& c1, End& c2) {  // read_full framing over many small reads
+template <class E>
+static void TestFramedStream(E& c1, E& c2) {  // read_full framing over many small reads
     std::vector<uint8_t> big(1 << 16);
     for (size_t i = 0; i < big.size(); ++i) big[i] = (uint8_t)(i * 131 + 7);
     std::thread w([&] {
@@ -215,33 +229,146 @@ static void TestFramedStream(End& c1, End& c2) {  // read_full framing over many
     CHECK(got == big);
 }
 
-int main() {
-    struct T {
-        const char* name;
-        void (*fn)(End&, End&);
-    } tests[] = {{"TestReadWrite", TestReadWrite},
-                 {"TestWriteRace", TestWriteRace},
-                 {"TestReadRace", TestReadRace},
-                 {"TestClose", TestClose},
-                 {"TestReadBeforeClose", TestReadBeforeClose},
-                 {"TestWriteBeforeClose", TestWriteBeforeClose},
-                 {"TestReadDeadLine", TestReadDeadLine},
-                 {"TestWriteDeadLine", TestWriteDeadLine},
-                 {"TestDeadLineWakesBlockedRead", TestDeadLineWakesBlockedRead},
-                 {"TestAddr", TestAddr},
-                 {"TestEmptyWrite", TestEmptyWrite},
-                 {"TestFramedStream", TestFramedStream}};
+// --- transport/test/buffered_conn.go (BufferedConnTestSuite) ---------------
+static void TestBothWrite(nsx::pipe::BufferedEnd& c1, nsx::pipe::BufferedEnd& c2) {  // buffered_conn.go:23-61
+    const size_t size1 = c1.read_buf_size(), size2 = c2.read_buf_size();
+    CHECK(c1.write_buf_size() == size2);
+    std::thread a([&] {
+        std::vector<uint8_t> b(size2, 1);
+        size_t n = 0;
+        CHECK(c1.write(b.data(), b.size(), &n) == Err::kOk && n == size2);
+        CHECK(c2.read(b.data(), b.size(), &n) == Err::kOk && n == size2);
+    });
+    std::thread b([&] {
+        std::vector<uint8_t> v(size1, 2);
+        size_t n = 0;
+        CHECK(c2.write(v.data(), v.size(), &n) == Err::kOk && n == size1);
+        CHECK(c1.read(v.data(), v.size(), &n) == Err::kOk && n == size1);
+    });
+    a.join();
+    b.join();
+}
+
+static void TestReadAfterClose(nsx::pipe::BufferedEnd& c1, nsx::pipe::BufferedEnd& c2) {  // buffered_conn.go:63-84
+    const size_t size1 = c1.read_buf_size();
+    std::vector<uint8_t> b(size1, 7);
+    size_t n = 0;
+    CHECK(c2.write(b.data(), size1, &n) == Err::kOk && n == size1);
+    CHECK(c2.close() == Err::kOk);
+    CHECK(c1.read(b.data(), size1, &n) == Err::kOk && n == size1);
+    n = 9;
+    CHECK(c1.read(b.data(), 1, &n) == Err::kClosed && n == 0);
+}
+
+static void TestWriteBlocksWhenFull(nsx::pipe::BufferedEnd& c1, nsx::pipe::BufferedEnd& c2) {
+    // a write larger than the buffer completes only as the reader drains it
+    std::vector<uint8_t> big(5 * c2.read_buf_size() + 3);
+    for (size_t i = 0; i < big.size(); ++i) big[i] = (uint8_t)(i * 29 + 1);
+    std::thread w([&] {
+        size_t n = 0;
+        CHECK(c1.write(big.data(), big.size(), &n) == Err::kOk && n == big.size());
+    });
+    std::vector<uint8_t> got(big.size());
+    CHECK(c2.read_full(got.data(), got.size()) == Err::kOk);
+    w.join();
+    CHECK(got == big);
+}
+
+static void TestPeekConsume(nsx::pipe::BufferedEnd& c1, nsx::pipe::BufferedEnd& c2) {
+    // zero-copy frames: the view is stable while writers keep appending
+    const size_t cap = c2.read_buf_size(), frame = 6;
+    std::vector<uint8_t> src(40 * frame);
+    for (size_t i = 0; i < src.size(); ++i) src[i] = (uint8_t)(i * 7 + 3);
+    std::thread w([&] {
+        for (size_t off = 0; off < src.size(); off += frame) {
+            size_t n = 0;
+            CHECK(c1.write(src.data() + off, frame, &n) == Err::kOk && n == frame);
+        }
+        c1.close();
+    });
+    std::vector<uint8_t> got;
+    for (;;) {
+        const uint8_t* v = nullptr;
+        size_t avail = 0;
+        const Err e = c2.peek(frame, &v, &avail);
+        if (e == Err::kClosed) break;
+        CHECK(e == Err::kOk && avail >= std::min(frame, cap) && avail <= cap);
+        const size_t take = avail / frame * frame;
+        std::vector<uint8_t> snap(v, v + take);
+        std::this_thread::sleep_for(std::chrono::microseconds(50));  // let the writer append behind the view
+        CHECK(std::memcmp(snap.data(), v, take) == 0);
+        got.insert(got.end(), v, v + take);
+        c2.consume(take);
+    }
+    w.join();
+    CHECK(got == src);
+}
+
+static void TestZeroSizeRefused() {  // buffered.go:38-40 panics on bufSize 0
+    bool threw = false;
+    try {
+        nsx::pipe::make_buffered_pipe("a", "b", 0);
+    } catch (const std::invalid_argument&) {
+        threw = true;
+    }
+    CHECK(threw);
+}
+
+template <class E>
+struct Case {
+    const char* name;
+    void (*fn)(E&, E&);
+};
+
+template <class E, class Make, size_t K>
+static void run_suite(const char* suite, const Case<E> (&tests)[K], Make make) {
     for (int rep = 0; rep < 20; ++rep)  // races: repeat
         for (auto& t : tests) {
             if (rep && std::strstr(t.name, "Before")) continue;  // 50 ms sleeps: once is enough
             Watchdog wd(t.name);
-            auto ends = nsx::pipe::make_pipe("c1", "c2");
+            auto ends = make();
             t.fn(ends.first, ends.second);
         }
+    std::printf("%s: %zu tests x 20 OK\n", suite, K);
+}
+
+int main() {
+    using nsx::pipe::BufferedEnd;
+    const Case<End> unbuffered[] = {{"TestReadWrite", TestReadWrite<End>},
+                                    {"TestWriteRace", TestWriteRace<End>},
+                                    {"TestReadRace", TestReadRace<End>},
+                                    {"TestClose", TestClose<End>},
+                                    {"TestReadBeforeClose", TestReadBeforeClose<End>},
+                                    {"TestWriteBeforeClose", TestWriteBeforeClose<End>},
+                                    {"TestReadDeadLine", TestReadDeadLine<End>},
+                                    {"TestWriteDeadLine", TestWriteDeadLine<End>},
+                                    {"TestDeadLineWakesBlockedRead", TestDeadLineWakesBlockedRead<End>},
+                                    {"TestAddr", TestAddr<End>},
+                                    {"TestEmptyWrite", TestEmptyWrite<End>},
+                                    {"TestFramedStream", TestFramedStream<End>}};
+    run_suite("pipe", unbuffered, [] { return nsx::pipe::make_pipe("c1", "c2"); });
+    // BufferedPipe("A", "B", clock, 20) as in pipe/buffered_test.go:18-21; the
+    // conn suite's TestWriteBeforeClose is skipped for buffered conns (conn.go:203-205).
+    const Case<BufferedEnd> buffered[] = {{"TestReadWrite", TestReadWrite<BufferedEnd>},
+                                          {"TestWriteRace", TestWriteRace<BufferedEnd>},
+                                          {"TestReadRace", TestReadRace<BufferedEnd>},
+                                          {"TestClose", TestClose<BufferedEnd>},
+                                          {"TestReadBeforeClose", TestReadBeforeClose<BufferedEnd>},
+                                          {"TestReadDeadLine", TestReadDeadLine<BufferedEnd>},
+                                          {"TestWriteDeadLine", TestWriteDeadLine<BufferedEnd>},
+                                          {"TestDeadLineWakesBlockedRead", TestDeadLineWakesBlockedRead<BufferedEnd>},
+                                          {"TestEmptyWrite", TestEmptyWrite<BufferedEnd>},
+                                          {"TestFramedStream", TestFramedStream<BufferedEnd>},
+                                          {"TestBothWrite", TestBothWrite},
+                                          {"TestReadAfterClose", TestReadAfterClose},
+                                          {"TestWriteBlocksWhenFull", TestWriteBlocksWhenFull},
+                                          {"TestPeekConsume", TestPeekConsume}};
+    run_suite("buffered", buffered, [] { return nsx::pipe::make_buffered_pipe("c1", "c2", 20); });
+    TestZeroSizeRefused();
     if (g_fail) {
         std::fprintf(stderr, "%d check(s) failed\n", g_fail);
         return 1;
     }
-    std::printf("pipe: %zu tests x 20 OK\n", sizeof tests / sizeof tests[0]);
+    std::printf("OK\n");
     return 0;
 }

@@ -27,7 +27,7 @@ def _build_pipe_test(tmp_path, extra=()):
 def test_pipe_conformance(tmp_path):
     out = subprocess.run([str(_build_pipe_test(tmp_path))], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
-    assert out.stdout.startswith("pipe: 12 tests")
+    assert out.stdout.split("\n")[:3] == ["pipe: 12 tests x 20 OK", "buffered: 14 tests x 20 OK", "OK"]
 
 
 def test_pipe_conformance_tsan(tmp_path):
@@ -47,36 +47,41 @@ def _loopback(*args):
     return out.returncode, json.loads(out.stdout.strip().splitlines()[-1])
 
 
-def test_loopback_config1_host_verifies_every_segment():
-    rc, r = _loopback("--mode", "host", "--reps", "20")
+@pytest.mark.parametrize("mode", ["host", "ring-host"])
+def test_loopback_config1_host_verifies_every_segment(mode):
+    rc, r = _loopback("--mode", mode, "--reps", "20")
     assert rc == 0 and r["bad"] == 0 and r["reps"] == 20
 
 
-def test_loopback_detects_corruption_host():
-    rc, r = _loopback("--mode", "host", "--reps", "3", "--corrupt", "17")
+@pytest.mark.parametrize("mode", ["host", "ring-host"])
+def test_loopback_detects_corruption_host(mode):
+    rc, r = _loopback("--mode", mode, "--reps", "3", "--corrupt", "17")
     assert rc == 0 and r["bad"] == 3
 
 
-def test_loopback_odd_lengths_host():
+@pytest.mark.parametrize("mode", ["host", "ring-host"])
+def test_loopback_odd_lengths_host(mode):
     for L in ("20", "21", "1501", "9001"):
-        rc, r = _loopback("--mode", "host", "--reps", "2", "--seg-len", L, "--segments", "9")
+        rc, r = _loopback("--mode", mode, "--reps", "2", "--seg-len", L, "--segments", "9")
         assert rc == 0 and r["bad"] == 0, L
 
 
-def test_loopback_batch_refuses_without_gpu():
+@pytest.mark.parametrize("mode", ["batch", "ring-gpu"])
+def test_loopback_gpu_modes_refuse_without_gpu(mode):
     if nsx.device_count() > 0:
         pytest.skip("GPU present")
-    rc, r = _loopback("--mode", "batch", "--reps", "1")
+    rc, r = _loopback("--mode", mode, "--reps", "1")
     assert rc == 1 and "error" in r
 
 
 @pytest.mark.gpu
-def test_loopback_config1_gpu_batch():
-    rc, r = _loopback("--mode", "batch", "--reps", "50")
+@pytest.mark.parametrize("mode", ["batch", "ring-gpu"])
+def test_loopback_config1_gpu_batch(mode):
+    rc, r = _loopback("--mode", mode, "--reps", "50")
     assert rc == 0 and r["bad"] == 0
-    rc, r = _loopback("--mode", "batch", "--reps", "3", "--corrupt", "63")
+    rc, r = _loopback("--mode", mode, "--reps", "3", "--corrupt", "63")
     assert rc == 0 and r["bad"] == 3
     for L in ("21", "1501", "9001"):
-        rc, r = _loopback("--mode", "batch", "--reps", "2", "--seg-len", L, "--segments", "9")
+        rc, r = _loopback("--mode", mode, "--reps", "2", "--seg-len", L, "--segments", "9")
         assert rc == 0 and r["bad"] == 0, L
 
