@@ -98,6 +98,19 @@ int nsx_pseudo_ipv4_partial_dev(const uint8_t* d_src, const uint8_t* d_dst,
                                 const uint32_t* d_len, uint8_t proto, uint64_t n,
                                 uint32_t* d_partial, nsx_stream_t stream);
 
+/* IPv6 TCP pseudo-header partials (RFC 8200 §8.1: src(16) dst(16) len(4)
+ * zero(3) next_header(1)) for n segments: d_src/d_dst are n×16 address bytes as
+ * ip.Addr.Raw() (network/ip/v6/ipv6.go:16), d_len the upper-layer length, and
+ * next_header e.g. ip.NextProtoTCP = 6. Same d_partial convention as above. */
+int nsx_pseudo_ipv6_partial_dev(const uint8_t* d_src, const uint8_t* d_dst,
+                                const uint32_t* d_len, uint8_t next_header, uint64_t n,
+                                uint32_t* d_partial, nsx_stream_t stream);
+
+/* Receive-side verify as a bitmask (tcp.go:70): bit (i % 64) of d_mask[i / 64]
+ * is set iff d_raw[i] == 0xFFFF; bits past n in the last word are 0. d_mask
+ * holds ceil(n/64) words. Pairs with nsx_csum_fixed_dev / nsx_csum_ragged_dev. */
+int nsx_verify_mask_dev(const uint16_t* d_raw, uint64_t n, uint64_t* d_mask, nsx_stream_t stream);
+
 /* Fused sender path: segment.bytes() + computeChecksum +
  * field write in one GPU pass (transport/tcp/tcp.go:98-128, :68-71). For each
  * segment i it writes the wire image — the 20-byte big-endian header built from

@@ -191,6 +191,26 @@ int nsx_pseudo_ipv4_partial_dev(const uint8_t* d_src, const uint8_t* d_dst, cons
                                            static_cast<hipStream_t>(stream)));
 }
 
+int nsx_pseudo_ipv6_partial_dev(const uint8_t* d_src, const uint8_t* d_dst, const uint32_t* d_len,
+                                uint8_t next_header, uint64_t n, uint32_t* d_partial, nsx_stream_t stream) {
+    if (n == 0) return NSX_OK;
+    if (!d_src || !d_dst || !d_len || !d_partial) return NSX_EINVAL;
+    const int dev = current_device();
+    if (dev < 0) return NSX_ENODEV;
+    const DevInfo* di = dev_info(dev);
+    return map_err(nsx::launch_pseudo_ipv6(d_src, d_dst, d_len, next_header, n, d_partial, (uint32_t)di->cus * 8,
+                                           static_cast<hipStream_t>(stream)));
+}
+
+int nsx_verify_mask_dev(const uint16_t* d_raw, uint64_t n, uint64_t* d_mask, nsx_stream_t stream) {
+    if (n == 0) return NSX_OK;
+    if (!d_raw || !d_mask) return NSX_EINVAL;
+    const int dev = current_device();
+    if (dev < 0) return NSX_ENODEV;
+    const DevInfo* di = dev_info(dev);
+    return map_err(nsx::launch_verify_mask(d_raw, n, d_mask, (uint32_t)di->cus * 8, static_cast<hipStream_t>(stream)));
+}
+
 uint64_t nsx_tcp_wire_len(uint64_t opt_len, uint64_t data_len) {
     return 20u + opt_len + (opt_len ? (20u + opt_len) % 4u : 0u) + data_len;
 }

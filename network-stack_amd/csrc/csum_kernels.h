@@ -35,6 +35,10 @@ hipError_t launch_ragged(const LaunchCfg& c, const void* d_base, const uint64_t*
                          const uint32_t* partial, uint16_t* out, uint8_t* ok, hipStream_t st);
 hipError_t launch_pseudo_ipv4(const uint8_t* src, const uint8_t* dst, const uint32_t* len, uint8_t proto,
                               uint64_t n, uint32_t* partial, uint32_t max_blocks, hipStream_t st);
+hipError_t launch_pseudo_ipv6(const uint8_t* src, const uint8_t* dst, const uint32_t* len, uint8_t nh,
+                              uint64_t n, uint32_t* partial, uint32_t max_blocks, hipStream_t st);
+hipError_t launch_verify_mask(const uint16_t* raw, uint64_t n, uint64_t* mask, uint32_t max_blocks,
+                              hipStream_t st);
 struct TcpHdrSoA {  // device arrays, one entry per segment (tcp.go:39-54 field order)
     const uint16_t* src_port;
     const uint16_t* dst_port;

@@ -1070,6 +1070,56 @@ __global__ __launch_bounds__(kBlock) void pseudo_ipv4_kernel(const uint8_t* __re
 }
 
 // ---------------------------------------------------------------------------
+// IPv6 pseudo-header partials: src(16) dst(16) len32 zero(3) nh (RFC 8200
+// §8.1). Addresses are 16-byte records, so a dwordx4 load per address when the
+// arrays are 4-aligned; byte loads otherwise.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t be_words_sum16(const uint8_t* a, bool aligned) {
+    uint32_t s = 0;
+    if (aligned) {
+        const uint4 v = *reinterpret_cast<const uint4*>(a);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)  // LE dword b0 b1 b2 b3 → BE words b0b1 + b2b3
+            s += ((w[k] & 0xFFu) << 8 | (w[k] >> 8 & 0xFFu)) + ((w[k] >> 16 & 0xFFu) << 8 | w[k] >> 24);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; k += 2) s += (uint32_t)a[k] << 8 | a[k + 1];
+    }
+    return s;
+}
+
+__global__ __launch_bounds__(kBlock) void pseudo_ipv6_kernel(const uint8_t* __restrict__ src,
+                                                             const uint8_t* __restrict__ dst,
+                                                             const uint32_t* __restrict__ len,
+                                                             uint32_t nh, uint64_t n, bool aligned,
+                                                             uint32_t* __restrict__ partial) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t l = len[i];
+        partial[i] = be_words_sum16(src + 16 * i, aligned) + be_words_sum16(dst + 16 * i, aligned) + (l >> 16) +
+                     (l & 0xFFFFu) + nh;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Receive-side verify as a bitmask (tcp.go:70): bit i of the mask is
+// (raw[i] == 0xFFFF). One wave covers 64 sums and its ballot is one u64 word.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void verify_mask_kernel(const uint16_t* __restrict__ raw, uint64_t n,
+                                                             uint64_t* __restrict__ mask) {
+    const uint64_t words = (n + 63) / 64;
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64; w < words;
+         w += (uint64_t)gridDim.x * blockDim.x / 64) {
+        const uint64_t i = w * 64 + lane;
+        const bool ok = i < n && raw[i] == 0xFFFFu;
+        const uint64_t bits = __ballot(ok);
+        if (lane == 0) mask[w] = bits;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // splitmix64 synthetic stream (bench/test data).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t splitmix64_at(uint64_t seed, uint64_t i) {
@@ -1360,6 +1410,24 @@ hipError_t launch_pseudo_ipv4(const uint8_t* src, const uint8_t* dst, const uint
     const uint32_t grid = (uint32_t)(want < max_blocks ? want : max_blocks);
     hipLaunchKernelGGL(pseudo_ipv4_kernel, dim3(grid), dim3(kBlock), 0, st, src, dst, len, (uint32_t)proto, n,
                        partial);
+    return hipGetLastError();
+}
+
+hipError_t launch_pseudo_ipv6(const uint8_t* src, const uint8_t* dst, const uint32_t* len, uint8_t nh,
+                              uint64_t n, uint32_t* partial, uint32_t max_blocks, hipStream_t st) {
+    const uint64_t want = (n + kBlock - 1) / kBlock;
+    const uint32_t grid = (uint32_t)(want < max_blocks ? want : max_blocks);
+    const bool aligned = (((uintptr_t)src | (uintptr_t)dst) & 3u) == 0;
+    hipLaunchKernelGGL(pseudo_ipv6_kernel, dim3(grid), dim3(kBlock), 0, st, src, dst, len, (uint32_t)nh, n,
+                       aligned, partial);
+    return hipGetLastError();
+}
+
+hipError_t launch_verify_mask(const uint16_t* raw, uint64_t n, uint64_t* mask, uint32_t max_blocks,
+                              hipStream_t st) {
+    const uint64_t want = (n + kBlock - 1) / kBlock;
+    const uint32_t grid = (uint32_t)(want < max_blocks ? want : max_blocks);
+    hipLaunchKernelGGL(verify_mask_kernel, dim3(grid), dim3(kBlock), 0, st, raw, n, mask);
     return hipGetLastError();
 }
 

@@ -50,6 +50,8 @@ def lib() -> ctypes.CDLL:
             "nsx_csum_ragged_dev": [vp, vp, u64, vp, vp, vp],
             "nsx_verify_ragged_dev": [vp, vp, u64, vp, vp, vp, vp],
             "nsx_pseudo_ipv4_partial_dev": [vp, vp, vp, u8, u64, vp, vp],
+            "nsx_pseudo_ipv6_partial_dev": [vp, vp, vp, u8, u64, vp, vp],
+            "nsx_verify_mask_dev": [vp, u64, vp, vp],
             "nsx_csum_fixed_host": [vp, u64, u32, u64, vp, vp, i32],
             "nsx_csum_ragged_host": [vp, vp, u64, vp, vp, i32],
             "nsx_alloc_pinned": [sz, ctypes.POINTER(vp)],
@@ -225,6 +227,26 @@ def pseudo_ipv4_partial_dev(src, dst, length, proto: int = 6, out=None, stream=N
         out = torch.empty(n, dtype=torch.int32, device=length.device)  # u32 bits
     _check(lib().nsx_pseudo_ipv4_partial_dev(_dev_ptr(src), _dev_ptr(dst), _dev_ptr(length), proto, n,
                                              _dev_ptr(out), _stream(stream)), "nsx_pseudo_ipv4_partial_dev")
+    return out
+
+
+def pseudo_ipv6_partial_dev(src, dst, length, next_header: int = 6, out=None, stream=None):
+    import torch
+    n = length.numel()
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=length.device)  # u32 bits
+    _check(lib().nsx_pseudo_ipv6_partial_dev(_dev_ptr(src), _dev_ptr(dst), _dev_ptr(length), next_header, n,
+                                             _dev_ptr(out), _stream(stream)), "nsx_pseudo_ipv6_partial_dev")
+    return out
+
+
+def verify_mask_dev(raw, out=None, stream=None):
+    """Bitmask of raw == 0xFFFF (tcp.go:70): int64 tensor of ceil(n/64) words."""
+    import torch
+    n = raw.numel()
+    if out is None:
+        out = torch.empty((n + 63) // 64, dtype=torch.int64, device=raw.device)  # u64 bits
+    _check(lib().nsx_verify_mask_dev(_dev_ptr(raw), n, _dev_ptr(out), _stream(stream)), "nsx_verify_mask_dev")
     return out
 
 

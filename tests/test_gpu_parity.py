@@ -287,6 +287,53 @@ def test_pseudo_ipv4_partial_and_verify_roundtrip():
     assert not okh[7] and okh.sum() == n - 1
 
 
+def test_pseudo_ipv6_partial_matches_oracle():
+    rng = np.random.default_rng(6)
+    n = 5000
+    src = rng.integers(0, 256, 16 * n + 1, dtype=np.uint8)
+    dst = rng.integers(0, 256, 16 * n + 1, dtype=np.uint8)
+    src[:32] = 0xFF  # saturating words
+    lens = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    lens[:3] = [0, 0xFFFFFFFF, 65536]
+    d_len = dev(lens.view(np.int32))
+    for off in (0, 1):  # 4-aligned (dwordx4 path) and misaligned address arrays (byte path)
+        d_src, d_dst = dev(src)[off:off + 16 * n], dev(dst)[off:off + 16 * n]
+        part = host(nsx.pseudo_ipv6_partial_dev(d_src, d_dst, d_len, 6)).view(np.uint32)
+        for i in list(range(0, n, 41)) + [0, 1, 2, n - 1]:
+            ph = O.ipv6_pseudo_header(src[off + 16 * i:off + 16 * i + 16].tobytes(),
+                                      dst[off + 16 * i:off + 16 * i + 16].tobytes(), 6, int(lens[i]))
+            assert int(part[i]) == O.be_word_sum(ph), (off, i)
+
+
+def test_ipv6_pseudo_partial_drives_fixed_checksum():
+    """IPv6 pseudo-header partials into the fixed-stride path == oracle over pseudo ‖ segment."""
+    rng = np.random.default_rng(61)
+    n, L = 3000, 1500
+    buf = rng.integers(0, 256, n * L, dtype=np.uint8)
+    src = rng.integers(0, 256, 16 * n, dtype=np.uint8)
+    dst = rng.integers(0, 256, 16 * n, dtype=np.uint8)
+    lens = np.full(n, L, np.uint32)
+    part = nsx.pseudo_ipv6_partial_dev(dev(src), dev(dst), dev(lens.view(np.int32)), 6)
+    raw = u16(nsx.fixed_dev(dev(buf), L, L, n, partial=part))
+    for i in range(0, n, 37):
+        ph = O.ipv6_pseudo_header(src[16 * i:16 * i + 16].tobytes(), dst[16 * i:16 * i + 16].tobytes(), 6, L)
+        assert raw[i] == O.go_checksum(ph, buf[i * L:(i + 1) * L].tobytes()), i
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 1000, 100_003])
+def test_verify_mask_matches_raw(n):
+    rng = np.random.default_rng(n)
+    raw = rng.integers(0, 1 << 16, n, dtype=np.uint64).astype(np.uint16)
+    raw[rng.random(n) < 0.5] = 0xFFFF
+    raw[0] = 0xFFFF
+    mask = host(nsx.verify_mask_dev(dev(raw.view(np.int16)))).view(np.uint64)
+    assert mask.size == (n + 63) // 64
+    bits = np.unpackbits(mask.view(np.uint8), bitorder="little")
+    want = np.zeros(mask.size * 64, np.uint8)
+    want[:n] = raw == 0xFFFF
+    assert np.array_equal(bits, want)
+
+
 # ------------------------------------------------------------------ host batch path
 
 def test_host_batch_paths_pageable_and_pinned():
