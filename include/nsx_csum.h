@@ -163,7 +163,8 @@ int nsx_ipv4_hdr_csum_dev(void* d_base, uint64_t stride, uint32_t hdr_off, uint6
 /* ----------------------------------------------------------------------------
  * Host-resident batches: pinned staging, H2D → kernel → D2H double-buffered
  * over two streams per GPU, segments sharded contiguously across num_gpus
- * devices (0 = all visible). No collective: shards are independent.
+ * devices (0 = auto: one GPU per 64 MiB of batch, up to all visible). No
+ * collective: shards are independent.
  * h_prefix_partial nullable.
  */
 int nsx_csum_fixed_host(const uint8_t* h_base, uint64_t stride, uint32_t seg_len, uint64_t n,
@@ -171,6 +172,12 @@ int nsx_csum_fixed_host(const uint8_t* h_base, uint64_t stride, uint32_t seg_len
 
 int nsx_csum_ragged_host(const uint8_t* h_base, const uint64_t* h_offsets, uint64_t n,
                          const uint32_t* h_prefix_partial, uint16_t* h_out, int num_gpus);
+
+/* The host batch calls keep per-device streams and grow-only device/pinned
+ * staging buffers across calls (a transport calls them once per batch). This
+ * frees the cached buffers; the next call re-allocates. Safe to call at any
+ * time; concurrent host batch calls on a device wait for each other. */
+int nsx_host_cache_release(void);
 
 /* Pinned (DMA-registered) host memory for zero-copy staging from Go via
  * unsafe.Slice (cgo forbids C retaining Go pointers; runtime.Pinner does not

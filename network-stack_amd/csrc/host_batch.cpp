@@ -7,11 +7,12 @@
 // double-buffers fixed-size chunks over two HIP streams: chunk k+1's H2D copy
 // overlaps chunk k's kernel and D2H. Caller memory that is already pinned
 // (nsx_alloc_pinned) is DMA'd directly; pageable memory is bounced through
-// pinned staging buffers.
+// pinned staging buffers. Streams and buffers persist per device (DevCtx).
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
 #include <cstring>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -97,6 +98,63 @@ std::vector<Chunk> plan_chunks(const Job& j) {
     return v;
 }
 
+// Per-device resources reused across calls: the transport calls the host
+// batch API once per received batch (tools/loopback.cpp), so stream creation,
+// hipMalloc and hipHostMalloc (page registration) must not sit on every call —
+// they cost milliseconds against a ~100 KB batch's tens of microseconds.
+// Buffers only grow; nsx_host_cache_release() frees them. Calls on the same
+// device serialise on the context's mutex (each call already fills the GPU's
+// copy engines with its own double-buffered chunks).
+template <bool kHost>
+struct Grow {
+    void* p = nullptr;
+    uint64_t cap = 0;
+    hipError_t ensure(uint64_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        release();
+        uint64_t c = 4096;
+        while (c < bytes) c <<= 1;
+        const hipError_t e = kHost ? hipHostMalloc(&p, c, hipHostMallocPortable) : hipMalloc(&p, c);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return e;
+        }
+        cap = c;
+        return hipSuccess;
+    }
+    void release() {
+        if (p) (void)(kHost ? hipHostFree(p) : hipFree(p));
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
+struct DevCtx {
+    std::mutex mu;
+    hipStream_t st[2] = {nullptr, nullptr};
+    Grow<false> d_data[2], d_out[2], d_part[2], d_off[2];
+    Grow<true> h_stage[2], h_ostage[2], h_pstage[2], h_offstage[2];
+    void release() {
+        for (int s = 0; s < 2; ++s) {
+            d_data[s].release(), d_out[s].release(), d_part[s].release(), d_off[s].release();
+            h_stage[s].release(), h_ostage[s].release(), h_pstage[s].release(), h_offstage[s].release();
+        }
+    }
+};
+
+constexpr int kMaxDevices = 64;
+std::mutex g_ctx_mu;
+DevCtx* g_ctx[kMaxDevices] = {};  // never destroyed: HIP may be torn down before static destructors run
+
+DevCtx* dev_ctx(int dev) {
+    if (dev < 0 || dev >= kMaxDevices) return nullptr;
+    std::lock_guard<std::mutex> g(g_ctx_mu);
+    if (!g_ctx[dev]) g_ctx[dev] = new DevCtx;
+    return g_ctx[dev];
+}
+
 void run_job(Job* j) {
     int rc = NSX_OK;
     const std::vector<Chunk> chunks = plan_chunks(*j);
@@ -108,92 +166,87 @@ void run_job(Job* j) {
     const bool in_pinned = is_pinned(j->h_base);
     const bool out_pinned = is_pinned(j->h_out);
     const bool ragged = j->h_offsets != nullptr;
-    hipStream_t st[2] = {nullptr, nullptr};
-    uint8_t* d_data[2] = {nullptr, nullptr};
-    uint16_t* d_out[2] = {nullptr, nullptr};
-    uint32_t* d_part[2] = {nullptr, nullptr};
-    uint64_t* d_off[2] = {nullptr, nullptr};
-    uint8_t* h_stage[2] = {nullptr, nullptr};
-    uint16_t* h_ostage[2] = {nullptr, nullptr};
-    uint32_t* h_pstage[2] = {nullptr, nullptr};
-    uint64_t* h_offstage[2] = {nullptr, nullptr};
+    const int nslots = chunks.size() > 1 ? 2 : 1;
+    DevCtx* ctx = dev_ctx(j->dev);
+    if (!ctx) {
+        j->rc = NSX_EINVAL;
+        return;
+    }
+    std::lock_guard<std::mutex> hold(ctx->mu);
+    hipStream_t* st = ctx->st;
     nsx::LaunchCfg cfg;
     const Chunk* pending[2] = {nullptr, nullptr};
 
     NSX_TRY(hipSetDevice(j->dev));
     cfg = default_cfg(j->dev, max_segs);
-    for (int s = 0; s < 2; ++s) {
-        NSX_TRY(hipStreamCreateWithFlags(&st[s], hipStreamNonBlocking));
-        NSX_TRY(hipMalloc(&d_data[s], std::max<uint64_t>(max_span, 16)));
-        NSX_TRY(hipMalloc(&d_out[s], max_segs * sizeof(uint16_t)));
+    for (int s = 0; s < nslots; ++s) {
+        if (!st[s]) NSX_TRY(hipStreamCreateWithFlags(&st[s], hipStreamNonBlocking));
+        NSX_TRY(ctx->d_data[s].ensure(std::max<uint64_t>(max_span, 16)));
+        NSX_TRY(ctx->d_out[s].ensure(max_segs * sizeof(uint16_t)));
         if (j->h_partial) {
-            NSX_TRY(hipMalloc(&d_part[s], max_segs * sizeof(uint32_t)));
-            NSX_TRY(hipHostMalloc(&h_pstage[s], max_segs * sizeof(uint32_t), hipHostMallocPortable));
+            NSX_TRY(ctx->d_part[s].ensure(max_segs * sizeof(uint32_t)));
+            NSX_TRY(ctx->h_pstage[s].ensure(max_segs * sizeof(uint32_t)));
         }
         if (ragged) {
-            NSX_TRY(hipMalloc(&d_off[s], (max_segs + 1) * sizeof(uint64_t)));
-            NSX_TRY(hipHostMalloc(&h_offstage[s], (max_segs + 1) * sizeof(uint64_t), hipHostMallocPortable));
+            NSX_TRY(ctx->d_off[s].ensure((max_segs + 1) * sizeof(uint64_t)));
+            NSX_TRY(ctx->h_offstage[s].ensure((max_segs + 1) * sizeof(uint64_t)));
         }
-        if (!in_pinned) NSX_TRY(hipHostMalloc(&h_stage[s], std::max<uint64_t>(max_span, 16), hipHostMallocPortable));
-        if (!out_pinned) NSX_TRY(hipHostMalloc(&h_ostage[s], max_segs * sizeof(uint16_t), hipHostMallocPortable));
+        if (!in_pinned) NSX_TRY(ctx->h_stage[s].ensure(std::max<uint64_t>(max_span, 16)));
+        if (!out_pinned) NSX_TRY(ctx->h_ostage[s].ensure(max_segs * sizeof(uint16_t)));
     }
 
     for (size_t k = 0; k < chunks.size(); ++k) {
-        const int s = (int)(k & 1);
+        const int s = (int)(k % nslots);
         const Chunk& c = chunks[k];
         const uint64_t cn = c.c1 - c.c0, span = c.byte_hi - c.byte_lo;
+        uint8_t* d_data = ctx->d_data[s].as<uint8_t>();
+        uint16_t* d_out = ctx->d_out[s].as<uint16_t>();
+        uint32_t* d_part = j->h_partial ? ctx->d_part[s].as<uint32_t>() : nullptr;
+        uint16_t* h_ostage = ctx->h_ostage[s].as<uint16_t>();
         if (pending[s]) {  // slot reuse: finish chunk k-2
             NSX_TRY(hipStreamSynchronize(st[s]));
             if (!out_pinned)
-                std::memcpy(j->h_out + pending[s]->c0, h_ostage[s],
-                            (pending[s]->c1 - pending[s]->c0) * sizeof(uint16_t));
+                std::memcpy(j->h_out + pending[s]->c0, h_ostage, (pending[s]->c1 - pending[s]->c0) * sizeof(uint16_t));
             pending[s] = nullptr;
         }
         const uint8_t* src = j->h_base + c.byte_lo;
         if (!in_pinned) {
-            std::memcpy(h_stage[s], src, span);
-            src = h_stage[s];
+            std::memcpy(ctx->h_stage[s].p, src, span);
+            src = ctx->h_stage[s].as<uint8_t>();
         }
-        if (span) NSX_TRY(hipMemcpyAsync(d_data[s], src, span, hipMemcpyHostToDevice, st[s]));
+        if (span) NSX_TRY(hipMemcpyAsync(d_data, src, span, hipMemcpyHostToDevice, st[s]));
         if (j->h_partial) {
-            std::memcpy(h_pstage[s], j->h_partial + c.c0, cn * sizeof(uint32_t));
-            NSX_TRY(hipMemcpyAsync(d_part[s], h_pstage[s], cn * sizeof(uint32_t), hipMemcpyHostToDevice, st[s]));
+            uint32_t* h_pstage = ctx->h_pstage[s].as<uint32_t>();
+            std::memcpy(h_pstage, j->h_partial + c.c0, cn * sizeof(uint32_t));
+            NSX_TRY(hipMemcpyAsync(d_part, h_pstage, cn * sizeof(uint32_t), hipMemcpyHostToDevice, st[s]));
         }
-        uint16_t* out_dst = out_pinned ? j->h_out + c.c0 : h_ostage[s];
+        uint16_t* out_dst = out_pinned ? j->h_out + c.c0 : h_ostage;
         hipError_t e;
         if (ragged) {
-            for (uint64_t i = 0; i <= cn; ++i) h_offstage[s][i] = j->h_offsets[c.c0 + i] - c.byte_lo;
-            NSX_TRY(hipMemcpyAsync(d_off[s], h_offstage[s], (cn + 1) * sizeof(uint64_t), hipMemcpyHostToDevice,
-                                   st[s]));
-            e = nsx::launch_ragged(cfg, d_data[s], d_off[s], cn, d_part[s], d_out[s], nullptr, st[s]);
+            uint64_t* h_offstage = ctx->h_offstage[s].as<uint64_t>();
+            uint64_t* d_off = ctx->d_off[s].as<uint64_t>();
+            for (uint64_t i = 0; i <= cn; ++i) h_offstage[i] = j->h_offsets[c.c0 + i] - c.byte_lo;
+            NSX_TRY(hipMemcpyAsync(d_off, h_offstage, (cn + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st[s]));
+            e = nsx::launch_ragged(cfg, d_data, d_off, cn, d_part, d_out, nullptr, st[s]);
         } else {
-            e = nsx::launch_fixed(cfg, d_data[s], j->stride, j->seg_len, cn, d_part[s], d_out[s], st[s]);
+            e = nsx::launch_fixed(cfg, d_data, j->stride, j->seg_len, cn, d_part, d_out, st[s]);
         }
         NSX_TRY(e);
-        NSX_TRY(hipMemcpyAsync(out_dst, d_out[s], cn * sizeof(uint16_t), hipMemcpyDeviceToHost, st[s]));
+        NSX_TRY(hipMemcpyAsync(out_dst, d_out, cn * sizeof(uint16_t), hipMemcpyDeviceToHost, st[s]));
         pending[s] = &c;
     }
-    for (int s = 0; s < 2; ++s) {
-        if (!st[s]) continue;
+    for (int s = 0; s < nslots; ++s) {
         NSX_TRY(hipStreamSynchronize(st[s]));
         if (pending[s] && !out_pinned)
-            std::memcpy(j->h_out + pending[s]->c0, h_ostage[s], (pending[s]->c1 - pending[s]->c0) * sizeof(uint16_t));
+            std::memcpy(j->h_out + pending[s]->c0, ctx->h_ostage[s].p,
+                        (pending[s]->c1 - pending[s]->c0) * sizeof(uint16_t));
         pending[s] = nullptr;
     }
 
 done:
-    for (int s = 0; s < 2; ++s) {
-        if (st[s]) (void)hipStreamSynchronize(st[s]);
-        if (d_data[s]) (void)hipFree(d_data[s]);
-        if (d_out[s]) (void)hipFree(d_out[s]);
-        if (d_part[s]) (void)hipFree(d_part[s]);
-        if (d_off[s]) (void)hipFree(d_off[s]);
-        if (h_stage[s]) (void)hipHostFree(h_stage[s]);
-        if (h_ostage[s]) (void)hipHostFree(h_ostage[s]);
-        if (h_pstage[s]) (void)hipHostFree(h_pstage[s]);
-        if (h_offstage[s]) (void)hipHostFree(h_offstage[s]);
-        if (st[s]) (void)hipStreamDestroy(st[s]);
-    }
+    if (rc != NSX_OK)  // leave the streams idle for the next call
+        for (int s = 0; s < 2; ++s)
+            if (st[s]) (void)hipStreamSynchronize(st[s]);
     j->rc = rc;
 }
 
@@ -205,7 +258,11 @@ int run_sharded(const uint8_t* h_base, uint64_t stride, uint32_t seg_len, const 
         count = 0;
     }
     if (count <= 0) return NSX_ENODEV;
-    if (num_gpus <= 0) num_gpus = count;
+    if (num_gpus <= 0) {  // auto: all GPUs, but no shard smaller than one chunk
+        const uint64_t bytes = h_offsets ? h_offsets[n] - h_offsets[0] : n * std::max<uint64_t>(stride, seg_len);
+        const uint64_t want = std::max<uint64_t>(1, (bytes + kChunkBytes - 1) / kChunkBytes);
+        num_gpus = (int)std::min<uint64_t>(want, (uint64_t)count);
+    }
     if (num_gpus > count) return NSX_ENODEV;
     int caller_dev = 0;
     (void)hipGetDevice(&caller_dev);
@@ -244,6 +301,23 @@ int nsx_csum_ragged_host(const uint8_t* h_base, const uint64_t* h_offsets, uint6
     for (uint64_t i = 0; i < n; ++i)
         if (h_offsets[i + 1] < h_offsets[i]) return NSX_EINVAL;
     return run_sharded(h_base, 0, 0, h_offsets, n, h_prefix_partial, h_out, num_gpus);
+}
+
+int nsx_host_cache_release(void) {
+    std::lock_guard<std::mutex> g(g_ctx_mu);
+    int dev0 = 0;
+    const bool restore = hipGetDevice(&dev0) == hipSuccess;
+    for (int d = 0; d < kMaxDevices; ++d) {
+        if (!g_ctx[d]) continue;
+        std::lock_guard<std::mutex> hold(g_ctx[d]->mu);
+        if (hipSetDevice(d) != hipSuccess) {
+            (void)hipGetLastError();
+            continue;
+        }
+        g_ctx[d]->release();  // streams stay: they are cheap and reused
+    }
+    if (restore) (void)hipSetDevice(dev0);
+    return NSX_OK;
 }
 
 }  // extern "C"

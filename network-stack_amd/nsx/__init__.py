@@ -52,6 +52,7 @@ def lib() -> ctypes.CDLL:
             "nsx_pseudo_ipv4_partial_dev": [vp, vp, vp, u8, u64, vp, vp],
             "nsx_pseudo_ipv6_partial_dev": [vp, vp, vp, u8, u64, vp, vp],
             "nsx_verify_mask_dev": [vp, u64, vp, vp],
+            "nsx_host_cache_release": [],
             "nsx_csum_fixed_host": [vp, u64, u32, u64, vp, vp, i32],
             "nsx_csum_ragged_host": [vp, vp, u64, vp, vp, i32],
             "nsx_alloc_pinned": [sz, ctypes.POINTER(vp)],

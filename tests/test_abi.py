@@ -162,6 +162,7 @@ def test_device_calls_fail_loudly_without_gpu():
         nsx.ragged_host(buf, np.array([0, 10, 3000], np.uint64))
     p = ctypes.c_void_p()
     assert L.nsx_alloc_pinned(64, ctypes.byref(p)) == nsx.NSX_ENODEV
+    assert L.nsx_host_cache_release() == 0  # nothing cached, nothing to do
 
 
 def test_device_calls_validate_before_device():

@@ -336,6 +336,27 @@ def test_verify_mask_matches_raw(n):
 
 # ------------------------------------------------------------------ host batch path
 
+def test_host_batch_cache_grows_and_releases():
+    """Host batch calls reuse per-device buffers: growing, shrinking and mixed
+    fixed/ragged/partial calls stay exact, also after nsx_host_cache_release."""
+    rng = np.random.default_rng(81)
+    L = 1500
+    for rel in (False, True, False):
+        for n in (64, 1, 5000, 64, 100_000, 3):
+            buf = rng.integers(0, 256, n * L, dtype=np.uint8)
+            part = rng.integers(0, 1 << 20, n, dtype=np.uint64).astype(np.uint32)
+            got = nsx.fixed_host(buf, L, L, n, partial=part)
+            want = O.c_batch(buf, n, stride=L, seg_len=L, partial=part)
+            assert np.array_equal(got, want), n
+            lens = rng.integers(0, 3000, n).astype(np.uint64)
+            offs = np.zeros(n + 1, np.uint64)
+            offs[1:] = np.cumsum(lens)
+            rb = rng.integers(0, 256, int(offs[-1]) + 1, dtype=np.uint8)
+            assert np.array_equal(nsx.ragged_host(rb, offs), O.c_batch(rb, n, offsets=offs)), n
+        if rel:
+            assert nsx.lib().nsx_host_cache_release() == 0
+
+
 def test_host_batch_paths_pageable_and_pinned():
     rng = np.random.default_rng(8)
     n, L = 100_003, 1500
