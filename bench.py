@@ -45,6 +45,14 @@ WORKLOADS = {
             name="config4: 256K x 64KiB TSO-size segments per GPU, device-resident"),
     5: dict(kind="fixed", n=1 << 24, seg_len=1500, stride=1500, seed=0x1071,
             name="config5: 16M x 1500B per GPU (128M x 1500B over 8 GPUs), device-resident"),
+    # SURVEY.md §8(f) rows measured to the same bar (not the headline metric):
+    6: dict(kind="tcp_build", n=1 << 20, payload=1480, seed=0x1074,
+            metric="GiB/s fused TCP segment build (serialize + checksum + field write), wire bytes",
+            name="f1: 1M option-less TCP segments per GPU, 1480B payload -> 1500B wire images, IPv4 pseudo-header "
+                 "partials, device-resident"),
+    7: dict(kind="ipv4_hdr", n=1 << 26, hdr=20, seed=0x1075,
+            metric="GiB/s IPv4 header checksum verify, header bytes",
+            name="f3: 64M packed 20B IPv4 headers per GPU (header-split ring), verify, device-resident"),
 }
 
 
@@ -53,7 +61,8 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", type=int, default=2, choices=sorted(WORKLOADS))
+    ap.add_argument("--config", type=int, default=2, choices=sorted(WORKLOADS),
+                    help="2-5: BASELINE configs (2 = headline); 6: f1 fused TCP build; 7: f3 IPv4 header verify")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--settle-s", type=float, default=0.5, help="device clock settle time before warmup (setup)")
     ap.add_argument("--param", action="append", default=[], metavar="NAME=V",
@@ -132,12 +141,12 @@ def timed_loop(step, sync, barrier, steps: int, warmup: int, ev_pair=None):
 
 
 def result_line(*, world, steps, warmup, wall_max, bytes_per_rank_step, units_total, workload, cfg, launch_ms,
-                alg_bytes_per_launch, cpu_baseline, traffic, dtype="u16") -> dict:
+                alg_bytes_per_launch, cpu_baseline, traffic, dtype="u16", metric=METRIC) -> dict:
     total_bytes = bytes_per_rank_step * world * steps
     mean_launch_ms = sum(launch_ms) / len(launch_ms) if launch_ms else None
     achieved = alg_bytes_per_launch / (mean_launch_ms * 1e-3) / 1e9 if mean_launch_ms else None
     return {
-        "metric": METRIC,
+        "metric": metric,
         "value": round(total_bytes / wall_max / GIB, 3),
         "unit": "GiB/s",
         "n_gpus": world,
@@ -149,7 +158,7 @@ def result_line(*, world, steps, warmup, wall_max, bytes_per_rank_step, units_to
         "vs_baseline": None,
         "dtype": dtype,
         "data": "synthetic: splitmix64 bytes (seed %#x + rank) generated on device" % cfg["seed"],
-        "config": {"workload": workload, "segments_per_gpu": cfg["n"], "bytes_per_gpu": bytes_per_rank_step,
+        "config": {"workload": workload, "units_per_gpu": cfg["n"], "bytes_per_gpu": bytes_per_rank_step,
                    "units_per_step_all_gpus": units_total,
                    "parallelism": f"shard{world} (independent per-GPU batches, no collective)"},
         "kernel_ms_mean": None if mean_launch_ms is None else round(mean_launch_ms, 5),
@@ -183,6 +192,40 @@ def build_workload(cfg, rank, device):
         out = torch.empty(n, dtype=torch.int16, device=device)
         w.update(buf=buf, out=out, bytes=n * L, alg=n * L + 2 * n,
                  step=lambda: nsx.fixed_dev(buf, S, L, n, out=out))
+    elif cfg["kind"] == "tcp_build":
+        n, P = cfg["n"], cfg["payload"]
+        W = P + 20
+        g = torch.Generator(device=device).manual_seed(seed)
+        data = torch.empty(n * P, dtype=torch.uint8, device=device)
+        nsx.fill_splitmix64_dev(data, seed)
+
+        def rnd(bits, dtype):
+            return torch.randint(0, 1 << bits, (n,), generator=g, device=device, dtype=torch.int64).to(dtype)
+
+        fields = {"src_port": rnd(16, torch.int16), "dst_port": rnd(16, torch.int16),
+                  "seq_num": rnd(32, torch.int32), "ack_num": rnd(32, torch.int32),
+                  "offset": torch.full((n,), 5, dtype=torch.uint8, device=device),  # computeOffset, no options
+                  "control": rnd(8, torch.uint8), "window": rnd(16, torch.int16), "urgent_ptr": rnd(16, torch.int16)}
+        addrs = torch.randint(0, 256, (2, n, 4), generator=g, device=device, dtype=torch.int64).to(torch.uint8)
+        wire_len = torch.full((n,), W, dtype=torch.int32, device=device)
+        part = nsx.pseudo_ipv4_partial_dev(addrs[0].reshape(-1), addrs[1].reshape(-1), wire_len, 6)
+        idx = torch.arange(n + 1, dtype=torch.int64, device=device)
+        data_off, out_off = idx * P, idx * W
+        out = torch.empty(n * W, dtype=torch.uint8, device=device)
+        raw = torch.empty(n, dtype=torch.int16, device=device)
+        # per segment: payload + 18 B of header fields + 2 offsets + partial read; wire image + raw sum written
+        w.update(out=raw, wire=out, fields=fields, addrs=addrs, data=data, bytes=n * W,
+                 alg=n * (P + 18 + 8 + 8 + 4 + W + 2) + 16,
+                 step=lambda: nsx.tcp_build_dev(fields, data, data_off, out, out_off, partial=part, raw=raw))
+    elif cfg["kind"] == "ipv4_hdr":
+        n, H = cfg["n"], cfg["hdr"]
+        buf = torch.empty(n * H, dtype=torch.uint8, device=device)
+        nsx.fill_splitmix64_dev(buf, seed)
+        buf.view(n, H)[:, 0] = 0x45  # version 4, IHL 5
+        nsx.ipv4_hdr_csum_dev(buf, H, n, mode=1)  # setup: fill valid checksums (RFC 791 §3.1)
+        out = torch.empty(n, dtype=torch.int16, device=device)
+        w.update(buf=buf, out=out, bytes=n * H, alg=n * (H + 2),
+                 step=lambda: nsx.ipv4_hdr_csum_dev(buf, H, n, mode=0, out=out))
     else:
         rng = np.random.default_rng(cfg["seed"])  # same lengths on every rank, bytes differ by seed
         n = cfg["n"]
@@ -211,6 +254,7 @@ def cpu_baseline(cfg, w, seconds: float) -> dict:
     from oracle import csum_oracle as O
     lib = O.c_oracle()
     torch.cuda.synchronize()
+    wire_ok = True  # workload 6 also compares the wire images
     if cfg["kind"] == "fixed":
         n, L, S = cfg["n"], cfg["seg_len"], cfg["stride"]
         m = min(n, max(1, (256 << 20) // S))  # sample: the first m segments (≤ 256 MiB)
@@ -227,6 +271,46 @@ def cpu_baseline(cfg, w, seconds: float) -> dict:
         dt = time.perf_counter() - t0
         nbytes = reps * m * L
         desc = f"first {m} segments x {L}B of rank 0's batch, {reps} pass(es), Go-faithful serial loop"
+    elif cfg["kind"] == "tcp_build":
+        n, P = cfg["n"], cfg["payload"]
+        W = P + 20
+        m = min(n, 65536)  # sample: the first 64K segments (~94 MiB of wire)
+        fields = {k: v[:m].cpu().numpy().view(dt) for (k, v), dt in
+                  zip(((k, w["fields"][k]) for k in O.TCP_FIELDS), O.TCP_FIELD_DTYPES)}
+        data = w["data"][: m * P].cpu().numpy()
+        a = w["addrs"][:, :m].cpu().numpy()
+        pseudo = np.concatenate([a[0], a[1], np.tile(np.array([0, 6, W >> 8, W & 0xFF], np.uint8), (m, 1))], 1)
+        data_off = np.arange(m + 1, dtype=np.uint64) * np.uint64(P)
+        out_off = np.arange(m + 1, dtype=np.uint64) * np.uint64(W)
+        gpu = w["out"][:m].cpu().numpy().view(np.uint16)
+        gpu_wire = w["wire"][: m * W].cpu().numpy()
+        t0, reps = time.perf_counter(), 0
+        while True:
+            wire, out = O.c_go_tcp_build(fields, data, data_off, out_off, pseudo)
+            reps += 1
+            if time.perf_counter() - t0 >= seconds:
+                break
+        dt = time.perf_counter() - t0
+        nbytes = reps * m * W
+        desc = (f"first {m} segments of rank 0's batch, {reps} pass(es), Go-faithful sender loop: bytes() + "
+                "computeChecksum(12B pseudo-header) + field store per segment")
+        wire_ok = bool(np.array_equal(wire, gpu_wire))
+    elif cfg["kind"] == "ipv4_hdr":
+        n, H = cfg["n"], cfg["hdr"]
+        m = min(n, 1 << 22)
+        sample = w["buf"][: m * H].cpu().numpy()
+        gpu = w["out"][:m].cpu().numpy().view(np.uint16)
+        out = np.empty(m, np.uint16)
+        t0, reps = time.perf_counter(), 0
+        while True:
+            lib.oracle_go_batch_fixed(sample.ctypes.data_as(ctypes.c_void_p), H, H, m, None, 0,
+                                      out.ctypes.data_as(ctypes.c_void_p))
+            reps += 1
+            if time.perf_counter() - t0 >= seconds:
+                break
+        dt = time.perf_counter() - t0
+        nbytes = reps * m * H
+        desc = f"first {m} headers of rank 0's batch, {reps} pass(es), the reference's serial checksum loop per header"
     else:
         offs = w["offsets"]
         m = int(min(len(offs) - 1, 50000))
@@ -247,7 +331,7 @@ def cpu_baseline(cfg, w, seconds: float) -> dict:
         nbytes = reps * hi
         desc = f"first {m} ragged segments of rank 0's batch, {reps} pass(es), Go-faithful serial loop"
     return {"value": round(nbytes / dt / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
-            "sample": desc, "seconds": round(dt, 2), "sample_parity_vs_gpu": bool(np.array_equal(out, gpu)),
+            "sample": desc, "seconds": round(dt, 2), "sample_parity_vs_gpu": bool(np.array_equal(out, gpu)) and wire_ok,
             "host_cpus": os.cpu_count()}
 
 
@@ -303,7 +387,7 @@ def main(argv=None):
     line = result_line(world=dist.world, steps=args.steps, warmup=args.warmup, wall_max=wall_max,
                        bytes_per_rank_step=w["bytes"], units_total=cfg["n"] * dist.world, workload=cfg["name"],
                        cfg=cfg, launch_ms=launch_ms, alg_bytes_per_launch=w["alg"], cpu_baseline=cpu,
-                       traffic=load_traffic(args.config))
+                       traffic=load_traffic(args.config), metric=cfg.get("metric", METRIC))
     if args.param:
         line["config"]["params"] = args.param
     if dist.rank == 0:

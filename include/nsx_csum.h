@@ -156,7 +156,8 @@ int nsx_tcp_layout_host(const uint64_t* h_opt_off, const uint64_t* h_data_off, u
  *   mode 1 (send):    d_out_raw[i] (nullable) = raw sum with bytes 10-11 taken
  *          as zero, and ~raw is written big-endian into bytes 10-11 in place.
  * A malformed header (IHL < 5, or hdr_off + IHL*4 > stride) yields 0 and is
- * left untouched. */
+ * left untouched. At least 20 bytes must be readable at every header start;
+ * stride and hdr_off ≤ 2^22 (NSX_EINVAL otherwise). */
 int nsx_ipv4_hdr_csum_dev(void* d_base, uint64_t stride, uint32_t hdr_off, uint64_t n, int mode,
                           uint16_t* d_out_raw, nsx_stream_t stream);
 
@@ -213,7 +214,7 @@ const char* nsx_strerror(int code);
  * Not needed for correctness; every variant is bit-exact. */
 #define NSX_PARAM_BLOCKS_PER_CU   1  /* persistent grid, 1..8 blocks of 256 threads per CU (default per path) */
 #define NSX_PARAM_SEGS_PER_WAVE   2  /* per-segment kernels: 1, 2, 4 or 8 segments per wave pass */
-#define NSX_PARAM_NONTEMPORAL     3  /* 1 nt loads (default), 2 default-policy loads */
+#define NSX_PARAM_NONTEMPORAL     3  /* 1 nt loads (default), 2 default-policy loads; nsx_tcp_build_dev: default plain, 1 nt, 3 nt loads + plain stores, 4 plain loads + nt stores */
 #define NSX_PARAM_BLOCK_MODE      4  /* 0 auto (a block per segment when n < 4*CUs), 1 never, 2 always */
 #define NSX_PARAM_XCD_MAP         5  /* task deal: 1 XCD-contiguous regions (default), 2 grid-stride, 3 one contiguous range per wave */
 #define NSX_PARAM_KERNEL          6  /* 1 row-stream, 2 per-segment, 3 buffer-load, 4 prefix-scan (ragged); 0 = per-path default */

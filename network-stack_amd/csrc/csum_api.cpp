@@ -242,8 +242,8 @@ int nsx_tcp_build_dev(const nsx_tcp_hdr_soa* hdr, const uint8_t* d_opts, const u
     const nsx::TcpHdrSoA h{hdr->src_port, hdr->dst_port, hdr->seq_num, hdr->ack_num,
                            hdr->offset,   hdr->control,  hdr->window,  hdr->urgent_ptr};
     return map_err(nsx::launch_tcp_build(h, d_opts, d_opt_off, d_data, d_data_off, data_bytes, d_prefix_partial, n,
-                                         d_out, d_out_off, d_raw, (uint32_t)di->cus * 2,
-                                         static_cast<hipStream_t>(stream)));
+                                         d_out, d_out_off, d_raw, (uint32_t)di->cus * 8,
+                                         (int)g_param[NSX_PARAM_NONTEMPORAL].load(), static_cast<hipStream_t>(stream)));
 }
 
 int nsx_ipv4_hdr_csum_dev(void* d_base, uint64_t stride, uint32_t hdr_off, uint64_t n, int mode,
@@ -251,6 +251,7 @@ int nsx_ipv4_hdr_csum_dev(void* d_base, uint64_t stride, uint32_t hdr_off, uint6
     if (n == 0) return NSX_OK;
     if (!d_base || (mode != 0 && mode != 1) || (mode == 0 && !d_out_raw)) return NSX_EINVAL;
     if (n > 1 && stride == 0) return NSX_EINVAL;
+    if (stride > ((uint64_t)1 << 22) || hdr_off > ((uint32_t)1 << 22)) return NSX_EINVAL;  // 32-bit block offsets
     const int dev = current_device();
     if (dev < 0) return NSX_ENODEV;
     const DevInfo* di = dev_info(dev);

@@ -922,6 +922,95 @@ __device__ __forceinline__ uint32_t bswap32u(uint32_t v) {
     return (v >> 24) | ((v >> 8) & 0xFF00u) | ((v << 8) & 0xFF0000u) | (v << 24);
 }
 
+// Wave task = a group of G ≤ 64 consecutive segments: lane j loads segment
+// g0+j's header fields and offsets (coalesced, one round trip per group), and the
+// wave then builds the group's segments one after another with the values
+// broadcast by v_readlane. Per segment, each lane owns 16-byte chunks of the
+// output (1 KiB rows). Payload source dwords come from one buffer descriptor
+// with unconditional loads — offsets before the payload, past the data end, or
+// of rows past the segment are out of range, read 0 and move nothing — so the
+// R rows of a batch are all in flight with no branch between them; bytes are
+// realigned by v_alignbyte with the segment-uniform shift. Row 0 (the header
+// row) loads its 5 source dwords one by one so that lanes straddling the
+// header/payload edge read correctly; only it and the row holding the wire end
+// take byte masks. Output goes through a descriptor ending at the segment's
+// last dword (per-dword range check, tools/probes/copy_ceiling.hip), so a tail
+// chunk needs no mask or branch. Dword 4 (urgent pointer + checksum field) is
+// written once, last, with the field.
+constexpr uint32_t kBuildRows = 2;
+
+__device__ __forceinline__ u32x4 realign(u32x4 lo, uint32_t hi, uint32_t sh) {
+    return u32x4{__builtin_amdgcn_alignbyte(lo.y, lo.x, sh), __builtin_amdgcn_alignbyte(lo.z, lo.y, sh),
+                 __builtin_amdgcn_alignbyte(lo.w, lo.z, sh), __builtin_amdgcn_alignbyte(hi, lo.w, sh)};
+}
+
+struct BuildSeg {  // wave-uniform description of one segment
+    uint32_t D0, D1, D2, D3, D4;  // header dwords as stored (LE view), field = 0
+    uint32_t optlen, hdr_end, wire, nb4, rows, sh;
+    int32_t sh0;                  // payload source offset (from the descriptor base) = wire pos + sh0
+    uint64_t ob;
+};
+
+// Source row r: 4+1 dwords per lane. Row 0 (head) clamps each dword separately.
+template <int LP>
+__device__ __forceinline__ void build_load_head(__amdgpu_buffer_rsrc_t drs, const BuildSeg& S, uint32_t lane,
+                                                u32x4& lo, uint32_t& hi) {
+    const int32_t t = ((int32_t)(lane * 16u) + S.sh0) >> 2;
+    uint32_t d[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+        d[j] = __builtin_amdgcn_raw_buffer_load_b32(drs, t + j >= 0 ? (uint32_t)(t + j) * 4u : kOOB, 0, LP);
+    lo = u32x4{d[0], d[1], d[2], d[3]};
+    hi = d[4];
+}
+
+template <int LP>
+__device__ __forceinline__ void build_load_body(__amdgpu_buffer_rsrc_t drs, const BuildSeg& S, uint32_t lane,
+                                                uint32_t r, u32x4& lo, uint32_t& hi) {
+    const bool live = r < S.rows;
+    const uint32_t a = (uint32_t)((int32_t)(r * kRow + lane * 16u) + S.sh0) & ~3u;  // ≥ 0 (hdr_end ≤ 1008)
+    lo = bld16<LP != 0>(drs, live ? a : kOOB);
+    hi = __builtin_amdgcn_raw_buffer_load_b32(drs, live && S.sh ? a + 16u : kOOB, 0, LP);
+}
+
+// Compose, sum and store row r of the wire image.
+template <int SP>
+__device__ __forceinline__ uint32_t build_row(const BuildSeg& S, __amdgpu_buffer_rsrc_t ors,
+                                              const uint8_t* __restrict__ opts, uint32_t lane, uint32_t r, u32x4 lo,
+                                              uint32_t hi, uint32_t acc) {
+    const uint32_t pos0 = r * kRow + lane * 16u;
+    u32x4 x = S.sh ? realign(lo, hi, S.sh) : lo;
+    if (r * kRow < S.hdr_end || (r + 1) * kRow > S.wire)  // keep payload bytes [hdr_end, wire) only
+        x = keep_bytes(x, min(max((int32_t)S.hdr_end - (int32_t)pos0, 0), 16),
+                       min(max((int32_t)S.wire - (int32_t)pos0, 0), 16));
+    if (r == 0) {  // header bytes 0-19
+        x.x |= lane == 0 ? S.D0 : lane == 1 ? S.D4 : 0u;
+        x.y |= lane == 0 ? S.D1 : 0u;
+        x.z |= lane == 0 ? S.D2 : 0u;
+        x.w |= lane == 0 ? S.D3 : 0u;
+    }
+    if (S.optlen && r * kRow < 20u + S.optlen) {  // option bytes [20, 20 + optlen): rare, byte by byte
+        const uint32_t lo_b = max(pos0, 20u), hi_b = min(pos0 + 16u, 20u + S.optlen);
+#pragma unroll 1
+        for (uint32_t pos = lo_b; pos < hi_b; ++pos) {
+            const uint32_t v = (uint32_t)opts[S.ob + (pos - 20u)] << (8 * (pos & 3));
+            const uint32_t j = (pos - pos0) >> 2;
+            x.x |= j == 0 ? v : 0u;
+            x.y |= j == 1 ? v : 0u;
+            x.z |= j == 2 ? v : 0u;
+            x.w |= j == 3 ? v : 0u;
+        }
+    }
+    acc = sad4(x, acc);
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    typedef uint32_t v3u __attribute__((ext_vector_type(3)));
+    const bool d4 = r == 0 && lane == 1;  // this chunk holds dword 4: store its other three now
+    __builtin_amdgcn_raw_buffer_store_b128(v4u{x.x, x.y, x.z, x.w}, ors, d4 ? kOOB : pos0, 0, SP);
+    if (r == 0) __builtin_amdgcn_raw_buffer_store_b96(v3u{x.y, x.z, x.w}, ors, d4 ? 20u : kOOB, 0, SP);
+    return acc;
+}
+
+template <int LP, int SP>
 __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const uint8_t* __restrict__ opts,
                                                            const uint64_t* __restrict__ opt_off,
                                                            const uint8_t* __restrict__ data,
@@ -929,78 +1018,98 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
                                                            const uint32_t* __restrict__ partial, uint64_t n,
                                                            uint8_t* __restrict__ out,
                                                            const uint64_t* __restrict__ out_off,
-                                                           uint16_t* __restrict__ raw_out) {
+                                                           uint16_t* __restrict__ raw_out, uint32_t group) {
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const uint64_t data_end4 = (data_bytes + 3) & ~3ull;  // last payload dword reads whole
-    const TaskIter it = task_iter(n, wave, 1);
-    for (uint64_t i = it.next; i < it.end; i += it.step) {
-        const uint32_t D0 = bswap16u(h.src_port[i]) | (bswap16u(h.dst_port[i]) << 16);
-        const uint32_t D1 = bswap32u(h.seq[i]), D2 = bswap32u(h.ack[i]);
-        const uint32_t D3 = (uint32_t)h.offset[i] | ((uint32_t)h.ctl[i] << 8) | (bswap16u(h.window[i]) << 16);
-        const uint32_t D4 = bswap16u(h.urgent[i]) << 16;  // checksum field (bytes 16-17) = 0 for the sum
-        const uint64_t ob = opt_off ? opt_off[i] : 0;
-        const uint32_t optlen = opt_off ? (uint32_t)(opt_off[i + 1] - ob) : 0u;
-        const uint32_t hdr_end = 20u + optlen + (optlen ? (20u + optlen) % 4u : 0u);
-        const uint64_t db = data_off[i];
-        const uint64_t dlen = data_off[i + 1] - db;
-        const uint64_t wire = hdr_end + dlen;
-        uint8_t* o = out + out_off[i];
-        const uint64_t nbytes4 = (wire + 3) & ~3ull;  // whole dwords this segment owns
-        // Payload descriptor based at the segment's first payload dword.
-        const uint64_t dbase = db & ~3ull;
-        const __amdgpu_buffer_rsrc_t drs = make_rsrc(data + dbase, data_end4 - dbase);
-        auto hdr_byte = [&](uint32_t pos) -> uint32_t {  // pos < 20
-            const uint32_t k = pos >> 2, sh = 8 * (pos & 3);
-            const uint32_t w = k == 0 ? D0 : k == 1 ? D1 : k == 2 ? D2 : k == 3 ? D3 : D4;
-            return (w >> sh) & 0xFFu;
+    const uint64_t data_end4 = (data_bytes + 3) & ~3ull;  // the last payload dword reads whole
+    const uint64_t ngroups = (n + group - 1) / group;
+    const TaskIter it = task_iter(ngroups, wave, 1);
+    for (uint64_t g = it.next; g < it.end; g += it.step) {
+        const uint64_t g0 = g * group;
+        const uint32_t cnt = (uint32_t)min((uint64_t)group, n - g0);
+        // Per-lane metadata of segment g0 + lane (lanes past cnt repeat the last one).
+        const uint64_t i = g0 + min(lane, cnt - 1);
+        const uint32_t mD0 = bswap16u(h.src_port[i]) | (bswap16u(h.dst_port[i]) << 16);
+        const uint32_t mD1 = bswap32u(h.seq[i]), mD2 = bswap32u(h.ack[i]);
+        const uint32_t mD3 = (uint32_t)h.offset[i] | ((uint32_t)h.ctl[i] << 8) | (bswap16u(h.window[i]) << 16);
+        const uint32_t mD4 = bswap16u(h.urgent[i]) << 16;  // checksum field (bytes 16-17) = 0 for the sum
+        const uint64_t mdb = data_off[i], mde = data_off[i + 1], moo = out_off[i];
+        const uint32_t mpart = partial ? partial[i] : 0u;
+        const uint64_t mob = opt_off ? opt_off[i] : 0;
+        const uint32_t moptlen = opt_off ? (uint32_t)(opt_off[i + 1] - mob) : 0u;
+        const uint32_t mhdr = 20u + moptlen + (moptlen ? (20u + moptlen) % 4u : 0u);  // tcp.go:118-121
+        const uint32_t mwire = mhdr + (uint32_t)(mde - mdb);                             // < 2^31
+        auto seg_at = [&](uint32_t k, BuildSeg& S, __amdgpu_buffer_rsrc_t& drs, __amdgpu_buffer_rsrc_t& ors) {
+            S.D0 = __builtin_amdgcn_readlane(mD0, k);
+            S.D1 = __builtin_amdgcn_readlane(mD1, k);
+            S.D2 = __builtin_amdgcn_readlane(mD2, k);
+            S.D3 = __builtin_amdgcn_readlane(mD3, k);
+            S.D4 = __builtin_amdgcn_readlane(mD4, k);
+            S.optlen = __builtin_amdgcn_readlane(moptlen, k);
+            S.hdr_end = __builtin_amdgcn_readlane(mhdr, k);
+            S.wire = __builtin_amdgcn_readlane(mwire, k);
+            S.nb4 = (S.wire + 3u) & ~3u;
+            S.rows = (S.nb4 + kRow - 1) / kRow;
+            S.ob = readlane64(mob, k);
+            const uint64_t db = readlane64(mdb, k);
+            S.sh0 = (int32_t)(db & 3u) - (int32_t)S.hdr_end;
+            S.sh = (uint32_t)S.sh0 & 3u;
+            const uint64_t dbase = db & ~3ull;
+            drs = make_rsrc(data + dbase, data_end4 - dbase);
+            ors = make_rsrc(out + readlane64(moo, k), S.nb4);
         };
-        uint32_t acc = 0;
-        for (uint64_t r0 = 0; r0 * kRow < nbytes4; ++r0) {
-            const uint64_t pos0 = r0 * kRow + lane * 16;
-            if (pos0 >= nbytes4) continue;
-            u32x4 x;
-            if (pos0 >= hdr_end && pos0 + 16 <= wire) {
-                // Payload fast path: 16 source bytes at any alignment.
-                const uint64_t s = (db & 3u) + (pos0 - hdr_end);  // relative to dbase (< 2^31)
-                const uint32_t a = (uint32_t)(s & ~3ull), sh = (uint32_t)(s & 3u);
-                typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-                const v4u w = __builtin_amdgcn_raw_buffer_load_b128(drs, a, 0, 2);
-                const uint32_t w4 = __builtin_amdgcn_raw_buffer_load_b32(drs, a + 16, 0, 2);
-                x.x = __builtin_amdgcn_alignbyte(w.y, w.x, sh);
-                x.y = __builtin_amdgcn_alignbyte(w.z, w.y, sh);
-                x.z = __builtin_amdgcn_alignbyte(w.w, w.z, sh);
-                x.w = __builtin_amdgcn_alignbyte(w4, w.w, sh);
-            } else {
-                // Header / options / padding / payload edges / slack: byte by byte.
-                uint32_t b[16];
+        auto seg_done = [&](uint32_t k, const BuildSeg& S, __amdgpu_buffer_rsrc_t ors, uint32_t acc) {
+            const uint32_t tot = wave_sum(acc);
+            const uint32_t raw = finish(tot, true, __builtin_amdgcn_readlane(mpart, k));  // images are 4-aligned
+            __builtin_amdgcn_raw_buffer_store_b32(S.D4 | bswap16u(~raw & 0xFFFFu), ors, lane == 0 ? 16u : kOOB, 0, SP);
+            if (raw_out && lane == 0) raw_out[g0 + k] = (uint16_t)raw;
+        };
+        uint32_t k = 0;
+        while (k < cnt) {
+            BuildSeg S;
+            __amdgpu_buffer_rsrc_t drs, ors;
+            seg_at(k, S, drs, ors);
+            uint32_t acc = 0;
+            if (S.hdr_end <= kRow - 16u) {
+                constexpr uint32_t R = kBuildRows;
+                // batch 0: the header row + rows 1..R-1, all loads in flight
+                u32x4 lo[R];
+                uint32_t hi[R];
+                build_load_head<LP>(drs, S, lane, lo[0], hi[0]);
 #pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    const uint64_t pos = pos0 + j;
-                    uint32_t v = 0;
-                    if (pos < 20) v = hdr_byte((uint32_t)pos);
-                    else if (pos < 20u + optlen) v = opts[ob + (pos - 20)];
-                    else if (pos >= hdr_end && pos < wire) v = data[db + (pos - hdr_end)];
-                    b[j] = v;
+                for (uint32_t rr = 1; rr < R; ++rr) build_load_body<LP>(drs, S, lane, rr, lo[rr], hi[rr]);
+#pragma unroll
+                for (uint32_t rr = 0; rr < R; ++rr)
+                    asm volatile("" : "+v"(lo[rr].x), "+v"(lo[rr].y), "+v"(lo[rr].z), "+v"(lo[rr].w), "+v"(hi[rr]));
+#pragma unroll
+                for (uint32_t rr = 0; rr < R; ++rr)
+                    if (rr < S.rows) acc = build_row<SP>(S, ors, opts, lane, rr, lo[rr], hi[rr], acc);
+                acc = fold32(acc);
+                for (uint32_t r0 = R; r0 < S.rows; r0 += R) {  // long segments: further batches
+#pragma unroll
+                    for (uint32_t rr = 0; rr < R; ++rr) build_load_body<LP>(drs, S, lane, r0 + rr, lo[rr], hi[rr]);
+#pragma unroll
+                    for (uint32_t rr = 0; rr < R; ++rr)
+                        asm volatile("" : "+v"(lo[rr].x), "+v"(lo[rr].y), "+v"(lo[rr].z), "+v"(lo[rr].w), "+v"(hi[rr]));
+#pragma unroll
+                    for (uint32_t rr = 0; rr < R; ++rr)
+                        if (r0 + rr < S.rows) acc = build_row<SP>(S, ors, opts, lane, r0 + rr, lo[rr], hi[rr], acc);
+                    acc = fold32(acc);
                 }
-                x.x = b[0] | b[1] << 8 | b[2] << 16 | b[3] << 24;
-                x.y = b[4] | b[5] << 8 | b[6] << 16 | b[7] << 24;
-                x.z = b[8] | b[9] << 8 | b[10] << 16 | b[11] << 24;
-                x.w = b[12] | b[13] << 8 | b[14] << 16 | b[15] << 24;
+            } else {
+                // options longer than ~1 KiB (not real TCP; the API allows it): every row clamps per dword
+                for (uint32_t r = 0; r < S.rows; ++r) {
+                    const int32_t t = ((int32_t)(r * kRow + lane * 16u) + S.sh0) >> 2;
+                    uint32_t d[5];
+#pragma unroll
+                    for (int j = 0; j < 5; ++j)
+                        d[j] = __builtin_amdgcn_raw_buffer_load_b32(drs, t + j >= 0 ? (uint32_t)(t + j) * 4u : kOOB, 0,
+                                                                     2);
+                    acc = fold32(build_row<SP>(S, ors, opts, lane, r, u32x4{d[0], d[1], d[2], d[3]}, d[4], acc));
+                }
             }
-            acc = sad4(x, acc);
-            uint32_t* od = reinterpret_cast<uint32_t*>(o + pos0);
-            const uint64_t left = nbytes4 - pos0;  // ≥ 4, multiple of 4
-            if (pos0 != 16 || r0 != 0) od[0] = x.x;  // dword 4 (bytes 16-19) is stored last
-            if (left > 4) od[1] = x.y;
-            if (left > 8) od[2] = x.z;
-            if (left > 12) od[3] = x.w;
-        }
-        const uint32_t tot = wave_sum(fold32(acc));
-        if (lane == 0) {
-            const uint32_t raw = finish(tot, true, partial ? partial[i] : 0u);  // o is 4-aligned (even)
-            *reinterpret_cast<uint32_t*>(o + 16) = D4 | bswap16u(~raw & 0xFFFFu);
-            if (raw_out) raw_out[i] = (uint16_t)raw;
+            seg_done(k, S, ors, acc);
+            k += 1;
         }
     }
 }
@@ -1009,40 +1118,61 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
 // IPv4 header checksum (RFC 791 §3.1 with the RFC 1071 sum), one thread per
 // packet: headers are 20-60 bytes, too short for a wave each. Packet i's header
 // starts at base + i*stride + hdr_off (any alignment, e.g. 14 behind an
-// Ethernet header) and is IHL*4 bytes (IHL = low nibble of byte 0). The thread
-// loads the ≤ 16 aligned dwords covering it with all loads in flight, masks to
-// the header (and, in fill mode, the checksum field at bytes 10-11), and applies
-// the same LE-half-sum / byte-swap rule as the segment kernels.
-// mode 0: out = raw sum over the header as it stands (valid iff 0xFFFF).
-// mode 1: out = raw sum with bytes 10-11 taken as zero; writes ~raw there.
+// Ethernet header) and is IHL*4 bytes (IHL = low nibble of byte 0).
+// A block takes 256 consecutive packets through one buffer descriptor based at
+// the first header (block-uniform, 32-bit per-lane offsets). Every lane issues
+// the loads of its header's first 20 bytes unconditionally (5 aligned dwords,
+// a 6th when the header is not dword-aligned); the dwords after those are loaded
+// only when some lane of the wave has IHL > 5 (wave-uniform branch), each with
+// an out-of-range offset beyond its own header, so no exec-masked load stalls
+// the wave. Then the LE-half-sum / byte-swap rule of the segment kernels.
+// MODE 0: out = raw sum over the header as it stands (valid iff 0xFFFF).
+// MODE 1: out = raw sum with bytes 10-11 taken as zero; writes ~raw there.
 // A malformed header (IHL < 5, or longer than the stride) gets out = 0 and is
 // not written.
 // ---------------------------------------------------------------------------
+template <int MODE>
 __global__ __launch_bounds__(kBlock) void ipv4_hdr_kernel(uint8_t* __restrict__ base, uint64_t stride,
-                                                          uint32_t hdr_off, uint64_t n, int mode,
-                                                          uint16_t* __restrict__ out) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        uint8_t* p = base + i * stride + hdr_off;
-        const uint32_t len = (uint32_t)(p[0] & 15u) * 4u;
-        const bool ok = len >= 20 && (stride == 0 || hdr_off + len <= stride);
-        const uint32_t head = (uint32_t)((uintptr_t)p & 3u);
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(p - head);
-        const uint32_t nd = ok ? (head + len + 3u) >> 2 : 0u;
+                                                          uint32_t hdr_off, uint64_t n, uint16_t* __restrict__ out) {
+    for (uint64_t c0 = (uint64_t)blockIdx.x * kBlock; c0 < n; c0 += (uint64_t)gridDim.x * kBlock) {
+        const uint32_t cnt = (uint32_t)min((uint64_t)kBlock, n - c0);
+        uint8_t* first = base + c0 * stride + hdr_off;
+        uint8_t* cbase = reinterpret_cast<uint8_t*>((uintptr_t)first & ~(uintptr_t)3);
+        const uint32_t lead = (uint32_t)(first - cbase);
+        // the last header may run 60 bytes; per-lane offsets never pass their own header
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(cbase, (uint64_t)(cnt - 1) * stride + lead + 64u);
+        const uint32_t t = threadIdx.x;
+        const bool live = t < cnt;
+        const uint32_t rel = (live ? t : 0u) * (uint32_t)stride + lead;
+        const uint32_t head = rel & 3u, a = rel - head;
         uint32_t d[16];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) d[k] = (uint32_t)k < nd ? __builtin_nontemporal_load(w + k) : 0u;
+        for (int k = 0; k < 5; ++k) d[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, live ? a + 4u * k : kOOB, 0, 0);
+        d[5] = __builtin_amdgcn_raw_buffer_load_b32(rs, live && head ? a + 20u : kOOB, 0, 0);
+        const uint32_t len = ((d[0] >> (8 * head)) & 15u) * 4u;
+        const bool ok = live && len >= 20u && (stride == 0 || hdr_off + len <= stride);
+        const uint32_t nd = ok ? (head + len + 3u) >> 2 : 0u;
+#pragma unroll
+        for (int k = 6; k < 16; ++k) d[k] = 0u;
+        if (__ballot(nd > (head ? 6u : 5u))) {  // options present somewhere in this wave
+            // dword 5 was loaded above only for unaligned headers
+            d[5] |= __builtin_amdgcn_raw_buffer_load_b32(rs, !head && 5u < nd ? a + 20u : kOOB, 0, 0);
+#pragma unroll
+            for (int k = 6; k < 16; ++k)
+                d[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, (uint32_t)k < nd ? a + 4u * k : kOOB, 0, 0);
+        }
         uint32_t acc = 0;
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             // keep window bytes [head, head+len), minus the field in fill mode
             uint32_t m = keep_mask((int32_t)head, (int32_t)(head + len), 4 * k);
-            if (mode == 1) m &= ~keep_mask((int32_t)head + 10, (int32_t)head + 12, 4 * k);
+            if (MODE == 1) m &= ~keep_mask((int32_t)head + 10, (int32_t)head + 12, 4 * k);
             acc = __builtin_amdgcn_sad_u16(d[k] & m, 0u, acc);
         }
+        uint8_t* p = cbase + rel;
         const uint32_t raw = ok ? finish(acc, ((uintptr_t)p & 1u) == 0, 0u) : 0u;
-        if (out) out[i] = (uint16_t)raw;
-        if (mode == 1 && ok) {
+        if (out && live) out[c0 + t] = (uint16_t)raw;
+        if (MODE == 1 && ok) {
             const uint16_t f = (uint16_t)~raw;
             p[10] = (uint8_t)(f >> 8);
             p[11] = (uint8_t)f;
@@ -1433,11 +1563,27 @@ hipError_t launch_verify_mask(const uint16_t* raw, uint64_t n, uint64_t* mask, u
 
 hipError_t launch_tcp_build(const TcpHdrSoA& h, const uint8_t* opts, const uint64_t* opt_off, const uint8_t* data,
                             const uint64_t* data_off, uint64_t data_bytes, const uint32_t* partial, uint64_t n,
-                            uint8_t* out, const uint64_t* out_off, uint16_t* raw, uint32_t max_blocks, hipStream_t st) {
-    const uint64_t want = (n + kWavesPerBlock - 1) / kWavesPerBlock;
+                            uint8_t* out, const uint64_t* out_off, uint16_t* raw, uint32_t max_blocks, int policy,
+                            hipStream_t st) {
+    // Group size: up to 64 segments per wave task, fewer when n would leave waves idle.
+    const uint64_t waves = (uint64_t)max_blocks * kWavesPerBlock;
+    const uint32_t group = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, (n + waves - 1) / waves));
+    const uint64_t tasks = (n + group - 1) / group;
+    const uint64_t want = (tasks + kWavesPerBlock - 1) / kWavesPerBlock;
     const uint32_t grid = (uint32_t)(want < max_blocks ? want : max_blocks);
-    hipLaunchKernelGGL(tcp_build_kernel, dim3(grid), dim3(kBlock), 0, st, h, opts, opt_off, data, data_off, data_bytes,
-                       partial, n, out, out_off, raw);
+    // policy: 0/2 = default cache policy (measured best: segment-boundary lines stay in L2 for
+    // the neighbour segment's load and partial-line stores merge there), 1 = nt loads and
+    // stores, 3 = nt loads + plain stores, 4 = plain loads + nt stores
+#define NSX_BUILD(LP, SP)                                                                                         \
+    hipLaunchKernelGGL((tcp_build_kernel<LP, SP>), dim3(grid), dim3(kBlock), 0, st, h, opts, opt_off, data, data_off, \
+                       data_bytes, partial, n, out, out_off, raw, group)
+    switch (policy) {
+        case 1: NSX_BUILD(2, 2); break;
+        case 3: NSX_BUILD(2, 0); break;
+        case 4: NSX_BUILD(0, 2); break;
+        default: NSX_BUILD(0, 0); break;
+    }
+#undef NSX_BUILD
     return hipGetLastError();
 }
 
@@ -1445,7 +1591,8 @@ hipError_t launch_ipv4_hdr(uint8_t* base, uint64_t stride, uint32_t hdr_off, uin
                            uint32_t max_blocks, hipStream_t st) {
     const uint64_t want = (n + kBlock - 1) / kBlock;
     const uint32_t grid = (uint32_t)(want < max_blocks ? want : max_blocks);
-    hipLaunchKernelGGL(ipv4_hdr_kernel, dim3(grid), dim3(kBlock), 0, st, base, stride, hdr_off, n, mode, out);
+    if (mode == 1) hipLaunchKernelGGL(ipv4_hdr_kernel<1>, dim3(grid), dim3(kBlock), 0, st, base, stride, hdr_off, n, out);
+    else hipLaunchKernelGGL(ipv4_hdr_kernel<0>, dim3(grid), dim3(kBlock), 0, st, base, stride, hdr_off, n, out);
     return hipGetLastError();
 }
 

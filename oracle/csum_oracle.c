@@ -213,6 +213,47 @@ ORACLE_EXPORT uint8_t oracle_compute_offset(const oracle_segment* s) {
     return (uint8_t)((off + 3) / 4);
 }
 
+/* Go-faithful sender loop for f1, option-less segments:
+ * per segment i, build segment{fields, data} with checksum 0, s.bytes()
+ * (tcp.go:98-128, a fresh allocation), sum = computeChecksum(pseudo_i)
+ * (tcp.go:72-95, oracle_go_checksum: allocate + concatenate + serial loop),
+ * store ^sum at bytes 16-17 (tcp.go:68,110) and copy the wire image to
+ * out + out_off[i] (the transport's send buffer). pseudo: n×pseudo_len bytes or
+ * NULL. raw (nullable) receives the sums. bench.py's cpu_baseline leg for
+ * workload 6 and the checker for the sampled GPU output. Returns 0, or -1 if an
+ * allocation failed (the Go code would panic). */
+ORACLE_EXPORT int oracle_go_tcp_build_batch(const uint16_t* src_port, const uint16_t* dst_port,
+                                            const uint32_t* seq_num, const uint32_t* ack_num,
+                                            const uint8_t* offset, const uint8_t* control,
+                                            const uint16_t* window, const uint16_t* urgent_ptr,
+                                            const uint8_t* data, const uint64_t* data_off,
+                                            const uint8_t* pseudo, size_t pseudo_len, uint64_t n,
+                                            uint8_t* out, const uint64_t* out_off, uint16_t* raw) {
+    for (uint64_t i = 0; i < n; i++) {
+        oracle_segment s;
+        memset(&s, 0, sizeof s);
+        s.src_port = src_port[i]; s.dst_port = dst_port[i];
+        s.seq_num = seq_num[i]; s.ack_num = ack_num[i];
+        s.offset = offset[i]; s.control = control[i];
+        s.window = window[i]; s.urgent_ptr = urgent_ptr[i];
+        s.data = data + data_off[i];
+        s.data_len = (size_t)(data_off[i + 1] - data_off[i]);
+        const size_t len = oracle_segment_bytes(&s, NULL, 0);
+        uint8_t* b = (uint8_t*)malloc(len ? len : 1);
+        if (!b) return -1;
+        oracle_segment_bytes(&s, b, len);
+        const uint32_t sum = oracle_go_checksum(pseudo ? pseudo + i * pseudo_len : NULL, pseudo ? pseudo_len : 0, b, len);
+        if (sum > 0xFFFFu) { free(b); return -1; }
+        const uint16_t f = (uint16_t)~sum;
+        b[16] = (uint8_t)(f >> 8);
+        b[17] = (uint8_t)f;
+        memcpy(out + out_off[i], b, len);
+        free(b);
+        if (raw) raw[i] = (uint16_t)sum;
+    }
+    return 0;
+}
+
 /* ---- synthetic data: splitmix64 stream, counter-based ---- */
 static inline uint64_t splitmix64_at(uint64_t seed, uint64_t i) {
     uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;

@@ -246,6 +246,8 @@ def c_oracle():
         lib.oracle_go_batch_fixed.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
                                               u8p, ctypes.c_size_t, u8p]
         lib.oracle_splitmix64_fill.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]
+        lib.oracle_go_tcp_build_batch.argtypes = [u8p] * 10 + [u8p, ctypes.c_size_t, ctypes.c_uint64, u8p, u8p, u8p]
+        lib.oracle_go_tcp_build_batch.restype = ctypes.c_int
         _c = lib
     return _c
 
@@ -254,6 +256,30 @@ def _ptr(a):
     if a is None:
         return None
     return a.ctypes.data_as(ctypes.c_void_p)
+
+
+TCP_FIELDS = ("src_port", "dst_port", "seq_num", "ack_num", "offset", "control", "window", "urgent_ptr")
+TCP_FIELD_DTYPES = (np.uint16, np.uint16, np.uint32, np.uint32, np.uint8, np.uint8, np.uint16, np.uint16)
+
+
+def c_go_tcp_build(fields: dict, data: np.ndarray, data_off: np.ndarray, out_off: np.ndarray,
+                   pseudo: np.ndarray | None = None):
+    """Go-faithful sender loop (oracle_go_tcp_build_batch): option-less segments
+    serialised (tcp.go:98-128), checksummed over pseudo_i ‖ bytes (tcp.go:72-95),
+    ^sum stored at 16-17. pseudo: (n, k) uint8 or None. Returns (wire, raw)."""
+    n = data_off.size - 1
+    cols = [np.ascontiguousarray(fields[k], dt) for k, dt in zip(TCP_FIELDS, TCP_FIELD_DTYPES)]
+    data = np.ascontiguousarray(data, np.uint8)
+    data_off = np.ascontiguousarray(data_off, np.uint64)
+    out_off = np.ascontiguousarray(out_off, np.uint64)
+    out = np.zeros(int(out_off[-1]), np.uint8)
+    raw = np.empty(n, np.uint16)
+    pl = 0 if pseudo is None else pseudo.shape[1]
+    ps = None if pseudo is None else np.ascontiguousarray(pseudo, np.uint8)
+    rc = c_oracle().oracle_go_tcp_build_batch(*[_ptr(c) for c in cols], _ptr(data), _ptr(data_off), _ptr(ps), pl, n,
+                                              _ptr(out), _ptr(out_off), _ptr(raw))
+    assert rc == 0
+    return out, raw
 
 
 def c_go_checksum(prefix: bytes, seg: bytes) -> int:

@@ -478,6 +478,28 @@ def test_ipv4_header_checksum_verify_and_fill(stride, hdr_off):
     assert (again[valid] == 0xFFFF).all()
 
 
+@pytest.mark.parametrize("stride,hdr_off", [(20, 0), (22, 2), (23, 3)])
+def test_ipv4_dense_headers_end_at_allocation_end(stride, hdr_off):
+    """Packed IHL=5 headers (header-split ring), the last one ending exactly at
+    the allocation's last byte: no read past a header's own 20 bytes."""
+    rng = np.random.default_rng(stride)
+    n = 70_001
+    buf = rng.integers(0, 256, n * stride, dtype=np.uint8)
+    buf[hdr_off::stride] = 0x45
+    d = dev(buf[: (n - 1) * stride + hdr_off + 20])
+    nsx.ipv4_hdr_csum_dev(d, stride, n, hdr_off=hdr_off, mode=1)
+    got = host(d)
+    want = buf[: (n - 1) * stride + hdr_off + 20].copy()
+    for i in list(range(0, n, 1013)) + [n - 1]:
+        b0 = i * stride + hdr_off
+        h = bytearray(want[b0:b0 + 20].tobytes())
+        h[10:12] = b"\0\0"
+        f = O.field_value(O.go_checksum(b"", bytes(h)))
+        assert got[b0 + 10] == f >> 8 and got[b0 + 11] == f & 0xFF, i
+    raw = u16(nsx.ipv4_hdr_csum_dev(d, stride, n, hdr_off=hdr_off, mode=0))
+    assert (raw == 0xFFFF).all()
+
+
 def test_ipv4_header_kat():
     h = np.frombuffer(bytes.fromhex("450000730000400040110000c0a80001c0a800c7"), np.uint8).copy()
     d = dev(h)

@@ -74,5 +74,8 @@ def main(tag, cfg, kernel_substr="csum"):
     print("\n".join(lines))
 
 
+KERNEL_OF_CONFIG = {6: "tcp_build", 7: "ipv4_hdr"}  # bench.py workloads beyond the checksum configs
+
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]), *(sys.argv[3:4]))
+    c = int(sys.argv[2])
+    main(sys.argv[1], c, *(sys.argv[3:4] or [KERNEL_OF_CONFIG.get(c, "csum")]))
