@@ -9,8 +9,15 @@ GPU (torchrun), each checksumming its own batch: the path shards with no
 exchange, so there is no data-path collective and scaling is
 weak. value = Σ bytes over all ranks ÷ max over ranks of the timed region.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5|6|7]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Configs 2-5 are BASELINE.json's device-resident configurations (2 is the
+headline and the default). Configs 6 and 7 measure SURVEY.md §8's next rows to
+the same bar, each with its own metric string: 6 = the fused sender pass
+(nsx_tcp_build_dev: segment.bytes() + computeChecksum + field write,
+tcp.go:98-128/:68-71) over 1M 1500 B wire images; 7 = IPv4 header checksum
+verify (nsx_ipv4_hdr_csum_dev) over 64M packed 20 B headers.
 
 Printed by rank 0: one JSON line with the contract fields plus
   roofline     — dominant kernel: algorithmic bytes per launch ÷ its mean

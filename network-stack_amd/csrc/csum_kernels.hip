@@ -909,13 +909,12 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
 
 // ---------------------------------------------------------------------------
 // Fused sender path: segment.bytes() + computeChecksum +
-// field write in one pass (transport/tcp/tcp.go:98-128 and :68-71). One wave
-// per segment writes the wire image — 20-byte BE header from SoA fields,
-// options, the reference's `remainder` padding (tcp.go:118-121), payload — as
+// field write in one pass (transport/tcp/tcp.go:98-128 and :68-71). Each wire
+// image — the 20-byte BE header built from SoA fields, options, the
+// reference's `remainder` padding (tcp.go:118-121), the payload — is written as
 // whole dwords at out + out_off[i] (4-aligned; up to 3 slack bytes after the
-// image are zero-filled), summing the dwords it writes (checksum field = 0),
-// then stores ~raw into bytes 16-17 with the last header dword. Payload bytes
-// at any source alignment are realigned with v_alignbyte_b32.
+// image are zero-filled) while its dwords are summed with the checksum field
+// at 0; ~raw then goes into bytes 16-17.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t bswap16u(uint32_t v) { return ((v & 0xFFu) << 8) | ((v >> 8) & 0xFFu); }
 __device__ __forceinline__ uint32_t bswap32u(uint32_t v) {
@@ -1119,8 +1118,9 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
 // packet: headers are 20-60 bytes, too short for a wave each. Packet i's header
 // starts at base + i*stride + hdr_off (any alignment, e.g. 14 behind an
 // Ethernet header) and is IHL*4 bytes (IHL = low nibble of byte 0).
-// A block takes 256 consecutive packets through one buffer descriptor based at
-// the first header (block-uniform, 32-bit per-lane offsets). Every lane issues
+// A block takes 4 × 256 consecutive packets per iteration, each 256 through one
+// buffer descriptor based at their first header (block-uniform, 32-bit per-lane
+// offsets), with the loads of all four in flight together. Every lane issues
 // the loads of its header's first 20 bytes unconditionally (5 aligned dwords,
 // a 6th when the header is not dword-aligned); the dwords after those are loaded
 // only when some lane of the wave has IHL > 5 (wave-uniform branch), each with
@@ -1131,51 +1131,83 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
 // A malformed header (IHL < 5, or longer than the stride) gets out = 0 and is
 // not written.
 // ---------------------------------------------------------------------------
+constexpr int kHdrUnroll = 4;  // 256-header chunks per block iteration, loads of all in flight
+
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void ipv4_hdr_kernel(uint8_t* __restrict__ base, uint64_t stride,
                                                           uint32_t hdr_off, uint64_t n, uint16_t* __restrict__ out) {
-    for (uint64_t c0 = (uint64_t)blockIdx.x * kBlock; c0 < n; c0 += (uint64_t)gridDim.x * kBlock) {
-        const uint32_t cnt = (uint32_t)min((uint64_t)kBlock, n - c0);
-        uint8_t* first = base + c0 * stride + hdr_off;
-        uint8_t* cbase = reinterpret_cast<uint8_t*>((uintptr_t)first & ~(uintptr_t)3);
-        const uint32_t lead = (uint32_t)(first - cbase);
-        // the last header may run 60 bytes; per-lane offsets never pass their own header
-        const __amdgpu_buffer_rsrc_t rs = make_rsrc(cbase, (uint64_t)(cnt - 1) * stride + lead + 64u);
-        const uint32_t t = threadIdx.x;
-        const bool live = t < cnt;
-        const uint32_t rel = (live ? t : 0u) * (uint32_t)stride + lead;
-        const uint32_t head = rel & 3u, a = rel - head;
-        uint32_t d[16];
+    constexpr int U = kHdrUnroll;
+    const uint32_t t = threadIdx.x;
+    for (uint64_t c00 = (uint64_t)blockIdx.x * kBlock * U; c00 < n; c00 += (uint64_t)gridDim.x * kBlock * U) {
+        __amdgpu_buffer_rsrc_t rs[U];
+        uint8_t* cbase[U];
+        uint32_t rel[U], head[U], a[U], len[U], nd[U];
+        bool live[U], ok[U];
+        uint32_t d[U][16];
 #pragma unroll
-        for (int k = 0; k < 5; ++k) d[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, live ? a + 4u * k : kOOB, 0, 0);
-        d[5] = __builtin_amdgcn_raw_buffer_load_b32(rs, live && head ? a + 20u : kOOB, 0, 0);
-        const uint32_t len = ((d[0] >> (8 * head)) & 15u) * 4u;
-        const bool ok = live && len >= 20u && (stride == 0 || hdr_off + len <= stride);
-        const uint32_t nd = ok ? (head + len + 3u) >> 2 : 0u;
-#pragma unroll
-        for (int k = 6; k < 16; ++k) d[k] = 0u;
-        if (__ballot(nd > (head ? 6u : 5u))) {  // options present somewhere in this wave
-            // dword 5 was loaded above only for unaligned headers
-            d[5] |= __builtin_amdgcn_raw_buffer_load_b32(rs, !head && 5u < nd ? a + 20u : kOOB, 0, 0);
-#pragma unroll
-            for (int k = 6; k < 16; ++k)
-                d[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, (uint32_t)k < nd ? a + 4u * k : kOOB, 0, 0);
+        for (int u = 0; u < U; ++u) {  // chunk u: packets [c0, c0 + 256), one descriptor each
+            const uint64_t c0 = c00 + (uint64_t)u * kBlock;
+            const uint32_t cnt = c0 < n ? (uint32_t)min((uint64_t)kBlock, n - c0) : 0u;
+            uint8_t* first = base + min(c0, n - 1) * stride + hdr_off;
+            cbase[u] = reinterpret_cast<uint8_t*>((uintptr_t)first & ~(uintptr_t)3);
+            const uint32_t lead = (uint32_t)(first - cbase[u]);
+            // the last header may run 60 bytes; per-lane offsets never pass their own header
+            rs[u] = make_rsrc(cbase[u], cnt ? (uint64_t)(cnt - 1) * stride + lead + 64u : 0u);
+            live[u] = t < cnt;
+            rel[u] = (live[u] ? t : 0u) * (uint32_t)stride + lead;
+            head[u] = rel[u] & 3u;
+            a[u] = rel[u] - head[u];
+            const u32x4 q = bld16<false>(rs[u], live[u] ? a[u] : kOOB);  // dword-aligned 16 B: one wide load
+            d[u][0] = q.x, d[u][1] = q.y, d[u][2] = q.z, d[u][3] = q.w;
+            d[u][4] = __builtin_amdgcn_raw_buffer_load_b32(rs[u], live[u] ? a[u] + 16u : kOOB, 0, 0);
+            d[u][5] = __builtin_amdgcn_raw_buffer_load_b32(rs[u], live[u] && head[u] ? a[u] + 20u : kOOB, 0, 0);
         }
-        uint32_t acc = 0;
+        bool opts = false;
+        uint32_t acc[U];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            // keep window bytes [head, head+len), minus the field in fill mode
-            uint32_t m = keep_mask((int32_t)head, (int32_t)(head + len), 4 * k);
-            if (MODE == 1) m &= ~keep_mask((int32_t)head + 10, (int32_t)head + 12, 4 * k);
-            acc = __builtin_amdgcn_sad_u16(d[k] & m, 0u, acc);
+        for (int u = 0; u < U; ++u) {
+            len[u] = ((d[u][0] >> (8 * head[u])) & 15u) * 4u;
+            ok[u] = live[u] && len[u] >= 20u && (stride == 0 || hdr_off + len[u] <= stride);
+            nd[u] = ok[u] ? (head[u] + len[u] + 3u) >> 2 : 0u;
+            opts |= nd[u] > (head[u] ? 6u : 5u);
+            acc[u] = 0;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                // keep window bytes [head, head+len), minus the field in fill mode
+                uint32_t m = keep_mask((int32_t)head[u], (int32_t)(head[u] + len[u]), 4 * k);
+                if (MODE == 1) m &= ~keep_mask((int32_t)head[u] + 10, (int32_t)head[u] + 12, 4 * k);
+                acc[u] = __builtin_amdgcn_sad_u16(d[u][k] & m, 0u, acc[u]);
+            }
         }
-        uint8_t* p = cbase + rel;
-        const uint32_t raw = ok ? finish(acc, ((uintptr_t)p & 1u) == 0, 0u) : 0u;
-        if (out && live) out[c0 + t] = (uint16_t)raw;
-        if (MODE == 1 && ok) {
-            const uint16_t f = (uint16_t)~raw;
-            p[10] = (uint8_t)(f >> 8);
-            p[11] = (uint8_t)f;
+        if (__ballot(opts)) {  // options present somewhere in this wave: dwords 5 (aligned headers) .. 15
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                d[u][5] = __builtin_amdgcn_raw_buffer_load_b32(rs[u], !head[u] && 5u < nd[u] ? a[u] + 20u : kOOB, 0, 0);
+#pragma unroll
+                for (int k = 6; k < 16; ++k)
+                    d[u][k] = __builtin_amdgcn_raw_buffer_load_b32(rs[u], (uint32_t)k < nd[u] ? a[u] + 4u * k : kOOB,
+                                                                    0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+#pragma unroll
+                for (int k = 5; k < 16; ++k) {  // dword 5 of an unaligned header was summed above: it reads 0 here
+                    uint32_t m = keep_mask((int32_t)head[u], (int32_t)(head[u] + len[u]), 4 * k);
+                    if (MODE == 1) m &= ~keep_mask((int32_t)head[u] + 10, (int32_t)head[u] + 12, 4 * k);
+                    acc[u] = __builtin_amdgcn_sad_u16(d[u][k] & m, 0u, acc[u]);
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            uint8_t* p = cbase[u] + rel[u];
+            const uint32_t raw = ok[u] ? finish(acc[u], ((uintptr_t)p & 1u) == 0, 0u) : 0u;
+            if (out && live[u]) out[c00 + (uint64_t)u * kBlock + t] = (uint16_t)raw;
+            if (MODE == 1 && ok[u]) {
+                const uint16_t f = (uint16_t)~raw;
+                p[10] = (uint8_t)(f >> 8);
+                p[11] = (uint8_t)f;
+            }
         }
     }
 }
@@ -1589,7 +1621,7 @@ hipError_t launch_tcp_build(const TcpHdrSoA& h, const uint8_t* opts, const uint6
 
 hipError_t launch_ipv4_hdr(uint8_t* base, uint64_t stride, uint32_t hdr_off, uint64_t n, int mode, uint16_t* out,
                            uint32_t max_blocks, hipStream_t st) {
-    const uint64_t want = (n + kBlock - 1) / kBlock;
+    const uint64_t want = (n + (uint64_t)kBlock * kHdrUnroll - 1) / ((uint64_t)kBlock * kHdrUnroll);
     const uint32_t grid = (uint32_t)(want < max_blocks ? want : max_blocks);
     if (mode == 1) hipLaunchKernelGGL(ipv4_hdr_kernel<1>, dim3(grid), dim3(kBlock), 0, st, base, stride, hdr_off, n, out);
     else hipLaunchKernelGGL(ipv4_hdr_kernel<0>, dim3(grid), dim3(kBlock), 0, st, base, stride, hdr_off, n, out);
