@@ -1,11 +1,13 @@
 #!/bin/bash
-# Full GPU evidence pass: parity tests, smoke, bench lines for configs 2-5,
-# end-to-end host rate, rocprofv3 profiles. Every GPU step has its own limit;
-# a timeout/crash (rc >= 124) ends the script.
+# GPU evidence pass, part 1: parity tests, smoke, bench lines for configs 2-7,
+# end-to-end host rate, config-1 loopback. Part 2 (profiles) is
+# tools/gpu_profiles.sh. Every GPU step has its own limit; a timeout/crash
+# (rc >= 124) ends the script.
 set -u
 tag=${1:-r01}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+SKIP_TESTS=${SKIP_TESTS:-0}
 step() {  # step <name> <timeout> cmd...
   local name=$1 t=$2; shift 2
   echo "=== $name"
@@ -16,11 +18,17 @@ step() {  # step <name> <timeout> cmd...
   return 0
 }
 nproc > gpurun_out/host.txt; lscpu | grep -E "Model name|^CPU\(s\)|Thread|Core|Socket" >> gpurun_out/host.txt
-step pytest_gpu 900 python -m pytest tests -q -m gpu
+[ "$SKIP_TESTS" = 1 ] || step pytest_gpu 900 python -m pytest tests -q -m gpu
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench_c2 300 python bench.py
 step bench_c3 300 python bench.py --config 3 --cpu-seconds 5
 step bench_c4 300 python bench.py --config 4 --steps 50 --cpu-seconds 5
 step bench_c5 300 python bench.py --config 5 --steps 20 --cpu-seconds 0
+step bench_c6 300 python bench.py --config 6 --steps 100 --cpu-seconds 5
+step bench_c7 300 python bench.py --config 7 --steps 100 --cpu-seconds 5
 step e2e_host 600 python tools/e2e_host.py
-for c in ${PROFILE_CONFIGS:-2 3 4}; do bash tools/profile.sh $c $tag || exit 1; done
+rm -f gpurun_out/loopback.jsonl
+for m in host batch ring-host ring-gpu; do
+  step loopback_$m 120 network-stack_amd/build/nsx_loopback --mode $m --reps 2000
+  cat gpurun_out/loopback_$m.log >> gpurun_out/loopback.jsonl
+done
