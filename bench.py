@@ -262,6 +262,7 @@ def cpu_baseline(cfg, w, seconds: float) -> dict:
     lib = O.c_oracle()
     torch.cuda.synchronize()
     wire_ok = True  # workload 6 also compares the wire images
+    extra = None
     if cfg["kind"] == "fixed":
         n, L, S = cfg["n"], cfg["seg_len"], cfg["stride"]
         m = min(n, max(1, (256 << 20) // S))  # sample: the first m segments (≤ 256 MiB)
@@ -278,6 +279,7 @@ def cpu_baseline(cfg, w, seconds: float) -> dict:
         dt = time.perf_counter() - t0
         nbytes = reps * m * L
         desc = f"first {m} segments x {L}B of rank 0's batch, {reps} pass(es), Go-faithful serial loop"
+        extra = cpu_extra_lines(lib, sample, S, L, m, out, max(1.0, seconds / 4))
     elif cfg["kind"] == "tcp_build":
         n, P = cfg["n"], cfg["payload"]
         W = P + 20
@@ -339,7 +341,51 @@ def cpu_baseline(cfg, w, seconds: float) -> dict:
         desc = f"first {m} ragged segments of rank 0's batch, {reps} pass(es), Go-faithful serial loop"
     return {"value": round(nbytes / dt / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
             "sample": desc, "seconds": round(dt, 2), "sample_parity_vs_gpu": bool(np.array_equal(out, gpu)) and wire_ok,
-            "host_cpus": os.cpu_count()}
+            "host_cpus": os.cpu_count(), "extra": extra}
+
+
+CPU_THREADS = 16  # the GPU box's CPU share per GPU (nproc shows the whole machine)
+
+
+def cpu_extra_lines(lib, sample, S, L, m, want, seconds):
+    """Reference CPU lines beside the 1-thread Go-faithful value:
+    the same Go-faithful loop on CPU_THREADS threads (contiguous shards, ctypes
+    releases the GIL), and a vectorised u64-accumulate restatement
+    (oracle/csum_cpu_fast.c) on 1 and CPU_THREADS threads. Same sample; each
+    result is checked against the 1-thread output."""
+    import ctypes
+    from concurrent.futures import ThreadPoolExecutor
+    import numpy as np
+    from oracle import csum_oracle as O
+    fast = O.c_fast()
+    out = np.empty(m, np.uint16)
+    ptr = sample.ctypes.data
+
+    def go_mt():
+        def shard(t):
+            lo, hi = m * t // CPU_THREADS, m * (t + 1) // CPU_THREADS
+            lib.oracle_go_batch_fixed(ctypes.c_void_p(ptr + lo * S), S, L, hi - lo, None, 0,
+                                      out[lo:].ctypes.data_as(ctypes.c_void_p))
+        with ThreadPoolExecutor(CPU_THREADS) as ex:
+            list(ex.map(shard, range(CPU_THREADS)))
+
+    def run(fn):
+        t0, reps = time.perf_counter(), 0
+        while True:
+            fn()
+            reps += 1
+            if time.perf_counter() - t0 >= seconds:
+                break
+        dt = time.perf_counter() - t0
+        return {"value": round(reps * m * L / dt / GIB, 3), "unit": "GiB/s", "parity": bool(np.array_equal(out, want))}
+
+    res = {"go_faithful_threads": dict(run(go_mt), cores=CPU_THREADS)}
+    res["optimized_1_thread"] = dict(run(lambda: fast.cpu_fast_batch_fixed(ptr, S, L, m, out.ctypes.data, 1)), cores=1)
+    res["optimized_threads"] = dict(run(lambda: fast.cpu_fast_batch_fixed(ptr, S, L, m, out.ctypes.data,
+                                                                          CPU_THREADS)), cores=CPU_THREADS)
+    res["note"] = ("optimized = oracle/csum_cpu_fast.c (8-byte loads, u64 accumulators, -O3 x86-64-v3): the best-CPU "
+                   "line; go_faithful = the reference's algorithm as written")
+    return res
 
 
 def load_traffic(config_id: int):

@@ -252,6 +252,25 @@ def c_oracle():
     return _c
 
 
+_fast = None
+FAST_PATH = os.path.join(os.path.dirname(LIB_PATH), "libnsx_cpu_fast.so")
+
+
+def c_fast():
+    """Vectorised multi-threaded CPU checksum (oracle/csum_cpu_fast.c): the
+    best-CPU reference line for bench.py, not a checker."""
+    global _fast
+    if _fast is None:
+        if not os.path.exists(FAST_PATH):
+            build_c_oracle(force=True)
+        lib = ctypes.CDLL(FAST_PATH)
+        lib.cpu_fast_batch_fixed.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+                                             ctypes.c_void_p, ctypes.c_int]
+        lib.cpu_fast_batch_fixed.restype = None
+        _fast = lib
+    return _fast
+
+
 def _ptr(a):
     if a is None:
         return None

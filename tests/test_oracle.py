@@ -182,3 +182,17 @@ def test_c_go_tcp_build_matches_segment_model():
         assert raw[i] == r
         s.checksum = O.field_value(r)
         assert wire[int(out_off[i]):int(out_off[i + 1])].tobytes() == s.bytes()
+
+
+def test_cpu_fast_line_matches_go_checksum():
+    """The best-CPU reference line (bench extras) computes the reference's sums."""
+    rng = np.random.default_rng(707)
+    for L in (0, 1, 2, 3, 31, 32, 33, 63, 1500, 1501, 9000):
+        n = 37
+        buf = rng.integers(0, 256, n * (L + 3) + 1, dtype=np.uint8)
+        buf[: L + 3] = 0xFF
+        out = np.empty(n, np.uint16)
+        O.c_fast().cpu_fast_batch_fixed(buf[1:].ctypes.data, L + 3, L, n, out.ctypes.data, 4)
+        for i in range(n):
+            seg = buf[1 + i * (L + 3):1 + i * (L + 3) + L].tobytes()
+            assert out[i] == O.c_go_checksum(b"", seg), (L, i)

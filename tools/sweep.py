@@ -23,6 +23,10 @@ import nsx  # noqa: E402
 
 def variants(kind):
     out = []
+    if kind == "fixed_big":  # config 5: the default buffer kernel's neighbourhood only
+        for bpc, spw, xcd in itertools.product((1, 2, 4), (2, 4), (1, 2, 3)):
+            out.append(dict(kernel=3, blocks_per_cu=bpc, segs_per_wave=spw, nontemporal=1, xcd_map=xcd))
+        return out
     for bpc, rows, nt, xcd in itertools.product((8, 4, 2), (4, 8, 16), (1,), (1, 3)):
         out.append(dict(kernel=1, blocks_per_cu=bpc, stream_rows=rows, nontemporal=nt, xcd_map=xcd))
     for bpc, spw, nt in itertools.product((8, 4, 2), (1, 2, 4), (1,)):
@@ -71,6 +75,8 @@ def main():
         cfg = bench.WORKLOADS[cid]
         w = bench.build_workload(cfg, 0, torch.device("cuda", 0))
         kind = "fixed2" if cfg["kind"] == "fixed" and cfg["seg_len"] <= 4093 else cfg["kind"]
+        if cid == 5:
+            kind = "fixed_big"
         vs = variants(kind)
         if cid in (3, 4):
             vs += [dict(v, block_mode=2) for v in vs if v["kernel"] == 2 and v["blocks_per_cu"] == 8]
