@@ -1212,6 +1212,93 @@ __global__ __launch_bounds__(kBlock) void ipv4_hdr_kernel(uint8_t* __restrict__ 
     }
 }
 
+// Dense header arrays (stride ≤ 64 B, e.g. a header-split ring): a wave takes
+// 64 consecutive headers and streams their contiguous span — up to the last
+// header's 20th byte — with full-width coalesced loads into its LDS slice
+// (one round trip, every line fetched once), then each lane reads its header's
+// dwords from LDS. Option dwords (IHL > 5) are loaded straight from memory,
+// only when some lane of the wave has them. Same results as ipv4_hdr_kernel.
+constexpr uint32_t kHdrDenseMaxStride = 64;
+
+template <int MODE, int ROWS, int U>
+__global__ __launch_bounds__(kBlock) void ipv4_hdr_dense_kernel(uint8_t* __restrict__ base, uint32_t stride,
+                                                                uint32_t hdr_off, uint64_t n,
+                                                                uint16_t* __restrict__ out) {
+    extern __shared__ uint32_t lds_hdr[];
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    uint32_t* my = lds_hdr + wave * (U * ROWS * (kRow / 4));
+    const uint64_t ntasks = (n + kWave - 1) / kWave;
+    const uint64_t wstep = (uint64_t)gridDim.x * kWavesPerBlock;
+    for (uint64_t t0 = (uint64_t)blockIdx.x * kWavesPerBlock + wave; t0 < ntasks; t0 += wstep * U) {
+        // U tasks (64 headers each) per iteration: all their rows in flight at once
+        uint8_t* fa[U];
+        uint32_t cnt[U], lead[U], last[U], nb[U];
+        u32x4 v[U][ROWS];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t task = t0 + (uint64_t)u * wstep;
+            const uint64_t i0 = min(task, ntasks - 1) * kWave;
+            cnt[u] = task < ntasks ? (uint32_t)min((uint64_t)kWave, n - i0) : 0u;
+            uint8_t* first = base + i0 * stride + hdr_off;
+            fa[u] = reinterpret_cast<uint8_t*>((uintptr_t)first & ~(uintptr_t)3);
+            lead[u] = (uint32_t)(first - fa[u]);
+            last[u] = (cnt[u] ? cnt[u] - 1 : 0u) * stride + lead[u];  // last header's offset from fa
+            nb[u] = cnt[u] ? (last[u] + 20u + 3u) & ~3u : 0u;         // every header's first 20 bytes
+            const __amdgpu_buffer_rsrc_t rs = make_rsrc(fa[u], nb[u]);
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r) v[u][r] = bld16<true>(rs, r * kRow + lane * 16u);
+        }
+        __builtin_amdgcn_wave_barrier();  // the previous iteration's LDS reads are done
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r)
+                *reinterpret_cast<u32x4*>(my + (u * ROWS + r) * (kRow / 4) + lane * 4) = v[u][r];
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!cnt[u]) break;
+            const uint32_t* mu = my + u * ROWS * (kRow / 4);
+            const bool live = lane < cnt[u];
+            const uint32_t rel = (live ? lane : 0u) * stride + lead[u];
+            const uint32_t head = rel & 3u, w0 = rel >> 2;
+            uint32_t d[16];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) d[k] = mu[min(w0 + k, nb[u] / 4u - 1u)];
+            const uint32_t len = ((d[0] >> (8 * head)) & 15u) * 4u;
+            const bool ok = live && len >= 20u && hdr_off + len <= stride;
+            const uint32_t nd = ok ? (head + len + 3u) >> 2 : 0u;
+            uint32_t acc = 0;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                uint32_t m = keep_mask((int32_t)head, (int32_t)min(head + len, head + 20u), 4 * k);
+                if (MODE == 1) m &= ~keep_mask((int32_t)head + 10, (int32_t)head + 12, 4 * k);
+                acc = __builtin_amdgcn_sad_u16(d[k] & m, 0u, acc);
+            }
+            if (__ballot(nd > (head ? 6u : 5u))) {  // option bytes [20, len) of some header in this wave
+                const __amdgpu_buffer_rsrc_t ro = make_rsrc(fa[u], (uint64_t)last[u] + 64u);
+#pragma unroll
+                for (int k = 5; k < 16; ++k)
+                    d[k] = __builtin_amdgcn_raw_buffer_load_b32(ro, (uint32_t)k < nd ? (rel - head) + 4u * k : kOOB, 0,
+                                                                 0);
+#pragma unroll
+                for (int k = 5; k < 16; ++k)
+                    acc = __builtin_amdgcn_sad_u16(d[k] & keep_mask((int32_t)head + 20, (int32_t)(head + len), 4 * k),
+                                                   0u, acc);
+            }
+            uint8_t* p = fa[u] + rel;
+            const uint32_t raw = ok ? finish(acc, ((uintptr_t)p & 1u) == 0, 0u) : 0u;
+            if (out && live) out[(t0 + (uint64_t)u * wstep) * kWave + lane] = (uint16_t)raw;
+            if (MODE == 1 && ok) {
+                const uint16_t f = (uint16_t)~raw;
+                p[10] = (uint8_t)(f >> 8);
+                p[11] = (uint8_t)f;
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // IPv4 pseudo-header partials: src(4) dst(4) 0 proto len16 (RFC 9293 §3.1).
 // ---------------------------------------------------------------------------
@@ -1620,9 +1707,36 @@ hipError_t launch_tcp_build(const TcpHdrSoA& h, const uint8_t* opts, const uint6
 }
 
 hipError_t launch_ipv4_hdr(uint8_t* base, uint64_t stride, uint32_t hdr_off, uint64_t n, int mode, uint16_t* out,
-                           uint32_t max_blocks, hipStream_t st) {
+                           uint32_t max_blocks, int kernel, hipStream_t st) {
     const uint64_t want = (n + (uint64_t)kBlock * kHdrUnroll - 1) / ((uint64_t)kBlock * kHdrUnroll);
     const uint32_t grid = (uint32_t)(want < max_blocks ? want : max_blocks);
+    if (stride >= 1 && stride <= kHdrDenseMaxStride && kernel != 1) {
+        // a wave's 64 headers span ≤ 63·stride + 3 + 20 bytes: ROWS 1 KiB rows per task in registers,
+        // U tasks per iteration, an LDS slice of U·ROWS KiB per wave
+        const uint32_t rows = (63u * (uint32_t)stride + 3u + 20u + 3u + kRow - 1) / kRow;
+        const uint64_t tasks = (n + kWave - 1) / kWave;
+        const uint64_t want_d = (tasks + kWavesPerBlock - 1) / kWavesPerBlock;
+        const uint32_t grid_d = (uint32_t)(want_d < max_blocks ? want_d : max_blocks);
+#define NSX_HDR(R, U)                                                                                              \
+    do {                                                                                                           \
+        const size_t lds = (size_t)(R) * (U) * kRow * kWavesPerBlock;                                              \
+        if (mode == 1)                                                                                             \
+            hipLaunchKernelGGL((ipv4_hdr_dense_kernel<1, R, U>), dim3(grid_d), dim3(kBlock), lds, st, base,        \
+                               (uint32_t)stride, hdr_off, n, out);                                                 \
+        else                                                                                                       \
+            hipLaunchKernelGGL((ipv4_hdr_dense_kernel<0, R, U>), dim3(grid_d), dim3(kBlock), lds, st, base,        \
+                               (uint32_t)stride, hdr_off, n, out);                                                 \
+    } while (0)
+        switch (rows) {
+            case 1: NSX_HDR(1, 4); break;
+            case 2: NSX_HDR(2, 2); break;
+            case 3: NSX_HDR(3, 1); break;
+            case 4: NSX_HDR(4, 1); break;
+            default: NSX_HDR(5, 1); break;
+        }
+#undef NSX_HDR
+        return hipGetLastError();
+    }
     if (mode == 1) hipLaunchKernelGGL(ipv4_hdr_kernel<1>, dim3(grid), dim3(kBlock), 0, st, base, stride, hdr_off, n, out);
     else hipLaunchKernelGGL(ipv4_hdr_kernel<0>, dim3(grid), dim3(kBlock), 0, st, base, stride, hdr_off, n, out);
     return hipGetLastError();

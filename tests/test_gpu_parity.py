@@ -29,6 +29,14 @@ def gpu():
         nsx.set_param(p, 0)
 
 
+@pytest.fixture
+def nsx_param():
+    """Set kernel knobs for one test; all reset to defaults afterwards."""
+    yield nsx.set_param
+    for p in nsx.ALL_PARAMS:
+        nsx.set_param(p, 0)
+
+
 def dev(a):
     return torch.from_numpy(np.ascontiguousarray(a)).cuda()
 
@@ -446,8 +454,10 @@ def _ipv4_headers(rng, n, stride, hdr_off):
     return buf, ihl
 
 
-@pytest.mark.parametrize("stride,hdr_off", [(64, 0), (61, 1), (1514, 14), (1500, 0), (60, 0)])
-def test_ipv4_header_checksum_verify_and_fill(stride, hdr_off):
+@pytest.mark.parametrize("kernel", [0, 1])  # 0: default (LDS-staged dense path for stride <= 64), 1: per-thread
+@pytest.mark.parametrize("stride,hdr_off", [(64, 0), (61, 1), (1514, 14), (1500, 0), (60, 0), (40, 3)])
+def test_ipv4_header_checksum_verify_and_fill(stride, hdr_off, kernel, nsx_param):
+    nsx_param(nsx.PARAM_KERNEL, kernel)
     rng = np.random.default_rng(stride * 31 + hdr_off)
     n = 3000
     buf, ihl = _ipv4_headers(rng, n, stride, hdr_off)
@@ -478,10 +488,12 @@ def test_ipv4_header_checksum_verify_and_fill(stride, hdr_off):
     assert (again[valid] == 0xFFFF).all()
 
 
+@pytest.mark.parametrize("kernel", [0, 1])
 @pytest.mark.parametrize("stride,hdr_off", [(20, 0), (22, 2), (23, 3)])
-def test_ipv4_dense_headers_end_at_allocation_end(stride, hdr_off):
+def test_ipv4_dense_headers_end_at_allocation_end(stride, hdr_off, kernel, nsx_param):
     """Packed IHL=5 headers (header-split ring), the last one ending exactly at
     the allocation's last byte: no read past a header's own 20 bytes."""
+    nsx_param(nsx.PARAM_KERNEL, kernel)
     rng = np.random.default_rng(stride)
     n = 70_001
     buf = rng.integers(0, 256, n * stride, dtype=np.uint8)
