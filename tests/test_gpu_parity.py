@@ -442,6 +442,93 @@ def test_config4_256K_x_64KiB_sampled_and_roundtrip():
     assert (ok == 0xFFFF).all()
 
 
+def test_config5_16M_x_1500_per_gpu_sampled():
+    """Config 5's per-GPU batch (16M x 1500 B = 23.4 GiB): every
+    4099th segment plus the segments either side of every 8-way shard boundary
+    against the oracle (bytes regenerated on the CPU from the counter-based
+    stream); every segment re-checked by the block-per-segment kernel."""
+    n, L, seed = 1 << 24, 1500, 0x1071 + 3  # the rank-3 seed
+    t = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    nsx.fill_splitmix64_dev(t, seed)
+    got = u16(nsx.fixed_dev(t, L, L, n, out=torch.empty(n, dtype=torch.int16, device="cuda")))
+    bounds = nsx.shard_plan(n, 8)
+    idx = set(range(0, n, 4099)) | {n - 1}
+    for b in bounds[1:-1]:
+        idx |= {int(b) - 1, int(b)}
+    for i in sorted(idx):
+        seg = O.c_splitmix64(seed, L, i * L)
+        assert got[i] == O.c_fold_checksum(b"", seg.tobytes()), i
+    nsx.set_param(nsx.PARAM_BLOCK_MODE, 2)
+    try:
+        alt = u16(nsx.fixed_dev(t, L, L, n, out=torch.empty(n, dtype=torch.int16, device="cuda")))
+    finally:
+        nsx.set_param(nsx.PARAM_BLOCK_MODE, 0)
+    assert np.array_equal(alt, got)
+
+
+def test_f1_build_1M_segments_full_size_roundtrip():
+    """The bench's f1 workload at full size (1M x 1500 B images): the raw sums the
+    build kernel reports equal an independent checksum of the images it wrote
+    (with the field re-zeroed), every receiver check passes, and sampled images
+    match the Go-faithful oracle byte for byte."""
+    import bench
+    w = bench.build_workload(bench.WORKLOADS[6], 0, torch.device("cuda", 0))
+    w["step"]()
+    n, W = bench.WORKLOADS[6]["n"], bench.WORKLOADS[6]["payload"] + 20
+    raw = u16(w["out"])
+    wire = w["wire"]
+    addrs = host(w["addrs"])
+    part = torch.from_numpy(np.array([O.be_word_sum(O.ipv4_pseudo_header(addrs[0, i].tobytes(), addrs[1, i].tobytes(),
+                                                                         6, W)) for i in range(0, n, 4099)],
+                                     np.uint32).view(np.int32)).cuda()
+    # receiver rule on every image: sum over pseudo ‖ image == 0xFFFF — partials for all segments on the device
+    full_part = nsx.pseudo_ipv4_partial_dev(w["addrs"][0].reshape(-1), w["addrs"][1].reshape(-1),
+                                            torch.full((n,), W, dtype=torch.int32, device="cuda"), 6)
+    ok = u16(nsx.fixed_dev(wire, W, W, n, partial=full_part))
+    assert (ok == 0xFFFF).all()
+    v = wire.view(n, W)
+    v[:, 16:18] = 0
+    again = u16(nsx.fixed_dev(wire, W, W, n, partial=full_part))
+    assert np.array_equal(again, raw)
+    del part
+    # sampled byte-exact images against the oracle (field restored)
+    w["step"]()
+    img = host(wire)
+    fields = {k: host(w["fields"][k]).view(dt) for k, dt in zip(O.TCP_FIELDS, O.TCP_FIELD_DTYPES)}
+    data = host(w["data"])
+    sel = np.arange(0, n, 65537)
+    sf = {k: v_[sel] for k, v_ in fields.items()}
+    d_off = np.zeros(sel.size + 1, np.uint64)
+    d_off[1:] = np.cumsum(np.full(sel.size, W - 20, np.uint64))
+    sdata = np.concatenate([data[i * (W - 20):(i + 1) * (W - 20)] for i in sel])
+    o_off = np.arange(sel.size + 1, dtype=np.uint64) * np.uint64(W)
+    pseudo = np.stack([np.concatenate([addrs[0, i], addrs[1, i], np.array([0, 6, W >> 8, W & 0xFF], np.uint8)])
+                       for i in sel])
+    want, wraw = O.c_go_tcp_build(sf, sdata, d_off, o_off, pseudo)
+    for j, i in enumerate(sel):
+        assert img[i * W:(i + 1) * W].tobytes() == want[j * W:(j + 1) * W].tobytes(), i
+        assert raw[i] == wraw[j], i
+
+
+def test_f3_64M_headers_full_size_fill_verify():
+    """The bench's f3 workload at full size: fill every header's checksum, then
+    every header verifies (0xFFFF); sampled fields match the oracle."""
+    n, H = 1 << 26, 20
+    t = torch.empty(n * H, dtype=torch.uint8, device="cuda")
+    nsx.fill_splitmix64_dev(t, 0x1075)
+    t.view(n, H)[:, 0] = 0x45
+    before = host(t.view(n, H)[::999_983])
+    nsx.ipv4_hdr_csum_dev(t, H, n, mode=1)
+    raw = u16(nsx.ipv4_hdr_csum_dev(t, H, n, mode=0))
+    assert (raw == 0xFFFF).all()
+    after = host(t.view(n, H)[::999_983])
+    for b, a in zip(before, after):
+        h = bytearray(b.tobytes())
+        h[10:12] = b"\0\0"
+        f = O.field_value(O.go_checksum(b"", bytes(h)))
+        assert a[10] == f >> 8 and a[11] == f & 0xFF
+
+
 # ------------------------------------------------------------------ IPv4 header checksum (SURVEY §8 f3)
 
 def _ipv4_headers(rng, n, stride, hdr_off):
