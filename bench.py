@@ -72,6 +72,8 @@ def parse_args(argv=None):
                     help="2-5: BASELINE configs (2 = headline); 6: f1 fused TCP build; 7: f3 IPv4 header verify")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--settle-s", type=float, default=0.5, help="device clock settle time before warmup (setup)")
+    ap.add_argument("--event-every", type=int, default=10,
+                    help="record the per-launch HIP event pair around every N-th timed launch")
     ap.add_argument("--param", action="append", default=[], metavar="NAME=V",
                     help="kernel knob (include/nsx_csum.h NSX_PARAM_*): " + ", ".join(
                         ["blocks_per_cu", "segs_per_wave", "nontemporal", "block_mode", "xcd_map", "kernel",
@@ -122,28 +124,31 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def timed_loop(step, sync, barrier, steps: int, warmup: int, ev_pair=None):
+def timed_loop(step, sync, barrier, steps: int, warmup: int, ev_pair=None, every: int = 1):
     """W untimed steps; then EXACTLY K steps bracketed by barrier + sync on both
-    sides. ev_pair() → (start, end) events recorded around each launch on the
-    launch stream (per-launch kernel duration). Returns (wall_s, [launch_ms])."""
+    sides. ev_pair() → (start, end) events recorded around every `every`-th
+    launch on the launch stream (per-launch kernel duration).
+    Returns (wall_s, [launch_ms])."""
     for _ in range(warmup):
         step()
     sync()
     barrier()
     sync()
-    evs = [ev_pair() for _ in range(steps)] if ev_pair else None
+    every = max(1, every)
+    evs = {i: ev_pair() for i in range(0, steps, every)} if ev_pair else {}
     t0 = time.perf_counter()
     for i in range(steps):
-        if evs:
-            evs[i][0].record()
+        e = evs.get(i)
+        if e:
+            e[0].record()
         step()
-        if evs:
-            evs[i][1].record()
+        if e:
+            e[1].record()
     sync()
     barrier()
     sync()
     wall = time.perf_counter() - t0
-    launch_ms = [a.elapsed_time(b) for a, b in evs] if evs else []
+    launch_ms = [a.elapsed_time(b) for a, b in evs.values()]
     return wall, launch_ms
 
 
@@ -432,7 +437,7 @@ def main(argv=None):
         return torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
     wall, launch_ms = timed_loop(w["step"], torch.cuda.synchronize, lambda: dist.barrier(dev_id),
-                                 args.steps, args.warmup, ev_pair)
+                                 args.steps, args.warmup, ev_pair, args.event_every)
     wall_max = dist.max(wall, device)
     cpu = None
     if dist.world == 1 and args.cpu_seconds > 0:
