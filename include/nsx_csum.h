@@ -215,13 +215,13 @@ const char* nsx_strerror(int code);
 /* Kernel-variant knobs for benchmarking (process-wide; 0 = the default).
  * Not needed for correctness; every variant is bit-exact. */
 #define NSX_PARAM_BLOCKS_PER_CU   1  /* persistent grid, 1..8 blocks of 256 threads per CU (default per path) */
-#define NSX_PARAM_SEGS_PER_WAVE   2  /* per-segment kernels: 1, 2, 4 or 8 segments per wave pass */
+#define NSX_PARAM_SEGS_PER_WAVE   2  /* per-segment kernels: 1, 2, 4 or 8 segments per wave pass; packed-20 B IPv4 header kernel: 1, 2 (default) or 4 tasks in flight per wave */
 #define NSX_PARAM_NONTEMPORAL     3  /* 1 nt loads (default), 2 default-policy loads; nsx_tcp_build_dev: default plain, 1 nt, 3 nt loads + plain stores, 4 plain loads + nt stores */
 #define NSX_PARAM_BLOCK_MODE      4  /* 0 auto (a block per segment when n < 4*CUs), 1 never, 2 always */
-#define NSX_PARAM_XCD_MAP         5  /* task deal: 1 XCD-contiguous regions (default), 2 grid-stride, 3 one contiguous range per wave */
-#define NSX_PARAM_KERNEL          6  /* 1 row-stream, 2 per-segment, 3 buffer-load, 4 prefix-scan (ragged); 0 = per-path default */
+#define NSX_PARAM_XCD_MAP         5  /* task deal: 1 XCD-contiguous regions (default), 2 grid-stride, 3 one contiguous range per wave, 4 byte-balanced contiguous range per wave (ragged scan kernel; its default) */
+#define NSX_PARAM_KERNEL          6  /* 1 row-stream, 2 per-segment, 3 buffer-load, 4 prefix-scan (ragged); IPv4 headers: 1 per-thread, 2 LDS-dense; 0 = per-path default */
 #define NSX_PARAM_STREAM_ROWS     7  /* row-stream / scan: 4, 8 (default) or 16 KiB in flight per wave */
-#define NSX_PARAM_RUN_SEGS        8  /* ragged scan kernel: segments per wave task, 1..63 (default 16) */
+#define NSX_PARAM_RUN_SEGS        8  /* ragged scan kernel: segments per wave task, 1..63 (default 63) */
 int nsx_set_param(int param, int64_t value);
 int nsx_get_param(int param, int64_t* value);
 

@@ -255,10 +255,10 @@ int nsx_ipv4_hdr_csum_dev(void* d_base, uint64_t stride, uint32_t hdr_off, uint6
     const int dev = current_device();
     if (dev < 0) return NSX_ENODEV;
     const DevInfo* di = dev_info(dev);
-    const int64_t bpc = g_param[NSX_PARAM_BLOCKS_PER_CU].load();
-    return map_err(nsx::launch_ipv4_hdr(static_cast<uint8_t*>(d_base), stride, hdr_off, n, mode, d_out_raw,
-                                        (uint32_t)di->cus * (uint32_t)(bpc > 0 ? bpc : 8),
+    return map_err(nsx::launch_ipv4_hdr(static_cast<uint8_t*>(d_base), stride, hdr_off, n, mode, d_out_raw, di->cus,
+                                        (int)g_param[NSX_PARAM_BLOCKS_PER_CU].load(),
                                         (int)g_param[NSX_PARAM_KERNEL].load(),
+                                        (int)g_param[NSX_PARAM_SEGS_PER_WAVE].load(),
                                         static_cast<hipStream_t>(stream)));
 }
 

@@ -801,6 +801,46 @@ __device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t src_lane) {
     return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane * 4), (int)v);
 }
 
+__device__ __forceinline__ uint64_t ld_off(__amdgpu_buffer_rsrc_t ofs, uint32_t i) {
+    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+    const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, i * 8, 0, 0);
+    return ((uint64_t)x.y << 32) | x.x;
+}
+
+// Two lower bounds over offsets[0..n] at once (first i with offsets[i] >= t[k]; n if
+// none), 64-ary: every round each lane probes one index per search, both loads in
+// flight together, and a ballot keeps the sub-range that holds the answer
+// (n = 1M: 1M → 16K → 256 → 4 → exact, four dependent rounds).
+__device__ __forceinline__ void seg_lower_bound2(__amdgpu_buffer_rsrc_t ofs, uint32_t n, uint64_t t0, uint64_t t1,
+                                                 uint32_t lane, uint32_t s[2]) {
+    uint32_t lo[2] = {0u, 0u}, hi[2] = {n, n};
+    const uint64_t t[2] = {t0, t1};
+    while (hi[0] - lo[0] > kWave || hi[1] - lo[1] > kWave) {
+        uint32_t step[2], idx[2];
+        uint64_t v[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            step[k] = (hi[k] - lo[k] + kWave - 1) / kWave;
+            idx[k] = min(lo[k] + lane * step[k], hi[k]);
+            v[k] = ld_off(ofs, idx[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            // probes lo + j·step (j = 0..63) are monotone: c of them lie below t
+            const uint32_t c = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(v[k] < t[k]));
+            const uint32_t l = c ? lo[k] + (c - 1) * step[k] + 1 : lo[k];
+            hi[k] = min(lo[k] + c * step[k], hi[k]);
+            lo[k] = min(l, hi[k]);
+        }
+    }
+    uint64_t v[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) v[k] = lo[k] + lane < hi[k] ? ld_off(ofs, lo[k] + lane) : ~0ull;
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+        s[k] = lo[k] + (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(v[k] < t[k]));
+}
+
 template <int R, bool NT, bool VERIFY>
 __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, uint32_t n,
@@ -809,24 +849,44 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
     typedef uint32_t v2u __attribute__((ext_vector_type(2)));
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const uint32_t ntasks = (n + run - 1) / run;  // run ≤ kScanRun segments per wave task
-    const TaskIter it = task_iter(ntasks, wave, xcd_map);
-    const uint32_t end = (uint32_t)it.end, step = (uint32_t)it.step;
     const __amdgpu_buffer_rsrc_t ofs = make_rsrc(offsets, ((uint64_t)n + 1) * 8);
     const __amdgpu_buffer_rsrc_t prs = make_rsrc(partial, partial ? (uint64_t)n * 4 : 0);
     const __amdgpu_buffer_rsrc_t ors = make_rsrc(out, out ? (uint64_t)n * 2 : 0);
     const __amdgpu_buffer_rsrc_t oks = make_rsrc(ok, VERIFY ? (uint64_t)n : 0);
-    auto load_offs = [&](uint32_t t) -> uint64_t {  // lane l ≤ run length: offsets[t*run + l]
-        const uint32_t a = t * run;
-        const uint32_t voff = (t < end && lane <= run && a + lane <= n) ? (a + lane) * 8 : kOOB;
+    // The wave's tasks are runs [a, a + cnt) of ≤ run segments, a = a0, a0 + a_step, ... < a_end;
+    // a run never crosses a_end.
+    uint32_t a0, a_step, a_end;
+    if (xcd_map == 3) {
+        // Byte-balanced: wave g (XCD-contiguous numbering) owns the segments that start in
+        // the g-th of W equal byte slices of the batch, so every wave streams the same bytes
+        // (± one segment) and none is left running alone at the end of the launch.
+        const uint32_t nb = gridDim.x, b = blockIdx.x, W = nb * kWavesPerBlock;
+        const uint32_t g = (nb >= 16 && (nb & 7) == 0) ? ((b & 7) * (nb >> 3) + (b >> 3)) * kWavesPerBlock + wave
+                                                        : b * kWavesPerBlock + wave;
+        const uint64_t o_lo = ld_off(ofs, 0), o_hi = ld_off(ofs, n);
+        const uint64_t tot = o_hi - o_lo;
+        uint32_t s[2];
+        seg_lower_bound2(ofs, n, o_lo + tot * g / W, o_lo + tot * (g + 1) / W, lane, s);
+        a0 = g == 0 ? 0u : s[0];
+        a_end = g + 1 == W ? n : s[1];
+        a_step = run;
+    } else {
+        const uint32_t ntasks = (n + run - 1) / run;  // run ≤ kScanRun segments per wave task
+        const TaskIter it = task_iter(ntasks, wave, xcd_map);
+        a0 = (uint32_t)it.next * run;
+        a_step = (uint32_t)it.step * run;
+        a_end = (uint32_t)min((uint64_t)it.end * run, (uint64_t)n);
+    }
+    auto load_offs = [&](uint32_t a) -> uint64_t {  // lane l ≤ run length: offsets[a + l]
+        const uint32_t voff = (a < a_end && lane <= run && a + lane <= n) ? (a + lane) * 8 : kOOB;
         const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, voff, 0, 0);
         return ((uint64_t)x.y << 32) | x.x;
     };
-    uint64_t nxt_off = load_offs((uint32_t)it.next);
-    for (uint32_t t = (uint32_t)it.next; t < end; t += step) {
-        const uint32_t a = t * run, cnt = min(run, n - a);
+    uint64_t nxt_off = load_offs(a0);
+    for (uint32_t a = a0; a < a_end; a += a_step) {
+        const uint32_t cnt = min(run, a_end - a);
         const uint64_t my_off = nxt_off;  // boundary `lane` of the run (lanes 0..cnt)
-        nxt_off = load_offs(t + step);
+        nxt_off = load_offs(a + a_step);
         const uint32_t my_part = __builtin_amdgcn_raw_buffer_load_b32(prs, lane < cnt ? (a + lane) * 4 : kOOB, 0, 0);
         const uint64_t lo = readlane64(my_off, 0), hi = readlane64(my_off, cnt);
         // Rows start on a 128-byte line so a 1 KiB row touches exactly 8 lines.
@@ -1299,6 +1359,92 @@ __global__ __launch_bounds__(kBlock) void ipv4_hdr_dense_kernel(uint8_t* __restr
     }
 }
 
+// Packed option-less headers (stride 20, hdr_off 0, 4-aligned base — a
+// header-split ring): the array is one flat stream of whole dwords and every
+// dword belongs to exactly one header. A wave task is 256 headers = 5 KiB = five
+// full coalesced rows (16 B per lane, no idle lane); the rows go through the
+// wave's 5 KiB LDS slice (ds_write_b128 lane-contiguous, then ds_read_b128 at an
+// 80 B lane stride — conflict-free), so lane l ends up with headers 4l..4l+3 whole
+// in registers: no byte masks, no per-header window. A 20-byte stride only fits
+// IHL = 5, so any other IHL is malformed (out 0, header untouched), the rule of
+// the general kernels. A lane's 4 results leave as one 8-byte store (512 B per
+// wave); U tasks in flight per wave, XCD-contiguous deal.
+constexpr uint32_t kHdr20Task = 256;
+constexpr uint32_t kHdr20Lds = kHdr20Task * 20u;  // bytes of LDS per wave
+
+template <int MODE, int U>
+__global__ __launch_bounds__(kBlock) void ipv4_hdr20_kernel(uint8_t* __restrict__ base, uint32_t n,
+                                                            uint16_t* __restrict__ out) {
+    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+    extern __shared__ u32x4 lds20[];
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    u32x4* my = lds20 + wave * (kHdr20Lds / 16u);
+    const uint32_t ntasks = (n + kHdr20Task - 1) / kHdr20Task;
+    const TaskIter it = task_iter(ntasks, wave, 1);
+    const uint32_t end = (uint32_t)it.end, step = (uint32_t)it.step;
+    const __amdgpu_buffer_rsrc_t ors = make_rsrc(out, out ? (uint64_t)n * 2 : 0);
+    for (uint32_t t0 = (uint32_t)it.next; t0 < end; t0 += step * U) {
+        __amdgpu_buffer_rsrc_t rs[U];
+        uint32_t cnt[U];
+        u32x4 v[U][5];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t task = t0 + (uint32_t)u * step;
+            cnt[u] = task < end ? min(kHdr20Task, n - task * kHdr20Task) : 0u;
+            rs[u] = make_rsrc(base + (uint64_t)min(task, ntasks - 1) * kHdr20Lds, cnt[u] * 20u);
+#pragma unroll
+            for (int j = 0; j < 5; ++j) v[u][j] = bld16<true>(rs[u], j * kRow + lane * 16u);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < 5; ++j) asm volatile("" : "+v"(v[u][j]));
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!cnt[u]) break;  // wave-uniform
+            __builtin_amdgcn_wave_barrier();  // the previous task's LDS reads are done
+#pragma unroll
+            for (int j = 0; j < 5; ++j) my[j * kWave + lane] = v[u][j];
+            __builtin_amdgcn_wave_barrier();
+            u32x4 q[5];
+#pragma unroll
+            for (int j = 0; j < 5; ++j) q[j] = my[lane * 5 + j];
+            const uint32_t d[20] = {q[0].x, q[0].y, q[0].z, q[0].w, q[1].x, q[1].y, q[1].z, q[1].w, q[2].x, q[2].y,
+                                    q[2].z, q[2].w, q[3].x, q[3].y, q[3].z, q[3].w, q[4].x, q[4].y, q[4].z, q[4].w};
+            uint32_t res[4];
+            bool ok[4];
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                const uint32_t* w = d + 5 * h;
+                ok[h] = (w[0] & 15u) == 5u;  // IHL (low nibble of byte 0)
+                uint32_t acc = __builtin_amdgcn_sad_u16(w[0], 0u, 0u);
+                acc = __builtin_amdgcn_sad_u16(w[1], 0u, acc);
+                acc = __builtin_amdgcn_sad_u16(MODE == 1 ? (w[2] & 0xFFFFu) : w[2], 0u, acc);  // bytes 10-11 = 0
+                acc = __builtin_amdgcn_sad_u16(w[3], 0u, acc);
+                acc = __builtin_amdgcn_sad_u16(w[4], 0u, acc);
+                res[h] = ok[h] ? finish(acc, true, 0u) : 0u;  // headers start 4-aligned: even
+            }
+            const uint32_t i0 = (t0 + (uint32_t)u * step) * kHdr20Task + lane * 4u;  // first header of this lane
+            if (cnt[u] == kHdr20Task) {
+                __builtin_amdgcn_raw_buffer_store_b64(v2u{res[0] | (res[1] << 16), res[2] | (res[3] << 16)}, ors,
+                                                      i0 * 2u, 0, 0);
+            } else {
+#pragma unroll
+                for (int h = 0; h < 4; ++h)
+                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res[h], ors, i0 + h < n ? (i0 + h) * 2u : kOOB, 0,
+                                                          0);
+            }
+            if constexpr (MODE == 1) {
+#pragma unroll
+                for (int h = 0; h < 4; ++h)  // ~raw big-endian into bytes 10-11
+                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)bswap16u(~res[h] & 0xFFFFu), rs[u],
+                                                          ok[h] ? lane * 80u + h * 20u + 10u : kOOB, 0, 0);
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // IPv4 pseudo-header partials: src(4) dst(4) 0 proto len16 (RFC 9293 §3.1).
 // ---------------------------------------------------------------------------
@@ -1412,8 +1558,9 @@ enum class Path { kFixedShort, kFixedLong, kRagged, kBlock };
 // Per-path defaults (tools/sweep.py, MI355X):
 //   fixed ≤4 rows : buffer-load kernel, 4 segments/wave, 2 blocks/CU (8 waves/CU)
 //   fixed long    : per-segment wave kernel, 2 blocks/CU (8 waves/CU, 4 KiB in flight each)
-//   ragged        : prefix-scan kernel, 16-segment runs, 8 rows/batch, 2 blocks/CU
-// nt loads and the XCD-contiguous deal everywhere.
+//   ragged        : prefix-scan kernel, byte-balanced contiguous wave ranges (XCD-ordered),
+//                   63-segment runs, 8 rows/batch, 2 blocks/CU
+// nt loads everywhere; the XCD-contiguous deal on the fixed paths.
 static Plan resolve(const LaunchCfg& c, Path p) {
     Plan r;
     int bpc = c.blocks_per_cu;
@@ -1422,9 +1569,11 @@ static Plan resolve(const LaunchCfg& c, Path p) {
     r.spw = (c.segs_per_wave == 1 || c.segs_per_wave == 2 || c.segs_per_wave == 4 || c.segs_per_wave == 8)
                 ? c.segs_per_wave : 4;
     r.rows = (c.rows == 4 || c.rows == 8 || c.rows == 16) ? c.rows : 8;
-    r.xcd = c.xcd_map == 2 ? 0 : (c.xcd_map == 3 ? 2 : 1);
+    r.xcd = c.xcd_map == 2 ? 0 : (c.xcd_map == 3 ? 2 : (c.xcd_map == 4 ? 3 : 1));
+    if (c.xcd_map == 0 && p == Path::kRagged && (c.kernel == 0 || c.kernel == kKernelScan))
+        r.xcd = 3;  // byte-balanced wave ranges (scan kernel only)
     r.nt = c.nontemporal != 2;
-    r.run = (c.run_segs >= 1 && c.run_segs <= (int)kScanRun) ? (uint32_t)c.run_segs : 16u;
+    r.run = (c.run_segs >= 1 && c.run_segs <= (int)kScanRun) ? (uint32_t)c.run_segs : kScanRun;
     return r;
 }
 
@@ -1707,10 +1856,43 @@ hipError_t launch_tcp_build(const TcpHdrSoA& h, const uint8_t* opts, const uint6
 }
 
 hipError_t launch_ipv4_hdr(uint8_t* base, uint64_t stride, uint32_t hdr_off, uint64_t n, int mode, uint16_t* out,
-                           uint32_t max_blocks, int kernel, hipStream_t st) {
+                           int cus, int bpc, int kernel, int unroll, hipStream_t st) {
+    // kernel: 0 = auto (flat for packed 20 B headers, else LDS-dense for stride ≤ 64, else per-thread),
+    // 1 = per-thread, 2 = LDS-dense (stride ≤ 64)
+    if (stride == 20 && hdr_off == 0 && ((uintptr_t)base & 3u) == 0 && kernel == 0) {
+        // packed option-less headers: flat-stream kernel. Default 1 block/CU with 2 tasks (10 KiB) in flight
+        // per wave = 40 KiB per CU (tools/sweep.py: 0.220 ms vs 0.232 at 2 blocks/CU, 0.284 at 1 task/wave);
+        // chunks keep each launch's results within one descriptor
+        const uint32_t mb = (uint32_t)cus * (uint32_t)(bpc >= 1 && bpc <= 8 ? bpc : 1);
+        constexpr uint64_t kChunk = 1ull << 28;
+        for (uint64_t c0 = 0; c0 < n; c0 += kChunk) {
+            const uint32_t cn = (uint32_t)std::min<uint64_t>(kChunk, n - c0);
+            const uint64_t tasks = (cn + kHdr20Task - 1) / kHdr20Task;
+            const uint64_t want_f = (tasks + kWavesPerBlock - 1) / kWavesPerBlock;
+            const uint32_t grid_f = (uint32_t)(want_f < mb ? want_f : mb);
+            uint8_t* b = base + c0 * 20u;
+            uint16_t* o = out ? out + c0 : nullptr;
+            const size_t lds = (size_t)kHdr20Lds * kWavesPerBlock;
+#define NSX_H20(U)                                                                                              \
+    do {                                                                                                        \
+        if (mode == 1) hipLaunchKernelGGL((ipv4_hdr20_kernel<1, U>), dim3(grid_f), dim3(kBlock), lds, st, b, cn, o); \
+        else hipLaunchKernelGGL((ipv4_hdr20_kernel<0, U>), dim3(grid_f), dim3(kBlock), lds, st, b, cn, o);        \
+    } while (0)
+            switch (unroll) {
+                case 1: NSX_H20(1); break;
+                case 4: NSX_H20(4); break;
+                default: NSX_H20(2); break;
+            }
+#undef NSX_H20
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
+    const uint32_t max_blocks = (uint32_t)cus * (uint32_t)(bpc >= 1 && bpc <= 8 ? bpc : 8);
     const uint64_t want = (n + (uint64_t)kBlock * kHdrUnroll - 1) / ((uint64_t)kBlock * kHdrUnroll);
     const uint32_t grid = (uint32_t)(want < max_blocks ? want : max_blocks);
-    if (stride >= 1 && stride <= kHdrDenseMaxStride && kernel != 1) {
+    if (stride >= 1 && stride <= kHdrDenseMaxStride && (kernel == 0 || kernel == 2)) {
         // a wave's 64 headers span ≤ 63·stride + 3 + 20 bytes: ROWS 1 KiB rows per task in registers,
         // U tasks per iteration, an LDS slice of U·ROWS KiB per wave
         const uint32_t rows = (63u * (uint32_t)stride + 3u + 20u + 3u + kRow - 1) / kRow;

@@ -224,7 +224,9 @@ RAGGED_VARIANTS = ([dict(kernel=k, rows=r, nt=nt, xcd=x, bpc=b, spw=0) for k in 
                     for nt in (1, 2) for x in (1, 2, 3) for b in (8, 2)] +
                    [dict(kernel=1, rows=r, nt=1, xcd=1, bpc=4, spw=0) for r in (4, 8, 16)] +
                    [dict(kernel=4, rows=8, nt=1, xcd=1, bpc=8, spw=0, run=rs) for rs in (1, 2, 7, 16, 33, 63)] +
-                   [dict(kernel=2, rows=0, nt=1, xcd=x, bpc=4, spw=0) for x in (1, 3)])
+                   [dict(kernel=2, rows=0, nt=1, xcd=x, bpc=4, spw=0) for x in (1, 3)] +
+                   [dict(kernel=4, rows=r, nt=1, xcd=4, bpc=b, spw=0, run=rs) for r in (4, 8, 16) for b in (1, 2, 8)
+                    for rs in (1, 16, 63)])
 
 
 def test_ragged_variants_bit_exact():
@@ -252,6 +254,36 @@ def test_ragged_variants_bit_exact():
                 assert np.array_equal(u16(out), want_p), (v, bm)
                 okv = host(nsx.verify_ragged_dev(d, o, partial=p))
                 assert np.array_equal(okv.astype(bool), want_p == 0xFFFF), (v, bm)
+    finally:
+        set_variant(dict(kernel=0, rows=0, spw=0, nt=0, xcd=0, bpc=0), 0)
+
+
+def test_ragged_byte_balanced_partition_edges():
+    """XCD_MAP=4 (byte-balanced wave ranges found by an in-kernel 64-ary search over
+    the offsets): skewed, sorted, all-empty and tiny batches, more waves than segments."""
+    rng = np.random.default_rng(77)
+    cases = {
+        "sorted": np.sort(rng.integers(0, 20000, 6000)).astype(np.uint64),
+        "one_giant": np.concatenate([np.full(3000, 3, np.uint64), [2_000_000], np.full(3000, 70, np.uint64)]),
+        "empties_at_ends": np.concatenate([np.zeros(1500, np.uint64), rng.integers(1, 3000, 2000).astype(np.uint64),
+                                           np.zeros(1500, np.uint64)]),
+        "all_empty": np.zeros(4000, np.uint64),
+        "few": rng.integers(0, 5000, 1030).astype(np.uint64),
+    }
+    try:
+        for name, lens in cases.items():
+            offs = np.zeros(lens.size + 1, np.uint64)
+            offs[1:] = np.cumsum(lens)
+            offs += np.uint64(3)
+            buf = O.c_splitmix64(0x1099, int(offs[-1]) + 8)
+            want = O.c_batch(buf, lens.size, offsets=offs)
+            d, o = dev(buf), dev(offs.view(np.int64))
+            for b in (1, 8):
+                for rs in (1, 16, 63):
+                    set_variant(dict(kernel=4, rows=8, nt=1, xcd=4, bpc=b, spw=0, run=rs), 1)
+                    out = torch.empty(lens.size, dtype=torch.int16, device="cuda")
+                    nsx.ragged_dev(d, o, out=out)
+                    assert np.array_equal(u16(out), want), (name, b, rs)
     finally:
         set_variant(dict(kernel=0, rows=0, spw=0, nt=0, xcd=0, bpc=0), 0)
 
@@ -407,8 +439,14 @@ def test_config3_1M_ragged_full():
     offs[1:] = np.cumsum(lens)
     t = torch.empty(int(offs[-1]), dtype=torch.uint8, device="cuda")
     nsx.fill_splitmix64_dev(t, 0x1072)
-    out = nsx.ragged_dev(t, dev(offs.view(np.int64)), out=torch.empty(n, dtype=torch.int16, device="cuda"))
-    assert np.array_equal(u16(out), O.c_batch(host(t), n, offsets=offs, threads=16))
+    want = O.c_batch(host(t), n, offsets=offs, threads=16)
+    try:
+        for xcd in (0, 1, 4):  # default, XCD deal, byte-balanced wave ranges
+            nsx.set_param(nsx.PARAM_XCD_MAP, xcd)
+            out = nsx.ragged_dev(t, dev(offs.view(np.int64)), out=torch.empty(n, dtype=torch.int16, device="cuda"))
+            assert np.array_equal(u16(out), want), xcd
+    finally:
+        nsx.set_param(nsx.PARAM_XCD_MAP, 0)
 
 
 def test_config4_256K_x_64KiB_sampled_and_roundtrip():
@@ -534,6 +572,9 @@ def test_f3_64M_headers_full_size_fill_verify():
 def _ipv4_headers(rng, n, stride, hdr_off):
     buf = rng.integers(0, 256, n * stride + 8, dtype=np.uint8)
     ihl = rng.integers(5, 16, n)
+    if stride == 20:  # packed ring: option-less headers, some with options that overrun the stride
+        ihl[:] = 5
+        ihl[::89] = rng.integers(6, 16, len(ihl[::89]))
     ihl[::97] = rng.integers(0, 5, len(ihl[::97]))  # some malformed
     for i in range(n):
         b0 = i * stride + hdr_off
@@ -541,8 +582,8 @@ def _ipv4_headers(rng, n, stride, hdr_off):
     return buf, ihl
 
 
-@pytest.mark.parametrize("kernel", [0, 1])  # 0: default (LDS-staged dense path for stride <= 64), 1: per-thread
-@pytest.mark.parametrize("stride,hdr_off", [(64, 0), (61, 1), (1514, 14), (1500, 0), (60, 0), (40, 3)])
+@pytest.mark.parametrize("kernel", [0, 1, 2])  # 0: default (flat for packed 20 B, LDS-dense for stride <= 64), 1: per-thread, 2: LDS-dense
+@pytest.mark.parametrize("stride,hdr_off", [(64, 0), (61, 1), (1514, 14), (1500, 0), (60, 0), (40, 3), (20, 0)])
 def test_ipv4_header_checksum_verify_and_fill(stride, hdr_off, kernel, nsx_param):
     nsx_param(nsx.PARAM_KERNEL, kernel)
     rng = np.random.default_rng(stride * 31 + hdr_off)
@@ -575,7 +616,7 @@ def test_ipv4_header_checksum_verify_and_fill(stride, hdr_off, kernel, nsx_param
     assert (again[valid] == 0xFFFF).all()
 
 
-@pytest.mark.parametrize("kernel", [0, 1])
+@pytest.mark.parametrize("kernel", [0, 1, 2])
 @pytest.mark.parametrize("stride,hdr_off", [(20, 0), (22, 2), (23, 3)])
 def test_ipv4_dense_headers_end_at_allocation_end(stride, hdr_off, kernel, nsx_param):
     """Packed IHL=5 headers (header-split ring), the last one ending exactly at

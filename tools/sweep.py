@@ -39,6 +39,17 @@ def variants(kind):
             out.append(dict(kernel=4, blocks_per_cu=bpc, stream_rows=rows, nontemporal=1, xcd_map=1, run_segs=run))
         for bpc, rows in itertools.product((8, 4), (8, 16)):
             out.append(dict(kernel=3, blocks_per_cu=bpc, stream_rows=rows, nontemporal=1, xcd_map=1))
+    if kind == "ragged_ab":  # the previous ragged default against the byte-balanced one
+        return [dict(kernel=4, blocks_per_cu=2, stream_rows=8, nontemporal=1, xcd_map=1, run_segs=16),
+                dict(kernel=4, blocks_per_cu=2, stream_rows=8, nontemporal=1, xcd_map=4, run_segs=63),
+                dict(kernel=4, blocks_per_cu=2, stream_rows=8, nontemporal=1, xcd_map=4, run_segs=16)]
+    if kind == "ipv4_hdr":  # 0 auto (flat for packed 20 B), 1 per-thread, 2 LDS-dense
+        return ([dict(kernel=0, blocks_per_cu=b, segs_per_wave=u) for b in (1, 2, 3, 4) for u in (1, 2, 4)] +
+                [dict(kernel=2, blocks_per_cu=8)])
+    if kind == "ragged_bal":  # scan kernel: XCD deal vs byte-balanced wave ranges
+        for bpc, rows, run, xcd in itertools.product((1, 2, 4, 8), (4, 8, 16), (8, 16, 32, 63), (1, 4)):
+            out.append(dict(kernel=4, blocks_per_cu=bpc, stream_rows=rows, nontemporal=1, xcd_map=xcd, run_segs=run))
+        return out
     if kind == "fixed2":
         for bpc, spw, xcd in itertools.product((8, 4, 2, 1), (1, 2, 4, 8), (1, 3)):
             out.append(dict(kernel=3, blocks_per_cu=bpc, segs_per_wave=spw, nontemporal=1, xcd_map=xcd))
@@ -67,6 +78,7 @@ def main():
     ap.add_argument("--configs", default="2,3,4")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--kind", default="", help="variant family override (e.g. ragged_bal)")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "sweep.json"))
     a = ap.parse_args()
     torch.cuda.set_device(0)
@@ -77,7 +89,7 @@ def main():
         kind = "fixed2" if cfg["kind"] == "fixed" and cfg["seg_len"] <= 4093 else cfg["kind"]
         if cid == 5:
             kind = "fixed_big"
-        vs = variants(kind)
+        vs = variants(a.kind or kind)
         if cid in (3, 4):
             vs += [dict(v, block_mode=2) for v in vs if v["kernel"] == 2 and v["blocks_per_cu"] == 8]
         times = {i: [] for i in range(len(vs))}
