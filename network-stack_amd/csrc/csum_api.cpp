@@ -239,10 +239,11 @@ int nsx_tcp_build_dev(const nsx_tcp_hdr_soa* hdr, const uint8_t* d_opts, const u
     const int dev = current_device();
     if (dev < 0) return NSX_ENODEV;
     const DevInfo* di = dev_info(dev);
+    const int64_t bpc = g_param[NSX_PARAM_BLOCKS_PER_CU].load();
     const nsx::TcpHdrSoA h{hdr->src_port, hdr->dst_port, hdr->seq_num, hdr->ack_num,
                            hdr->offset,   hdr->control,  hdr->window,  hdr->urgent_ptr};
     return map_err(nsx::launch_tcp_build(h, d_opts, d_opt_off, d_data, d_data_off, data_bytes, d_prefix_partial, n,
-                                         d_out, d_out_off, d_raw, (uint32_t)di->cus * 8,
+                                         d_out, d_out_off, d_raw, (uint32_t)di->cus * (uint32_t)(bpc >= 1 && bpc <= 8 ? bpc : 8),
                                          (int)g_param[NSX_PARAM_NONTEMPORAL].load(), static_cast<hipStream_t>(stream)));
 }
 

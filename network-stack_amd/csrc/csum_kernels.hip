@@ -1007,7 +1007,8 @@ struct BuildSeg {  // wave-uniform description of one segment
     uint32_t D0, D1, D2, D3, D4;  // header dwords as stored (LE view), field = 0
     uint32_t optlen, hdr_end, wire, nb4, rows, sh;
     int32_t sh0;                  // payload source offset (from the descriptor base) = wire pos + sh0
-    uint64_t ob;
+    uint64_t ob, db;              // option / payload byte offsets
+    bool fast;                    // no options, payload 4-aligned, whole dwords, ≥ 20 B into the data array
 };
 
 // Source row r: 4+1 dwords per lane. Row 0 (head) clamps each dword separately.
@@ -1078,6 +1079,8 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
                                                            uint8_t* __restrict__ out,
                                                            const uint64_t* __restrict__ out_off,
                                                            uint16_t* __restrict__ raw_out, uint32_t group) {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    typedef uint32_t v3u __attribute__((ext_vector_type(3)));
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint64_t data_end4 = (data_bytes + 3) & ~3ull;  // the last payload dword reads whole
@@ -1114,6 +1117,8 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
             S.sh0 = (int32_t)(db & 3u) - (int32_t)S.hdr_end;
             S.sh = (uint32_t)S.sh0 & 3u;
             const uint64_t dbase = db & ~3ull;
+            S.db = db;
+            S.fast = S.optlen == 0 && (db & 3u) == 0 && db >= 20u && (S.wire & 3u) == 0;
             drs = make_rsrc(data + dbase, data_end4 - dbase);
             ors = make_rsrc(out + readlane64(moo, k), S.nb4);
         };
@@ -1129,7 +1134,41 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
             __amdgpu_buffer_rsrc_t drs, ors;
             seg_at(k, S, drs, ors);
             uint32_t acc = 0;
-            if (S.hdr_end <= kRow - 16u) {
+            if (S.fast) {
+                // Option-less segment with a 4-aligned payload of whole dwords at data offset ≥ 20: the
+                // image is the payload shifted by exactly 5 dwords. One descriptor based 20 bytes before
+                // the payload (inside the data array) maps image dword k to source dword k, so every row is
+                // one plain 16 B load per lane with no shift and no byte mask; dwords 0-4 (the header) are
+                // replaced by the built header, dwords past the image read 0 (range check).
+                constexpr uint32_t R = kBuildRows;
+                const __amdgpu_buffer_rsrc_t frs = make_rsrc(data + S.db - 20u, S.nb4);
+                for (uint32_t r0 = 0; r0 < S.rows; r0 += R) {
+                    u32x4 v[R];
+#pragma unroll
+                    for (uint32_t rr = 0; rr < R; ++rr) v[rr] = bld16<LP != 0>(frs, (r0 + rr) * kRow + lane * 16u);
+#pragma unroll
+                    for (uint32_t rr = 0; rr < R; ++rr) asm volatile("" : "+v"(v[rr]));
+#pragma unroll
+                    for (uint32_t rr = 0; rr < R; ++rr) {
+                        const uint32_t r = r0 + rr;
+                        if (r >= S.rows) break;
+                        u32x4 x = v[rr];
+                        if (r == 0) {
+                            x.x = lane == 0 ? S.D0 : (lane == 1 ? S.D4 : x.x);
+                            x.y = lane == 0 ? S.D1 : x.y;
+                            x.z = lane == 0 ? S.D2 : x.z;
+                            x.w = lane == 0 ? S.D3 : x.w;
+                        }
+                        acc = sad4(x, acc);
+                        const uint32_t pos0 = r * kRow + lane * 16u;
+                        const bool d4 = r == 0 && lane == 1;  // dword 4 waits for the field
+                        __builtin_amdgcn_raw_buffer_store_b128(v4u{x.x, x.y, x.z, x.w}, ors, d4 ? kOOB : pos0, 0, SP);
+                        if (r == 0)
+                            __builtin_amdgcn_raw_buffer_store_b96(v3u{x.y, x.z, x.w}, ors, d4 ? 20u : kOOB, 0, SP);
+                    }
+                    acc = fold32(acc);
+                }
+            } else if (S.hdr_end <= kRow - 16u) {
                 constexpr uint32_t R = kBuildRows;
                 // batch 0: the header row + rows 1..R-1, all loads in flight
                 u32x4 lo[R];

@@ -652,8 +652,12 @@ def test_ipv4_header_kat():
 
 # ------------------------------------------------------------------ fused serialize + checksum
 
-def test_tcp_build_matches_reference_bytes_and_checksum():
-    rng = np.random.default_rng(77)
+@pytest.mark.parametrize("lead,align4", [(1, False), (0, True), (20, True)])
+def test_tcp_build_matches_reference_bytes_and_checksum(lead, align4):
+    """lead = bytes before the first payload; align4 = most payloads are whole dwords at
+    4-aligned offsets (the kernel's no-shift/no-mask fast path, interleaved with the
+    general path for segments with options or ragged payloads)."""
+    rng = np.random.default_rng(77 + lead)
     n = 3000
     opt_sets = [[], [O.Option(kind=1)], [O.Option(kind=2, length=4, data=b"\x05\xb4\0\0")],
                 [O.Option(kind=1), O.Option(kind=1), O.Option(kind=0)],
@@ -661,25 +665,28 @@ def test_tcp_build_matches_reference_bytes_and_checksum():
     segs, pseudos = [], []
     for i in range(n):
         L = int(rng.integers(0, 3000)) if i % 10 else int(rng.integers(0, 8))
+        if align4 and i % 7:
+            L &= ~3
         s = O.Segment(src_port=int(rng.integers(1 << 16)), dst_port=int(rng.integers(1 << 16)),
                       seq_num=int(rng.integers(1 << 32)), ack_num=int(rng.integers(1 << 32)),
                       control=O.Ctl.from_byte(int(rng.integers(256))), window=int(rng.integers(1 << 16)),
-                      urgent_ptr=int(rng.integers(1 << 16)), options=list(opt_sets[i % len(opt_sets)]),
+                      urgent_ptr=int(rng.integers(1 << 16)),
+                      options=list(opt_sets[i % len(opt_sets)]) if not align4 or i % 3 == 0 else [],
                       data=rng.integers(0, 256, L, dtype=np.uint8).tobytes())
         s.offset = s.compute_offset()
         segs.append(s)
         pseudos.append(O.ipv4_pseudo_header(rng.integers(0, 256, 4, dtype=np.uint8).tobytes(),
                                             rng.integers(0, 256, 4, dtype=np.uint8).tobytes(), 6,
                                             len(s.bytes())))
-    # payloads densely packed behind a 1-byte lead (odd source alignment)
-    data = b"\x99" + b"".join(s.data for s in segs)
+    # payloads densely packed behind a `lead`-byte lead (lead 1: odd source alignment)
+    data = b"\x99" * lead + b"".join(s.data for s in segs)
     data_off = np.zeros(n + 1, np.uint64)
     data_off[1:] = np.cumsum([len(s.data) for s in segs])
-    data_off += np.uint64(1)
+    data_off += np.uint64(lead)
     opts = b"".join(o.bytes() for s in segs for o in s.options) or b"\0"
     opt_off = np.zeros(n + 1, np.uint64)
     opt_off[1:] = np.cumsum([sum(len(o.bytes()) for o in s.options) for s in segs])
-    out_off = nsx.tcp_layout_host(data_off - np.uint64(1), opt_off)
+    out_off = nsx.tcp_layout_host(data_off - np.uint64(lead), opt_off)
     u = lambda a, dt: dev(np.asarray(a, dt).view({np.uint16: np.int16, np.uint32: np.int32, np.uint8: np.uint8}[dt]))
     fields = {"src_port": u([s.src_port for s in segs], np.uint16), "dst_port": u([s.dst_port for s in segs], np.uint16),
               "seq_num": u([s.seq_num for s in segs], np.uint32), "ack_num": u([s.ack_num for s in segs], np.uint32),
