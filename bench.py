@@ -188,7 +188,7 @@ def result_line(*, world, steps, warmup, wall_max, bytes_per_rank_step, units_to
 # GPU workload
 # ---------------------------------------------------------------------------
 PARAMS = {"blocks_per_cu": 1, "segs_per_wave": 2, "nontemporal": 3, "block_mode": 4, "xcd_map": 5, "kernel": 6,
-          "stream_rows": 7, "run_segs": 8}
+          "stream_rows": 7, "run_segs": 8, "xcd_chunk": 9}
 
 
 def build_workload(cfg, rank, device):

@@ -24,6 +24,7 @@ struct LaunchCfg {
     int kernel;          // kKernelRowStream / kKernelPerSegment
     int rows;            // row-stream rows per batch: 4, 8, 16
     int run_segs;        // ragged scan kernel: segments per wave task, 1..63
+    int xcd_chunk;       // fixed buffer kernel: XCD-interleaved chunks of 2^k tasks (0 = default 12, >20 = eighths)
 };
 
 // Launch configuration from the process-wide NSX_PARAM_* knobs (csum_api.cpp).

@@ -114,6 +114,16 @@ struct TaskIter {
     uint64_t next, end, step;
 };
 
+// XCD-interleaved deal (fixed-stride kernel): the batch is cut into chunks of 2^clog tasks and XCD x
+// takes chunks x, x+8, x+16, ...; its waves walk their chunks' tasks in order. i = the wave's local
+// sequence index (start slot*4 + wave, step per*4).
+struct ChunkDeal {
+    uint32_t x, clog;  // clog = 0: off (task = i)
+    __device__ __forceinline__ uint32_t task(uint32_t i) const {
+        return clog ? ((((i >> clog) << 3) + x) << clog) | (i & ((1u << clog) - 1u)) : i;
+    }
+};
+
 // xcd_map: 1 = each XCD's blocks stream one contiguous eighth of the batch,
 // dealt round-robin inside it; 0 = plain grid-stride; 2 = every wave owns one
 // contiguous range of tasks and walks it in order (a sequential stream per wave).
@@ -289,9 +299,9 @@ __device__ __forceinline__ u32x4 edge_mask(u32x4 x, const SegWin& w, uint32_t k,
 
 template <int U>
 __device__ __forceinline__ void fixed_flush(uint32_t res, uint32_t first, uint32_t step, uint32_t count, uint32_t n,
-                                            __amdgpu_buffer_rsrc_t ors, uint32_t lane) {
+                                            __amdgpu_buffer_rsrc_t ors, uint32_t lane, const ChunkDeal& cd) {
     const uint32_t j = lane / U;
-    const uint32_t seg = (first + j * step) * U + lane % U;
+    const uint32_t seg = cd.task(first + j * step) * U + lane % U;
     const uint32_t off = (j < count && seg < n) ? seg * 2 : kOOB;
     __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, off, 0, 0);
 }
@@ -309,24 +319,34 @@ __device__ __forceinline__ void fixed_flush(uint32_t res, uint32_t first, uint32
 template <int U, int NROWS, bool NT, bool ALIGNED>
 __global__ __launch_bounds__(kBlock) void csum_fixed_buf_kernel(
     const uint8_t* __restrict__ base, uint64_t stride, uint32_t seg_len, uint32_t n,
-    const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, int xcd_map) {
+    const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, int xcd_map, uint32_t chunk_log2) {
     constexpr uint32_t G = kWave / U;
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint32_t ntasks = (n + U - 1) / U;
-    const TaskIter it = task_iter(ntasks, wave, xcd_map);
+    TaskIter it = task_iter(ntasks, wave, xcd_map);
+    ChunkDeal cd{0u, 0u};
+    if (chunk_log2 && xcd_map == 1 && gridDim.x >= 16 && (gridDim.x & 7) == 0) {
+        cd.x = blockIdx.x & 7;
+        cd.clog = chunk_log2;
+        it.next = (blockIdx.x >> 3) * kWavesPerBlock + wave;
+        it.step = (gridDim.x >> 3) * kWavesPerBlock;
+        it.end = 0xFFFFFFFFu;
+    }
     const uint32_t end = (uint32_t)it.end, step = (uint32_t)it.step;
     const __amdgpu_buffer_rsrc_t ors = make_rsrc(out, (uint64_t)n * 2);
     const __amdgpu_buffer_rsrc_t prs = make_rsrc(partial, partial ? (uint64_t)n * 4 : 0);
-    // Lane l's segment within a group that starts at task `first`.
-    auto group_seg = [&](uint32_t first) { return (first + (lane / U) * step) * U + lane % U; };
+    // Lane l's segment within a group that starts at sequence index `first`.
+    auto group_seg = [&](uint32_t first) { return cd.task(first + (lane / U) * step) * U + lane % U; };
     uint32_t res = 0, k = 0, first = (uint32_t)it.next;
     uint32_t gpart = 0;
     if constexpr (ALIGNED) {
         const uint32_t sg = group_seg(first);
         gpart = __builtin_amdgcn_raw_buffer_load_b32(prs, sg < n ? sg * 4 : kOOB, 0, 0);
     }
-    for (uint32_t t = (uint32_t)it.next; t < end; t += step) {
+    for (uint32_t i = (uint32_t)it.next; i < end; i += step) {
+        const uint32_t t = cd.task(i);
+        if (t >= ntasks) break;
         const uint32_t s0 = t * U;
         u32x4 v[U][NROWS];
         SegWin w[U];
@@ -368,9 +388,9 @@ __global__ __launch_bounds__(kBlock) void csum_fixed_buf_kernel(
         }
         if (++k == G) {
             if constexpr (ALIGNED) res = finish(res, true, gpart);
-            fixed_flush<U>(res, first, step, k, n, ors, lane);
+            fixed_flush<U>(res, first, step, k, n, ors, lane, cd);
             k = 0;
-            first = t + step;
+            first = i + step;
             if constexpr (ALIGNED) {
                 const uint32_t sg = group_seg(first);
                 gpart = __builtin_amdgcn_raw_buffer_load_b32(prs, (first < end && sg < n) ? sg * 4 : kOOB, 0, 0);
@@ -379,7 +399,7 @@ __global__ __launch_bounds__(kBlock) void csum_fixed_buf_kernel(
     }
     if (k) {
         if constexpr (ALIGNED) res = finish(res, true, gpart);
-        fixed_flush<U>(res, first, step, k, n, ors, lane);
+        fixed_flush<U>(res, first, step, k, n, ors, lane, cd);
     }
 }
 
@@ -1589,7 +1609,8 @@ struct Plan {
     uint32_t max_blocks;
     int spw, rows, xcd;
     bool nt;
-    uint32_t run;  // ragged scan kernel: segments per wave task (1..kScanRun)
+    uint32_t run;     // ragged scan kernel: segments per wave task (1..kScanRun)
+    uint32_t xchunk;  // fixed buffer kernel, XCD deal: log2 tasks per interleaved chunk (0 = contiguous eighths)
 };
 
 enum class Path { kFixedShort, kFixedLong, kRagged, kBlock };
@@ -1613,6 +1634,9 @@ static Plan resolve(const LaunchCfg& c, Path p) {
         r.xcd = 3;  // byte-balanced wave ranges (scan kernel only)
     r.nt = c.nontemporal != 2;
     r.run = (c.run_segs >= 1 && c.run_segs <= (int)kScanRun) ? (uint32_t)c.run_segs : kScanRun;
+    // XCD-interleaved chunks of 2^12 wave tasks by default: contiguous eighths measured 8% slow on some
+    // allocations on some boxes (tools/alloc_study.py), chunks of 2^10-2^14 never
+    r.xchunk = (c.xcd_chunk >= 1 && c.xcd_chunk <= 20) ? (uint32_t)c.xcd_chunk : (c.xcd_chunk == 0 ? 12u : 0u);
     return r;
 }
 
@@ -1655,17 +1679,17 @@ static hipError_t launch_fixed_pipe(const Plan& c, const uint8_t* base, uint64_t
         if (aligned) {                                                                                      \
             if (c.nt)                                                                                       \
                 hipLaunchKernelGGL((csum_fixed_buf_kernel<U_, NR_, true, true>), dim3(grid), dim3(kBlock), 0, st, \
-                                   base, stride, seg_len, (uint32_t)n, partial, out, c.xcd);                \
+                                   base, stride, seg_len, (uint32_t)n, partial, out, c.xcd, c.xchunk);      \
             else                                                                                            \
                 hipLaunchKernelGGL((csum_fixed_buf_kernel<U_, NR_, false, true>), dim3(grid), dim3(kBlock), 0, \
-                                   st, base, stride, seg_len, (uint32_t)n, partial, out, c.xcd);            \
+                                   st, base, stride, seg_len, (uint32_t)n, partial, out, c.xcd, c.xchunk);  \
         } else {                                                                                            \
             if (c.nt)                                                                                       \
                 hipLaunchKernelGGL((csum_fixed_buf_kernel<U_, NR_, true, false>), dim3(grid), dim3(kBlock), 0, \
-                                   st, base, stride, seg_len, (uint32_t)n, partial, out, c.xcd);            \
+                                   st, base, stride, seg_len, (uint32_t)n, partial, out, c.xcd, c.xchunk);  \
             else                                                                                            \
                 hipLaunchKernelGGL((csum_fixed_buf_kernel<U_, NR_, false, false>), dim3(grid), dim3(kBlock), 0, \
-                                   st, base, stride, seg_len, (uint32_t)n, partial, out, c.xcd);            \
+                                   st, base, stride, seg_len, (uint32_t)n, partial, out, c.xcd, c.xchunk);  \
         }                                                                                                   \
         return hipGetLastError();                                                                           \
     }

@@ -187,11 +187,14 @@ VARIANTS = ([dict(kernel=2, spw=s, nt=nt, xcd=x, bpc=b, rows=0) for s in (1, 2, 
             [dict(kernel=1, spw=0, nt=nt, xcd=x, bpc=b, rows=r) for r in (4, 8, 16) for nt in (1, 2) for x in (1, 2)
              for b in (8, 3)] +
             [dict(kernel=3, spw=s, nt=nt, xcd=x, bpc=b, rows=0) for s in (1, 2, 4, 8) for nt in (1, 2)
-             for x in (1, 2, 3) for b in (8, 3)])
+             for x in (1, 2, 3) for b in (8, 3)] +
+            [dict(kernel=3, spw=s, nt=1, xcd=1, bpc=b, rows=0, chunk=c) for s in (1, 4) for b in (8, 2)
+             for c in (1, 3, 6, 10, 99)])
 
 
 def set_variant(v, block_mode=0):
     nsx.set_param(nsx.PARAM_RUN_SEGS, v.get("run", 0))
+    nsx.set_param(nsx.PARAM_XCD_CHUNK, v.get("chunk", 0))
     nsx.set_param(nsx.PARAM_KERNEL, v["kernel"])
     nsx.set_param(nsx.PARAM_STREAM_ROWS, v["rows"])
     nsx.set_param(nsx.PARAM_SEGS_PER_WAVE, v["spw"])
@@ -651,6 +654,74 @@ def test_ipv4_header_kat():
 
 
 # ------------------------------------------------------------------ fused serialize + checksum
+
+def _uniform_build_case(rng, n, P, lead, pseudo=True):
+    """n option-less segments, payload P each, payloads back to back behind `lead`
+    bytes, images back to back: the kernel's uniform-group (flat) layout."""
+    fields = {"src_port": rng.integers(0, 1 << 16, n).astype(np.uint16),
+              "dst_port": rng.integers(0, 1 << 16, n).astype(np.uint16),
+              "seq_num": rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32),
+              "ack_num": rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32),
+              "offset": np.full(n, 5, np.uint8), "control": rng.integers(0, 256, n).astype(np.uint8),
+              "window": rng.integers(0, 1 << 16, n).astype(np.uint16),
+              "urgent_ptr": rng.integers(0, 1 << 16, n).astype(np.uint16)}
+    data = rng.integers(0, 256, lead + n * P + 8, dtype=np.uint8)
+    data_off = (np.arange(n + 1, dtype=np.uint64) * np.uint64(P)) + np.uint64(lead)
+    out_off = nsx.tcp_layout_host(data_off - np.uint64(lead))
+    ps = None
+    if pseudo:
+        ps = np.concatenate([rng.integers(0, 256, (n, 8), dtype=np.uint8),
+                             np.tile(np.array([0, 6, (20 + P) >> 8 & 0xFF, (20 + P) & 0xFF], np.uint8), (n, 1))], 1)
+    return fields, data, data_off, out_off, ps
+
+
+def _run_build(fields, data, data_off, out_off, ps):
+    n = data_off.size - 1
+    dt = {np.uint16: np.int16, np.uint32: np.int32, np.uint8: np.uint8}
+    f = {k: dev(v.view(dt[v.dtype.type])) for k, v in fields.items()}
+    part = None if ps is None else dev(np.array([O.be_word_sum(p.tobytes()) for p in ps], np.uint32).view(np.int32))
+    out = torch.full((int(out_off[-1]),), 0xAB, dtype=torch.uint8, device="cuda")
+    raw = torch.empty(n, dtype=torch.int16, device="cuda")
+    nsx.tcp_build_dev(f, dev(data), dev(data_off.view(np.int64)), out, dev(out_off.view(np.int64)), partial=part,
+                      raw=raw)
+    return host(out), u16(raw)
+
+
+@pytest.mark.parametrize("P", [0, 4, 8, 12, 16, 100, 1004, 1480, 4096, 8996, 65536])
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 300])
+def test_tcp_build_uniform_batches(P, n):
+    """Packed option-less batches (same payload length, payloads and images back to
+    back — the bench's f1 layout): images and raw sums equal the Go-faithful oracle's
+    for tiny, row-sized and 64 KiB payloads."""
+    if n * (P + 20) > 40 << 20:
+        n = 65
+    rng = np.random.default_rng(P * 1000 + n)
+    for lead in (20, 28, 0):  # lead 0: segment 0 has no 20 bytes before its payload (general path)
+        fields, data, data_off, out_off, ps = _uniform_build_case(rng, n, P, lead)
+        got, raw = _run_build(fields, data, data_off, out_off, ps)
+        want, wraw = O.c_go_tcp_build(fields, data, data_off, out_off, ps)
+        assert np.array_equal(raw, wraw), (P, n, lead)
+        assert np.array_equal(got, want), (P, n, lead)
+
+
+def test_tcp_build_whole_dword_and_ragged_payloads_interleaved():
+    """Whole-dword payloads (the kernel's no-shift fast path) next to a 1476 B payload
+    in every other group of 64, which shifts every later payload's alignment."""
+    rng = np.random.default_rng(9)
+    n, P = 64 * 12, 1480
+    lens = np.full(n, P, np.uint64)
+    lens[64 * np.arange(0, 12, 2) + 17] = 1476  # every other group is not uniform
+    data = rng.integers(0, 256, 24 + int(lens.sum()) + 8, dtype=np.uint8)
+    data_off = np.zeros(n + 1, np.uint64)
+    data_off[1:] = np.cumsum(lens)
+    data_off += np.uint64(24)
+    out_off = nsx.tcp_layout_host(data_off - np.uint64(24))
+    fields = _uniform_build_case(rng, n, P, 24, pseudo=False)[0]
+    got, raw = _run_build(fields, data, data_off, out_off, None)
+    want, wraw = O.c_go_tcp_build(fields, data, data_off, out_off, None)
+    assert np.array_equal(raw, wraw)
+    assert np.array_equal(got, want)
+
 
 @pytest.mark.parametrize("lead,align4", [(1, False), (0, True), (20, True)])
 def test_tcp_build_matches_reference_bytes_and_checksum(lead, align4):
