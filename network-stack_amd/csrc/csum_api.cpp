@@ -245,7 +245,8 @@ int nsx_tcp_build_dev(const nsx_tcp_hdr_soa* hdr, const uint8_t* d_opts, const u
                            hdr->offset,   hdr->control,  hdr->window,  hdr->urgent_ptr};
     return map_err(nsx::launch_tcp_build(h, d_opts, d_opt_off, d_data, d_data_off, data_bytes, d_prefix_partial, n,
                                          d_out, d_out_off, d_raw, (uint32_t)di->cus * (uint32_t)(bpc >= 1 && bpc <= 8 ? bpc : 8),
-                                         (int)g_param[NSX_PARAM_NONTEMPORAL].load(), static_cast<hipStream_t>(stream)));
+                                         (int)g_param[NSX_PARAM_NONTEMPORAL].load(),
+                                         (int)g_param[NSX_PARAM_XCD_CHUNK].load(), static_cast<hipStream_t>(stream)));
 }
 
 int nsx_ipv4_hdr_csum_dev(void* d_base, uint64_t stride, uint32_t hdr_off, uint64_t n, int mode,
@@ -261,7 +262,7 @@ int nsx_ipv4_hdr_csum_dev(void* d_base, uint64_t stride, uint32_t hdr_off, uint6
                                         (int)g_param[NSX_PARAM_BLOCKS_PER_CU].load(),
                                         (int)g_param[NSX_PARAM_KERNEL].load(),
                                         (int)g_param[NSX_PARAM_SEGS_PER_WAVE].load(),
-                                        static_cast<hipStream_t>(stream)));
+                                        (int)g_param[NSX_PARAM_XCD_CHUNK].load(), static_cast<hipStream_t>(stream)));
 }
 
 int nsx_fill_splitmix64_dev(void* d_buf, uint64_t byte_off, uint64_t nbytes, uint64_t seed,

@@ -24,7 +24,7 @@ struct LaunchCfg {
     int kernel;          // kKernelRowStream / kKernelPerSegment
     int rows;            // row-stream rows per batch: 4, 8, 16
     int run_segs;        // ragged scan kernel: segments per wave task, 1..63
-    int xcd_chunk;       // fixed buffer kernel: XCD-interleaved chunks of 2^k tasks (0 = default 12, >20 = eighths)
+    int xcd_chunk;       // XCD deal: interleaved chunks of 2^k tasks (0 = auto, 1..20 fixed, else contiguous eighths)
 };
 
 // Launch configuration from the process-wide NSX_PARAM_* knobs (csum_api.cpp).
@@ -53,10 +53,10 @@ struct TcpHdrSoA {  // device arrays, one entry per segment (tcp.go:39-54 field 
 hipError_t launch_tcp_build(const TcpHdrSoA& h, const uint8_t* opts, const uint64_t* opt_off, const uint8_t* data,
                             const uint64_t* data_off, uint64_t data_bytes, const uint32_t* partial, uint64_t n,
                             uint8_t* out, const uint64_t* out_off, uint16_t* raw, uint32_t max_blocks, int policy,
-                            hipStream_t st);
+                            int xchunk, hipStream_t st);
 // bpc / unroll: raw NSX_PARAM_BLOCKS_PER_CU / NSX_PARAM_SEGS_PER_WAVE (0 = per-kernel default)
 hipError_t launch_ipv4_hdr(uint8_t* base, uint64_t stride, uint32_t hdr_off, uint64_t n, int mode, uint16_t* out,
-                           int cus, int bpc, int kernel, int unroll, hipStream_t st);
+                           int cus, int bpc, int kernel, int unroll, int xchunk, hipStream_t st);
 hipError_t launch_fill_splitmix64(void* d_buf, uint64_t byte_off, uint64_t nbytes, uint64_t seed,
                                   uint32_t max_blocks, hipStream_t st);
 

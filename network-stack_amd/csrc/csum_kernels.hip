@@ -150,6 +150,23 @@ __device__ __forceinline__ TaskIter task_iter(uint64_t ntasks, uint32_t wave, in
     return it;
 }
 
+// Switch a wave's xcd_map = 1 iteration to the XCD-interleaved chunk deal when clog > 0 and the grid
+// allows it; the wave then walks i = it.next, it.next + it.step, ... < it.end with task cd.task(i),
+// stopping at the first task ≥ ntasks (task(i) increases with i). With clog = 0 nothing changes
+// (task(i) = i < it.end ≤ ntasks).
+__device__ __forceinline__ ChunkDeal chunk_deal(TaskIter& it, uint32_t wave, int xcd_map, uint32_t clog,
+                                                uint64_t ntasks) {
+    ChunkDeal cd{0u, 0u};
+    if (clog && xcd_map == 1 && gridDim.x >= 16 && (gridDim.x & 7) == 0 && ntasks < (1ull << 31)) {
+        cd.x = blockIdx.x & 7;
+        cd.clog = clog;
+        it.next = (blockIdx.x >> 3) * kWavesPerBlock + wave;
+        it.step = (gridDim.x >> 3) * kWavesPerBlock;
+        it.end = 0xFFFFFFFFu;
+    }
+    return cd;
+}
+
 // ---------------------------------------------------------------------------
 // Fixed stride, U segments per wave pass, NROWS rows per segment (compile-time:
 // every load of the pass is issued before the first is consumed).
@@ -325,14 +342,7 @@ __global__ __launch_bounds__(kBlock) void csum_fixed_buf_kernel(
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint32_t ntasks = (n + U - 1) / U;
     TaskIter it = task_iter(ntasks, wave, xcd_map);
-    ChunkDeal cd{0u, 0u};
-    if (chunk_log2 && xcd_map == 1 && gridDim.x >= 16 && (gridDim.x & 7) == 0) {
-        cd.x = blockIdx.x & 7;
-        cd.clog = chunk_log2;
-        it.next = (blockIdx.x >> 3) * kWavesPerBlock + wave;
-        it.step = (gridDim.x >> 3) * kWavesPerBlock;
-        it.end = 0xFFFFFFFFu;
-    }
+    const ChunkDeal cd = chunk_deal(it, wave, xcd_map, chunk_log2, ntasks);
     const uint32_t end = (uint32_t)it.end, step = (uint32_t)it.step;
     const __amdgpu_buffer_rsrc_t ors = make_rsrc(out, (uint64_t)n * 2);
     const __amdgpu_buffer_rsrc_t prs = make_rsrc(partial, partial ? (uint64_t)n * 4 : 0);
@@ -461,12 +471,15 @@ template <bool RAGGED, int R, bool NT, bool VERIFY>
 __global__ __launch_bounds__(kBlock) void csum_wave_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, uint64_t stride,
     uint32_t seg_len, uint64_t n, const uint32_t* __restrict__ partial, uint16_t* __restrict__ out,
-    uint8_t* __restrict__ ok, const uint8_t* safe_end, int xcd_map) {
+    uint8_t* __restrict__ ok, const uint8_t* safe_end, int xcd_map, uint32_t clog) {
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     if constexpr (RAGGED) safe_end = align_up4(base + offsets[n]);
     TaskIter it = task_iter(n, wave, xcd_map);
-    for (uint64_t i = it.next; i < it.end; i += it.step) {
+    const ChunkDeal cd = chunk_deal(it, wave, xcd_map, clog, n);
+    for (uint64_t k = it.next; k < it.end; k += it.step) {
+        const uint64_t i = cd.clog ? cd.task((uint32_t)k) : k;
+        if (i >= n) break;
         const SegRef s = seg_ref<RAGGED>(base, offsets, stride, seg_len, i);
         const uint32_t tot = wave_sum(seg_lane_sum<R, NT>(s.p, s.len, lane, safe_end, 0, 1));
         if (lane == 0) {
@@ -1098,15 +1111,19 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
                                                            const uint32_t* __restrict__ partial, uint64_t n,
                                                            uint8_t* __restrict__ out,
                                                            const uint64_t* __restrict__ out_off,
-                                                           uint16_t* __restrict__ raw_out, uint32_t group) {
+                                                           uint16_t* __restrict__ raw_out, uint32_t group,
+                                                           uint32_t clog) {
     typedef uint32_t v4u __attribute__((ext_vector_type(4)));
     typedef uint32_t v3u __attribute__((ext_vector_type(3)));
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint64_t data_end4 = (data_bytes + 3) & ~3ull;  // the last payload dword reads whole
     const uint64_t ngroups = (n + group - 1) / group;
-    const TaskIter it = task_iter(ngroups, wave, 1);
-    for (uint64_t g = it.next; g < it.end; g += it.step) {
+    TaskIter it = task_iter(ngroups, wave, 1);
+    const ChunkDeal cd = chunk_deal(it, wave, 1, clog, ngroups);
+    for (uint64_t q = it.next; q < it.end; q += it.step) {
+        const uint64_t g = cd.clog ? cd.task((uint32_t)q) : q;
+        if (g >= ngroups) break;
         const uint64_t g0 = g * group;
         const uint32_t cnt = (uint32_t)min((uint64_t)group, n - g0);
         // Per-lane metadata of segment g0 + lane (lanes past cnt repeat the last one).
@@ -1433,24 +1450,28 @@ constexpr uint32_t kHdr20Lds = kHdr20Task * 20u;  // bytes of LDS per wave
 
 template <int MODE, int U>
 __global__ __launch_bounds__(kBlock) void ipv4_hdr20_kernel(uint8_t* __restrict__ base, uint32_t n,
-                                                            uint16_t* __restrict__ out) {
+                                                            uint16_t* __restrict__ out, uint32_t clog) {
     typedef uint32_t v2u __attribute__((ext_vector_type(2)));
     extern __shared__ u32x4 lds20[];
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     u32x4* my = lds20 + wave * (kHdr20Lds / 16u);
     const uint32_t ntasks = (n + kHdr20Task - 1) / kHdr20Task;
-    const TaskIter it = task_iter(ntasks, wave, 1);
+    TaskIter it = task_iter(ntasks, wave, 1);
+    const ChunkDeal cd = chunk_deal(it, wave, 1, clog, ntasks);
     const uint32_t end = (uint32_t)it.end, step = (uint32_t)it.step;
     const __amdgpu_buffer_rsrc_t ors = make_rsrc(out, out ? (uint64_t)n * 2 : 0);
     for (uint32_t t0 = (uint32_t)it.next; t0 < end; t0 += step * U) {
+        if (cd.task(t0) >= ntasks) break;
         __amdgpu_buffer_rsrc_t rs[U];
-        uint32_t cnt[U];
+        uint32_t cnt[U], tk[U];
         u32x4 v[U][5];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint32_t task = t0 + (uint32_t)u * step;
-            cnt[u] = task < end ? min(kHdr20Task, n - task * kHdr20Task) : 0u;
+            const uint32_t ii = t0 + (uint32_t)u * step;
+            const uint32_t task = cd.task(ii);
+            tk[u] = task;
+            cnt[u] = (ii < end && task < ntasks) ? min(kHdr20Task, n - task * kHdr20Task) : 0u;
             rs[u] = make_rsrc(base + (uint64_t)min(task, ntasks - 1) * kHdr20Lds, cnt[u] * 20u);
 #pragma unroll
             for (int j = 0; j < 5; ++j) v[u][j] = bld16<true>(rs[u], j * kRow + lane * 16u);
@@ -1484,7 +1505,7 @@ __global__ __launch_bounds__(kBlock) void ipv4_hdr20_kernel(uint8_t* __restrict_
                 acc = __builtin_amdgcn_sad_u16(w[4], 0u, acc);
                 res[h] = ok[h] ? finish(acc, true, 0u) : 0u;  // headers start 4-aligned: even
             }
-            const uint32_t i0 = (t0 + (uint32_t)u * step) * kHdr20Task + lane * 4u;  // first header of this lane
+            const uint32_t i0 = tk[u] * kHdr20Task + lane * 4u;  // first header of this lane
             if (cnt[u] == kHdr20Task) {
                 __builtin_amdgcn_raw_buffer_store_b64(v2u{res[0] | (res[1] << 16), res[2] | (res[3] << 16)}, ors,
                                                       i0 * 2u, 0, 0);
@@ -1610,8 +1631,22 @@ struct Plan {
     int spw, rows, xcd;
     bool nt;
     uint32_t run;     // ragged scan kernel: segments per wave task (1..kScanRun)
-    uint32_t xchunk;  // fixed buffer kernel, XCD deal: log2 tasks per interleaved chunk (0 = contiguous eighths)
+    int xcd_chunk_param;  // raw NSX_PARAM_XCD_CHUNK (deal_clog)
 };
+
+// XCD-interleaved chunk deal (chunk_deal): log2 of the tasks per chunk. param = NSX_PARAM_XCD_CHUNK:
+// 1..20 fixed, 0 auto, anything else off (contiguous eighths). Auto: chunks of at most 24 MiB of batch
+// (config 2: 2^12 tasks of 4 × 1500 B), but at least 64 chunks; off when that leaves < 4 tasks a chunk.
+// Contiguous eighths ran 8% slow on some allocations on some boxes; 2^10-2^14-task chunks never did
+// (tools/alloc_study.py).
+static uint32_t deal_clog(int param, uint64_t ntasks, uint64_t task_bytes) {
+    if (param >= 1 && param <= 20) return (uint32_t)param;
+    if (param != 0) return 0u;
+    uint32_t k = 0;
+    while (k < 20 && (task_bytes << (k + 1)) <= (24ull << 20)) ++k;
+    while (k > 0 && (ntasks >> k) < 64) --k;
+    return k >= 2 ? k : 0u;
+}
 
 enum class Path { kFixedShort, kFixedLong, kRagged, kBlock };
 
@@ -1634,9 +1669,7 @@ static Plan resolve(const LaunchCfg& c, Path p) {
         r.xcd = 3;  // byte-balanced wave ranges (scan kernel only)
     r.nt = c.nontemporal != 2;
     r.run = (c.run_segs >= 1 && c.run_segs <= (int)kScanRun) ? (uint32_t)c.run_segs : kScanRun;
-    // XCD-interleaved chunks of 2^12 wave tasks by default: contiguous eighths measured 8% slow on some
-    // allocations on some boxes (tools/alloc_study.py), chunks of 2^10-2^14 never
-    r.xchunk = (c.xcd_chunk >= 1 && c.xcd_chunk <= 20) ? (uint32_t)c.xcd_chunk : (c.xcd_chunk == 0 ? 12u : 0u);
+    r.xcd_chunk_param = c.xcd_chunk;
     return r;
 }
 
@@ -1674,22 +1707,23 @@ static hipError_t launch_fixed_pipe(const Plan& c, const uint8_t* base, uint64_t
     const uint64_t want = (ntasks + kWavesPerBlock - 1) / kWavesPerBlock;
     const uint32_t grid = (uint32_t)(want < c.max_blocks ? want : c.max_blocks);
     const bool aligned = ((uintptr_t)base & 3u) == 0 && (stride & 3u) == 0 && (seg_len & 3u) == 0;
+    const uint32_t clog = deal_clog(c.xcd_chunk_param, ntasks, (uint64_t)u * stride);
 #define NSX_PIPE(U_, NR_)                                                                                  \
     if (u == U_ && nrows == NR_) {                                                                          \
         if (aligned) {                                                                                      \
             if (c.nt)                                                                                       \
                 hipLaunchKernelGGL((csum_fixed_buf_kernel<U_, NR_, true, true>), dim3(grid), dim3(kBlock), 0, st, \
-                                   base, stride, seg_len, (uint32_t)n, partial, out, c.xcd, c.xchunk);      \
+                                   base, stride, seg_len, (uint32_t)n, partial, out, c.xcd, clog);          \
             else                                                                                            \
                 hipLaunchKernelGGL((csum_fixed_buf_kernel<U_, NR_, false, true>), dim3(grid), dim3(kBlock), 0, \
-                                   st, base, stride, seg_len, (uint32_t)n, partial, out, c.xcd, c.xchunk);  \
+                                   st, base, stride, seg_len, (uint32_t)n, partial, out, c.xcd, clog);      \
         } else {                                                                                            \
             if (c.nt)                                                                                       \
                 hipLaunchKernelGGL((csum_fixed_buf_kernel<U_, NR_, true, false>), dim3(grid), dim3(kBlock), 0, \
-                                   st, base, stride, seg_len, (uint32_t)n, partial, out, c.xcd, c.xchunk);  \
+                                   st, base, stride, seg_len, (uint32_t)n, partial, out, c.xcd, clog);      \
             else                                                                                            \
                 hipLaunchKernelGGL((csum_fixed_buf_kernel<U_, NR_, false, false>), dim3(grid), dim3(kBlock), 0, \
-                                   st, base, stride, seg_len, (uint32_t)n, partial, out, c.xcd, c.xchunk);  \
+                                   st, base, stride, seg_len, (uint32_t)n, partial, out, c.xcd, clog);      \
         }                                                                                                   \
         return hipGetLastError();                                                                           \
     }
@@ -1715,12 +1749,13 @@ static hipError_t launch_seg(const Plan& c, const uint8_t* base, const uint64_t*
     } else {
         const uint64_t want = (n + kWavesPerBlock - 1) / kWavesPerBlock;
         const uint32_t grid = (uint32_t)(want < c.max_blocks ? want : c.max_blocks);
+        const uint32_t clog = RAGGED ? 0u : deal_clog(c.xcd_chunk_param, n, std::max<uint64_t>(stride, 1));
         if (c.nt)
             hipLaunchKernelGGL((csum_wave_kernel<RAGGED, 4, true, VERIFY>), dim3(grid), dim3(kBlock), 0, st, base,
-                               offsets, stride, seg_len, n, partial, out, ok, safe_end, c.xcd);
+                               offsets, stride, seg_len, n, partial, out, ok, safe_end, c.xcd, clog);
         else
             hipLaunchKernelGGL((csum_wave_kernel<RAGGED, 4, false, VERIFY>), dim3(grid), dim3(kBlock), 0, st, base,
-                               offsets, stride, seg_len, n, partial, out, ok, safe_end, c.xcd);
+                               offsets, stride, seg_len, n, partial, out, ok, safe_end, c.xcd, clog);
     }
     return hipGetLastError();
 }
@@ -1895,19 +1930,20 @@ hipError_t launch_verify_mask(const uint16_t* raw, uint64_t n, uint64_t* mask, u
 hipError_t launch_tcp_build(const TcpHdrSoA& h, const uint8_t* opts, const uint64_t* opt_off, const uint8_t* data,
                             const uint64_t* data_off, uint64_t data_bytes, const uint32_t* partial, uint64_t n,
                             uint8_t* out, const uint64_t* out_off, uint16_t* raw, uint32_t max_blocks, int policy,
-                            hipStream_t st) {
+                            int xchunk, hipStream_t st) {
     // Group size: up to 64 segments per wave task, fewer when n would leave waves idle.
     const uint64_t waves = (uint64_t)max_blocks * kWavesPerBlock;
     const uint32_t group = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, (n + waves - 1) / waves));
     const uint64_t tasks = (n + group - 1) / group;
     const uint64_t want = (tasks + kWavesPerBlock - 1) / kWavesPerBlock;
     const uint32_t grid = (uint32_t)(want < max_blocks ? want : max_blocks);
+    const uint32_t clog = deal_clog(xchunk, tasks, (uint64_t)group * 3000u);  // ~payload + image per segment
     // policy: 0/2 = default cache policy (measured best: segment-boundary lines stay in L2 for
     // the neighbour segment's load and partial-line stores merge there), 1 = nt loads and
     // stores, 3 = nt loads + plain stores, 4 = plain loads + nt stores
 #define NSX_BUILD(LP, SP)                                                                                         \
     hipLaunchKernelGGL((tcp_build_kernel<LP, SP>), dim3(grid), dim3(kBlock), 0, st, h, opts, opt_off, data, data_off, \
-                       data_bytes, partial, n, out, out_off, raw, group)
+                       data_bytes, partial, n, out, out_off, raw, group, clog)
     switch (policy) {
         case 1: NSX_BUILD(2, 2); break;
         case 3: NSX_BUILD(2, 0); break;
@@ -1919,7 +1955,7 @@ hipError_t launch_tcp_build(const TcpHdrSoA& h, const uint8_t* opts, const uint6
 }
 
 hipError_t launch_ipv4_hdr(uint8_t* base, uint64_t stride, uint32_t hdr_off, uint64_t n, int mode, uint16_t* out,
-                           int cus, int bpc, int kernel, int unroll, hipStream_t st) {
+                           int cus, int bpc, int kernel, int unroll, int xchunk, hipStream_t st) {
     // kernel: 0 = auto (flat for packed 20 B headers, else LDS-dense for stride ≤ 64, else per-thread),
     // 1 = per-thread, 2 = LDS-dense (stride ≤ 64)
     if (stride == 20 && hdr_off == 0 && ((uintptr_t)base & 3u) == 0 && kernel == 0) {
@@ -1936,10 +1972,13 @@ hipError_t launch_ipv4_hdr(uint8_t* base, uint64_t stride, uint32_t hdr_off, uin
             uint8_t* b = base + c0 * 20u;
             uint16_t* o = out ? out + c0 : nullptr;
             const size_t lds = (size_t)kHdr20Lds * kWavesPerBlock;
+            const uint32_t clog = deal_clog(xchunk, tasks, kHdr20Lds + kHdr20Task * 2u);
 #define NSX_H20(U)                                                                                              \
     do {                                                                                                        \
-        if (mode == 1) hipLaunchKernelGGL((ipv4_hdr20_kernel<1, U>), dim3(grid_f), dim3(kBlock), lds, st, b, cn, o); \
-        else hipLaunchKernelGGL((ipv4_hdr20_kernel<0, U>), dim3(grid_f), dim3(kBlock), lds, st, b, cn, o);        \
+        if (mode == 1)                                                                                          \
+            hipLaunchKernelGGL((ipv4_hdr20_kernel<1, U>), dim3(grid_f), dim3(kBlock), lds, st, b, cn, o, clog);   \
+        else                                                                                                    \
+            hipLaunchKernelGGL((ipv4_hdr20_kernel<0, U>), dim3(grid_f), dim3(kBlock), lds, st, b, cn, o, clog);   \
     } while (0)
             switch (unroll) {
                 case 1: NSX_H20(1); break;

@@ -189,7 +189,8 @@ VARIANTS = ([dict(kernel=2, spw=s, nt=nt, xcd=x, bpc=b, rows=0) for s in (1, 2, 
             [dict(kernel=3, spw=s, nt=nt, xcd=x, bpc=b, rows=0) for s in (1, 2, 4, 8) for nt in (1, 2)
              for x in (1, 2, 3) for b in (8, 3)] +
             [dict(kernel=3, spw=s, nt=1, xcd=1, bpc=b, rows=0, chunk=c) for s in (1, 4) for b in (8, 2)
-             for c in (1, 3, 6, 10, 99)])
+             for c in (1, 3, 6, 10, 99)] +
+            [dict(kernel=2, spw=1, nt=1, xcd=1, bpc=b, rows=0, chunk=c) for b in (8, 2) for c in (2, 5, 99)])
 
 
 def set_variant(v, block_mode=0):
@@ -641,6 +642,26 @@ def test_ipv4_dense_headers_end_at_allocation_end(stride, hdr_off, kernel, nsx_p
         assert got[b0 + 10] == f >> 8 and got[b0 + 11] == f & 0xFF, i
     raw = u16(nsx.ipv4_hdr_csum_dev(d, stride, n, hdr_off=hdr_off, mode=0))
     assert (raw == 0xFFFF).all()
+
+
+def test_xcd_deal_variants_agree_build_and_headers(nsx_param):
+    """The XCD deal (auto interleaved chunks, fixed small chunks, contiguous eighths)
+    changes only which wave takes which task: TCP build images and IPv4 header sums
+    are identical under every deal."""
+    rng = np.random.default_rng(31)
+    n, P = 64 * 700 + 13, 1480
+    fields, data, data_off, out_off, ps = _uniform_build_case(rng, n, P, 20)
+    ref_img, ref_raw = O.c_go_tcp_build(fields, data, data_off, out_off, ps)
+    nh = 256 * 900 + 77
+    hb = rng.integers(0, 256, nh * 20, dtype=np.uint8)
+    hb[::20] = 0x45
+    want_h = O.c_batch(hb, nh, stride=20, seg_len=20)
+    for chunk in (0, 2, 4, 99):
+        nsx_param(nsx.PARAM_XCD_CHUNK, chunk)
+        img, raw = _run_build(fields, data, data_off, out_off, ps)
+        assert np.array_equal(raw, ref_raw) and np.array_equal(img, ref_img), chunk
+        got = u16(nsx.ipv4_hdr_csum_dev(dev(hb), 20, nh, mode=0))
+        assert np.array_equal(got, want_h), chunk
 
 
 def test_ipv4_header_kat():

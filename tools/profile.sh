@@ -1,7 +1,7 @@
 #!/bin/bash
 # rocprofv3 evidence for one bench workload: kernel-trace stats, then each PMC
 # group in its own pass (never combined with other trace domains).
-# usage: [GROUPS_ONLY="kt fetch write sq sq2 tcc"] tools/profile.sh <config> [tag]
+# usage: [GROUPS_ONLY="kt fetch write sq sq2 tlb tcc"] tools/profile.sh <config> [tag]
 set -u
 cfg=${1:-2}; tag=${2:-r01}
 out=gpurun_out/prof_${tag}_c${cfg}
@@ -22,4 +22,5 @@ if want fetch; then run fetch 300 --kernel-trace --pmc FETCH_SIZE; fi
 if want write; then run write 300 --kernel-trace --pmc WRITE_SIZE; fi
 if want sq; then run sq 300 --kernel-trace --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE; fi
 if want sq2; then run sq2 300 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA SQ_INST_LEVEL_VMEM SQ_WAVE_CYCLES SQ_ACTIVE_INST_VMEM SQ_INSTS_VMEM_WR; fi
+if want tlb; then run tlb 300 --kernel-trace --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_REQUEST_sum TCP_UTCL1_STALL_MULTI_MISS_sum; fi
 if want tcc; then run tcc 300 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum; fi
