@@ -75,9 +75,7 @@ def parse_args(argv=None):
     ap.add_argument("--event-every", type=int, default=10,
                     help="record the per-launch HIP event pair around every N-th timed launch")
     ap.add_argument("--param", action="append", default=[], metavar="NAME=V",
-                    help="kernel knob (include/nsx_csum.h NSX_PARAM_*): " + ", ".join(
-                        ["blocks_per_cu", "segs_per_wave", "nontemporal", "block_mode", "xcd_map", "kernel",
-                         "stream_rows", "run_segs"]))
+                    help="kernel knob (include/nsx_csum.h NSX_PARAM_*): " + ", ".join(PARAMS))
     return ap.parse_args(argv)
 
 

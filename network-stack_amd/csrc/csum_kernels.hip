@@ -413,6 +413,87 @@ __global__ __launch_bounds__(kBlock) void csum_fixed_buf_kernel(
     }
 }
 
+// Software-pipelined form of the ALIGNED csum_fixed_buf_kernel: two register sets of one task each
+// (U segments × NROWS rows); the next task's loads are issued before the current task is reduced, so a
+// wave keeps its loads in flight through its own reduce/park/flush phases instead of leaving them to
+// other waves. Same deal, parking and flush as the unpipelined kernel.
+template <int U, int NROWS, bool NT>
+__global__ __launch_bounds__(kBlock) void csum_fixed_swp_kernel(
+    const uint8_t* __restrict__ base, uint64_t stride, uint32_t seg_len, uint32_t n,
+    const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, int xcd_map, uint32_t chunk_log2) {
+    constexpr uint32_t G = kWave / U;
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const uint32_t ntasks = (n + U - 1) / U;
+    TaskIter it = task_iter(ntasks, wave, xcd_map);
+    const ChunkDeal cd = chunk_deal(it, wave, xcd_map, chunk_log2, ntasks);
+    const uint32_t end = (uint32_t)it.end, step = (uint32_t)it.step;
+    const __amdgpu_buffer_rsrc_t ors = make_rsrc(out, (uint64_t)n * 2);
+    const __amdgpu_buffer_rsrc_t prs = make_rsrc(partial, partial ? (uint64_t)n * 4 : 0);
+    auto group_seg = [&](uint32_t first) { return cd.task(first + (lane / U) * step) * U + lane % U; };
+    struct Set {
+        u32x4 v[U][NROWS];
+        bool ok;
+    };
+    auto issue = [&](uint32_t i, Set& S) {
+        const uint32_t t = cd.task(i);
+        S.ok = i < end && t < ntasks;
+        const uint32_t s0 = (S.ok ? t : 0u) * U;
+        const uint8_t* p = base + (uint64_t)s0 * stride;
+#pragma unroll
+        for (int u = 0; u < U; ++u, p += stride) {
+            const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<uint8_t*>(p), 0, (S.ok && s0 + u < n) ? (int)seg_len : 0, 0x00020000);
+#pragma unroll
+            for (int rr = 0; rr < NROWS; ++rr) S.v[u][rr] = bld16<NT>(r, rr * kRow + lane * 16);
+        }
+    };
+    uint32_t res = 0, k = 0, first = (uint32_t)it.next;
+    uint32_t gpart;
+    {
+        const uint32_t sg = group_seg(first);
+        gpart = __builtin_amdgcn_raw_buffer_load_b32(prs, sg < n ? sg * 4 : kOOB, 0, 0);
+    }
+    auto consume = [&](uint32_t i, Set& S) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int rr = 0; rr < NROWS; ++rr) asm volatile("" : "+v"(S.v[u][rr]));
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            uint32_t acc = 0;
+#pragma unroll
+            for (int rr = 0; rr < NROWS; ++rr) acc = sad4(S.v[u][rr], acc);
+            const uint32_t tot = wave_sum(fold32(acc));
+            res = lane == k * U + u ? tot : res;
+        }
+        if (++k == G) {
+            res = finish(res, true, gpart);
+            fixed_flush<U>(res, first, step, k, n, ors, lane, cd);
+            k = 0;
+            first = i + step;
+            const uint32_t sg = group_seg(first);
+            gpart = __builtin_amdgcn_raw_buffer_load_b32(prs, (first < end && sg < n) ? sg * 4 : kOOB, 0, 0);
+        }
+    };
+    Set A, B;
+    uint32_t i = (uint32_t)it.next;
+    issue(i, A);
+    while (A.ok) {
+        const uint32_t i1 = i + step;
+        issue(i1, B);
+        consume(i, A);
+        if (!B.ok) break;
+        i = i1 + step;
+        issue(i, A);
+        consume(i1, B);
+    }
+    if (k) {
+        res = finish(res, true, gpart);
+        fixed_flush<U>(res, first, step, k, n, ors, lane, cd);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // One segment per wave, runtime row count, rows issued R at a time. Serves the
 // ragged batch (offsets) and fixed batches with long segments.
@@ -1525,6 +1606,102 @@ __global__ __launch_bounds__(kBlock) void ipv4_hdr20_kernel(uint8_t* __restrict_
     }
 }
 
+// Software-pipelined variant of ipv4_hdr20_kernel: two register sets of U tasks; the loads of the next
+// set are issued before the current set goes through LDS, so every wave keeps loads in flight while it
+// computes and stores (one wave per SIMD at 1 block/CU has no other wave to cover those phases).
+template <int MODE, int U>
+__global__ __launch_bounds__(kBlock) void ipv4_hdr20_pipe_kernel(uint8_t* __restrict__ base, uint32_t n,
+                                                                 uint16_t* __restrict__ out, uint32_t clog) {
+    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+    extern __shared__ u32x4 lds20[];
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    u32x4* my = lds20 + wave * (kHdr20Lds / 16u);
+    const uint32_t ntasks = (n + kHdr20Task - 1) / kHdr20Task;
+    TaskIter it = task_iter(ntasks, wave, 1);
+    const ChunkDeal cd = chunk_deal(it, wave, 1, clog, ntasks);
+    const uint32_t end = (uint32_t)it.end, step = (uint32_t)it.step;
+    const __amdgpu_buffer_rsrc_t ors = make_rsrc(out, out ? (uint64_t)n * 2 : 0);
+    struct Set {
+        __amdgpu_buffer_rsrc_t rs[U];
+        uint32_t cnt[U], tk[U];
+        u32x4 v[U][5];
+    };
+    auto live = [&](uint32_t t0) { return t0 < end && cd.task(t0) < ntasks; };
+    auto issue = [&](uint32_t t0, Set& S) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t ii = t0 + (uint32_t)u * step;
+            const uint32_t task = cd.task(ii);
+            S.tk[u] = task;
+            S.cnt[u] = (ii < end && task < ntasks) ? min(kHdr20Task, n - task * kHdr20Task) : 0u;
+            S.rs[u] = make_rsrc(base + (uint64_t)min(task, ntasks - 1) * kHdr20Lds, S.cnt[u] * 20u);
+#pragma unroll
+            for (int j = 0; j < 5; ++j) S.v[u][j] = bld16<true>(S.rs[u], j * kRow + lane * 16u);
+        }
+    };
+    auto consume = [&](Set& S) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < 5; ++j) asm volatile("" : "+v"(S.v[u][j]));
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!S.cnt[u]) break;  // wave-uniform
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int j = 0; j < 5; ++j) my[j * kWave + lane] = S.v[u][j];
+            __builtin_amdgcn_wave_barrier();
+            u32x4 q[5];
+#pragma unroll
+            for (int j = 0; j < 5; ++j) q[j] = my[lane * 5 + j];
+            const uint32_t d[20] = {q[0].x, q[0].y, q[0].z, q[0].w, q[1].x, q[1].y, q[1].z, q[1].w, q[2].x, q[2].y,
+                                    q[2].z, q[2].w, q[3].x, q[3].y, q[3].z, q[3].w, q[4].x, q[4].y, q[4].z, q[4].w};
+            uint32_t res[4];
+            bool ok[4];
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                const uint32_t* w = d + 5 * h;
+                ok[h] = (w[0] & 15u) == 5u;
+                uint32_t acc = __builtin_amdgcn_sad_u16(w[0], 0u, 0u);
+                acc = __builtin_amdgcn_sad_u16(w[1], 0u, acc);
+                acc = __builtin_amdgcn_sad_u16(MODE == 1 ? (w[2] & 0xFFFFu) : w[2], 0u, acc);
+                acc = __builtin_amdgcn_sad_u16(w[3], 0u, acc);
+                acc = __builtin_amdgcn_sad_u16(w[4], 0u, acc);
+                res[h] = ok[h] ? finish(acc, true, 0u) : 0u;
+            }
+            const uint32_t i0 = S.tk[u] * kHdr20Task + lane * 4u;
+            if (S.cnt[u] == kHdr20Task) {
+                __builtin_amdgcn_raw_buffer_store_b64(v2u{res[0] | (res[1] << 16), res[2] | (res[3] << 16)}, ors,
+                                                      i0 * 2u, 0, 0);
+            } else {
+#pragma unroll
+                for (int h = 0; h < 4; ++h)
+                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res[h], ors, i0 + h < n ? (i0 + h) * 2u : kOOB, 0,
+                                                          0);
+            }
+            if constexpr (MODE == 1) {
+#pragma unroll
+                for (int h = 0; h < 4; ++h)
+                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)bswap16u(~res[h] & 0xFFFFu), S.rs[u],
+                                                          ok[h] ? lane * 80u + h * 20u + 10u : kOOB, 0, 0);
+            }
+        }
+    };
+    Set A, B;
+    uint32_t t0 = (uint32_t)it.next;
+    issue(t0, A);
+    while (live(t0)) {
+        const uint32_t t1 = t0 + step * U;
+        issue(t1, B);
+        consume(A);
+        if (!live(t1)) break;
+        t0 = t1 + step * U;
+        issue(t0, A);
+        consume(B);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // IPv4 pseudo-header partials: src(4) dst(4) 0 proto len16 (RFC 9293 §3.1).
 // ---------------------------------------------------------------------------
@@ -1702,7 +1879,7 @@ static hipError_t launch_fixed_rows(const Plan& c, const uint8_t* base, uint64_t
 
 static hipError_t launch_fixed_pipe(const Plan& c, const uint8_t* base, uint64_t stride, uint32_t seg_len,
                                     uint64_t n, const uint32_t* partial, uint16_t* out, const uint8_t* safe_end,
-                                    int nrows, int u, hipStream_t st) {
+                                    int nrows, int u, bool swp, hipStream_t st) {
     const uint64_t ntasks = (n + u - 1) / u;
     const uint64_t want = (ntasks + kWavesPerBlock - 1) / kWavesPerBlock;
     const uint32_t grid = (uint32_t)(want < c.max_blocks ? want : c.max_blocks);
@@ -1710,7 +1887,14 @@ static hipError_t launch_fixed_pipe(const Plan& c, const uint8_t* base, uint64_t
     const uint32_t clog = deal_clog(c.xcd_chunk_param, ntasks, (uint64_t)u * stride);
 #define NSX_PIPE(U_, NR_)                                                                                  \
     if (u == U_ && nrows == NR_) {                                                                          \
-        if (aligned) {                                                                                      \
+        if (aligned && swp) {                                                                               \
+            if (c.nt)                                                                                       \
+                hipLaunchKernelGGL((csum_fixed_swp_kernel<U_, NR_, true>), dim3(grid), dim3(kBlock), 0, st,    \
+                                   base, stride, seg_len, (uint32_t)n, partial, out, c.xcd, clog);          \
+            else                                                                                            \
+                hipLaunchKernelGGL((csum_fixed_swp_kernel<U_, NR_, false>), dim3(grid), dim3(kBlock), 0, st,   \
+                                   base, stride, seg_len, (uint32_t)n, partial, out, c.xcd, clog);          \
+        } else if (aligned) {                                                                               \
             if (c.nt)                                                                                       \
                 hipLaunchKernelGGL((csum_fixed_buf_kernel<U_, NR_, true, true>), dim3(grid), dim3(kBlock), 0, st, \
                                    base, stride, seg_len, (uint32_t)n, partial, out, c.xcd, clog);          \
@@ -1798,14 +1982,15 @@ hipError_t launch_fixed(const LaunchCfg& c, const void* d_base, uint64_t stride,
         return launch_stream<false, false>(p, base, nullptr, stride, seg_len, n, partial, out, nullptr, safe_end, st);
     if (path == Path::kFixedShort) {
         const int nrows = rows <= 1 ? 1 : (rows <= 2 ? 2 : 4);
-        if (c.kernel == kKernelPipelined || c.kernel == 0) {
+        if (c.kernel == kKernelPipelined || c.kernel == kKernelSwPipe || c.kernel == 0) {
             const int u = (nrows == 4 && p.spw > 4) ? 4 : p.spw;
             // Buffer descriptors address ≤ 2^31 bytes of results/partials: chunk huge batches.
             constexpr uint64_t kChunk = 1ull << 28;
             for (uint64_t c0 = 0; c0 < n; c0 += kChunk) {
                 const uint64_t cn = n - c0 < kChunk ? n - c0 : kChunk;
                 hipError_t e = launch_fixed_pipe(p, base + c0 * stride, stride, seg_len, cn,
-                                                 partial ? partial + c0 : nullptr, out + c0, safe_end, nrows, u, st);
+                                                 partial ? partial + c0 : nullptr, out + c0, safe_end, nrows, u,
+                                                 c.kernel == kKernelSwPipe, st);
                 if (e != hipSuccess) return e;
             }
             return hipSuccess;
@@ -1956,9 +2141,10 @@ hipError_t launch_tcp_build(const TcpHdrSoA& h, const uint8_t* opts, const uint6
 
 hipError_t launch_ipv4_hdr(uint8_t* base, uint64_t stride, uint32_t hdr_off, uint64_t n, int mode, uint16_t* out,
                            int cus, int bpc, int kernel, int unroll, int xchunk, hipStream_t st) {
-    // kernel: 0 = auto (flat for packed 20 B headers, else LDS-dense for stride ≤ 64, else per-thread),
-    // 1 = per-thread, 2 = LDS-dense (stride ≤ 64)
-    if (stride == 20 && hdr_off == 0 && ((uintptr_t)base & 3u) == 0 && kernel == 0) {
+    // kernel: 0 = auto (pipelined flat kernel for packed 20 B headers, else LDS-dense for stride ≤ 64, else
+    // per-thread), 1 = per-thread, 2 = LDS-dense (stride ≤ 64), 3 = flat without pipelining
+    if (stride == 20 && hdr_off == 0 && ((uintptr_t)base & 3u) == 0 && (kernel == 0 || kernel == 3)) {
+        const bool pipe = kernel == 0;  // kernel 3: the unpipelined flat kernel (measured alternative)
         // packed option-less headers: flat-stream kernel. Default 1 block/CU with 2 tasks (10 KiB) in flight
         // per wave = 40 KiB per CU (tools/sweep.py: 0.220 ms vs 0.232 at 2 blocks/CU, 0.284 at 1 task/wave);
         // chunks keep each launch's results within one descriptor
@@ -1975,7 +2161,14 @@ hipError_t launch_ipv4_hdr(uint8_t* base, uint64_t stride, uint32_t hdr_off, uin
             const uint32_t clog = deal_clog(xchunk, tasks, kHdr20Lds + kHdr20Task * 2u);
 #define NSX_H20(U)                                                                                              \
     do {                                                                                                        \
-        if (mode == 1)                                                                                          \
+        if (pipe) {                                                                                             \
+            if (mode == 1)                                                                                      \
+                hipLaunchKernelGGL((ipv4_hdr20_pipe_kernel<1, U>), dim3(grid_f), dim3(kBlock), lds, st, b, cn, o, \
+                                   clog);                                                                       \
+            else                                                                                                \
+                hipLaunchKernelGGL((ipv4_hdr20_pipe_kernel<0, U>), dim3(grid_f), dim3(kBlock), lds, st, b, cn, o, \
+                                   clog);                                                                       \
+        } else if (mode == 1)                                                                                   \
             hipLaunchKernelGGL((ipv4_hdr20_kernel<1, U>), dim3(grid_f), dim3(kBlock), lds, st, b, cn, o, clog);   \
         else                                                                                                    \
             hipLaunchKernelGGL((ipv4_hdr20_kernel<0, U>), dim3(grid_f), dim3(kBlock), lds, st, b, cn, o, clog);   \

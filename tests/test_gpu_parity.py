@@ -190,7 +190,9 @@ VARIANTS = ([dict(kernel=2, spw=s, nt=nt, xcd=x, bpc=b, rows=0) for s in (1, 2, 
              for x in (1, 2, 3) for b in (8, 3)] +
             [dict(kernel=3, spw=s, nt=1, xcd=1, bpc=b, rows=0, chunk=c) for s in (1, 4) for b in (8, 2)
              for c in (1, 3, 6, 10, 99)] +
-            [dict(kernel=2, spw=1, nt=1, xcd=1, bpc=b, rows=0, chunk=c) for b in (8, 2) for c in (2, 5, 99)])
+            [dict(kernel=2, spw=1, nt=1, xcd=1, bpc=b, rows=0, chunk=c) for b in (8, 2) for c in (2, 5, 99)] +
+            [dict(kernel=5, spw=s, nt=nt, xcd=x, bpc=b, rows=0, chunk=c) for s in (1, 2, 4, 8) for nt in (1, 2)
+             for x in (1, 2) for b in (8, 1) for c in (0, 99)])
 
 
 def set_variant(v, block_mode=0):
@@ -586,7 +588,7 @@ def _ipv4_headers(rng, n, stride, hdr_off):
     return buf, ihl
 
 
-@pytest.mark.parametrize("kernel", [0, 1, 2])  # 0: default (flat for packed 20 B, LDS-dense for stride <= 64), 1: per-thread, 2: LDS-dense
+@pytest.mark.parametrize("kernel", [0, 1, 2, 3])  # 0: default (pipelined flat for packed 20 B, LDS-dense for stride <= 64), 1: per-thread, 2: LDS-dense, 3: flat
 @pytest.mark.parametrize("stride,hdr_off", [(64, 0), (61, 1), (1514, 14), (1500, 0), (60, 0), (40, 3), (20, 0)])
 def test_ipv4_header_checksum_verify_and_fill(stride, hdr_off, kernel, nsx_param):
     nsx_param(nsx.PARAM_KERNEL, kernel)
@@ -620,7 +622,7 @@ def test_ipv4_header_checksum_verify_and_fill(stride, hdr_off, kernel, nsx_param
     assert (again[valid] == 0xFFFF).all()
 
 
-@pytest.mark.parametrize("kernel", [0, 1, 2])
+@pytest.mark.parametrize("kernel", [0, 1, 2, 3])
 @pytest.mark.parametrize("stride,hdr_off", [(20, 0), (22, 2), (23, 3)])
 def test_ipv4_dense_headers_end_at_allocation_end(stride, hdr_off, kernel, nsx_param):
     """Packed IHL=5 headers (header-split ring), the last one ending exactly at
