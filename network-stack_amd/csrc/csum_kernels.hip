@@ -1193,7 +1193,7 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
                                                            uint8_t* __restrict__ out,
                                                            const uint64_t* __restrict__ out_off,
                                                            uint16_t* __restrict__ raw_out, uint32_t group,
-                                                           uint32_t clog) {
+                                                           uint32_t clog, int pipe) {
     typedef uint32_t v4u __attribute__((ext_vector_type(4)));
     typedef uint32_t v3u __attribute__((ext_vector_type(3)));
     const uint32_t lane = threadIdx.x & (kWave - 1);
@@ -1246,6 +1246,57 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
             __builtin_amdgcn_raw_buffer_store_b32(S.D4 | bswap16u(~raw & 0xFFFFu), ors, lane == 0 ? 16u : kOOB, 0, SP);
             if (raw_out && lane == 0) raw_out[g0 + k] = (uint16_t)raw;
         };
+        // Every segment of the group on the fast path and at most 2 rows long (the bench layout): software-
+        // pipelined — segment k+1's two rows are loaded before segment k is built, so the wave keeps its loads
+        // in flight through its own header/sum/store phases (tools/probes/copy_layout.hip seg_swp vs seg).
+        const bool mfast = moptlen == 0 && (mdb & 3u) == 0 && mdb >= 20u && (mwire & 3u) == 0 && mwire <= 2u * kRow;
+        if (pipe && __builtin_amdgcn_ballot_w64(!(mfast || lane >= cnt)) == 0) {
+            struct Rows {
+                u32x4 v[2];
+            };
+            auto fload = [&](uint32_t kk, Rows& F) {  // kk ≥ cnt: an empty descriptor, the loads move nothing
+                const uint32_t kc = min(kk, cnt - 1u);
+                const uint64_t db = readlane64(mdb, kc);
+                const uint32_t nb4 = kk < cnt ? __builtin_amdgcn_readlane(mwire, kc) : 0u;
+                const __amdgpu_buffer_rsrc_t frs = make_rsrc(data + db - 20u, nb4);
+                F.v[0] = bld16<LP != 0>(frs, lane * 16u);
+                F.v[1] = bld16<LP != 0>(frs, kRow + lane * 16u);
+            };
+            auto fdone = [&](uint32_t kk, Rows& F) {
+                asm volatile("" : "+v"(F.v[0]), "+v"(F.v[1]));
+                BuildSeg S;
+                S.D0 = __builtin_amdgcn_readlane(mD0, kk);
+                S.D1 = __builtin_amdgcn_readlane(mD1, kk);
+                S.D2 = __builtin_amdgcn_readlane(mD2, kk);
+                S.D3 = __builtin_amdgcn_readlane(mD3, kk);
+                S.D4 = __builtin_amdgcn_readlane(mD4, kk);
+                const uint32_t nb4 = __builtin_amdgcn_readlane(mwire, kk);
+                const __amdgpu_buffer_rsrc_t ors = make_rsrc(out + readlane64(moo, kk), nb4);
+                u32x4 x = F.v[0];
+                x.x = lane == 0 ? S.D0 : (lane == 1 ? S.D4 : x.x);
+                x.y = lane == 0 ? S.D1 : x.y;
+                x.z = lane == 0 ? S.D2 : x.z;
+                x.w = lane == 0 ? S.D3 : x.w;
+                uint32_t acc = sad4(x, 0u);
+                const bool d4 = lane == 1;  // dword 4 waits for the field
+                __builtin_amdgcn_raw_buffer_store_b128(v4u{x.x, x.y, x.z, x.w}, ors, d4 ? kOOB : lane * 16u, 0, SP);
+                __builtin_amdgcn_raw_buffer_store_b96(v3u{x.y, x.z, x.w}, ors, d4 ? 20u : kOOB, 0, SP);
+                const u32x4 y = F.v[1];  // row 1: zeros past the image (range check), stores clipped likewise
+                acc = sad4(y, acc);
+                __builtin_amdgcn_raw_buffer_store_b128(v4u{y.x, y.y, y.z, y.w}, ors, kRow + lane * 16u, 0, SP);
+                seg_done(kk, S, ors, fold32(acc));
+            };
+            Rows A, B;
+            fload(0, A);
+            for (uint32_t kk = 0; kk < cnt; kk += 2) {
+                fload(kk + 1, B);
+                fdone(kk, A);
+                if (kk + 1 >= cnt) break;
+                fload(kk + 2, A);
+                fdone(kk + 1, B);
+            }
+            continue;
+        }
         uint32_t k = 0;
         while (k < cnt) {
             BuildSeg S;
@@ -2115,7 +2166,8 @@ hipError_t launch_verify_mask(const uint16_t* raw, uint64_t n, uint64_t* mask, u
 hipError_t launch_tcp_build(const TcpHdrSoA& h, const uint8_t* opts, const uint64_t* opt_off, const uint8_t* data,
                             const uint64_t* data_off, uint64_t data_bytes, const uint32_t* partial, uint64_t n,
                             uint8_t* out, const uint64_t* out_off, uint16_t* raw, uint32_t max_blocks, int policy,
-                            int xchunk, hipStream_t st) {
+                            int xchunk, int kernel, hipStream_t st) {
+    // kernel: 0 = groups of fast-path segments ≤ 2 rows software-pipelined, 2 = never pipelined
     // Group size: up to 64 segments per wave task, fewer when n would leave waves idle.
     const uint64_t waves = (uint64_t)max_blocks * kWavesPerBlock;
     const uint32_t group = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, (n + waves - 1) / waves));
@@ -2128,7 +2180,7 @@ hipError_t launch_tcp_build(const TcpHdrSoA& h, const uint8_t* opts, const uint6
     // stores, 3 = nt loads + plain stores, 4 = plain loads + nt stores
 #define NSX_BUILD(LP, SP)                                                                                         \
     hipLaunchKernelGGL((tcp_build_kernel<LP, SP>), dim3(grid), dim3(kBlock), 0, st, h, opts, opt_off, data, data_off, \
-                       data_bytes, partial, n, out, out_off, raw, group, clog)
+                       data_bytes, partial, n, out, out_off, raw, group, clog, kernel != 2)
     switch (policy) {
         case 1: NSX_BUILD(2, 2); break;
         case 3: NSX_BUILD(2, 0); break;

@@ -712,19 +712,22 @@ def _run_build(fields, data, data_off, out_off, ps):
 
 @pytest.mark.parametrize("P", [0, 4, 8, 12, 16, 100, 1004, 1480, 4096, 8996, 65536])
 @pytest.mark.parametrize("n", [1, 63, 64, 65, 300])
-def test_tcp_build_uniform_batches(P, n):
+def test_tcp_build_uniform_batches(P, n, nsx_param):
     """Packed option-less batches (same payload length, payloads and images back to
     back — the bench's f1 layout): images and raw sums equal the Go-faithful oracle's
-    for tiny, row-sized and 64 KiB payloads."""
+    for tiny, row-sized and 64 KiB payloads, with the pipelined fast-group path
+    (kernel 0, images ≤ 2 KiB) and without it (kernel 2)."""
     if n * (P + 20) > 40 << 20:
         n = 65
     rng = np.random.default_rng(P * 1000 + n)
     for lead in (20, 28, 0):  # lead 0: segment 0 has no 20 bytes before its payload (general path)
         fields, data, data_off, out_off, ps = _uniform_build_case(rng, n, P, lead)
-        got, raw = _run_build(fields, data, data_off, out_off, ps)
         want, wraw = O.c_go_tcp_build(fields, data, data_off, out_off, ps)
-        assert np.array_equal(raw, wraw), (P, n, lead)
-        assert np.array_equal(got, want), (P, n, lead)
+        for kern in (0, 2):
+            nsx_param(nsx.PARAM_KERNEL, kern)
+            got, raw = _run_build(fields, data, data_off, out_off, ps)
+            assert np.array_equal(raw, wraw), (P, n, lead, kern)
+            assert np.array_equal(got, want), (P, n, lead, kern)
 
 
 def test_tcp_build_whole_dword_and_ragged_payloads_interleaved():

@@ -6,6 +6,7 @@
 //              images at stride 1500 (20 B header gap), 2 rows in flight: the build
 //              kernel's access pattern with no header, no checksum
 //   seg_al   : the same with source/destination strides rounded to 1536 (16 B aligned)
+//   seg_swp  : seg, software-pipelined (the next segment's loads issue before this one's stores)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -52,6 +53,37 @@ __global__ __launch_bounds__(256) void seg_copy(const uint8_t* s, uint8_t* d, ui
     }
 }
 
+// the same per-segment copy, software-pipelined: segment i+nw's loads are issued before segment i is stored
+template <int LP, int SP>
+__global__ __launch_bounds__(256) void seg_copy_swp(const uint8_t* s, uint8_t* d, uint32_t n, uint32_t sstride,
+                                                    uint32_t dstride, uint32_t plen, uint32_t gap) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t nw = gridDim.x * 4;
+    auto ld = [&](uint32_t i, v4u& a, v4u& b) {
+        const __amdgpu_buffer_rsrc_t rs = rsrc(s + (uint64_t)(i < n ? i : 0) * sstride, i < n ? plen : 0);
+        a = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, 0, LP);
+        b = __builtin_amdgcn_raw_buffer_load_b128(rs, 1024 + lane * 16, 0, LP);
+    };
+    auto st = [&](uint32_t i, v4u& a, v4u& b) {
+        asm volatile("" : "+v"(a), "+v"(b));
+        const __amdgpu_buffer_rsrc_t rd = rsrc(d + (uint64_t)i * dstride + gap, plen);
+        __builtin_amdgcn_raw_buffer_store_b128(a, rd, lane * 16, 0, SP);
+        __builtin_amdgcn_raw_buffer_store_b128(b, rd, 1024 + lane * 16 < plen ? 1024 + lane * 16 : kOOB, 0, SP);
+    };
+    uint32_t i = blockIdx.x * 4 + wave;
+    v4u a0, b0, a1, b1;
+    ld(i, a0, b0);
+    while (i < n) {
+        const uint32_t i1 = i + nw;
+        ld(i1, a1, b1);
+        st(i, a0, b0);
+        if (i1 >= n) break;
+        i = i1 + nw;
+        ld(i, a0, b0);
+        st(i1, a1, b1);
+    }
+}
+
 template <typename F>
 float timeit(F f) {
     hipEvent_t a, b;
@@ -84,7 +116,7 @@ int main() {
     const uint64_t n16 = fb / 16 - 64;
     for (int k = 0; k < 50; ++k) hipLaunchKernelGGL(flat_mis, dim3(cus * 4), dim3(256), 0, 0, src, dst, n16, 0u, 0u);
     (void)hipDeviceSynchronize();
-    for (int bpc : {2, 4, 8}) {
+    for (int bpc : {1, 2, 4, 8}) {
         const int g = cus * bpc;
         const float a = timeit([&] { hipLaunchKernelGGL(flat_mis, dim3(g), dim3(256), 0, 0, src, dst, n16, 0u, 0u); });
         const float b = timeit([&] { hipLaunchKernelGGL(flat_mis, dim3(g), dim3(256), 0, 0, src, dst, n16, 4u, 12u); });
@@ -97,7 +129,11 @@ int main() {
         const float e = timeit([&] {
             hipLaunchKernelGGL((seg_copy<0, 0>), dim3(g), dim3(256), 0, 0, src, dst, n, 1536u, 1536u, 1480u, 32u);
         });
+        const float f = timeit([&] {
+            hipLaunchKernelGGL((seg_copy_swp<0, 0>), dim3(g), dim3(256), 0, 0, src, dst, n, 1480u, 1500u, 1480u, 20u);
+        });
         const double ab = 2.0 * n16 * 16, sb = 2.0 * n * 1480.0;
+        printf("bpc=%d seg_swp %.4f ms %.0f GB/s\n", bpc, f, sb / f / 1e6);
         printf("bpc=%d flat16 %.4f ms %.0f GB/s | flatmis %.4f ms %.0f GB/s | seg %.4f ms %.0f GB/s | seg(nt ld) %.4f ms "
                "%.0f GB/s | seg_al %.4f ms %.0f GB/s\n",
                bpc, a, ab / a / 1e6, b, ab / b / 1e6, c, sb / c / 1e6, c2, sb / c2 / 1e6, e, sb / e / 1e6);
