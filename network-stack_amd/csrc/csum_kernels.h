@@ -11,6 +11,7 @@ constexpr int kKernelPerSegment = 2; // csum_fixed_kernel / csum_wave_kernel
 constexpr int kKernelPipelined = 3;  // buffer-load kernels: csum_fixed_buf_kernel / csum_ragged_buf_kernel
 constexpr int kKernelScan = 4;       // csum_ragged_scan_kernel (ragged; the default there)
 constexpr int kKernelSwPipe = 5;     // csum_fixed_swp_kernel: software-pipelined fixed-stride buffer kernel
+constexpr int kKernelScanPipe = 6;   // csum_ragged_scan_kernel, software-pipelined row batches (nt loads)
 
 // Raw NSX_PARAM_* values (0 = "default for this path"); the launchers resolve
 // them per path (fixed short / fixed long / ragged) to the defaults measured

@@ -955,7 +955,7 @@ __device__ __forceinline__ void seg_lower_bound2(__amdgpu_buffer_rsrc_t ofs, uin
         s[k] = lo[k] + (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(v[k] < t[k]));
 }
 
-template <int R, bool NT, bool VERIFY>
+template <int R, bool NT, bool VERIFY, bool PIPE>
 __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, uint32_t n,
     const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, uint8_t* __restrict__ ok, int xcd_map,
@@ -1012,14 +1012,15 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
         const int64_t brel = lane <= cnt ? (int64_t)((base + my_off) - rbase) : -1;
         uint64_t bval = 0;
         uint64_t carry = 0;  // S over all rows before the current one
-        for (uint64_t r0 = 0; r0 < nrows; r0 += R) {
-            // One descriptor per batch, based at the batch's first row.
+        // Batch r0 = rows [r0, r0 + R), one descriptor based at its first row (rows past the run read 0).
+        auto issue = [&](uint64_t r0, u32x4 (&v)[R]) {
             const uint8_t* bb = rbase + r0 * kRow;
-            const uint64_t rem = span - r0 * kRow;
+            const uint64_t rem = r0 < nrows ? span - r0 * kRow : 0;
             const __amdgpu_buffer_rsrc_t rs = make_rsrc(bb, (rem + 3) & ~3ull);
-            u32x4 v[R];
 #pragma unroll
             for (int j = 0; j < R; ++j) v[j] = bld16<NT>(rs, j * kRow + lane * 16);
+        };
+        auto process = [&](uint64_t r0, u32x4 (&v)[R]) {
 #pragma unroll
             for (int j = 0; j < R; ++j) asm volatile("" : "+v"(v[j]));
             // Phase 1: edge masks (first/last row of the run only), lane half-sums
@@ -1066,6 +1067,24 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
             }
 #pragma unroll
             for (int j = 0; j < R; ++j) carry += __builtin_amdgcn_readlane(incl[j], 63);
+        };
+        if constexpr (PIPE) {
+            // two register sets: batch r0 + R loads while batch r0 is reduced
+            u32x4 A[R], B[R];
+            issue(0, A);
+            for (uint64_t r0 = 0; r0 < nrows; r0 += 2 * R) {
+                issue(r0 + R, B);
+                process(r0, A);
+                if (r0 + R >= nrows) break;
+                issue(r0 + 2 * R, A);
+                process(r0 + R, B);
+            }
+        } else {
+            for (uint64_t r0 = 0; r0 < nrows; r0 += R) {
+                u32x4 v[R];
+                issue(r0, v);
+                process(r0, v);
+            }
         }
         if (brel >= (int64_t)(nrows * kRow)) bval = carry;  // boundary at the very end of the rows
         // Segment `lane` = [boundary lane, boundary lane+1).
@@ -1893,7 +1912,7 @@ static Plan resolve(const LaunchCfg& c, Path p) {
                 ? c.segs_per_wave : 4;
     r.rows = (c.rows == 4 || c.rows == 8 || c.rows == 16) ? c.rows : 8;
     r.xcd = c.xcd_map == 2 ? 0 : (c.xcd_map == 3 ? 2 : (c.xcd_map == 4 ? 3 : 1));
-    if (c.xcd_map == 0 && p == Path::kRagged && (c.kernel == 0 || c.kernel == kKernelScan))
+    if (c.xcd_map == 0 && p == Path::kRagged && (c.kernel == 0 || c.kernel == kKernelScan || c.kernel == kKernelScanPipe))
         r.xcd = 3;  // byte-balanced wave ranges (scan kernel only)
     r.nt = c.nontemporal != 2;
     r.run = (c.run_segs >= 1 && c.run_segs <= (int)kScanRun) ? (uint32_t)c.run_segs : kScanRun;
@@ -2084,7 +2103,8 @@ static hipError_t launch_ragged_buf(const Plan& c, const uint8_t* base, const ui
 
 template <bool VERIFY>
 static hipError_t launch_ragged_scan(const Plan& c, const uint8_t* base, const uint64_t* offsets, uint64_t n,
-                                     const uint32_t* partial, uint16_t* out, uint8_t* ok, hipStream_t st) {
+                                     const uint32_t* partial, uint16_t* out, uint8_t* ok, bool pipe,
+                                     hipStream_t st) {
     constexpr uint64_t kChunk = 1ull << 27;
     for (uint64_t c0 = 0; c0 < n; c0 += kChunk) {
         const uint32_t cn = (uint32_t)(n - c0 < kChunk ? n - c0 : kChunk);
@@ -2096,12 +2116,15 @@ static hipError_t launch_ragged_scan(const Plan& c, const uint8_t* base, const u
         uint8_t* kc = ok ? ok + c0 : nullptr;
 #define NSX_RSCAN(R_)                                                                                             \
         if (c.rows == R_) {                                                                                        \
-            if (c.nt)                                                                                              \
-                hipLaunchKernelGGL((csum_ragged_scan_kernel<R_, true, VERIFY>), dim3(grid), dim3(kBlock), 0, st,   \
-                                   base, offsets + c0, cn, pc, oc, kc, c.xcd, c.run);                              \
+            if (pipe)                                                                                              \
+                hipLaunchKernelGGL((csum_ragged_scan_kernel<R_, true, VERIFY, true>), dim3(grid), dim3(kBlock), 0, \
+                                   st, base, offsets + c0, cn, pc, oc, kc, c.xcd, c.run);                          \
+            else if (c.nt)                                                                                         \
+                hipLaunchKernelGGL((csum_ragged_scan_kernel<R_, true, VERIFY, false>), dim3(grid), dim3(kBlock), 0, \
+                                   st, base, offsets + c0, cn, pc, oc, kc, c.xcd, c.run);                          \
             else                                                                                                   \
-                hipLaunchKernelGGL((csum_ragged_scan_kernel<R_, false, VERIFY>), dim3(grid), dim3(kBlock), 0, st,  \
-                                   base, offsets + c0, cn, pc, oc, kc, c.xcd, c.run);                              \
+                hipLaunchKernelGGL((csum_ragged_scan_kernel<R_, false, VERIFY, false>), dim3(grid), dim3(kBlock), 0, \
+                                   st, base, offsets + c0, cn, pc, oc, kc, c.xcd, c.run);                          \
         }
         NSX_RSCAN(4) NSX_RSCAN(8) NSX_RSCAN(16)
 #undef NSX_RSCAN
@@ -2120,9 +2143,10 @@ hipError_t launch_ragged(const LaunchCfg& c, const void* d_base, const uint64_t*
         return launch_seg<true, false>(p, base, d_offsets, 0, 0, n, partial, out, nullptr, nullptr, true, st);
     }
     const Plan p = resolve(c, Path::kRagged);
-    if (c.kernel == 0 || c.kernel == kKernelScan) {
-        if (ok) return launch_ragged_scan<true>(p, base, d_offsets, n, partial, out, ok, st);
-        return launch_ragged_scan<false>(p, base, d_offsets, n, partial, out, nullptr, st);
+    if (c.kernel == 0 || c.kernel == kKernelScan || c.kernel == kKernelScanPipe) {
+        const bool pipe = c.kernel == kKernelScanPipe;
+        if (ok) return launch_ragged_scan<true>(p, base, d_offsets, n, partial, out, ok, pipe, st);
+        return launch_ragged_scan<false>(p, base, d_offsets, n, partial, out, nullptr, pipe, st);
     }
     if (c.kernel == kKernelPipelined) {
         if (ok) return launch_ragged_buf<true>(p, base, d_offsets, n, partial, out, ok, st);

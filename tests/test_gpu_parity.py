@@ -232,7 +232,9 @@ RAGGED_VARIANTS = ([dict(kernel=k, rows=r, nt=nt, xcd=x, bpc=b, spw=0) for k in 
                    [dict(kernel=4, rows=8, nt=1, xcd=1, bpc=8, spw=0, run=rs) for rs in (1, 2, 7, 16, 33, 63)] +
                    [dict(kernel=2, rows=0, nt=1, xcd=x, bpc=4, spw=0) for x in (1, 3)] +
                    [dict(kernel=4, rows=r, nt=1, xcd=4, bpc=b, spw=0, run=rs) for r in (4, 8, 16) for b in (1, 2, 8)
-                    for rs in (1, 16, 63)])
+                    for rs in (1, 16, 63)] +
+                   [dict(kernel=6, rows=r, nt=1, xcd=x, bpc=b, spw=0, run=rs) for r in (4, 8, 16) for x in (1, 4)
+                    for b in (2, 8) for rs in (1, 63)])
 
 
 def test_ragged_variants_bit_exact():

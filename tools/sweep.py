@@ -39,10 +39,10 @@ def variants(kind):
             out.append(dict(kernel=4, blocks_per_cu=bpc, stream_rows=rows, nontemporal=1, xcd_map=1, run_segs=run))
         for bpc, rows in itertools.product((8, 4), (8, 16)):
             out.append(dict(kernel=3, blocks_per_cu=bpc, stream_rows=rows, nontemporal=1, xcd_map=1))
-    if kind == "ragged_ab":  # the previous ragged default against the byte-balanced one
-        return [dict(kernel=4, blocks_per_cu=2, stream_rows=8, nontemporal=1, xcd_map=1, run_segs=16),
-                dict(kernel=4, blocks_per_cu=2, stream_rows=8, nontemporal=1, xcd_map=4, run_segs=63),
-                dict(kernel=4, blocks_per_cu=2, stream_rows=8, nontemporal=1, xcd_map=4, run_segs=16)]
+    if kind == "ragged_ab":  # the default scan kernel against its software-pipelined form
+        return ([dict(kernel=4, blocks_per_cu=2, stream_rows=8, nontemporal=1, xcd_map=4, run_segs=63)] +
+                [dict(kernel=6, blocks_per_cu=b, stream_rows=r, nontemporal=1, xcd_map=4, run_segs=63)
+                 for b in (1, 2, 4) for r in (4, 8)])
     if kind == "ipv4_hdr":  # 0 auto (flat for packed 20 B), 1 per-thread, 2 LDS-dense
         return ([dict(kernel=0, blocks_per_cu=b, segs_per_wave=u) for b in (1, 2, 3, 4) for u in (1, 2, 4)] +
                 [dict(kernel=2, blocks_per_cu=8)])
