@@ -215,7 +215,7 @@ const char* nsx_strerror(int code);
 /* Kernel-variant knobs for benchmarking (process-wide; 0 = the default).
  * Not needed for correctness; every variant is bit-exact. */
 #define NSX_PARAM_BLOCKS_PER_CU   1  /* persistent grid, 1..8 blocks of 256 threads per CU (default per path) */
-#define NSX_PARAM_SEGS_PER_WAVE   2  /* per-segment kernels: 1, 2, 4 or 8 segments per wave pass; packed-20 B IPv4 header kernel: 1, 2 (default) or 4 tasks in flight per wave */
+#define NSX_PARAM_SEGS_PER_WAVE   2  /* per-segment kernels: 1, 2, 4 or 8 segments per wave pass; packed-20 B IPv4 header kernel: 1, 2 (default) or 4 tasks in flight per wave; nsx_tcp_build_dev: 1 or 2 (default) segments per pipelined register set */
 #define NSX_PARAM_NONTEMPORAL     3  /* 1 nt loads (default), 2 default-policy loads; nsx_tcp_build_dev: default plain, 1 nt, 3 nt loads + plain stores, 4 plain loads + nt stores */
 #define NSX_PARAM_BLOCK_MODE      4  /* 0 auto (a block per segment when n < 4*CUs), 1 never, 2 always */
 #define NSX_PARAM_XCD_MAP         5  /* task deal: 1 XCD-contiguous regions (default), 2 grid-stride, 3 one contiguous range per wave, 4 byte-balanced contiguous range per wave (ragged scan kernel; its default) */

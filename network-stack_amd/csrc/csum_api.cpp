@@ -244,10 +244,10 @@ int nsx_tcp_build_dev(const nsx_tcp_hdr_soa* hdr, const uint8_t* d_opts, const u
     const nsx::TcpHdrSoA h{hdr->src_port, hdr->dst_port, hdr->seq_num, hdr->ack_num,
                            hdr->offset,   hdr->control,  hdr->window,  hdr->urgent_ptr};
     return map_err(nsx::launch_tcp_build(h, d_opts, d_opt_off, d_data, d_data_off, data_bytes, d_prefix_partial, n,
-                                         d_out, d_out_off, d_raw, (uint32_t)di->cus * (uint32_t)(bpc >= 1 && bpc <= 8 ? bpc : 2),
+                                         d_out, d_out_off, d_raw, (uint32_t)di->cus * (uint32_t)(bpc >= 1 && bpc <= 8 ? bpc : 4),
                                          (int)g_param[NSX_PARAM_NONTEMPORAL].load(),
                                          (int)g_param[NSX_PARAM_XCD_CHUNK].load(), (int)g_param[NSX_PARAM_KERNEL].load(),
-                                         static_cast<hipStream_t>(stream)));
+                                         (int)g_param[NSX_PARAM_SEGS_PER_WAVE].load(), static_cast<hipStream_t>(stream)));
 }
 
 int nsx_ipv4_hdr_csum_dev(void* d_base, uint64_t stride, uint32_t hdr_off, uint64_t n, int mode,

@@ -55,7 +55,7 @@ struct TcpHdrSoA {  // device arrays, one entry per segment (tcp.go:39-54 field 
 hipError_t launch_tcp_build(const TcpHdrSoA& h, const uint8_t* opts, const uint64_t* opt_off, const uint8_t* data,
                             const uint64_t* data_off, uint64_t data_bytes, const uint32_t* partial, uint64_t n,
                             uint8_t* out, const uint64_t* out_off, uint16_t* raw, uint32_t max_blocks, int policy,
-                            int xchunk, int kernel, hipStream_t st);
+                            int xchunk, int kernel, int spw, hipStream_t st);
 // bpc / unroll: raw NSX_PARAM_BLOCKS_PER_CU / NSX_PARAM_SEGS_PER_WAVE (0 = per-kernel default)
 hipError_t launch_ipv4_hdr(uint8_t* base, uint64_t stride, uint32_t hdr_off, uint64_t n, int mode, uint16_t* out,
                            int cus, int bpc, int kernel, int unroll, int xchunk, hipStream_t st);

@@ -1203,7 +1203,8 @@ __device__ __forceinline__ uint32_t build_row(const BuildSeg& S, __amdgpu_buffer
     return acc;
 }
 
-template <int LP, int SP>
+// PS: segments per register set on the pipelined fast-group path
+template <int LP, int SP, int PS>
 __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const uint8_t* __restrict__ opts,
                                                            const uint64_t* __restrict__ opt_off,
                                                            const uint8_t* __restrict__ data,
@@ -1271,48 +1272,58 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
         const bool mfast = moptlen == 0 && (mdb & 3u) == 0 && mdb >= 20u && (mwire & 3u) == 0 && mwire <= 2u * kRow;
         if (pipe && __builtin_amdgcn_ballot_w64(!(mfast || lane >= cnt)) == 0) {
             struct Rows {
-                u32x4 v[2];
+                u32x4 v[PS][2];
             };
-            auto fload = [&](uint32_t kk, Rows& F) {  // kk ≥ cnt: an empty descriptor, the loads move nothing
-                const uint32_t kc = min(kk, cnt - 1u);
-                const uint64_t db = readlane64(mdb, kc);
-                const uint32_t nb4 = kk < cnt ? __builtin_amdgcn_readlane(mwire, kc) : 0u;
-                const __amdgpu_buffer_rsrc_t frs = make_rsrc(data + db - 20u, nb4);
-                F.v[0] = bld16<LP != 0>(frs, lane * 16u);
-                F.v[1] = bld16<LP != 0>(frs, kRow + lane * 16u);
+            auto fload = [&](uint32_t k0, Rows& F) {  // kk ≥ cnt: an empty descriptor, the loads move nothing
+#pragma unroll
+                for (uint32_t e = 0; e < (uint32_t)PS; ++e) {
+                    const uint32_t kk = k0 + e, kc = min(kk, cnt - 1u);
+                    const uint64_t db = readlane64(mdb, kc);
+                    const uint32_t nb4 = kk < cnt ? __builtin_amdgcn_readlane(mwire, kc) : 0u;
+                    const __amdgpu_buffer_rsrc_t frs = make_rsrc(data + db - 20u, nb4);
+                    F.v[e][0] = bld16<LP != 0>(frs, lane * 16u);
+                    F.v[e][1] = bld16<LP != 0>(frs, kRow + lane * 16u);
+                }
             };
-            auto fdone = [&](uint32_t kk, Rows& F) {
-                asm volatile("" : "+v"(F.v[0]), "+v"(F.v[1]));
-                BuildSeg S;
-                S.D0 = __builtin_amdgcn_readlane(mD0, kk);
-                S.D1 = __builtin_amdgcn_readlane(mD1, kk);
-                S.D2 = __builtin_amdgcn_readlane(mD2, kk);
-                S.D3 = __builtin_amdgcn_readlane(mD3, kk);
-                S.D4 = __builtin_amdgcn_readlane(mD4, kk);
-                const uint32_t nb4 = __builtin_amdgcn_readlane(mwire, kk);
-                const __amdgpu_buffer_rsrc_t ors = make_rsrc(out + readlane64(moo, kk), nb4);
-                u32x4 x = F.v[0];
-                x.x = lane == 0 ? S.D0 : (lane == 1 ? S.D4 : x.x);
-                x.y = lane == 0 ? S.D1 : x.y;
-                x.z = lane == 0 ? S.D2 : x.z;
-                x.w = lane == 0 ? S.D3 : x.w;
-                uint32_t acc = sad4(x, 0u);
-                const bool d4 = lane == 1;  // dword 4 waits for the field
-                __builtin_amdgcn_raw_buffer_store_b128(v4u{x.x, x.y, x.z, x.w}, ors, d4 ? kOOB : lane * 16u, 0, SP);
-                __builtin_amdgcn_raw_buffer_store_b96(v3u{x.y, x.z, x.w}, ors, d4 ? 20u : kOOB, 0, SP);
-                const u32x4 y = F.v[1];  // row 1: zeros past the image (range check), stores clipped likewise
-                acc = sad4(y, acc);
-                __builtin_amdgcn_raw_buffer_store_b128(v4u{y.x, y.y, y.z, y.w}, ors, kRow + lane * 16u, 0, SP);
-                seg_done(kk, S, ors, fold32(acc));
+            auto fdone = [&](uint32_t k0, Rows& F) {
+#pragma unroll
+                for (uint32_t e = 0; e < (uint32_t)PS; ++e) asm volatile("" : "+v"(F.v[e][0]), "+v"(F.v[e][1]));
+#pragma unroll
+                for (uint32_t e = 0; e < (uint32_t)PS; ++e) {
+                    const uint32_t kk = k0 + e;
+                    if (kk >= cnt) break;  // wave-uniform
+                    BuildSeg S;
+                    S.D0 = __builtin_amdgcn_readlane(mD0, kk);
+                    S.D1 = __builtin_amdgcn_readlane(mD1, kk);
+                    S.D2 = __builtin_amdgcn_readlane(mD2, kk);
+                    S.D3 = __builtin_amdgcn_readlane(mD3, kk);
+                    S.D4 = __builtin_amdgcn_readlane(mD4, kk);
+                    const uint32_t nb4 = __builtin_amdgcn_readlane(mwire, kk);
+                    const __amdgpu_buffer_rsrc_t ors = make_rsrc(out + readlane64(moo, kk), nb4);
+                    u32x4 x = F.v[e][0];
+                    x.x = lane == 0 ? S.D0 : (lane == 1 ? S.D4 : x.x);
+                    x.y = lane == 0 ? S.D1 : x.y;
+                    x.z = lane == 0 ? S.D2 : x.z;
+                    x.w = lane == 0 ? S.D3 : x.w;
+                    uint32_t acc = sad4(x, 0u);
+                    const bool d4 = lane == 1;  // dword 4 waits for the field
+                    __builtin_amdgcn_raw_buffer_store_b128(v4u{x.x, x.y, x.z, x.w}, ors, d4 ? kOOB : lane * 16u, 0,
+                                                           SP);
+                    __builtin_amdgcn_raw_buffer_store_b96(v3u{x.y, x.z, x.w}, ors, d4 ? 20u : kOOB, 0, SP);
+                    const u32x4 y = F.v[e][1];  // row 1: zeros past the image (range check), stores clipped likewise
+                    acc = sad4(y, acc);
+                    __builtin_amdgcn_raw_buffer_store_b128(v4u{y.x, y.y, y.z, y.w}, ors, kRow + lane * 16u, 0, SP);
+                    seg_done(kk, S, ors, fold32(acc));
+                }
             };
             Rows A, B;
             fload(0, A);
-            for (uint32_t kk = 0; kk < cnt; kk += 2) {
-                fload(kk + 1, B);
+            for (uint32_t kk = 0; kk < cnt; kk += 2u * PS) {
+                fload(kk + PS, B);
                 fdone(kk, A);
-                if (kk + 1 >= cnt) break;
-                fload(kk + 2, A);
-                fdone(kk + 1, B);
+                if (kk + PS >= cnt) break;
+                fload(kk + 2u * PS, A);
+                fdone(kk + PS, B);
             }
             continue;
         }
@@ -2190,8 +2201,9 @@ hipError_t launch_verify_mask(const uint16_t* raw, uint64_t n, uint64_t* mask, u
 hipError_t launch_tcp_build(const TcpHdrSoA& h, const uint8_t* opts, const uint64_t* opt_off, const uint8_t* data,
                             const uint64_t* data_off, uint64_t data_bytes, const uint32_t* partial, uint64_t n,
                             uint8_t* out, const uint64_t* out_off, uint16_t* raw, uint32_t max_blocks, int policy,
-                            int xchunk, int kernel, hipStream_t st) {
-    // kernel: 0 = groups of fast-path segments ≤ 2 rows software-pipelined, 2 = never pipelined
+                            int xchunk, int kernel, int spw, hipStream_t st) {
+    // kernel: 0 = groups of fast-path segments ≤ 2 rows software-pipelined, 2 = never pipelined;
+    // spw: segments per pipelined register set, 2 (default) or 1
     // Group size: up to 64 segments per wave task, fewer when n would leave waves idle.
     const uint64_t waves = (uint64_t)max_blocks * kWavesPerBlock;
     const uint32_t group = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, (n + waves - 1) / waves));
@@ -2202,9 +2214,13 @@ hipError_t launch_tcp_build(const TcpHdrSoA& h, const uint8_t* opts, const uint6
     // policy: 0/2 = default cache policy (measured best: segment-boundary lines stay in L2 for
     // the neighbour segment's load and partial-line stores merge there), 1 = nt loads and
     // stores, 3 = nt loads + plain stores, 4 = plain loads + nt stores
-#define NSX_BUILD(LP, SP)                                                                                         \
-    hipLaunchKernelGGL((tcp_build_kernel<LP, SP>), dim3(grid), dim3(kBlock), 0, st, h, opts, opt_off, data, data_off, \
-                       data_bytes, partial, n, out, out_off, raw, group, clog, kernel != 2)
+#define NSX_BUILD(LP, SP)                                                                                          \
+    if (spw != 1)                                                                                                  \
+        hipLaunchKernelGGL((tcp_build_kernel<LP, SP, 2>), dim3(grid), dim3(kBlock), 0, st, h, opts, opt_off, data,  \
+                           data_off, data_bytes, partial, n, out, out_off, raw, group, clog, kernel != 2);         \
+    else                                                                                                           \
+        hipLaunchKernelGGL((tcp_build_kernel<LP, SP, 1>), dim3(grid), dim3(kBlock), 0, st, h, opts, opt_off, data,  \
+                           data_off, data_bytes, partial, n, out, out_off, raw, group, clog, kernel != 2)
     switch (policy) {
         case 1: NSX_BUILD(2, 2); break;
         case 3: NSX_BUILD(2, 0); break;

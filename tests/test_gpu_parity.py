@@ -725,11 +725,12 @@ def test_tcp_build_uniform_batches(P, n, nsx_param):
     for lead in (20, 28, 0):  # lead 0: segment 0 has no 20 bytes before its payload (general path)
         fields, data, data_off, out_off, ps = _uniform_build_case(rng, n, P, lead)
         want, wraw = O.c_go_tcp_build(fields, data, data_off, out_off, ps)
-        for kern in (0, 2):
+        for kern, spw in ((0, 0), (0, 2), (2, 0)):
             nsx_param(nsx.PARAM_KERNEL, kern)
+            nsx_param(nsx.PARAM_SEGS_PER_WAVE, spw)
             got, raw = _run_build(fields, data, data_off, out_off, ps)
-            assert np.array_equal(raw, wraw), (P, n, lead, kern)
-            assert np.array_equal(got, want), (P, n, lead, kern)
+            assert np.array_equal(raw, wraw), (P, n, lead, kern, spw)
+            assert np.array_equal(got, want), (P, n, lead, kern, spw)
 
 
 def test_tcp_build_whole_dword_and_ragged_payloads_interleaved():

@@ -47,7 +47,8 @@ def variants(kind):
         return ([dict(kernel=0, blocks_per_cu=b, segs_per_wave=u) for b in (1, 2, 3, 4) for u in (1, 2, 4)] +
                 [dict(kernel=2, blocks_per_cu=8)])
     if kind == "tcp_build":  # cache policy (nontemporal knob) x grid
-        return [dict(nontemporal=nt, blocks_per_cu=b, kernel=k) for nt in (0, 1) for b in (2, 4, 8) for k in (0, 2)]
+        return ([dict(blocks_per_cu=b, segs_per_wave=ps) for b in (1, 2, 4) for ps in (1, 2)] +
+                [dict(blocks_per_cu=b, kernel=2) for b in (4, 8)])
     if kind == "ragged_bal":  # scan kernel: XCD deal vs byte-balanced wave ranges
         for bpc, rows, run, xcd in itertools.product((1, 2, 4, 8), (4, 8, 16), (8, 16, 32, 63), (1, 4)):
             out.append(dict(kernel=4, blocks_per_cu=bpc, stream_rows=rows, nontemporal=1, xcd_map=xcd, run_segs=run))
