@@ -20,9 +20,9 @@
 // Work decomposition (HBM-bound streaming reduction, no MFMA, no LDS needed on
 // the fast path): one wave64 owns a segment; a "row" is one wave-wide 16-B/lane
 // load = 1 KiB of the segment window, fully coalesced. Persistent grid of
-// 256-thread blocks; tasks are dealt so that the 8 XCDs each stream one
-// contiguous region of the batch (their 2-byte result stores then fill whole
-// lines in one XCD's L2 instead of being split across XCDs).
+// 256-thread blocks; tasks are dealt to the 8 XCDs in interleaved chunks, each
+// XCD walking its chunks in order (their 2-byte result stores then fill whole
+// lines in one XCD's L2 instead of being split across XCDs; see chunk_deal).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -114,9 +114,9 @@ struct TaskIter {
     uint64_t next, end, step;
 };
 
-// XCD-interleaved deal (fixed-stride kernel): the batch is cut into chunks of 2^clog tasks and XCD x
-// takes chunks x, x+8, x+16, ...; its waves walk their chunks' tasks in order. i = the wave's local
-// sequence index (start slot*4 + wave, step per*4).
+// XCD-interleaved deal: the batch is cut into chunks of 2^clog tasks and XCD x takes chunks x, x+8,
+// x+16, ...; its waves walk their chunks' tasks in order. i = the wave's local sequence index (start
+// slot*4 + wave, step per*4). Set up by chunk_deal below; chunk sizes by deal_clog (launchers).
 struct ChunkDeal {
     uint32_t x, clog;  // clog = 0: off (task = i)
     __device__ __forceinline__ uint32_t task(uint32_t i) const {
@@ -125,8 +125,10 @@ struct ChunkDeal {
 };
 
 // xcd_map: 1 = each XCD's blocks stream one contiguous eighth of the batch,
-// dealt round-robin inside it; 0 = plain grid-stride; 2 = every wave owns one
-// contiguous range of tasks and walks it in order (a sequential stream per wave).
+// dealt round-robin inside it (kernels that take a chunk size then switch to
+// the interleaved chunks with chunk_deal); 0 = plain grid-stride; 2 = every wave
+// owns one contiguous range of tasks and walks it in order (a sequential stream
+// per wave); 3 = byte-balanced wave ranges (ragged scan kernel, its own setup).
 __device__ __forceinline__ TaskIter task_iter(uint64_t ntasks, uint32_t wave, int xcd_map) {
     const uint32_t nb = gridDim.x, b = blockIdx.x;
     TaskIter it;
