@@ -512,6 +512,65 @@ def test_config5_16M_x_1500_per_gpu_sampled():
     assert np.array_equal(alt, got)
 
 
+def test_fixed_batch_past_the_launch_chunk():
+    """n > 2^28 segments: nsx_csum_fixed_dev splits the batch into launches of 2^28
+    (buffer descriptors address < 2^31 bytes of results); segments either side of the
+    split, a stride sample and the last one against the oracle, and all of them
+    against a grid-stride launch of the same kernel."""
+    n, L, seed = (1 << 28) + 4099, 4, 0x28
+    t = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    nsx.fill_splitmix64_dev(t, seed)
+    got = u16(nsx.fixed_dev(t, L, L, n, out=torch.empty(n, dtype=torch.int16, device="cuda")))
+    idx = sorted(set(range(0, n, 1_000_003)) | set(range((1 << 28) - 5, (1 << 28) + 5)) | {n - 1})
+    for i in idx:
+        assert got[i] == O.c_fold_checksum(b"", O.c_splitmix64(seed, L, i * L).tobytes()), i
+    nsx.set_param(nsx.PARAM_XCD_MAP, 2)
+    try:
+        alt = u16(nsx.fixed_dev(t, L, L, n, out=torch.empty(n, dtype=torch.int16, device="cuda")))
+    finally:
+        nsx.set_param(nsx.PARAM_XCD_MAP, 0)
+    assert np.array_equal(alt, got)
+
+
+def test_ragged_batch_past_the_launch_chunk():
+    """n > 2^27 ragged segments (0-16 B, odd starts): nsx_csum_ragged_dev splits the
+    batch into launches of 2^27; segments either side of the split and a sample
+    against the oracle."""
+    n, seed = (1 << 27) + 999, 0x27
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, 17, n).astype(np.uint64)
+    offs = np.zeros(n + 1, np.uint64)
+    np.cumsum(lens, out=offs[1:])
+    t = torch.empty(int(offs[-1]) + 4, dtype=torch.uint8, device="cuda")
+    nsx.fill_splitmix64_dev(t, seed)
+    got = u16(nsx.ragged_dev(t, dev(offs.view(np.int64)), out=torch.empty(n, dtype=torch.int16, device="cuda")))
+    idx = sorted(set(range(0, n, 999_983)) | set(range((1 << 27) - 5, (1 << 27) + 5)) | {n - 1})
+    for i in idx:
+        o, ln = int(offs[i]), int(lens[i])
+        assert got[i] == O.c_fold_checksum(b"", O.c_splitmix64(seed, ln, o).tobytes() if ln else b""), i
+
+
+def test_ipv4_packed_headers_past_the_launch_chunk():
+    """n > 2^28 packed 20 B headers (5.4 GB): the header kernel splits the batch into
+    launches of 2^28; fill then verify gives 0xFFFF everywhere, and fields either side
+    of the split match the oracle."""
+    n, H, seed = (1 << 28) + 77, 20, 0x29
+    t = torch.empty(n * H, dtype=torch.uint8, device="cuda")
+    nsx.fill_splitmix64_dev(t, seed)
+    t.view(n, H)[:, 0] = 0x45
+    near = list(range((1 << 28) - 3, (1 << 28) + 3)) + [n - 1]
+    before = {i: host(t[i * H:(i + 1) * H]) for i in near}
+    nsx.ipv4_hdr_csum_dev(t, H, n, mode=1)
+    raw = u16(nsx.ipv4_hdr_csum_dev(t, H, n, mode=0))
+    assert (raw == 0xFFFF).all()
+    for i in near:
+        h = bytearray(before[i].tobytes())
+        h[10:12] = b"\0\0"
+        f = O.field_value(O.go_checksum(b"", bytes(h)))
+        after = host(t[i * H:(i + 1) * H])
+        assert after[10] == f >> 8 and after[11] == f & 0xFF, i
+
+
 def test_f1_build_1M_segments_full_size_roundtrip():
     """The bench's f1 workload at full size (1M x 1500 B images): the raw sums the
     build kernel reports equal an independent checksum of the images it wrote
