@@ -1608,93 +1608,16 @@ __global__ __launch_bounds__(kBlock) void ipv4_hdr_dense_kernel(uint8_t* __restr
 // in registers: no byte masks, no per-header window. A 20-byte stride only fits
 // IHL = 5, so any other IHL is malformed (out 0, header untouched), the rule of
 // the general kernels. A lane's 4 results leave as one 8-byte store (512 B per
-// wave); U tasks in flight per wave, XCD-contiguous deal.
+// wave); U tasks per register set, XCD-interleaved chunk deal.
 constexpr uint32_t kHdr20Task = 256;
 constexpr uint32_t kHdr20Lds = kHdr20Task * 20u;  // bytes of LDS per wave
 
-template <int MODE, int U>
+// PIPE: software-pipelined — two register sets of U tasks; the loads of the next set are issued before
+// the current set goes through LDS, so every wave keeps loads in flight while it computes and stores (one
+// wave per SIMD at 1 block/CU has no other wave to cover those phases). !PIPE: one set, load then use.
+template <int MODE, int U, bool PIPE>
 __global__ __launch_bounds__(kBlock) void ipv4_hdr20_kernel(uint8_t* __restrict__ base, uint32_t n,
                                                             uint16_t* __restrict__ out, uint32_t clog) {
-    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
-    extern __shared__ u32x4 lds20[];
-    const uint32_t lane = threadIdx.x & (kWave - 1);
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    u32x4* my = lds20 + wave * (kHdr20Lds / 16u);
-    const uint32_t ntasks = (n + kHdr20Task - 1) / kHdr20Task;
-    TaskIter it = task_iter(ntasks, wave, 1);
-    const ChunkDeal cd = chunk_deal(it, wave, 1, clog, ntasks);
-    const uint32_t end = (uint32_t)it.end, step = (uint32_t)it.step;
-    const __amdgpu_buffer_rsrc_t ors = make_rsrc(out, out ? (uint64_t)n * 2 : 0);
-    for (uint32_t t0 = (uint32_t)it.next; t0 < end; t0 += step * U) {
-        if (cd.task(t0) >= ntasks) break;
-        __amdgpu_buffer_rsrc_t rs[U];
-        uint32_t cnt[U], tk[U];
-        u32x4 v[U][5];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t ii = t0 + (uint32_t)u * step;
-            const uint32_t task = cd.task(ii);
-            tk[u] = task;
-            cnt[u] = (ii < end && task < ntasks) ? min(kHdr20Task, n - task * kHdr20Task) : 0u;
-            rs[u] = make_rsrc(base + (uint64_t)min(task, ntasks - 1) * kHdr20Lds, cnt[u] * 20u);
-#pragma unroll
-            for (int j = 0; j < 5; ++j) v[u][j] = bld16<true>(rs[u], j * kRow + lane * 16u);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-            for (int j = 0; j < 5; ++j) asm volatile("" : "+v"(v[u][j]));
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (!cnt[u]) break;  // wave-uniform
-            __builtin_amdgcn_wave_barrier();  // the previous task's LDS reads are done
-#pragma unroll
-            for (int j = 0; j < 5; ++j) my[j * kWave + lane] = v[u][j];
-            __builtin_amdgcn_wave_barrier();
-            u32x4 q[5];
-#pragma unroll
-            for (int j = 0; j < 5; ++j) q[j] = my[lane * 5 + j];
-            const uint32_t d[20] = {q[0].x, q[0].y, q[0].z, q[0].w, q[1].x, q[1].y, q[1].z, q[1].w, q[2].x, q[2].y,
-                                    q[2].z, q[2].w, q[3].x, q[3].y, q[3].z, q[3].w, q[4].x, q[4].y, q[4].z, q[4].w};
-            uint32_t res[4];
-            bool ok[4];
-#pragma unroll
-            for (int h = 0; h < 4; ++h) {
-                const uint32_t* w = d + 5 * h;
-                ok[h] = (w[0] & 15u) == 5u;  // IHL (low nibble of byte 0)
-                uint32_t acc = __builtin_amdgcn_sad_u16(w[0], 0u, 0u);
-                acc = __builtin_amdgcn_sad_u16(w[1], 0u, acc);
-                acc = __builtin_amdgcn_sad_u16(MODE == 1 ? (w[2] & 0xFFFFu) : w[2], 0u, acc);  // bytes 10-11 = 0
-                acc = __builtin_amdgcn_sad_u16(w[3], 0u, acc);
-                acc = __builtin_amdgcn_sad_u16(w[4], 0u, acc);
-                res[h] = ok[h] ? finish(acc, true, 0u) : 0u;  // headers start 4-aligned: even
-            }
-            const uint32_t i0 = tk[u] * kHdr20Task + lane * 4u;  // first header of this lane
-            if (cnt[u] == kHdr20Task) {
-                __builtin_amdgcn_raw_buffer_store_b64(v2u{res[0] | (res[1] << 16), res[2] | (res[3] << 16)}, ors,
-                                                      i0 * 2u, 0, 0);
-            } else {
-#pragma unroll
-                for (int h = 0; h < 4; ++h)
-                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res[h], ors, i0 + h < n ? (i0 + h) * 2u : kOOB, 0,
-                                                          0);
-            }
-            if constexpr (MODE == 1) {
-#pragma unroll
-                for (int h = 0; h < 4; ++h)  // ~raw big-endian into bytes 10-11
-                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)bswap16u(~res[h] & 0xFFFFu), rs[u],
-                                                          ok[h] ? lane * 80u + h * 20u + 10u : kOOB, 0, 0);
-            }
-        }
-    }
-}
-
-// Software-pipelined variant of ipv4_hdr20_kernel: two register sets of U tasks; the loads of the next
-// set are issued before the current set goes through LDS, so every wave keeps loads in flight while it
-// computes and stores (one wave per SIMD at 1 block/CU has no other wave to cover those phases).
-template <int MODE, int U>
-__global__ __launch_bounds__(kBlock) void ipv4_hdr20_pipe_kernel(uint8_t* __restrict__ base, uint32_t n,
-                                                                 uint16_t* __restrict__ out, uint32_t clog) {
     typedef uint32_t v2u __attribute__((ext_vector_type(2)));
     extern __shared__ u32x4 lds20[];
     const uint32_t lane = threadIdx.x & (kWave - 1);
@@ -1771,17 +1694,25 @@ __global__ __launch_bounds__(kBlock) void ipv4_hdr20_pipe_kernel(uint8_t* __rest
             }
         }
     };
-    Set A, B;
-    uint32_t t0 = (uint32_t)it.next;
-    issue(t0, A);
-    while (live(t0)) {
-        const uint32_t t1 = t0 + step * U;
-        issue(t1, B);
-        consume(A);
-        if (!live(t1)) break;
-        t0 = t1 + step * U;
+    if constexpr (PIPE) {
+        Set A, B;
+        uint32_t t0 = (uint32_t)it.next;
         issue(t0, A);
-        consume(B);
+        while (live(t0)) {
+            const uint32_t t1 = t0 + step * U;
+            issue(t1, B);
+            consume(A);
+            if (!live(t1)) break;
+            t0 = t1 + step * U;
+            issue(t0, A);
+            consume(B);
+        }
+    } else {
+        for (uint32_t t0 = (uint32_t)it.next; live(t0); t0 += step * U) {
+            Set A;
+            issue(t0, A);
+            consume(A);
+        }
     }
 }
 
@@ -2257,15 +2188,17 @@ hipError_t launch_ipv4_hdr(uint8_t* base, uint64_t stride, uint32_t hdr_off, uin
     do {                                                                                                        \
         if (pipe) {                                                                                             \
             if (mode == 1)                                                                                      \
-                hipLaunchKernelGGL((ipv4_hdr20_pipe_kernel<1, U>), dim3(grid_f), dim3(kBlock), lds, st, b, cn, o, \
+                hipLaunchKernelGGL((ipv4_hdr20_kernel<1, U, true>), dim3(grid_f), dim3(kBlock), lds, st, b, cn, o, \
                                    clog);                                                                       \
             else                                                                                                \
-                hipLaunchKernelGGL((ipv4_hdr20_pipe_kernel<0, U>), dim3(grid_f), dim3(kBlock), lds, st, b, cn, o, \
+                hipLaunchKernelGGL((ipv4_hdr20_kernel<0, U, true>), dim3(grid_f), dim3(kBlock), lds, st, b, cn, o, \
                                    clog);                                                                       \
         } else if (mode == 1)                                                                                   \
-            hipLaunchKernelGGL((ipv4_hdr20_kernel<1, U>), dim3(grid_f), dim3(kBlock), lds, st, b, cn, o, clog);   \
+            hipLaunchKernelGGL((ipv4_hdr20_kernel<1, U, false>), dim3(grid_f), dim3(kBlock), lds, st, b, cn, o,    \
+                               clog);                                                                           \
         else                                                                                                    \
-            hipLaunchKernelGGL((ipv4_hdr20_kernel<0, U>), dim3(grid_f), dim3(kBlock), lds, st, b, cn, o, clog);   \
+            hipLaunchKernelGGL((ipv4_hdr20_kernel<0, U, false>), dim3(grid_f), dim3(kBlock), lds, st, b, cn, o,    \
+                               clog);                                                                           \
     } while (0)
             switch (unroll) {
                 case 1: NSX_H20(1); break;
