@@ -159,6 +159,7 @@ def result_line(*, world, steps, warmup, wall_max, bytes_per_rank_step, units_to
         "metric": metric,
         "value": round(total_bytes / wall_max / GIB, 3),
         "unit": "GiB/s",
+        "value_per_gpu": round(total_bytes / wall_max / GIB / world, 3),
         "n_gpus": world,
         "steps": steps,
         "warmup": warmup,

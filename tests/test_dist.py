@@ -66,6 +66,7 @@ def _worker(rank, world, port, q):
         full = O.c_batch(rb, lens.size, offsets=offs)
         stitched = [x for _, _, part in sorted(gathered) for x in part]
         q.put(json.dumps({"rank": rank, "wall": wall, "wmax": wmax, "value": line["value"],
+                          "value_per_gpu": line["value_per_gpu"],
                           "n_gpus": line["n_gpus"], "stitched_ok": stitched == full.tolist(),
                           "sizes": [int(offs[b2] - offs[b1]) for b1, b2 in zip(bounds[:-1], bounds[1:])]}))
         d.close()
@@ -92,6 +93,7 @@ def test_bench_dist_logic_gloo_ws2():
         assert r["wmax"] == pytest.approx(wmax)      # MAX over ranks, identical everywhere
         assert r["n_gpus"] == 2
         assert r["value"] == pytest.approx(round(2 * 512 * 1500 * 4 / wmax / GIB, 3))  # whole-job bytes
+        assert r["value_per_gpu"] == pytest.approx(r["value"] / 2, rel=1e-3)           # per-GPU beside it
         assert r["stitched_ok"]                      # shards cover the batch exactly once
     sizes = by[0]["sizes"]
     assert abs(sizes[0] - sizes[1]) <= 9000          # byte-balanced split
