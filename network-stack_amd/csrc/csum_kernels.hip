@@ -1991,11 +1991,20 @@ hipError_t launch_fixed(const LaunchCfg& c, const void* d_base, uint64_t stride,
     // Rows a segment window can span (the window starts up to 3 bytes early).
     const uint64_t rows = ((uint64_t)seg_len + 3 + kRow - 1) / kRow;
     const Path path = rows <= 4 ? Path::kFixedShort : Path::kFixedLong;
-    const Plan p = resolve(c, path);
+    Plan p = resolve(c, path);
     if (c.kernel == kKernelRowStream)
         return launch_stream<false, false>(p, base, nullptr, stride, seg_len, n, partial, out, nullptr, safe_end, st);
     if (path == Path::kFixedShort) {
         const int nrows = rows <= 1 ? 1 : (rows <= 2 ? 2 : 4);
+        const bool aligned = ((uintptr_t)base & 3u) == 0 && (stride & 3u) == 0 && (seg_len & 3u) == 0;
+        // Default for aligned batches (config 2): the software-pipelined kernel with 8-segment tasks at one
+        // block per CU — two register sets of 8 × 2 KiB per wave, a wave per SIMD (tools/alloc_study.py:
+        // config 2 0.2222 → 0.2184 ms, config 5 3.712 → 3.626 ms against the unpipelined 4 × 2 blocks/CU).
+        const bool swp = c.kernel == kKernelSwPipe || (c.kernel == 0 && aligned);
+        if (c.kernel == 0 && aligned) {
+            if (c.blocks_per_cu == 0) p.max_blocks = (uint32_t)c.cus;
+            if (c.segs_per_wave == 0) p.spw = 8;
+        }
         if (c.kernel == kKernelPipelined || c.kernel == kKernelSwPipe || c.kernel == 0) {
             const int u = (nrows == 4 && p.spw > 4) ? 4 : p.spw;
             // Buffer descriptors address ≤ 2^31 bytes of results/partials: chunk huge batches.
@@ -2004,7 +2013,7 @@ hipError_t launch_fixed(const LaunchCfg& c, const void* d_base, uint64_t stride,
                 const uint64_t cn = n - c0 < kChunk ? n - c0 : kChunk;
                 hipError_t e = launch_fixed_pipe(p, base + c0 * stride, stride, seg_len, cn,
                                                  partial ? partial + c0 : nullptr, out + c0, safe_end, nrows, u,
-                                                 c.kernel == kKernelSwPipe, st);
+                                                 swp, st);
                 if (e != hipSuccess) return e;
             }
             return hipSuccess;
