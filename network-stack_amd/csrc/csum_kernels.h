@@ -12,6 +12,7 @@ constexpr int kKernelPipelined = 3;  // buffer-load kernels: csum_fixed_buf_kern
 constexpr int kKernelScan = 4;       // csum_ragged_scan_kernel (ragged; the default there)
 constexpr int kKernelSwPipe = 5;     // csum_fixed_swp_kernel: software-pipelined fixed-stride buffer kernel
 constexpr int kKernelScanPipe = 6;   // csum_ragged_scan_kernel, software-pipelined row batches (nt loads)
+constexpr int kKernelLongSwp = 7;    // csum_long_swp_kernel: long aligned fixed-stride segments, pipelined rows
 
 // Raw NSX_PARAM_* values (0 = "default for this path"); the launchers resolve
 // them per path (fixed short / fixed long / ragged) to the defaults measured

@@ -573,6 +573,51 @@ __global__ __launch_bounds__(kBlock) void csum_wave_kernel(
     }
 }
 
+// Long aligned fixed-stride segments (> 4 KiB, base/stride/len ≡ 0 mod 4, len < 2^31): one wave per
+// segment through one buffer descriptor ending at the segment's last byte, rows in batches of R with two
+// register sets — batch r0 + R loads while batch r0 is summed — and no masks (the range check zero-fills
+// past the end). Segments start 4-aligned, so the finish needs no byte-swap decision per segment.
+template <int R, bool NT>
+__global__ __launch_bounds__(kBlock) void csum_long_swp_kernel(const uint8_t* __restrict__ base, uint64_t stride,
+                                                               uint32_t seg_len, uint64_t n,
+                                                               const uint32_t* __restrict__ partial,
+                                                               uint16_t* __restrict__ out, int xcd_map, uint32_t clog) {
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    TaskIter it = task_iter(n, wave, xcd_map);
+    const ChunkDeal cd = chunk_deal(it, wave, xcd_map, clog, n);
+    const uint32_t rows = (seg_len + kRow - 1) / kRow;
+    for (uint64_t k = it.next; k < it.end; k += it.step) {
+        const uint64_t i = cd.clog ? cd.task((uint32_t)k) : k;
+        if (i >= n) break;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t*>(base + i * stride), 0, (int)seg_len, 0x00020000);
+        auto issue = [&](uint32_t r0, u32x4 (&v)[R]) {
+#pragma unroll
+            for (int j = 0; j < R; ++j) v[j] = bld16<NT>(rs, r0 < rows ? (r0 + j) * kRow + lane * 16u : kOOB);
+        };
+        uint32_t acc = 0;
+        auto consume = [&](u32x4 (&v)[R]) {
+#pragma unroll
+            for (int j = 0; j < R; ++j) asm volatile("" : "+v"(v[j]));
+#pragma unroll
+            for (int j = 0; j < R; ++j) acc = sad4(v[j], acc);
+            acc = fold32(acc);
+        };
+        u32x4 A[R], B[R];
+        issue(0, A);
+        for (uint32_t r0 = 0; r0 < rows; r0 += 2 * R) {
+            issue(r0 + R, B);
+            consume(A);
+            if (r0 + R >= rows) break;
+            issue(r0 + 2 * R, A);
+            consume(B);
+        }
+        const uint32_t res = finish(wave_sum(acc), true, partial ? partial[i] : 0u);
+        if (lane == 0 && out) out[i] = (uint16_t)res;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // One segment per 256-thread block (few, very long segments): wave w takes rows
 // w, w+4, ... so the block reads 4 KiB contiguous per step; cross-wave total
@@ -2020,6 +2065,24 @@ hipError_t launch_fixed(const LaunchCfg& c, const void* d_base, uint64_t stride,
         }
         const int u = (nrows == 4 && p.spw > 2) ? 2 : (p.spw > 4 ? 4 : p.spw);
         return launch_fixed_rows(p, base, stride, seg_len, n, partial, out, safe_end, nrows, u, st);
+    }
+    const bool aligned = ((uintptr_t)base & 3u) == 0 && (stride & 3u) == 0 && (seg_len & 3u) == 0;
+    if (aligned && seg_len < (1u << 31) && (c.kernel == kKernelSwPipe || c.kernel == kKernelLongSwp)) {
+        const uint64_t want = (n + kWavesPerBlock - 1) / kWavesPerBlock;
+        const uint32_t grid = (uint32_t)(want < p.max_blocks ? want : p.max_blocks);
+        const uint32_t clog = deal_clog(p.xcd_chunk_param, n, stride);
+#define NSX_LONG(R_)                                                                                            \
+        if (p.rows == R_) {                                                                                      \
+            if (p.nt)                                                                                            \
+                hipLaunchKernelGGL((csum_long_swp_kernel<R_, true>), dim3(grid), dim3(kBlock), 0, st, base, stride, \
+                                   seg_len, n, partial, out, p.xcd, clog);                                       \
+            else                                                                                                 \
+                hipLaunchKernelGGL((csum_long_swp_kernel<R_, false>), dim3(grid), dim3(kBlock), 0, st, base,      \
+                                   stride, seg_len, n, partial, out, p.xcd, clog);                               \
+            return hipGetLastError();                                                                            \
+        }
+        NSX_LONG(4) NSX_LONG(8) NSX_LONG(16)
+#undef NSX_LONG
     }
     return launch_seg<false, false>(p, base, nullptr, stride, seg_len, n, partial, out, nullptr, safe_end, false, st);
 }

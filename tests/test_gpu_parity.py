@@ -192,7 +192,9 @@ VARIANTS = ([dict(kernel=2, spw=s, nt=nt, xcd=x, bpc=b, rows=0) for s in (1, 2, 
              for c in (1, 3, 6, 10, 99)] +
             [dict(kernel=2, spw=1, nt=1, xcd=1, bpc=b, rows=0, chunk=c) for b in (8, 2) for c in (2, 5, 99)] +
             [dict(kernel=5, spw=s, nt=nt, xcd=x, bpc=b, rows=0, chunk=c) for s in (1, 2, 4, 8) for nt in (1, 2)
-             for x in (1, 2) for b in (8, 1) for c in (0, 99)])
+             for x in (1, 2) for b in (8, 1) for c in (0, 99)] +
+            [dict(kernel=7, spw=0, nt=nt, xcd=x, bpc=b, rows=r, chunk=c) for nt in (1, 2) for x in (1, 2)
+             for b in (8, 1) for r in (4, 8, 16) for c in (0, 99)])
 
 
 def set_variant(v, block_mode=0):
