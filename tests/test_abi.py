@@ -44,9 +44,10 @@ def test_library_exports_every_declared_symbol():
 
 def test_library_has_gfx950_code_object():
     out = subprocess.run(["/opt/rocm/bin/roc-obj-ls", nsx.LIB_PATH], capture_output=True, text=True)
-    if out.returncode != 0:
-        pytest.skip("roc-obj-ls unavailable")
-    assert "gfx950" in out.stdout
+    if out.returncode == 0:
+        assert "gfx950" in out.stdout
+    else:  # no roc-obj-ls: the offload bundle names its target triple in the clear
+        assert b"amdgcn-amd-amdhsa--gfx950" in open(nsx.LIB_PATH, "rb").read()
 
 
 def test_abi_version():
