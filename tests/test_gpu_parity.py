@@ -786,7 +786,7 @@ def test_tcp_build_uniform_batches(P, n, nsx_param):
     for lead in (20, 28, 0):  # lead 0: segment 0 has no 20 bytes before its payload (general path)
         fields, data, data_off, out_off, ps = _uniform_build_case(rng, n, P, lead)
         want, wraw = O.c_go_tcp_build(fields, data, data_off, out_off, ps)
-        for kern, spw in ((0, 0), (0, 2), (2, 0)):
+        for kern, spw in ((0, 0), (0, 1), (2, 0)):  # pipelined, 2 / 1 segments per register set; unpipelined
             nsx_param(nsx.PARAM_KERNEL, kern)
             nsx_param(nsx.PARAM_SEGS_PER_WAVE, spw)
             got, raw = _run_build(fields, data, data_off, out_off, ps)
