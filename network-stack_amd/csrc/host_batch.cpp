@@ -7,10 +7,12 @@
 // double-buffers fixed-size chunks over two HIP streams: chunk k+1's H2D copy
 // overlaps chunk k's kernel and D2H. Caller memory that is already pinned
 // (nsx_alloc_pinned) is DMA'd directly; pageable memory is bounced through
-// pinned staging buffers. Streams and buffers persist per device (DevCtx).
+// pinned staging buffers (multi-threaded copy, stage_copy). Streams and buffers
+// persist per device (DevCtx).
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <thread>
@@ -23,6 +25,39 @@
 namespace {
 
 constexpr uint64_t kChunkBytes = 64ull << 20;
+
+// Pageable caller memory is bounced through pinned staging; one thread's memcpy (~10-25 GB/s) would
+// then, not PCIe, set the end-to-end rate. Large copies are split over up to kCopyThreads threads
+// (NSX_HOST_COPY_THREADS overrides; 1 = serial).
+constexpr int kCopyThreads = 8;
+constexpr uint64_t kCopySplitMin = 4ull << 20;
+
+int copy_threads() {
+    static const int n = [] {
+        const char* e = std::getenv("NSX_HOST_COPY_THREADS");
+        int v = e ? std::atoi(e) : 0;
+        if (v < 1) v = std::min<int>(kCopyThreads, (int)std::max(1u, std::thread::hardware_concurrency()));
+        return std::min(v, 64);
+    }();
+    return n;
+}
+
+void stage_copy(void* dst, const void* src, uint64_t bytes) {
+    const int nt = bytes >= kCopySplitMin ? copy_threads() : 1;
+    if (nt <= 1) {
+        std::memcpy(dst, src, bytes);
+        return;
+    }
+    const uint64_t part = ((bytes + nt - 1) / nt + 4095) & ~4095ull;  // page-sized pieces
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) {
+        const uint64_t lo = part * t;
+        if (lo >= bytes) break;
+        th.emplace_back([=] { std::memcpy((uint8_t*)dst + lo, (const uint8_t*)src + lo, std::min(part, bytes - lo)); });
+    }
+    std::memcpy(dst, src, std::min(part, bytes));
+    for (auto& x : th) x.join();
+}
 
 bool is_pinned(const void* p) {
     if (!p) return false;
@@ -211,7 +246,7 @@ void run_job(Job* j) {
         }
         const uint8_t* src = j->h_base + c.byte_lo;
         if (!in_pinned) {
-            std::memcpy(ctx->h_stage[s].p, src, span);
+            stage_copy(ctx->h_stage[s].p, src, span);
             src = ctx->h_stage[s].as<uint8_t>();
         }
         if (span) NSX_TRY(hipMemcpyAsync(d_data, src, span, hipMemcpyHostToDevice, st[s]));
