@@ -1,0 +1,139 @@
+"""Randomised GPU parity (seeded, bounded to a few seconds): every device entry
+point on batches whose sizes, alignments, lengths and kernel knobs are drawn at
+random, against the CPU oracle. Complements the hand-picked edge cases of
+test_gpu_parity.py with combinations nobody wrote down."""
+import numpy as np
+import pytest
+
+from oracle import csum_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+import nsx  # noqa: E402
+
+FIXED_KNOBS = [dict(), dict(kernel=3), dict(kernel=5), dict(kernel=2), dict(kernel=7), dict(kernel=1),
+               dict(blocks_per_cu=1, segs_per_wave=8), dict(xcd_map=2), dict(xcd_chunk=99), dict(block_mode=2)]
+RAGGED_KNOBS = [dict(), dict(xcd_map=1), dict(kernel=6), dict(kernel=3), dict(run_segs=1), dict(stream_rows=16),
+                dict(block_mode=2)]
+
+
+def _apply(knobs):
+    import bench
+    for p in nsx.ALL_PARAMS:
+        nsx.set_param(p, 0)
+    for k, v in knobs.items():
+        nsx.set_param(bench.PARAMS[k], v)
+
+
+@pytest.fixture(autouse=True)
+def _reset_knobs():
+    yield
+    for p in nsx.ALL_PARAMS:
+        nsx.set_param(p, 0)
+
+
+def _dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def _u16(t):
+    return t.cpu().numpy().view(np.uint16)
+
+
+@pytest.mark.parametrize("case", range(120))
+def test_fuzz_fixed(case):
+    rng = np.random.default_rng(1000 + case)
+    seg_len = int(rng.choice([int(rng.integers(0, 64)), int(rng.integers(64, 4200)), int(rng.integers(4200, 70000))]))
+    stride = seg_len + int(rng.choice([0, 0, int(rng.integers(0, 9)), int(rng.integers(0, 300))]))
+    stride = max(stride, 1)
+    n = int(rng.integers(1, max(2, min(60000, (24 << 20) // stride))))
+    lead = int(rng.integers(0, 8))
+    buf = rng.integers(0, 256, lead + (n - 1) * stride + seg_len, dtype=np.uint8)
+    if case % 7 == 0:
+        buf[:] = 0xFF
+    part = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32) if case % 3 == 0 else None
+    knobs = FIXED_KNOBS[case % len(FIXED_KNOBS)]
+    _apply(knobs)
+    d = _dev(buf)[lead:]
+    want = O.c_batch(buf[lead:], n, stride=stride, seg_len=seg_len, partial=part)
+    got = _u16(nsx.fixed_dev(d, stride, seg_len, n, partial=None if part is None else _dev(part.view(np.int32))))
+    assert np.array_equal(got, want), (case, knobs, seg_len, stride, n, lead)
+
+
+@pytest.mark.parametrize("case", range(90))
+def test_fuzz_ragged(case):
+    rng = np.random.default_rng(2000 + case)
+    n = int(rng.integers(1, 30000))
+    hi = int(rng.choice([8, 100, 2000, 9000, 40000]))
+    lens = rng.integers(0, hi + 1, n).astype(np.uint64)
+    if case % 5 == 0:
+        lens[rng.integers(0, n, max(1, n // 10))] = 0
+    offs = np.zeros(n + 1, np.uint64)
+    np.cumsum(lens, out=offs[1:])
+    lead = int(rng.integers(0, 8))
+    offs += np.uint64(lead)
+    buf = rng.integers(0, 256, int(offs[-1]) + int(rng.integers(0, 5)), dtype=np.uint8)
+    part = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32) if case % 2 else None
+    knobs = RAGGED_KNOBS[case % len(RAGGED_KNOBS)]
+    _apply(knobs)
+    want = O.c_batch(buf, n, offsets=offs, partial=part)
+    d, o = _dev(buf), _dev(offs.view(np.int64))
+    p = None if part is None else _dev(part.view(np.int32))
+    got = _u16(nsx.ragged_dev(d, o, partial=p))
+    assert np.array_equal(got, want), (case, knobs, n, hi, lead)
+    okv = nsx.verify_ragged_dev(d, o, partial=p).cpu().numpy().astype(bool)
+    assert np.array_equal(okv, want == 0xFFFF), (case, knobs)
+
+
+@pytest.mark.parametrize("case", range(60))
+def test_fuzz_ipv4_headers(case):
+    rng = np.random.default_rng(3000 + case)
+    stride = int(rng.choice([20, 20, 24, 28, 40, 60, 64, int(rng.integers(20, 200)), 1514]))
+    hdr_off = 0 if stride == 20 and case % 2 else int(rng.integers(0, min(16, stride - 19)))
+    n = int(rng.integers(1, max(2, min(200000, (16 << 20) // stride))))
+    buf = rng.integers(0, 256, n * stride + 64, dtype=np.uint8)
+    ihl = rng.integers(5, 16, n)
+    ihl[rng.random(n) < 0.6] = 5
+    ihl[::53] = rng.integers(0, 5, len(ihl[::53]))
+    buf[hdr_off:n * stride:stride] = (0x40 | ihl).astype(np.uint8)
+    _apply(dict(kernel=int(rng.choice([0, 0, 1, 2, 3]))))
+    got = _u16(nsx.ipv4_hdr_csum_dev(_dev(buf), stride, n, hdr_off=hdr_off, mode=0))
+    for i in list(range(0, n, max(1, n // 500))) + [n - 1]:
+        L = int(ihl[i]) * 4
+        ok = L >= 20 and hdr_off + L <= stride
+        b0 = i * stride + hdr_off
+        assert got[i] == (O.c_fold_checksum(b"", buf[b0:b0 + L].tobytes()) if ok else 0), (case, stride, hdr_off, i)
+
+
+@pytest.mark.parametrize("case", range(40))
+def test_fuzz_tcp_build(case):
+    rng = np.random.default_rng(4000 + case)
+    n = int(rng.integers(1, 3000))
+    P = int(rng.choice([int(rng.integers(0, 40)), 1480, int(rng.integers(0, 3000)), int(rng.integers(0, 9000))]))
+    uniform = case % 2 == 0
+    lens = np.full(n, P & ~3 if uniform else P, np.uint64) if uniform else rng.integers(0, P + 1, n).astype(np.uint64)
+    lead = int(rng.choice([0, 1, 20, 24, 33]))
+    data_off = np.zeros(n + 1, np.uint64)
+    np.cumsum(lens, out=data_off[1:])
+    data_off += np.uint64(lead)
+    data = rng.integers(0, 256, int(data_off[-1]) + 8, dtype=np.uint8)
+    out_off = nsx.tcp_layout_host(data_off - np.uint64(lead))
+    fields = {"src_port": rng.integers(0, 1 << 16, n).astype(np.uint16),
+              "dst_port": rng.integers(0, 1 << 16, n).astype(np.uint16),
+              "seq_num": rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32),
+              "ack_num": rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32),
+              "offset": np.full(n, 5, np.uint8), "control": rng.integers(0, 256, n).astype(np.uint8),
+              "window": rng.integers(0, 1 << 16, n).astype(np.uint16),
+              "urgent_ptr": rng.integers(0, 1 << 16, n).astype(np.uint16)}
+    _apply(dict(kernel=int(rng.choice([0, 2])), segs_per_wave=int(rng.choice([0, 1])),
+                blocks_per_cu=int(rng.choice([0, 1, 8]))))
+    want, wraw = O.c_go_tcp_build(fields, data, data_off, out_off, None)
+    dt = {np.uint16: np.int16, np.uint32: np.int32, np.uint8: np.uint8}
+    f = {k: _dev(v.view(dt[v.dtype.type])) for k, v in fields.items()}
+    out = torch.full((int(out_off[-1]),), 0xAB, dtype=torch.uint8, device="cuda")
+    raw = torch.empty(n, dtype=torch.int16, device="cuda")
+    nsx.tcp_build_dev(f, _dev(data), _dev(data_off.view(np.int64)), out, _dev(out_off.view(np.int64)), raw=raw)
+    assert np.array_equal(_u16(raw), wraw), (case, n, P, lead)
+    assert np.array_equal(out.cpu().numpy(), want), (case, n, P, lead)
