@@ -9,7 +9,7 @@ GPU (torchrun), each checksumming its own batch: the path shards with no
 exchange, so there is no data-path collective and scaling is
 weak. value = Σ bytes over all ranks ÷ max over ranks of the timed region.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5|6|7]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5|6|7|8]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 Configs 2-5 are BASELINE.json's device-resident configurations (2 is the
@@ -17,7 +17,8 @@ headline and the default). Configs 6 and 7 measure SURVEY.md §8's next rows to
 the same bar, each with its own metric string: 6 = the fused sender pass
 (nsx_tcp_build_dev: segment.bytes() + computeChecksum + field write,
 tcp.go:98-128/:68-71) over 1M 1500 B wire images; 7 = IPv4 header checksum
-verify (nsx_ipv4_hdr_csum_dev) over 64M packed 20 B headers.
+verify (nsx_ipv4_hdr_csum_dev) over 64M packed 20 B headers; 8 = config 6 with a
+12 B option block per segment (the build kernel's option path; no CPU baseline).
 
 Printed by rank 0: one JSON line with the contract fields plus
   roofline     — dominant kernel: algorithmic bytes per launch ÷ its mean
@@ -57,6 +58,12 @@ WORKLOADS = {
             metric="GiB/s fused TCP segment build (serialize + checksum + field write), wire bytes",
             name="f1: 1M option-less TCP segments per GPU, 1480B payload -> 1500B wire images, IPv4 pseudo-header "
                  "partials, device-resident"),
+    # not a BASELINE config: f1 with a 12-byte option block per segment (the size of Linux's NOP NOP timestamps
+    # block); no CPU baseline (the oracle's batch sender is option-less)
+    8: dict(kind="tcp_build", n=1 << 20, payload=1468, opt=12, seed=0x1076,
+            metric="GiB/s fused TCP segment build (serialize + checksum + field write), wire bytes",
+            name="f1+options: 1M TCP segments per GPU, 12B options (NOP NOP kind-2 len 10), 1468B payload -> 1500B wire images, "
+                 "IPv4 pseudo-header partials, device-resident"),
     7: dict(kind="ipv4_hdr", n=1 << 26, hdr=20, seed=0x1075,
             metric="GiB/s IPv4 header checksum verify, header bytes",
             name="f3: 64M packed 20B IPv4 headers per GPU (header-split ring), verify, device-resident"),
@@ -69,7 +76,8 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", type=int, default=2, choices=sorted(WORKLOADS),
-                    help="2-5: BASELINE configs (2 = headline); 6: f1 fused TCP build; 7: f3 IPv4 header verify")
+                    help="2-5: BASELINE configs (2 = headline); 6: f1 fused TCP build; 7: f3 IPv4 header verify; "
+                         "8: f1 with 12 B options")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--settle-s", type=float, default=0.5, help="device clock settle time before warmup (setup)")
     ap.add_argument("--event-every", type=int, default=10,
@@ -204,8 +212,8 @@ def build_workload(cfg, rank, device):
         w.update(buf=buf, out=out, bytes=n * L, alg=n * L + 2 * n,
                  step=lambda: nsx.fixed_dev(buf, S, L, n, out=out))
     elif cfg["kind"] == "tcp_build":
-        n, P = cfg["n"], cfg["payload"]
-        W = P + 20
+        n, P, OL = cfg["n"], cfg["payload"], cfg.get("opt", 0)
+        W = P + 20 + OL  # OL ≡ 0 mod 4: tcp.go:118-121 pads nothing
         g = torch.Generator(device=device).manual_seed(seed)
         data = torch.empty(n * P, dtype=torch.uint8, device=device)
         nsx.fill_splitmix64_dev(data, seed)
@@ -215,7 +223,7 @@ def build_workload(cfg, rank, device):
 
         fields = {"src_port": rnd(16, torch.int16), "dst_port": rnd(16, torch.int16),
                   "seq_num": rnd(32, torch.int32), "ack_num": rnd(32, torch.int32),
-                  "offset": torch.full((n,), 5, dtype=torch.uint8, device=device),  # computeOffset, no options
+                  "offset": torch.full((n,), 5 + OL // 4, dtype=torch.uint8, device=device),  # computeOffset
                   "control": rnd(8, torch.uint8), "window": rnd(16, torch.int16), "urgent_ptr": rnd(16, torch.int16)}
         addrs = torch.randint(0, 256, (2, n, 4), generator=g, device=device, dtype=torch.int64).to(torch.uint8)
         wire_len = torch.full((n,), W, dtype=torch.int32, device=device)
@@ -224,10 +232,19 @@ def build_workload(cfg, rank, device):
         data_off, out_off = idx * P, idx * W
         out = torch.empty(n * W, dtype=torch.uint8, device=device)
         raw = torch.empty(n, dtype=torch.int16, device=device)
-        # per segment: payload + 18 B of header fields + 2 offsets + partial read; wire image + raw sum written
+        opts = opt_off = None
+        if OL:  # NOP, NOP, a kind-2 option of length 10 with 8 random data bytes (tcp.go:225-231 serialises
+            # kind 2 as kind, length, data; every other kind as its kind byte): the layout of a timestamps block
+            opts = torch.randint(0, 256, (n, OL), generator=g, device=device, dtype=torch.int64).to(torch.uint8)
+            opts[:, :4] = torch.tensor([1, 1, 2, 10], dtype=torch.uint8, device=device)
+            opts = opts.reshape(-1)
+            opt_off = idx * OL
+        # per segment: payload + options + 18 B of header fields + 2 (+2) offsets + partial read; wire image + raw
+        # sum written
         w.update(out=raw, wire=out, fields=fields, addrs=addrs, data=data, bytes=n * W,
-                 alg=n * (P + 18 + 8 + 8 + 4 + W + 2) + 16,
-                 step=lambda: nsx.tcp_build_dev(fields, data, data_off, out, out_off, partial=part, raw=raw))
+                 alg=n * (P + OL + 18 + 8 + 8 + (8 if OL else 0) + 4 + W + 2) + 16 + (8 if OL else 0),
+                 step=lambda: nsx.tcp_build_dev(fields, data, data_off, out, out_off, opts=opts, opt_off=opt_off,
+                                                partial=part, raw=raw))
     elif cfg["kind"] == "ipv4_hdr":
         n, H = cfg["n"], cfg["hdr"]
         buf = torch.empty(n * H, dtype=torch.uint8, device=device)
@@ -285,6 +302,8 @@ def cpu_baseline(cfg, w, seconds: float) -> dict:
         desc = f"first {m} segments x {L}B of rank 0's batch, {reps} pass(es), Go-faithful serial loop"
         extra = cpu_extra_lines(lib, sample, S, L, m, out, max(1.0, seconds / 4))
     elif cfg["kind"] == "tcp_build":
+        if cfg.get("opt"):
+            return None  # the oracle's batch sender is option-less
         n, P = cfg["n"], cfg["payload"]
         W = P + 20
         m = min(n, 65536)  # sample: the first 64K segments (~94 MiB of wire)

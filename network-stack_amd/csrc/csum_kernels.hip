@@ -1213,11 +1213,66 @@ __device__ __forceinline__ void build_load_body(__amdgpu_buffer_rsrc_t drs, cons
     hi = __builtin_amdgcn_raw_buffer_load_b32(drs, live && S.sh ? a + 16u : kOOB, 0, LP);
 }
 
-// Compose, sum and store row r of the wire image.
+// Option bytes of one 16 B image chunk at image byte pos0: image byte p in [20, 20 + optlen) is option byte
+// p - 20 (tcp.go:103-107). One descriptor over the segment's options, based at ob rounded down to 4 B and
+// ending at the last option dword; five dword loads per lane (index pos0/4 - 5 + j, negative or past the
+// options: out of range, 0, no traffic), realigned by ob & 3 and masked to the option bytes, so the header
+// padding (tcp.go:118-121) reads 0. Issue (opt_load) and compose (opt_fin) are split so that the loads go
+// out with the payload's.
+struct OptRaw {
+    u32x4 lo;
+    uint32_t hi;
+};
+
+__device__ __forceinline__ OptRaw opt_load(const uint8_t* __restrict__ opts, uint64_t ob, uint32_t optlen,
+                                           uint32_t pos0) {
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(opts + (ob & ~3ull), ((ob & 3u) + optlen + 3u) & ~3u);
+    const int32_t t = (int32_t)(pos0 >> 2) - 5;
+    uint32_t d[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) d[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, t + j >= 0 ? (uint32_t)(t + j) * 4u : kOOB, 0, 0);
+    return OptRaw{u32x4{d[0], d[1], d[2], d[3]}, d[4]};
+}
+
+__device__ __forceinline__ u32x4 opt_fin(OptRaw o, uint64_t ob, uint32_t optlen, uint32_t pos0) {
+    const uint32_t sh = (uint32_t)ob & 3u;
+    const u32x4 x = sh ? realign(o.lo, o.hi, sh) : o.lo;
+    return keep_bytes(x, min(max(20 - (int32_t)pos0, 0), 16), min(max(20 + (int32_t)optlen - (int32_t)pos0, 0), 16));
+}
+
+// Staged options: when every segment of a wave's group has ≤ 40 option bytes (all valid TCP: data offset ≤ 15),
+// lane j loads segment g0+j's option bytes once per group (the group's options are one contiguous run, so the
+// 11 dword loads are dense), realigns them by its own ob & 3 and zeroes the bytes past optlen: od[m] = option
+// dword m. Building segment k then takes option dword m to image dword 5 + m — lane (5+m)/4, component
+// (5+m)%4 — by v_readlane + v_cndmask, with no per-segment memory access. REPLACE: overwrite image dwords
+// [5, hdr/4) (4-aligned header, fast paths; pad dwords get od's zeros); else OR into a zeroed chunk.
+constexpr int kOptDw = 10;
+
+__device__ __forceinline__ void set_comp(u32x4& x, int c, uint32_t v, bool on) {
+    if (c == 0) x.x = on ? v : x.x;
+    if (c == 1) x.y = on ? v : x.y;
+    if (c == 2) x.z = on ? v : x.z;
+    if (c == 3) x.w = on ? v : x.w;
+}
+
+template <bool REPLACE>
+__device__ __forceinline__ u32x4 staged_opts(const uint32_t (&od)[kOptDw], uint32_t k, uint32_t ndw, uint32_t lane,
+                                             u32x4 x) {
+    if (!REPLACE) x = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int m = 0; m < kOptDw; ++m) {
+        if ((uint32_t)m < ndw) {  // wave-uniform
+            const uint32_t v = __builtin_amdgcn_readlane(od[m], k);
+            set_comp(x, (5 + m) & 3, v, lane == (uint32_t)((5 + m) >> 2));
+        }
+    }
+    return x;
+}
+
+// Compose, sum and store row r of the wire image; oc = the chunk's option bytes (opt_fin, 0 when none).
 template <int SP>
-__device__ __forceinline__ uint32_t build_row(const BuildSeg& S, __amdgpu_buffer_rsrc_t ors,
-                                              const uint8_t* __restrict__ opts, uint32_t lane, uint32_t r, u32x4 lo,
-                                              uint32_t hi, uint32_t acc) {
+__device__ __forceinline__ uint32_t build_row(const BuildSeg& S, __amdgpu_buffer_rsrc_t ors, u32x4 oc, uint32_t lane,
+                                              uint32_t r, u32x4 lo, uint32_t hi, uint32_t acc) {
     const uint32_t pos0 = r * kRow + lane * 16u;
     u32x4 x = S.sh ? realign(lo, hi, S.sh) : lo;
     if (r * kRow < S.hdr_end || (r + 1) * kRow > S.wire)  // keep payload bytes [hdr_end, wire) only
@@ -1229,18 +1284,7 @@ __device__ __forceinline__ uint32_t build_row(const BuildSeg& S, __amdgpu_buffer
         x.z |= lane == 0 ? S.D2 : 0u;
         x.w |= lane == 0 ? S.D3 : 0u;
     }
-    if (S.optlen && r * kRow < 20u + S.optlen) {  // option bytes [20, 20 + optlen): rare, byte by byte
-        const uint32_t lo_b = max(pos0, 20u), hi_b = min(pos0 + 16u, 20u + S.optlen);
-#pragma unroll 1
-        for (uint32_t pos = lo_b; pos < hi_b; ++pos) {
-            const uint32_t v = (uint32_t)opts[S.ob + (pos - 20u)] << (8 * (pos & 3));
-            const uint32_t j = (pos - pos0) >> 2;
-            x.x |= j == 0 ? v : 0u;
-            x.y |= j == 1 ? v : 0u;
-            x.z |= j == 2 ? v : 0u;
-            x.w |= j == 3 ? v : 0u;
-        }
-    }
+    x.x |= oc.x, x.y |= oc.y, x.z |= oc.z, x.w |= oc.w;  // option bytes [20, 20 + optlen)
     acc = sad4(x, acc);
     typedef uint32_t v4u __attribute__((ext_vector_type(4)));
     typedef uint32_t v3u __attribute__((ext_vector_type(3)));
@@ -1250,8 +1294,9 @@ __device__ __forceinline__ uint32_t build_row(const BuildSeg& S, __amdgpu_buffer
     return acc;
 }
 
-// PS: segments per register set on the pipelined fast-group path
-template <int LP, int SP, int PS>
+// PS: segments per register set on the pipelined fast-group path; OPT: the batch has an option array (else
+// every option branch compiles out: 61 VGPRs vs 120 at PS 2)
+template <int LP, int SP, int PS, bool OPT>
 __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const uint8_t* __restrict__ opts,
                                                            const uint64_t* __restrict__ opt_off,
                                                            const uint8_t* __restrict__ data,
@@ -1282,10 +1327,33 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
         const uint32_t mD4 = bswap16u(h.urgent[i]) << 16;  // checksum field (bytes 16-17) = 0 for the sum
         const uint64_t mdb = data_off[i], mde = data_off[i + 1], moo = out_off[i];
         const uint32_t mpart = partial ? partial[i] : 0u;
-        const uint64_t mob = opt_off ? opt_off[i] : 0;
-        const uint32_t moptlen = opt_off ? (uint32_t)(opt_off[i + 1] - mob) : 0u;
+        const uint64_t mob = OPT ? opt_off[i] : 0;
+        const uint32_t moptlen = OPT ? (uint32_t)(opt_off[i + 1] - mob) : 0u;
         const uint32_t mhdr = 20u + moptlen + (moptlen ? (20u + moptlen) % 4u : 0u);  // tcp.go:118-121
         const uint32_t mwire = mhdr + (uint32_t)(mde - mdb);                             // < 2^31
+        uint32_t od[kOptDw];
+        bool staged = false;  // wave-uniform: the group's options are held in od (see staged_opts)
+        if (OPT) {
+            // every lane's option bytes inside [first segment's ob, last segment's end) (so the group descriptor
+            // covers them and its range cannot wrap), at most 40 each
+            const uint64_t gb = readlane64(mob, 0) & ~3ull;
+            const uint64_t ge = readlane64(mob, cnt - 1u) + __builtin_amdgcn_readlane(moptlen, cnt - 1u);
+            staged = __builtin_amdgcn_ballot_w64(moptlen > 4u * kOptDw || mob < gb || mob + moptlen > ge) == 0;
+            if (staged && __builtin_amdgcn_ballot_w64(moptlen != 0) != 0) {
+                const __amdgpu_buffer_rsrc_t rs = make_rsrc(opts + gb, ((ge - gb) + 3u) & ~3ull);
+                const uint32_t sh = (uint32_t)mob & 3u, off = (uint32_t)((mob & ~3ull) - gb);
+                uint32_t d[kOptDw + 1];
+#pragma unroll
+                for (int m = 0; m <= kOptDw; ++m)
+                    d[m] = __builtin_amdgcn_raw_buffer_load_b32(rs, 4u * m < sh + moptlen ? off + 4u * m : kOOB, 0, 0);
+#pragma unroll
+                for (int m = 0; m < kOptDw; ++m)
+                    od[m] = __builtin_amdgcn_alignbyte(d[m + 1], d[m], sh) & keep_mask(0, (int32_t)moptlen, 4 * m);
+            } else {
+#pragma unroll
+                for (int m = 0; m < kOptDw; ++m) od[m] = 0u;
+            }
+        }
         auto seg_at = [&](uint32_t k, BuildSeg& S, __amdgpu_buffer_rsrc_t& drs, __amdgpu_buffer_rsrc_t& ors) {
             S.D0 = __builtin_amdgcn_readlane(mD0, k);
             S.D1 = __builtin_amdgcn_readlane(mD1, k);
@@ -1303,7 +1371,8 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
             S.sh = (uint32_t)S.sh0 & 3u;
             const uint64_t dbase = db & ~3ull;
             S.db = db;
-            S.fast = S.optlen == 0 && (db & 3u) == 0 && db >= 20u && (S.wire & 3u) == 0;
+            S.fast = (S.hdr_end & 3u) == 0 && S.hdr_end <= kRow && (db & 3u) == 0 && db >= S.hdr_end &&
+                     (S.wire & 3u) == 0;
             drs = make_rsrc(data + dbase, data_end4 - dbase);
             ors = make_rsrc(out + readlane64(moo, k), S.nb4);
         };
@@ -1313,11 +1382,12 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
             __builtin_amdgcn_raw_buffer_store_b32(S.D4 | bswap16u(~raw & 0xFFFFu), ors, lane == 0 ? 16u : kOOB, 0, SP);
             if (raw_out && lane == 0) raw_out[g0 + k] = (uint16_t)raw;
         };
-        // Every segment of the group on the fast path and at most 2 rows long (the bench layout): software-
+        // Every segment of the group on the fast path and at most 2 rows long (the bench layouts): software-
         // pipelined — segment k+1's two rows are loaded before segment k is built, so the wave keeps its loads
         // in flight through its own header/sum/store phases (tools/probes/copy_layout.hip seg_swp vs seg).
-        const bool mfast = moptlen == 0 && (mdb & 3u) == 0 && mdb >= 20u && (mwire & 3u) == 0 && mwire <= 2u * kRow;
-        if (pipe && __builtin_amdgcn_ballot_w64(!(mfast || lane >= cnt)) == 0) {
+        const bool mfast = (mhdr & 3u) == 0 && (mdb & 3u) == 0 && mdb >= mhdr && (mwire & 3u) == 0 &&
+                           mwire <= 2u * kRow;
+        if (pipe && (!OPT || staged) && __builtin_amdgcn_ballot_w64(!(mfast || lane >= cnt)) == 0) {
             struct Rows {
                 u32x4 v[PS][2];
             };
@@ -1327,7 +1397,7 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
                     const uint32_t kk = k0 + e, kc = min(kk, cnt - 1u);
                     const uint64_t db = readlane64(mdb, kc);
                     const uint32_t nb4 = kk < cnt ? __builtin_amdgcn_readlane(mwire, kc) : 0u;
-                    const __amdgpu_buffer_rsrc_t frs = make_rsrc(data + db - 20u, nb4);
+                    const __amdgpu_buffer_rsrc_t frs = make_rsrc(data + db - __builtin_amdgcn_readlane(mhdr, kc), nb4);
                     F.v[e][0] = bld16<LP != 0>(frs, lane * 16u);
                     F.v[e][1] = bld16<LP != 0>(frs, kRow + lane * 16u);
                 }
@@ -1348,6 +1418,8 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
                     const uint32_t nb4 = __builtin_amdgcn_readlane(mwire, kk);
                     const __amdgpu_buffer_rsrc_t ors = make_rsrc(out + readlane64(moo, kk), nb4);
                     u32x4 x = F.v[e][0];
+                    if (OPT)  // image dwords [5, hdr/4): options and padding, not the source bytes under them
+                        x = staged_opts<true>(od, kk, (__builtin_amdgcn_readlane(mhdr, kk) - 20u) >> 2, lane, x);
                     x.x = lane == 0 ? S.D0 : (lane == 1 ? S.D4 : x.x);
                     x.y = lane == 0 ? S.D1 : x.y;
                     x.z = lane == 0 ? S.D2 : x.z;
@@ -1381,13 +1453,16 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
             seg_at(k, S, drs, ors);
             uint32_t acc = 0;
             if (S.fast) {
-                // Option-less segment with a 4-aligned payload of whole dwords at data offset ≥ 20: the
-                // image is the payload shifted by exactly 5 dwords. One descriptor based 20 bytes before
-                // the payload (inside the data array) maps image dword k to source dword k, so every row is
-                // one plain 16 B load per lane with no shift and no byte mask; dwords 0-4 (the header) are
-                // replaced by the built header, dwords past the image read 0 (range check).
+                // A 4-aligned header (no options, or options padded to a dword) and a 4-aligned payload of
+                // whole dwords at data offset ≥ hdr_end: the image is the payload shifted by exactly hdr_end/4
+                // dwords. One descriptor based hdr_end bytes before the payload (inside the data array) maps
+                // image dword k to source dword k, so every row is one plain 16 B load per lane with no shift
+                // and no byte mask; bytes [0, hdr_end) of row 0 are replaced by the built header and options,
+                // dwords past the image read 0 (range check).
                 constexpr uint32_t R = kBuildRows;
-                const __amdgpu_buffer_rsrc_t frs = make_rsrc(data + S.db - 20u, S.nb4);
+                const __amdgpu_buffer_rsrc_t frs = make_rsrc(data + S.db - S.hdr_end, S.nb4);
+                OptRaw o{};
+                if (S.optlen && !staged) o = opt_load(opts, S.ob, S.optlen, lane * 16u);
                 for (uint32_t r0 = 0; r0 < S.rows; r0 += R) {
                     u32x4 v[R];
 #pragma unroll
@@ -1400,6 +1475,13 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
                         if (r >= S.rows) break;
                         u32x4 x = v[rr];
                         if (r == 0) {
+                            if (S.optlen && staged) {
+                                x = staged_opts<true>(od, k, (S.hdr_end - 20u) >> 2, lane, x);
+                            } else if (S.optlen) {
+                                const u32x4 oc = opt_fin(o, S.ob, S.optlen, lane * 16u);
+                                x = keep_bytes(x, min(max((int32_t)S.hdr_end - (int32_t)(lane * 16u), 0), 16), 16);
+                                x.x |= oc.x, x.y |= oc.y, x.z |= oc.z, x.w |= oc.w;
+                            }
                             x.x = lane == 0 ? S.D0 : (lane == 1 ? S.D4 : x.x);
                             x.y = lane == 0 ? S.D1 : x.y;
                             x.z = lane == 0 ? S.D2 : x.z;
@@ -1419,15 +1501,21 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
                 // batch 0: the header row + rows 1..R-1, all loads in flight
                 u32x4 lo[R];
                 uint32_t hi[R];
+                OptRaw o{};
+                if (S.optlen && !staged) o = opt_load(opts, S.ob, S.optlen, lane * 16u);  // hdr_end ≤ 1008: row 0
                 build_load_head<LP>(drs, S, lane, lo[0], hi[0]);
 #pragma unroll
                 for (uint32_t rr = 1; rr < R; ++rr) build_load_body<LP>(drs, S, lane, rr, lo[rr], hi[rr]);
 #pragma unroll
                 for (uint32_t rr = 0; rr < R; ++rr)
                     asm volatile("" : "+v"(lo[rr].x), "+v"(lo[rr].y), "+v"(lo[rr].z), "+v"(lo[rr].w), "+v"(hi[rr]));
+                const u32x4 oc0 = !S.optlen ? u32x4{0u, 0u, 0u, 0u}
+                                  : staged  ? staged_opts<false>(od, k, (S.optlen + 3u) >> 2, lane, u32x4{0u, 0u, 0u, 0u})
+                                            : opt_fin(o, S.ob, S.optlen, lane * 16u);
 #pragma unroll
                 for (uint32_t rr = 0; rr < R; ++rr)
-                    if (rr < S.rows) acc = build_row<SP>(S, ors, opts, lane, rr, lo[rr], hi[rr], acc);
+                    if (rr < S.rows)
+                        acc = build_row<SP>(S, ors, rr == 0 ? oc0 : u32x4{0u, 0u, 0u, 0u}, lane, rr, lo[rr], hi[rr], acc);
                 acc = fold32(acc);
                 for (uint32_t r0 = R; r0 < S.rows; r0 += R) {  // long segments: further batches
 #pragma unroll
@@ -1437,19 +1525,24 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
                         asm volatile("" : "+v"(lo[rr].x), "+v"(lo[rr].y), "+v"(lo[rr].z), "+v"(lo[rr].w), "+v"(hi[rr]));
 #pragma unroll
                     for (uint32_t rr = 0; rr < R; ++rr)
-                        if (r0 + rr < S.rows) acc = build_row<SP>(S, ors, opts, lane, r0 + rr, lo[rr], hi[rr], acc);
+                        if (r0 + rr < S.rows)
+                            acc = build_row<SP>(S, ors, u32x4{0u, 0u, 0u, 0u}, lane, r0 + rr, lo[rr], hi[rr], acc);
                     acc = fold32(acc);
                 }
             } else {
                 // options longer than ~1 KiB (not real TCP; the API allows it): every row clamps per dword
                 for (uint32_t r = 0; r < S.rows; ++r) {
-                    const int32_t t = ((int32_t)(r * kRow + lane * 16u) + S.sh0) >> 2;
+                    const uint32_t pos0 = r * kRow + lane * 16u;
+                    const int32_t t = ((int32_t)pos0 + S.sh0) >> 2;
                     uint32_t d[5];
 #pragma unroll
                     for (int j = 0; j < 5; ++j)
                         d[j] = __builtin_amdgcn_raw_buffer_load_b32(drs, t + j >= 0 ? (uint32_t)(t + j) * 4u : kOOB, 0,
                                                                      2);
-                    acc = fold32(build_row<SP>(S, ors, opts, lane, r, u32x4{d[0], d[1], d[2], d[3]}, d[4], acc));
+                    const u32x4 oc = r * kRow < 20u + S.optlen ? opt_fin(opt_load(opts, S.ob, S.optlen, pos0), S.ob,
+                                                                         S.optlen, pos0)
+                                                               : u32x4{0u, 0u, 0u, 0u};
+                    acc = fold32(build_row<SP>(S, ors, oc, lane, r, u32x4{d[0], d[1], d[2], d[3]}, d[4], acc));
                 }
             }
             seg_done(k, S, ors, acc);
@@ -2219,13 +2312,20 @@ hipError_t launch_tcp_build(const TcpHdrSoA& h, const uint8_t* opts, const uint6
     // policy: 0/2 = default cache policy (measured best: segment-boundary lines stay in L2 for
     // the neighbour segment's load and partial-line stores merge there), 1 = nt loads and
     // stores, 3 = nt loads + plain stores, 4 = plain loads + nt stores
-#define NSX_BUILD(LP, SP)                                                                                          \
-    if (spw != 1)                                                                                                  \
-        hipLaunchKernelGGL((tcp_build_kernel<LP, SP, 2>), dim3(grid), dim3(kBlock), 0, st, h, opts, opt_off, data,  \
-                           data_off, data_bytes, partial, n, out, out_off, raw, group, clog, kernel != 2);         \
+#define NSX_BUILD_PS(LP, SP, PS)                                                                                   \
+    if (opt_off)                                                                                                   \
+        hipLaunchKernelGGL((tcp_build_kernel<LP, SP, PS, true>), dim3(grid), dim3(kBlock), 0, st, h, opts, opt_off, \
+                           data, data_off, data_bytes, partial, n, out, out_off, raw, group, clog, kernel != 2);   \
     else                                                                                                           \
-        hipLaunchKernelGGL((tcp_build_kernel<LP, SP, 1>), dim3(grid), dim3(kBlock), 0, st, h, opts, opt_off, data,  \
-                           data_off, data_bytes, partial, n, out, out_off, raw, group, clog, kernel != 2)
+        hipLaunchKernelGGL((tcp_build_kernel<LP, SP, PS, false>), dim3(grid), dim3(kBlock), 0, st, h, opts,        \
+                           opt_off, data, data_off, data_bytes, partial, n, out, out_off, raw, group, clog,        \
+                           kernel != 2)
+#define NSX_BUILD(LP, SP)        \
+    if (spw != 1) {              \
+        NSX_BUILD_PS(LP, SP, 2); \
+    } else {                     \
+        NSX_BUILD_PS(LP, SP, 1); \
+    }
     switch (policy) {
         case 1: NSX_BUILD(2, 2); break;
         case 3: NSX_BUILD(2, 0); break;
@@ -2233,6 +2333,7 @@ hipError_t launch_tcp_build(const TcpHdrSoA& h, const uint8_t* opts, const uint6
         default: NSX_BUILD(0, 0); break;
     }
 #undef NSX_BUILD
+#undef NSX_BUILD_PS
     return hipGetLastError();
 }
 

@@ -137,3 +137,79 @@ def test_fuzz_tcp_build(case):
     nsx.tcp_build_dev(f, _dev(data), _dev(data_off.view(np.int64)), out, _dev(out_off.view(np.int64)), raw=raw)
     assert np.array_equal(_u16(raw), wraw), (case, n, P, lead)
     assert np.array_equal(out.cpu().numpy(), want), (case, n, P, lead)
+
+
+@pytest.mark.parametrize("case", range(30))
+def test_fuzz_tcp_build_options(case):
+    """Random option lists per segment (1-byte kinds and kind-2 options with random
+    lengths, tcp.go:225-231), mostly ≤ 40 bytes (group-staged in the kernel), some
+    longer; option and payload arrays at random alignments; random kernel knobs.
+    Expected images from the Python oracle's Segment.bytes() / computeChecksum."""
+    rng = np.random.default_rng(5000 + case)
+    n = int(rng.integers(1, 400))
+    P = int(rng.choice([int(rng.integers(0, 40)), 1468, int(rng.integers(0, 3000))]))
+    uniform = case % 2 == 0
+    rb = lambda k: rng.integers(0, 256, k, dtype=np.uint8).tobytes()
+    long_p = 0.0 if case % 3 else 0.05
+
+    def opts():
+        if rng.random() < 0.15:
+            return []
+        out, left = [], int(rng.integers(1, 41)) if rng.random() >= long_p else int(rng.integers(41, 130))
+        while left > 0:
+            if left >= 3 and rng.random() < 0.5:
+                k = int(rng.integers(1, left - 1))  # kind 2: 2 + k bytes
+                out.append(O.Option(kind=2, length=int(rng.integers(0, 256)), data=rb(k)))
+                left -= 2 + k
+            else:
+                out.append(O.Option(kind=int(rng.choice([0, 1, 3, 4, 8]))))
+                left -= 1
+        return out
+
+    segs, pseudos = [], []
+    for i in range(n):
+        L = P & ~3 if uniform else int(rng.integers(0, P + 1))
+        sg = O.Segment(src_port=int(rng.integers(1 << 16)), dst_port=int(rng.integers(1 << 16)),
+                       seq_num=int(rng.integers(1 << 32)), ack_num=int(rng.integers(1 << 32)),
+                       control=O.Ctl.from_byte(int(rng.integers(256))), window=int(rng.integers(1 << 16)),
+                       urgent_ptr=int(rng.integers(1 << 16)), options=opts(), data=rb(L))
+        sg.offset = sg.compute_offset() & 0xFF
+        segs.append(sg)
+        pseudos.append(O.ipv4_pseudo_header(rb(4), rb(4), 6, len(sg.bytes())))
+    want_raw, want = np.empty(n, np.uint16), []
+    for i, sg in enumerate(segs):
+        sg.checksum = 0
+        want_raw[i] = O.c_go_checksum(pseudos[i], sg.bytes())
+        sg.checksum = O.field_value(int(want_raw[i]))
+        want.append(sg.bytes())
+    ob = [b"".join(o.bytes() for o in sg.options) for sg in segs]
+    olead, dlead = int(rng.integers(0, 8)), int(rng.choice([0, 3, 60, 64, 130]))
+    optarr = np.frombuffer(bytes(olead) + b"".join(ob) + bytes(4), np.uint8)
+    opt_off = np.zeros(n + 1, np.uint64)
+    opt_off[1:] = np.cumsum([len(b) for b in ob])
+    opt_off += np.uint64(olead)
+    data = np.frombuffer(rb(dlead) + b"".join(sg.data for sg in segs) + rb(8), np.uint8)
+    data_off = np.zeros(n + 1, np.uint64)
+    data_off[1:] = np.cumsum([len(sg.data) for sg in segs])
+    data_off += np.uint64(dlead)
+    out_off = nsx.tcp_layout_host(data_off, opt_off)
+    _apply(dict(kernel=int(rng.choice([0, 2])), segs_per_wave=int(rng.choice([0, 1])),
+                blocks_per_cu=int(rng.choice([0, 1, 8]))))
+    col = lambda k, dt: _dev(np.array([getattr(sg, k) for sg in segs], dt).view(
+        {np.uint16: np.int16, np.uint32: np.int32, np.uint8: np.uint8}[dt]))
+    f = {"src_port": col("src_port", np.uint16), "dst_port": col("dst_port", np.uint16),
+         "seq_num": col("seq_num", np.uint32), "ack_num": col("ack_num", np.uint32),
+         "offset": col("offset", np.uint8),
+         "control": _dev(np.array([sg.control.byte() for sg in segs], np.uint8)),
+         "window": col("window", np.uint16), "urgent_ptr": col("urgent_ptr", np.uint16)}
+    part = _dev(np.array([O.be_word_sum(p) for p in pseudos], np.uint32).view(np.int32))
+    out = torch.full((int(out_off[-1]),), 0xAB, dtype=torch.uint8, device="cuda")
+    raw = torch.empty(n, dtype=torch.int16, device="cuda")
+    nsx.tcp_build_dev(f, _dev(data), _dev(data_off.view(np.int64)), out, _dev(out_off.view(np.int64)),
+                      opts=_dev(optarr), opt_off=_dev(opt_off.view(np.int64)), partial=part, raw=raw)
+    got = out.cpu().numpy()
+    assert np.array_equal(_u16(raw), want_raw), (case, n, P)
+    for i in range(n):
+        o = int(out_off[i])
+        assert got[o:o + len(want[i])].tobytes() == want[i], (case, i)
+        assert not got[o + len(want[i]):int(out_off[i + 1])].any(), (case, i)

@@ -794,6 +794,82 @@ def test_tcp_build_uniform_batches(P, n, nsx_param):
             assert np.array_equal(got, want), (P, n, lead, kern, spw)
 
 
+_OPT_SETS = {  # option lists as the reference serialises them (tcp.go:225-231: kind 2 carries length + data)
+    "nop_nop_k2len10": lambda r: [O.Option(kind=1), O.Option(kind=1), O.Option(kind=2, length=10, data=r(8))],
+    "mss": lambda r: [O.Option(kind=2, length=4, data=r(2))],
+    "nop_nop": lambda r: [O.Option(kind=1)] * 2,           # 22 B header: 2 pad bytes, still 4-aligned
+    "nop": lambda r: [O.Option(kind=1)],                   # 21 B + 1 pad: a 22 B header (general path)
+    "nop3": lambda r: [O.Option(kind=1)] * 3,              # 23 B + 3 pad: 26 B
+    "k2len40": lambda r: [O.Option(kind=2, length=40, data=r(38))],  # 60 B header, the TCP maximum
+    # longer than TCP allows (the data offset field wraps; the ABI still builds the bytes): > 40 option bytes
+    # take the per-segment option loads instead of the group-staged ones
+    "k2len41": lambda r: [O.Option(kind=2, length=41, data=r(39))],  # 61 B + 1 pad: 62 B header
+    "k2len100": lambda r: [O.Option(kind=2, length=100, data=r(98))],  # 120 B header, 4-aligned
+}
+
+
+@pytest.mark.parametrize("P", [0, 12, 1468, 3000])
+@pytest.mark.parametrize("opt", sorted(_OPT_SETS))
+def test_tcp_build_uniform_batches_with_options(opt, P, nsx_param):
+    """Packed batches whose every segment carries the same option list (the bench's
+    config 8 layout): images and raw sums equal the Python oracle's Segment.bytes() /
+    computeChecksum (tcp.go:98-128, :72-95) with the options at image byte 20, the
+    reference's padding rule, option arrays at every byte alignment, payloads with and
+    without hdr_end bytes before them, pipelined and unpipelined."""
+    rng = np.random.default_rng(P * 7 + len(opt))
+    n = 130
+    rb = lambda k: rng.integers(0, 256, k, dtype=np.uint8).tobytes()
+    segs, pseudos = [], []
+    for i in range(n):
+        sg = O.Segment(src_port=int(rng.integers(1 << 16)), dst_port=int(rng.integers(1 << 16)),
+                       seq_num=int(rng.integers(1 << 32)), ack_num=int(rng.integers(1 << 32)),
+                       control=O.Ctl.from_byte(int(rng.integers(256))), window=int(rng.integers(1 << 16)),
+                       urgent_ptr=int(rng.integers(1 << 16)), options=_OPT_SETS[opt](rb), data=rb(P))
+        sg.offset = sg.compute_offset()
+        segs.append(sg)
+        pseudos.append(O.ipv4_pseudo_header(rb(4), rb(4), 6, len(sg.bytes())))
+    want_raw = np.empty(n, np.uint16)
+    want_wire = []
+    for i, sg in enumerate(segs):
+        sg.checksum = 0
+        want_raw[i] = O.c_go_checksum(pseudos[i], sg.bytes())
+        sg.checksum = O.field_value(int(want_raw[i]))
+        want_wire.append(sg.bytes())
+    ob = [b"".join(o.bytes() for o in sg.options) for sg in segs]
+    u = lambda a, dt: dev(np.asarray(a, dt).view({np.uint16: np.int16, np.uint32: np.int32, np.uint8: np.uint8}[dt]))
+    fields = {"src_port": u([sg.src_port for sg in segs], np.uint16),
+              "dst_port": u([sg.dst_port for sg in segs], np.uint16),
+              "seq_num": u([sg.seq_num for sg in segs], np.uint32), "ack_num": u([sg.ack_num for sg in segs], np.uint32),
+              "offset": u([sg.offset for sg in segs], np.uint8),
+              "control": u([sg.control.byte() for sg in segs], np.uint8),
+              "window": u([sg.window for sg in segs], np.uint16),
+              "urgent_ptr": u([sg.urgent_ptr for sg in segs], np.uint16)}
+    part = dev(np.array([O.be_word_sum(p) for p in pseudos], np.uint32).view(np.int32))
+    for opt_lead, data_lead in ((0, 60), (2, 32), (3, 0), (1, 64)):
+        opts = np.frombuffer(b"\x77" * opt_lead + b"".join(ob) + b"\x77" * 3, np.uint8)
+        opt_off = np.zeros(n + 1, np.uint64)
+        opt_off[1:] = np.cumsum([len(b) for b in ob])
+        opt_off += np.uint64(opt_lead)
+        data = np.frombuffer(b"\x99" * data_lead + b"".join(sg.data for sg in segs) + b"\x99" * 8, np.uint8)
+        data_off = np.arange(n + 1, dtype=np.uint64) * np.uint64(P) + np.uint64(data_lead)
+        out_off = nsx.tcp_layout_host(data_off, opt_off)
+        assert all(int(out_off[i + 1] - out_off[i]) >= len(want_wire[i]) for i in range(n))
+        for kern, spw in ((0, 0), (0, 1), (2, 0)):
+            nsx_param(nsx.PARAM_KERNEL, kern)
+            nsx_param(nsx.PARAM_SEGS_PER_WAVE, spw)
+            out = torch.full((int(out_off[-1]),), 0xAB, dtype=torch.uint8, device="cuda")
+            raw = torch.empty(n, dtype=torch.int16, device="cuda")
+            nsx.tcp_build_dev(fields, dev(data), dev(data_off.view(np.int64)), out, dev(out_off.view(np.int64)),
+                              opts=dev(opts), opt_off=dev(opt_off.view(np.int64)), partial=part, raw=raw)
+            got, raw_h = host(out), u16(raw)
+            key = (opt, P, opt_lead, data_lead, kern, spw)
+            assert np.array_equal(raw_h, want_raw), key
+            for i in range(n):
+                o = int(out_off[i])
+                assert got[o:o + len(want_wire[i])].tobytes() == want_wire[i], key + (i,)
+                assert not got[o + len(want_wire[i]):int(out_off[i + 1])].any(), key + (i,)
+
+
 def test_tcp_build_whole_dword_and_ragged_payloads_interleaved():
     """Whole-dword payloads (the kernel's no-shift fast path) next to a 1476 B payload
     in every other group of 64, which shifts every later payload's alignment."""
