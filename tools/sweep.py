@@ -49,6 +49,10 @@ def variants(kind):
     if kind == "tcp_build":  # cache policy (nontemporal knob) x grid
         return ([dict(blocks_per_cu=b, segs_per_wave=ps) for b in (1, 2, 4) for ps in (1, 2)] +
                 [dict(blocks_per_cu=b, kernel=2) for b in (4, 8)])
+    if kind == "ragged_deep":  # deeper in-flight windows: 16-row batches, pipelined, 1-2 blocks/CU
+        return ([dict(kernel=4, blocks_per_cu=2, stream_rows=8, nontemporal=1, xcd_map=4, run_segs=63)] +
+                [dict(kernel=k, blocks_per_cu=b, stream_rows=r, nontemporal=1, xcd_map=4, run_segs=63)
+                 for k in (4, 6) for b in (1, 2, 3) for r in (8, 16)])
     if kind == "ragged_bal":  # scan kernel: XCD deal vs byte-balanced wave ranges
         for bpc, rows, run, xcd in itertools.product((1, 2, 4, 8), (4, 8, 16), (8, 16, 32, 63), (1, 4)):
             out.append(dict(kernel=4, blocks_per_cu=bpc, stream_rows=rows, nontemporal=1, xcd_map=xcd, run_segs=run))
