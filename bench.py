@@ -9,7 +9,7 @@ GPU (torchrun), each checksumming its own batch: the path shards with no
 exchange, so there is no data-path collective and scaling is
 weak. value = Σ bytes over all ranks ÷ max over ranks of the timed region.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5|6|7|8]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2-9]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 Configs 2-5 are BASELINE.json's device-resident configurations (2 is the
@@ -18,7 +18,8 @@ the same bar, each with its own metric string: 6 = the fused sender pass
 (nsx_tcp_build_dev: segment.bytes() + computeChecksum + field write,
 tcp.go:98-128/:68-71) over 1M 1500 B wire images; 7 = IPv4 header checksum
 verify (nsx_ipv4_hdr_csum_dev) over 64M packed 20 B headers; 8 = config 6 with a
-12 B option block per segment (the build kernel's option path; no CPU baseline).
+12 B option block per segment (the build kernel's option path; no CPU baseline); 9 =
+workload 7 verified straight into a validity bitmask (nsx_ipv4_hdr_verify_mask_dev).
 
 Printed by rank 0: one JSON line with the contract fields plus
   roofline     — dominant kernel: algorithmic bytes per launch ÷ its mean
@@ -64,6 +65,11 @@ WORKLOADS = {
             metric="GiB/s fused TCP segment build (serialize + checksum + field write), wire bytes",
             name="f1+options: 1M TCP segments per GPU, 12B options (NOP NOP kind-2 len 10), 1468B payload -> 1500B wire images, "
                  "IPv4 pseudo-header partials, device-resident"),
+    # not a BASELINE config: f3's receive side fused with f2's bitmask (1 bit written per header)
+    9: dict(kind="ipv4_hdr", mask=True, n=1 << 26, hdr=20, seed=0x1077,
+            metric="GiB/s IPv4 header checksum verify into a bitmask, header bytes",
+            name="f3+f2: 64M packed 20B IPv4 headers per GPU (header-split ring), verify into a validity bitmask, "
+                 "device-resident"),
     7: dict(kind="ipv4_hdr", n=1 << 26, hdr=20, seed=0x1075,
             metric="GiB/s IPv4 header checksum verify, header bytes",
             name="f3: 64M packed 20B IPv4 headers per GPU (header-split ring), verify, device-resident"),
@@ -77,7 +83,7 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", type=int, default=2, choices=sorted(WORKLOADS),
                     help="2-5: BASELINE configs (2 = headline); 6: f1 fused TCP build; 7: f3 IPv4 header verify; "
-                         "8: f1 with 12 B options")
+                         "8: f1 with 12 B options; 9: f3 verify into a bitmask")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--settle-s", type=float, default=0.5, help="device clock settle time before warmup (setup)")
     ap.add_argument("--event-every", type=int, default=10,
@@ -251,9 +257,15 @@ def build_workload(cfg, rank, device):
         nsx.fill_splitmix64_dev(buf, seed)
         buf.view(n, H)[:, 0] = 0x45  # version 4, IHL 5
         nsx.ipv4_hdr_csum_dev(buf, H, n, mode=1)  # setup: fill valid checksums (RFC 791 §3.1)
-        out = torch.empty(n, dtype=torch.int16, device=device)
-        w.update(buf=buf, out=out, bytes=n * H, alg=n * (H + 2),
-                 step=lambda: nsx.ipv4_hdr_csum_dev(buf, H, n, mode=0, out=out))
+        if cfg.get("mask"):
+            buf.view(n, H)[::1000, 8] ^= 1  # some invalid headers (TTL flipped after the fill)
+            out = torch.empty((n + 63) // 64, dtype=torch.int64, device=device)
+            w.update(buf=buf, out=out, bytes=n * H, alg=n * H + (n + 63) // 64 * 8,
+                     step=lambda: nsx.ipv4_hdr_verify_mask_dev(buf, H, n, mask=out))
+        else:
+            out = torch.empty(n, dtype=torch.int16, device=device)
+            w.update(buf=buf, out=out, bytes=n * H, alg=n * (H + 2),
+                     step=lambda: nsx.ipv4_hdr_csum_dev(buf, H, n, mode=0, out=out))
     else:
         rng = np.random.default_rng(cfg["seed"])  # same lengths on every rank, bytes differ by seed
         n = cfg["n"]
@@ -331,18 +343,24 @@ def cpu_baseline(cfg, w, seconds: float) -> dict:
         n, H = cfg["n"], cfg["hdr"]
         m = min(n, 1 << 22)
         sample = w["buf"][: m * H].cpu().numpy()
-        gpu = w["out"][:m].cpu().numpy().view(np.uint16)
-        out = np.empty(m, np.uint16)
+        mask = cfg.get("mask", False)
+        gpu = (w["out"][: m // 64].cpu().numpy().view(np.uint64) if mask
+               else w["out"][:m].cpu().numpy().view(np.uint16))
+        raw = np.empty(m, np.uint16)
+        out = None
         t0, reps = time.perf_counter(), 0
         while True:
             lib.oracle_go_batch_fixed(sample.ctypes.data_as(ctypes.c_void_p), H, H, m, None, 0,
-                                      out.ctypes.data_as(ctypes.c_void_p))
+                                      raw.ctypes.data_as(ctypes.c_void_p))
+            # IHL 5 on every header of this workload, so well-formed; valid iff the sum is 0xFFFF
+            out = np.packbits(raw == 0xFFFF, bitorder="little").view(np.uint64) if mask else raw
             reps += 1
             if time.perf_counter() - t0 >= seconds:
                 break
         dt = time.perf_counter() - t0
         nbytes = reps * m * H
-        desc = f"first {m} headers of rank 0's batch, {reps} pass(es), the reference's serial checksum loop per header"
+        desc = (f"first {m} headers of rank 0's batch, {reps} pass(es), the reference's serial checksum loop per "
+                "header" + (" + bit packing of sum == 0xFFFF" if mask else ""))
     else:
         offs = w["offsets"]
         m = int(min(len(offs) - 1, 50000))

@@ -163,6 +163,16 @@ int nsx_tcp_layout_host(const uint64_t* h_opt_off, const uint64_t* h_data_off, u
 int nsx_ipv4_hdr_csum_dev(void* d_base, uint64_t stride, uint32_t hdr_off, uint64_t n, int mode,
                           uint16_t* d_out_raw, nsx_stream_t stream);
 
+/* IPv4 header verify straight into a bitmask (the receive side of f3 fused with
+ * the f2 mask convention, tcp.go:70 rule applied to RFC 791 headers): bit
+ * (i % 64) of d_mask[i / 64] is set iff header i is well-formed and its raw sum
+ * is 0xFFFF (= nsx_ipv4_hdr_csum_dev mode 0 followed by nsx_verify_mask_dev,
+ * one pass, 1 bit written per header instead of 16); bits past n in the last
+ * word are 0. d_mask holds ceil(n/64) words. Same layout rules and limits as
+ * nsx_ipv4_hdr_csum_dev; the headers are only read. */
+int nsx_ipv4_hdr_verify_mask_dev(const void* d_base, uint64_t stride, uint32_t hdr_off, uint64_t n,
+                                 uint64_t* d_mask, nsx_stream_t stream);
+
 /* ----------------------------------------------------------------------------
  * Host-resident batches: pinned staging, H2D → kernel → D2H double-buffered
  * over two streams per GPU, segments sharded contiguously across num_gpus

@@ -259,8 +259,25 @@ int nsx_ipv4_hdr_csum_dev(void* d_base, uint64_t stride, uint32_t hdr_off, uint6
     const int dev = current_device();
     if (dev < 0) return NSX_ENODEV;
     const DevInfo* di = dev_info(dev);
-    return map_err(nsx::launch_ipv4_hdr(static_cast<uint8_t*>(d_base), stride, hdr_off, n, mode, d_out_raw, di->cus,
-                                        (int)g_param[NSX_PARAM_BLOCKS_PER_CU].load(),
+    return map_err(nsx::launch_ipv4_hdr(static_cast<uint8_t*>(d_base), stride, hdr_off, n, mode, d_out_raw, nullptr,
+                                        di->cus, (int)g_param[NSX_PARAM_BLOCKS_PER_CU].load(),
+                                        (int)g_param[NSX_PARAM_KERNEL].load(),
+                                        (int)g_param[NSX_PARAM_SEGS_PER_WAVE].load(),
+                                        (int)g_param[NSX_PARAM_XCD_CHUNK].load(), static_cast<hipStream_t>(stream)));
+}
+
+int nsx_ipv4_hdr_verify_mask_dev(const void* d_base, uint64_t stride, uint32_t hdr_off, uint64_t n, uint64_t* d_mask,
+                                 nsx_stream_t stream) {
+    if (n == 0) return NSX_OK;
+    if (!d_base || !d_mask) return NSX_EINVAL;
+    if (n > 1 && stride == 0) return NSX_EINVAL;
+    if (stride > ((uint64_t)1 << 22) || hdr_off > ((uint32_t)1 << 22)) return NSX_EINVAL;  // 32-bit block offsets
+    const int dev = current_device();
+    if (dev < 0) return NSX_ENODEV;
+    const DevInfo* di = dev_info(dev);
+    // mode 2 only reads the headers (the kernels take a non-const base for fill mode)
+    return map_err(nsx::launch_ipv4_hdr(static_cast<uint8_t*>(const_cast<void*>(d_base)), stride, hdr_off, n, 2,
+                                        nullptr, d_mask, di->cus, (int)g_param[NSX_PARAM_BLOCKS_PER_CU].load(),
                                         (int)g_param[NSX_PARAM_KERNEL].load(),
                                         (int)g_param[NSX_PARAM_SEGS_PER_WAVE].load(),
                                         (int)g_param[NSX_PARAM_XCD_CHUNK].load(), static_cast<hipStream_t>(stream)));

@@ -57,9 +57,10 @@ hipError_t launch_tcp_build(const TcpHdrSoA& h, const uint8_t* opts, const uint6
                             const uint64_t* data_off, uint64_t data_bytes, const uint32_t* partial, uint64_t n,
                             uint8_t* out, const uint64_t* out_off, uint16_t* raw, uint32_t max_blocks, int policy,
                             int xchunk, int kernel, int spw, hipStream_t st);
-// bpc / unroll: raw NSX_PARAM_BLOCKS_PER_CU / NSX_PARAM_SEGS_PER_WAVE (0 = per-kernel default)
+// bpc / unroll: raw NSX_PARAM_BLOCKS_PER_CU / NSX_PARAM_SEGS_PER_WAVE (0 = per-kernel default);
+// mode 0 verify (out), 1 fill (out nullable), 2 verify into the bitmask `mask` (ceil(n/64) words)
 hipError_t launch_ipv4_hdr(uint8_t* base, uint64_t stride, uint32_t hdr_off, uint64_t n, int mode, uint16_t* out,
-                           int cus, int bpc, int kernel, int unroll, int xchunk, hipStream_t st);
+                           uint64_t* mask, int cus, int bpc, int kernel, int unroll, int xchunk, hipStream_t st);
 hipError_t launch_fill_splitmix64(void* d_buf, uint64_t byte_off, uint64_t nbytes, uint64_t seed,
                                   uint32_t max_blocks, hipStream_t st);
 

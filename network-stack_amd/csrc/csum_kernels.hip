@@ -26,6 +26,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "csum_kernels.h"
 
 namespace nsx {
@@ -1566,6 +1568,9 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
 // the wave. Then the LE-half-sum / byte-swap rule of the segment kernels.
 // MODE 0: out = raw sum over the header as it stands (valid iff 0xFFFF).
 // MODE 1: out = raw sum with bytes 10-11 taken as zero; writes ~raw there.
+// MODE 2: receive-side verify as a bitmask: bit (i % 64) of mask[i / 64] set iff
+//         header i is well-formed and its raw sum is 0xFFFF (one v_cmp + ballot
+//         per wave; 1 bit written per header instead of 16).
 // A malformed header (IHL < 5, or longer than the stride) gets out = 0 and is
 // not written.
 // ---------------------------------------------------------------------------
@@ -1573,7 +1578,8 @@ constexpr int kHdrUnroll = 4;  // 256-header chunks per block iteration, loads o
 
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void ipv4_hdr_kernel(uint8_t* __restrict__ base, uint64_t stride,
-                                                          uint32_t hdr_off, uint64_t n, uint16_t* __restrict__ out) {
+                                                          uint32_t hdr_off, uint64_t n, uint16_t* __restrict__ out,
+                                                          uint64_t* __restrict__ mask) {
     constexpr int U = kHdrUnroll;
     const uint32_t t = threadIdx.x;
     for (uint64_t c00 = (uint64_t)blockIdx.x * kBlock * U; c00 < n; c00 += (uint64_t)gridDim.x * kBlock * U) {
@@ -1641,6 +1647,11 @@ __global__ __launch_bounds__(kBlock) void ipv4_hdr_kernel(uint8_t* __restrict__ 
             uint8_t* p = cbase[u] + rel[u];
             const uint32_t raw = ok[u] ? finish(acc[u], ((uintptr_t)p & 1u) == 0, 0u) : 0u;
             if (out && live[u]) out[c00 + (uint64_t)u * kBlock + t] = (uint16_t)raw;
+            if constexpr (MODE == 2) {  // the wave's 64 headers start at a multiple of 64
+                const uint64_t bits = __builtin_amdgcn_ballot_w64(ok[u] && raw == 0xFFFFu);
+                const uint64_t h0 = c00 + (uint64_t)u * kBlock + (t & ~(kWave - 1));
+                if ((t & (kWave - 1)) == 0 && h0 < n) mask[h0 / kWave] = bits;
+            }
             if (MODE == 1 && ok[u]) {
                 const uint16_t f = (uint16_t)~raw;
                 p[10] = (uint8_t)(f >> 8);
@@ -1661,7 +1672,8 @@ constexpr uint32_t kHdrDenseMaxStride = 64;
 template <int MODE, int ROWS, int U>
 __global__ __launch_bounds__(kBlock) void ipv4_hdr_dense_kernel(uint8_t* __restrict__ base, uint32_t stride,
                                                                 uint32_t hdr_off, uint64_t n,
-                                                                uint16_t* __restrict__ out) {
+                                                                uint16_t* __restrict__ out,
+                                                                uint64_t* __restrict__ mask) {
     extern __shared__ uint32_t lds_hdr[];
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -1728,6 +1740,10 @@ __global__ __launch_bounds__(kBlock) void ipv4_hdr_dense_kernel(uint8_t* __restr
             uint8_t* p = fa[u] + rel;
             const uint32_t raw = ok ? finish(acc, ((uintptr_t)p & 1u) == 0, 0u) : 0u;
             if (out && live) out[(t0 + (uint64_t)u * wstep) * kWave + lane] = (uint16_t)raw;
+            if constexpr (MODE == 2) {  // task = 64 headers = one mask word
+                const uint64_t bits = __builtin_amdgcn_ballot_w64(ok && raw == 0xFFFFu);
+                if (lane == 0) mask[t0 + (uint64_t)u * wstep] = bits;
+            }
             if (MODE == 1 && ok) {
                 const uint16_t f = (uint16_t)~raw;
                 p[10] = (uint8_t)(f >> 8);
@@ -1755,7 +1771,8 @@ constexpr uint32_t kHdr20Lds = kHdr20Task * 20u;  // bytes of LDS per wave
 // wave per SIMD at 1 block/CU has no other wave to cover those phases). !PIPE: one set, load then use.
 template <int MODE, int U, bool PIPE>
 __global__ __launch_bounds__(kBlock) void ipv4_hdr20_kernel(uint8_t* __restrict__ base, uint32_t n,
-                                                            uint16_t* __restrict__ out, uint32_t clog) {
+                                                            uint16_t* __restrict__ out, uint32_t clog,
+                                                            uint64_t* __restrict__ mask) {
     typedef uint32_t v2u __attribute__((ext_vector_type(2)));
     extern __shared__ u32x4 lds20[];
     const uint32_t lane = threadIdx.x & (kWave - 1);
@@ -1815,7 +1832,27 @@ __global__ __launch_bounds__(kBlock) void ipv4_hdr20_kernel(uint8_t* __restrict_
                 res[h] = ok[h] ? finish(acc, true, 0u) : 0u;
             }
             const uint32_t i0 = S.tk[u] * kHdr20Task + lane * 4u;
-            if (S.cnt[u] == kHdr20Task) {
+            if constexpr (MODE == 2) {
+                // lane l holds headers 4l..4l+3 of the task, so word k (headers 64k..64k+63) is the 16 nibbles of
+                // DPP row k: each lane shifts its nibble into place (lanes 0-7 of a row the low dword, 8-15 the
+                // high), a 4-step row_shr sum (disjoint bits: sum = OR) leaves the word in the row's last lane.
+                // Headers past n read as zeros (IHL 0: malformed, bit 0).
+                const uint32_t nib = (uint32_t)(ok[0] && res[0] == 0xFFFFu) | ((uint32_t)(ok[1] && res[1] == 0xFFFFu) << 1) |
+                                     ((uint32_t)(ok[2] && res[2] == 0xFFFFu) << 2) |
+                                     ((uint32_t)(ok[3] && res[3] == 0xFFFFu) << 3);
+                const uint32_t j = lane & 15u;
+                uint32_t lo = j < 8u ? nib << (4u * j) : 0u, hi = j >= 8u ? nib << (4u * (j - 8u)) : 0u;
+                lo += __builtin_amdgcn_update_dpp(0u, lo, 0x111, 0xF, 0xF, false);  // row_shr:1
+                hi += __builtin_amdgcn_update_dpp(0u, hi, 0x111, 0xF, 0xF, false);
+                lo += __builtin_amdgcn_update_dpp(0u, lo, 0x112, 0xF, 0xF, false);  // row_shr:2
+                hi += __builtin_amdgcn_update_dpp(0u, hi, 0x112, 0xF, 0xF, false);
+                lo += __builtin_amdgcn_update_dpp(0u, lo, 0x114, 0xF, 0xF, false);  // row_shr:4
+                hi += __builtin_amdgcn_update_dpp(0u, hi, 0x114, 0xF, 0xF, false);
+                lo += __builtin_amdgcn_update_dpp(0u, lo, 0x118, 0xF, 0xF, false);  // row_shr:8
+                hi += __builtin_amdgcn_update_dpp(0u, hi, 0x118, 0xF, 0xF, false);
+                const uint32_t wi = S.tk[u] * (kHdr20Task / kWave) + (lane >> 4);  // < 2^22 (n < 2^28 per launch)
+                if (j == 15u && wi * kWave < n) mask[wi] = ((uint64_t)hi << 32) | lo;
+            } else if (S.cnt[u] == kHdr20Task) {
                 __builtin_amdgcn_raw_buffer_store_b64(v2u{res[0] | (res[1] << 16), res[2] | (res[3] << 16)}, ors,
                                                       i0 * 2u, 0, 0);
             } else {
@@ -2338,14 +2375,22 @@ hipError_t launch_tcp_build(const TcpHdrSoA& h, const uint8_t* opts, const uint6
 }
 
 hipError_t launch_ipv4_hdr(uint8_t* base, uint64_t stride, uint32_t hdr_off, uint64_t n, int mode, uint16_t* out,
-                           int cus, int bpc, int kernel, int unroll, int xchunk, hipStream_t st) {
+                           uint64_t* mask, int cus, int bpc, int kernel, int unroll, int xchunk, hipStream_t st) {
     // kernel: 0 = auto (pipelined flat kernel for packed 20 B headers, else LDS-dense for stride ≤ 64, else
-    // per-thread), 1 = per-thread, 2 = LDS-dense (stride ≤ 64), 3 = flat without pipelining
+    // per-thread), 1 = per-thread, 2 = LDS-dense (stride ≤ 64), 3 = flat without pipelining.
+    // mode: 0 verify (raw sums), 1 fill in place, 2 verify into the bitmask `mask`.
+    auto by_mode = [&](auto launch) {
+        switch (mode) {
+            case 1: launch(std::integral_constant<int, 1>{}); break;
+            case 2: launch(std::integral_constant<int, 2>{}); break;
+            default: launch(std::integral_constant<int, 0>{}); break;
+        }
+    };
     if (stride == 20 && hdr_off == 0 && ((uintptr_t)base & 3u) == 0 && (kernel == 0 || kernel == 3)) {
         const bool pipe = kernel == 0;  // kernel 3: the unpipelined flat kernel (measured alternative)
         // packed option-less headers: flat-stream kernel. Default 1 block/CU with 2 tasks (10 KiB) in flight
         // per wave = 40 KiB per CU (tools/sweep.py: 0.220 ms vs 0.232 at 2 blocks/CU, 0.284 at 1 task/wave);
-        // chunks keep each launch's results within one descriptor
+        // chunks keep each launch's results within one descriptor (2^28 headers = 2^22 mask words)
         const uint32_t mb = (uint32_t)cus * (uint32_t)(bpc >= 1 && bpc <= 8 ? bpc : 1);
         constexpr uint64_t kChunk = 1ull << 28;
         for (uint64_t c0 = 0; c0 < n; c0 += kChunk) {
@@ -2355,30 +2400,27 @@ hipError_t launch_ipv4_hdr(uint8_t* base, uint64_t stride, uint32_t hdr_off, uin
             const uint32_t grid_f = (uint32_t)(want_f < mb ? want_f : mb);
             uint8_t* b = base + c0 * 20u;
             uint16_t* o = out ? out + c0 : nullptr;
+            uint64_t* mk = mask ? mask + c0 / kWave : nullptr;
             const size_t lds = (size_t)kHdr20Lds * kWavesPerBlock;
             const uint32_t clog = deal_clog(xchunk, tasks, kHdr20Lds + kHdr20Task * 2u);
+            by_mode([&](auto m) {
+                constexpr int M = decltype(m)::value;
 #define NSX_H20(U)                                                                                              \
     do {                                                                                                        \
-        if (pipe) {                                                                                             \
-            if (mode == 1)                                                                                      \
-                hipLaunchKernelGGL((ipv4_hdr20_kernel<1, U, true>), dim3(grid_f), dim3(kBlock), lds, st, b, cn, o, \
-                                   clog);                                                                       \
-            else                                                                                                \
-                hipLaunchKernelGGL((ipv4_hdr20_kernel<0, U, true>), dim3(grid_f), dim3(kBlock), lds, st, b, cn, o, \
-                                   clog);                                                                       \
-        } else if (mode == 1)                                                                                   \
-            hipLaunchKernelGGL((ipv4_hdr20_kernel<1, U, false>), dim3(grid_f), dim3(kBlock), lds, st, b, cn, o,    \
-                               clog);                                                                           \
+        if (pipe)                                                                                               \
+            hipLaunchKernelGGL((ipv4_hdr20_kernel<M, U, true>), dim3(grid_f), dim3(kBlock), lds, st, b, cn, o,   \
+                               clog, mk);                                                                       \
         else                                                                                                    \
-            hipLaunchKernelGGL((ipv4_hdr20_kernel<0, U, false>), dim3(grid_f), dim3(kBlock), lds, st, b, cn, o,    \
-                               clog);                                                                           \
+            hipLaunchKernelGGL((ipv4_hdr20_kernel<M, U, false>), dim3(grid_f), dim3(kBlock), lds, st, b, cn, o,  \
+                               clog, mk);                                                                       \
     } while (0)
-            switch (unroll) {
-                case 1: NSX_H20(1); break;
-                case 4: NSX_H20(4); break;
-                default: NSX_H20(2); break;
-            }
+                switch (unroll) {
+                    case 1: NSX_H20(1); break;
+                    case 4: NSX_H20(4); break;
+                    default: NSX_H20(2); break;
+                }
 #undef NSX_H20
+            });
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
@@ -2394,28 +2436,26 @@ hipError_t launch_ipv4_hdr(uint8_t* base, uint64_t stride, uint32_t hdr_off, uin
         const uint64_t tasks = (n + kWave - 1) / kWave;
         const uint64_t want_d = (tasks + kWavesPerBlock - 1) / kWavesPerBlock;
         const uint32_t grid_d = (uint32_t)(want_d < max_blocks ? want_d : max_blocks);
+        by_mode([&](auto m) {
+            constexpr int M = decltype(m)::value;
 #define NSX_HDR(R, U)                                                                                              \
-    do {                                                                                                           \
-        const size_t lds = (size_t)(R) * (U) * kRow * kWavesPerBlock;                                              \
-        if (mode == 1)                                                                                             \
-            hipLaunchKernelGGL((ipv4_hdr_dense_kernel<1, R, U>), dim3(grid_d), dim3(kBlock), lds, st, base,        \
-                               (uint32_t)stride, hdr_off, n, out);                                                 \
-        else                                                                                                       \
-            hipLaunchKernelGGL((ipv4_hdr_dense_kernel<0, R, U>), dim3(grid_d), dim3(kBlock), lds, st, base,        \
-                               (uint32_t)stride, hdr_off, n, out);                                                 \
-    } while (0)
-        switch (rows) {
-            case 1: NSX_HDR(1, 4); break;
-            case 2: NSX_HDR(2, 2); break;
-            case 3: NSX_HDR(3, 1); break;
-            case 4: NSX_HDR(4, 1); break;
-            default: NSX_HDR(5, 1); break;
-        }
+    hipLaunchKernelGGL((ipv4_hdr_dense_kernel<M, R, U>), dim3(grid_d), dim3(kBlock),                               \
+                       (size_t)(R) * (U) * kRow * kWavesPerBlock, st, base, (uint32_t)stride, hdr_off, n, out, mask)
+            switch (rows) {
+                case 1: NSX_HDR(1, 4); break;
+                case 2: NSX_HDR(2, 2); break;
+                case 3: NSX_HDR(3, 1); break;
+                case 4: NSX_HDR(4, 1); break;
+                default: NSX_HDR(5, 1); break;
+            }
 #undef NSX_HDR
+        });
         return hipGetLastError();
     }
-    if (mode == 1) hipLaunchKernelGGL(ipv4_hdr_kernel<1>, dim3(grid), dim3(kBlock), 0, st, base, stride, hdr_off, n, out);
-    else hipLaunchKernelGGL(ipv4_hdr_kernel<0>, dim3(grid), dim3(kBlock), 0, st, base, stride, hdr_off, n, out);
+    by_mode([&](auto m) {
+        constexpr int M = decltype(m)::value;
+        hipLaunchKernelGGL(ipv4_hdr_kernel<M>, dim3(grid), dim3(kBlock), 0, st, base, stride, hdr_off, n, out, mask);
+    });
     return hipGetLastError();
 }
 

@@ -60,6 +60,7 @@ def lib() -> ctypes.CDLL:
             "nsx_shard_plan": [vp, u64, i32, vp],
             "nsx_fill_splitmix64_dev": [vp, u64, u64, u64, vp],
             "nsx_ipv4_hdr_csum_dev": [vp, u64, u32, u64, i32, vp, vp],
+            "nsx_ipv4_hdr_verify_mask_dev": [vp, u64, u32, u64, vp, vp],
             "nsx_tcp_build_dev": [vp, vp, vp, vp, vp, u64, vp, u64, vp, vp, vp, vp],
             "nsx_tcp_layout_host": [vp, vp, u64, vp],
             "nsx_abi_version": [],
@@ -259,6 +260,16 @@ def ipv4_hdr_csum_dev(buf, stride: int, n: int, hdr_off: int = 0, mode: int = 0,
     _check(lib().nsx_ipv4_hdr_csum_dev(_dev_ptr(buf), stride, hdr_off, n, mode, _dev_ptr(out), _stream(stream)),
            "nsx_ipv4_hdr_csum_dev")
     return out
+
+
+def ipv4_hdr_verify_mask_dev(buf, stride: int, n: int, hdr_off: int = 0, mask=None, stream=None):
+    """Fused IPv4 header verify into a bitmask: bit i%64 of mask[i//64] iff header i is valid."""
+    import torch
+    if mask is None:
+        mask = torch.empty((n + 63) // 64, dtype=torch.int64, device=buf.device)  # u64 bits
+    _check(lib().nsx_ipv4_hdr_verify_mask_dev(_dev_ptr(buf), stride, hdr_off, n, _dev_ptr(mask), _stream(stream)),
+           "nsx_ipv4_hdr_verify_mask_dev")
+    return mask
 
 
 class TcpHdrSoA(ctypes.Structure):

@@ -571,6 +571,8 @@ def test_ipv4_packed_headers_past_the_launch_chunk():
         f = O.field_value(O.go_checksum(b"", bytes(h)))
         after = host(t[i * H:(i + 1) * H])
         assert after[10] == f >> 8 and after[11] == f & 0xFF, i
+    mask = host(nsx.ipv4_hdr_verify_mask_dev(t, H, n)).view(np.uint64)  # mask words either side of the split
+    assert (mask[:-1] == np.uint64(0xFFFFFFFFFFFFFFFF)).all() and mask[-1] == np.uint64((1 << (n % 64)) - 1)
 
 
 def test_f1_build_1M_segments_full_size_roundtrip():
@@ -683,6 +685,43 @@ def test_ipv4_header_checksum_verify_and_fill(stride, hdr_off, kernel, nsx_param
     again = u16(nsx.ipv4_hdr_csum_dev(d, stride, n, hdr_off=hdr_off, mode=0))
     valid = np.array([int(ihl[i]) * 4 >= 20 and hdr_off + int(ihl[i]) * 4 <= stride for i in range(n)])
     assert (again[valid] == 0xFFFF).all()
+
+
+def _mask_words(valid):
+    pad = np.zeros((valid.size + 63) // 64 * 64, np.uint8)
+    pad[:valid.size] = valid
+    return np.packbits(pad, bitorder="little").view(np.uint64)
+
+
+@pytest.mark.parametrize("kernel", [0, 1, 2, 3])
+@pytest.mark.parametrize("stride,hdr_off", [(20, 0), (22, 2), (60, 0), (61, 1), (1514, 14)])
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 255, 256, 257, 3001])
+def test_ipv4_header_verify_mask(n, stride, hdr_off, kernel, nsx_param):
+    """nsx_ipv4_hdr_verify_mask_dev: bit i set iff header i is well-formed and sums to
+    0xFFFF — the oracle's go_checksum over the header (RFC 791 §3.1 with tcp.go:72-95's
+    sum) on about half the headers made valid, the rest corrupted or malformed; every
+    mask word written (garbage before), bits past n zero; all four kernels."""
+    nsx_param(nsx.PARAM_KERNEL, kernel)
+    rng = np.random.default_rng(n * 7 + stride)
+    buf, ihl = _ipv4_headers(rng, n, stride, hdr_off)
+    valid = np.zeros(n, bool)
+    for i in range(n):
+        L, b0 = int(ihl[i]) * 4, i * stride + hdr_off
+        if not (L >= 20 and hdr_off + L <= stride):
+            continue
+        if rng.random() < 0.6:  # give it a correct checksum field
+            h = bytearray(buf[b0:b0 + L].tobytes())
+            h[10:12] = b"\0\0"
+            f = O.field_value(O.go_checksum(b"", bytes(h)))
+            buf[b0 + 10], buf[b0 + 11] = f >> 8, f & 0xFF
+        valid[i] = O.go_checksum(b"", buf[b0:b0 + L].tobytes()) == 0xFFFF
+    mask = torch.full(((n + 63) // 64,), 0x5A5A5A5A5A5A5A5A, dtype=torch.int64, device="cuda")
+    nsx.ipv4_hdr_verify_mask_dev(dev(buf), stride, n, hdr_off=hdr_off, mask=mask)
+    got = host(mask).view(np.uint64)
+    assert np.array_equal(got, _mask_words(valid)), (n, stride, kernel)
+    # the same answer as verify-into-raw-sums followed by the f2 mask kernel
+    raw = nsx.ipv4_hdr_csum_dev(dev(buf), stride, n, hdr_off=hdr_off, mode=0)
+    assert np.array_equal(host(nsx.verify_mask_dev(raw)).view(np.uint64), got)
 
 
 @pytest.mark.parametrize("kernel", [0, 1, 2, 3])
