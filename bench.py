@@ -18,7 +18,7 @@ the same bar, each with its own metric string: 6 = the fused sender pass
 (nsx_tcp_build_dev: segment.bytes() + computeChecksum + field write,
 tcp.go:98-128/:68-71) over 1M 1500 B wire images; 7 = IPv4 header checksum
 verify (nsx_ipv4_hdr_csum_dev) over 64M packed 20 B headers; 8 = config 6 with a
-12 B option block per segment (the build kernel's option path; no CPU baseline); 9 =
+12 B option block per segment (the build kernel's option path); 9 =
 workload 7 verified straight into a validity bitmask (nsx_ipv4_hdr_verify_mask_dev).
 
 Printed by rank 0: one JSON line with the contract fields plus
@@ -60,7 +60,7 @@ WORKLOADS = {
             name="f1: 1M option-less TCP segments per GPU, 1480B payload -> 1500B wire images, IPv4 pseudo-header "
                  "partials, device-resident"),
     # not a BASELINE config: f1 with a 12-byte option block per segment (the size of Linux's NOP NOP timestamps
-    # block); no CPU baseline (the oracle's batch sender is option-less)
+    # block)
     8: dict(kind="tcp_build", n=1 << 20, payload=1468, opt=12, seed=0x1076,
             metric="GiB/s fused TCP segment build (serialize + checksum + field write), wire bytes",
             name="f1+options: 1M TCP segments per GPU, 12B options (NOP NOP kind-2 len 10), 1468B payload -> 1500B wire images, "
@@ -247,7 +247,7 @@ def build_workload(cfg, rank, device):
             opt_off = idx * OL
         # per segment: payload + options + 18 B of header fields + 2 (+2) offsets + partial read; wire image + raw
         # sum written
-        w.update(out=raw, wire=out, fields=fields, addrs=addrs, data=data, bytes=n * W,
+        w.update(out=raw, wire=out, fields=fields, addrs=addrs, data=data, opts=opts, bytes=n * W,
                  alg=n * (P + OL + 18 + 8 + 8 + (8 if OL else 0) + 4 + W + 2) + 16 + (8 if OL else 0),
                  step=lambda: nsx.tcp_build_dev(fields, data, data_off, out, out_off, opts=opts, opt_off=opt_off,
                                                 partial=part, raw=raw))
@@ -314,10 +314,8 @@ def cpu_baseline(cfg, w, seconds: float) -> dict:
         desc = f"first {m} segments x {L}B of rank 0's batch, {reps} pass(es), Go-faithful serial loop"
         extra = cpu_extra_lines(lib, sample, S, L, m, out, max(1.0, seconds / 4))
     elif cfg["kind"] == "tcp_build":
-        if cfg.get("opt"):
-            return None  # the oracle's batch sender is option-less
-        n, P = cfg["n"], cfg["payload"]
-        W = P + 20
+        n, P, OL = cfg["n"], cfg["payload"], cfg.get("opt", 0)
+        W = P + 20 + OL
         m = min(n, 65536)  # sample: the first 64K segments (~94 MiB of wire)
         fields = {k: v[:m].cpu().numpy().view(dt) for (k, v), dt in
                   zip(((k, w["fields"][k]) for k in O.TCP_FIELDS), O.TCP_FIELD_DTYPES)}
@@ -328,16 +326,23 @@ def cpu_baseline(cfg, w, seconds: float) -> dict:
         out_off = np.arange(m + 1, dtype=np.uint64) * np.uint64(W)
         gpu = w["out"][:m].cpu().numpy().view(np.uint16)
         gpu_wire = w["wire"][: m * W].cpu().numpy()
+        if OL:
+            opts = w["opts"][: m * OL].cpu().numpy()
+            opt_off = np.arange(m + 1, dtype=np.uint64) * np.uint64(OL)
+            build = lambda: O.c_go_tcp_build_opts(fields, opts, opt_off, data, data_off, out_off, pseudo)
+        else:
+            build = lambda: O.c_go_tcp_build(fields, data, data_off, out_off, pseudo)
         t0, reps = time.perf_counter(), 0
         while True:
-            wire, out = O.c_go_tcp_build(fields, data, data_off, out_off, pseudo)
+            wire, out = build()
             reps += 1
             if time.perf_counter() - t0 >= seconds:
                 break
         dt = time.perf_counter() - t0
         nbytes = reps * m * W
-        desc = (f"first {m} segments of rank 0's batch, {reps} pass(es), Go-faithful sender loop: bytes() + "
-                "computeChecksum(12B pseudo-header) + field store per segment")
+        desc = (f"first {m} segments of rank 0's batch, {reps} pass(es), Go-faithful sender loop: bytes()"
+                f"{' with ' + str(OL) + ' B of options' if OL else ''} + computeChecksum(12B pseudo-header) + "
+                "field store per segment")
         wire_ok = bool(np.array_equal(wire, gpu_wire))
     elif cfg["kind"] == "ipv4_hdr":
         n, H = cfg["n"], cfg["hdr"]

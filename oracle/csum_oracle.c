@@ -254,6 +254,66 @@ ORACLE_EXPORT int oracle_go_tcp_build_batch(const uint16_t* src_port, const uint
     return 0;
 }
 
+/* The same sender loop for segments with options, the options of segment i given
+ * as their serialization opts[opt_off[i], opt_off[i+1]) (what a caller's
+ * []option renders to, tcp.go:225-231). The span is read back into option units
+ * (a byte 2 starts a kind-2 option: its next byte is the length and the rest of
+ * the span its data; any other byte is a one-byte option), so the segment goes
+ * through oracle_segment_bytes — tcp.go:113-123's loop and its `remainder`
+ * padding — like a Go segment with that []option. Returns -1 for a span ending
+ * in a lone 2 (no []option serialises to it) or a failed allocation. */
+ORACLE_EXPORT int oracle_go_tcp_build_batch_opts(const uint16_t* src_port, const uint16_t* dst_port,
+                                                 const uint32_t* seq_num, const uint32_t* ack_num,
+                                                 const uint8_t* offset, const uint8_t* control,
+                                                 const uint16_t* window, const uint16_t* urgent_ptr,
+                                                 const uint8_t* opts, const uint64_t* opt_off,
+                                                 const uint8_t* data, const uint64_t* data_off,
+                                                 const uint8_t* pseudo, size_t pseudo_len, uint64_t n,
+                                                 uint8_t* out, const uint64_t* out_off, uint16_t* raw) {
+    for (uint64_t i = 0; i < n; i++) {
+        const uint8_t* ob = opts + opt_off[i];
+        const size_t olen = (size_t)(opt_off[i + 1] - opt_off[i]);
+        oracle_option* ol = (oracle_option*)malloc((olen ? olen : 1) * sizeof(oracle_option));
+        if (!ol) return -1;
+        size_t no = 0;
+        for (size_t p = 0; p < olen;) {
+            if (ob[p] == 2) {
+                if (p + 1 >= olen) { free(ol); return -1; }
+                ol[no].kind = 2; ol[no].length = ob[p + 1];
+                ol[no].data = ob + p + 2; ol[no].data_len = olen - p - 2;
+                no++;
+                break;
+            }
+            ol[no].kind = ob[p]; ol[no].length = 0; ol[no].data = NULL; ol[no].data_len = 0;
+            no++;
+            p++;
+        }
+        oracle_segment s;
+        memset(&s, 0, sizeof s);
+        s.src_port = src_port[i]; s.dst_port = dst_port[i];
+        s.seq_num = seq_num[i]; s.ack_num = ack_num[i];
+        s.offset = offset[i]; s.control = control[i];
+        s.window = window[i]; s.urgent_ptr = urgent_ptr[i];
+        s.options = ol; s.n_options = no;
+        s.data = data + data_off[i];
+        s.data_len = (size_t)(data_off[i + 1] - data_off[i]);
+        const size_t len = oracle_segment_bytes(&s, NULL, 0);
+        uint8_t* b = (uint8_t*)malloc(len ? len : 1);
+        if (!b) { free(ol); return -1; }
+        oracle_segment_bytes(&s, b, len);
+        free(ol);
+        const uint32_t sum = oracle_go_checksum(pseudo ? pseudo + i * pseudo_len : NULL, pseudo ? pseudo_len : 0, b, len);
+        if (sum > 0xFFFFu) { free(b); return -1; }
+        const uint16_t f = (uint16_t)~sum;
+        b[16] = (uint8_t)(f >> 8);
+        b[17] = (uint8_t)f;
+        memcpy(out + out_off[i], b, len);
+        free(b);
+        if (raw) raw[i] = (uint16_t)sum;
+    }
+    return 0;
+}
+
 /* ---- synthetic data: splitmix64 stream, counter-based ---- */
 static inline uint64_t splitmix64_at(uint64_t seed, uint64_t i) {
     uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;

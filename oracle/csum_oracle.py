@@ -248,6 +248,9 @@ def c_oracle():
         lib.oracle_splitmix64_fill.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]
         lib.oracle_go_tcp_build_batch.argtypes = [u8p] * 10 + [u8p, ctypes.c_size_t, ctypes.c_uint64, u8p, u8p, u8p]
         lib.oracle_go_tcp_build_batch.restype = ctypes.c_int
+        lib.oracle_go_tcp_build_batch_opts.argtypes = ([u8p] * 12 + [u8p, ctypes.c_size_t, ctypes.c_uint64, u8p, u8p,
+                                                                    u8p])
+        lib.oracle_go_tcp_build_batch_opts.restype = ctypes.c_int
         _c = lib
     return _c
 
@@ -297,6 +300,28 @@ def c_go_tcp_build(fields: dict, data: np.ndarray, data_off: np.ndarray, out_off
     ps = None if pseudo is None else np.ascontiguousarray(pseudo, np.uint8)
     rc = c_oracle().oracle_go_tcp_build_batch(*[_ptr(c) for c in cols], _ptr(data), _ptr(data_off), _ptr(ps), pl, n,
                                               _ptr(out), _ptr(out_off), _ptr(raw))
+    assert rc == 0
+    return out, raw
+
+
+def c_go_tcp_build_opts(fields: dict, opts: np.ndarray, opt_off: np.ndarray, data: np.ndarray,
+                        data_off: np.ndarray, out_off: np.ndarray, pseudo: np.ndarray | None = None):
+    """c_go_tcp_build for segments with options given as their serialisation
+    (oracle_go_tcp_build_batch_opts). Returns (wire, raw)."""
+    n = data_off.size - 1
+    cols = [np.ascontiguousarray(fields[k], dt) for k, dt in zip(TCP_FIELDS, TCP_FIELD_DTYPES)]
+    opts = np.ascontiguousarray(opts, np.uint8) if len(opts) else np.zeros(1, np.uint8)
+    opt_off = np.ascontiguousarray(opt_off, np.uint64)
+    data = np.ascontiguousarray(data, np.uint8)
+    data_off = np.ascontiguousarray(data_off, np.uint64)
+    out_off = np.ascontiguousarray(out_off, np.uint64)
+    out = np.zeros(int(out_off[-1]), np.uint8)
+    raw = np.empty(n, np.uint16)
+    pl = 0 if pseudo is None else pseudo.shape[1]
+    ps = None if pseudo is None else np.ascontiguousarray(pseudo, np.uint8)
+    rc = c_oracle().oracle_go_tcp_build_batch_opts(*[_ptr(c) for c in cols], _ptr(opts), _ptr(opt_off), _ptr(data),
+                                                   _ptr(data_off), _ptr(ps), pl, n, _ptr(out), _ptr(out_off),
+                                                   _ptr(raw))
     assert rc == 0
     return out, raw
 

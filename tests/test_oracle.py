@@ -184,6 +184,52 @@ def test_c_go_tcp_build_matches_segment_model():
         assert wire[int(out_off[i]):int(out_off[i + 1])].tobytes() == s.bytes()
 
 
+def test_c_go_tcp_build_opts_matches_segment_model():
+    """The C sender loop for segments with options (bench cpu_baseline / checker for
+    workload 8) agrees with the Python Segment model, including the reference's
+    `remainder` option padding (tcp.go:118-121), for option lists of every kind."""
+    rng = np.random.default_rng(607)
+    n = 200
+    rb = lambda k: rng.integers(0, 256, k, dtype=np.uint8).tobytes()
+    sets = [lambda: [], lambda: [O.Option(kind=1)], lambda: [O.Option(kind=1)] * 3,
+            lambda: [O.Option(kind=1), O.Option(kind=1), O.Option(kind=2, length=10, data=rb(8))],
+            lambda: [O.Option(kind=2, length=4, data=rb(2)), O.Option(kind=0)],
+            lambda: [O.Option(kind=2, length=200, data=rb(int(rng.integers(0, 60))))]]
+    segs = []
+    for i in range(n):
+        sg = O.Segment(src_port=int(rng.integers(1 << 16)), dst_port=int(rng.integers(1 << 16)),
+                       seq_num=int(rng.integers(1 << 32)), ack_num=int(rng.integers(1 << 32)),
+                       control=O.Ctl.from_byte(int(rng.integers(256))), window=int(rng.integers(1 << 16)),
+                       urgent_ptr=int(rng.integers(1 << 16)), options=sets[i % len(sets)](),
+                       data=rb(int(rng.integers(0, 1600))))
+        sg.offset = sg.compute_offset() & 0xFF
+        segs.append(sg)
+    ob = [b"".join(o.bytes() for o in sg.options) for sg in segs]
+    opts = np.frombuffer(b"".join(ob), np.uint8)
+    opt_off = np.zeros(n + 1, np.uint64)
+    opt_off[1:] = np.cumsum([len(b) for b in ob])
+    data = np.frombuffer(b"".join(sg.data for sg in segs) + b"\0", np.uint8)
+    data_off = np.zeros(n + 1, np.uint64)
+    data_off[1:] = np.cumsum([len(sg.data) for sg in segs])
+    out_off = np.zeros(n + 1, np.uint64)
+    out_off[1:] = np.cumsum([len(sg.bytes()) for sg in segs])
+    pseudo = rng.integers(0, 256, (n, 12), dtype=np.uint8)
+    fields = {"src_port": np.array([sg.src_port for sg in segs], np.uint16),
+              "dst_port": np.array([sg.dst_port for sg in segs], np.uint16),
+              "seq_num": np.array([sg.seq_num for sg in segs], np.uint32),
+              "ack_num": np.array([sg.ack_num for sg in segs], np.uint32),
+              "offset": np.array([sg.offset for sg in segs], np.uint8),
+              "control": np.array([sg.control.byte() for sg in segs], np.uint8),
+              "window": np.array([sg.window for sg in segs], np.uint16),
+              "urgent_ptr": np.array([sg.urgent_ptr for sg in segs], np.uint16)}
+    wire, raw = O.c_go_tcp_build_opts(fields, opts, opt_off, data, data_off, out_off, pseudo)
+    for i, sg in enumerate(segs):
+        r = sg.compute_checksum(pseudo[i].tobytes())
+        assert raw[i] == r, i
+        sg.checksum = O.field_value(r)
+        assert wire[int(out_off[i]):int(out_off[i + 1])].tobytes() == sg.bytes(), i
+
+
 def test_cpu_fast_line_matches_go_checksum():
     """The best-CPU reference line (bench extras) computes the reference's sums."""
     rng = np.random.default_rng(707)

@@ -49,6 +49,10 @@ def variants(kind):
     if kind == "tcp_build":  # cache policy (nontemporal knob) x grid
         return ([dict(blocks_per_cu=b, segs_per_wave=ps) for b in (1, 2, 4) for ps in (1, 2)] +
                 [dict(blocks_per_cu=b, kernel=2) for b in (4, 8)])
+    if kind == "swp_big":  # config 5: the default software-pipelined kernel at more blocks / other depths
+        return [dict(kernel=5, blocks_per_cu=b, segs_per_wave=u, nontemporal=1) for b in (1, 2, 3) for u in (4, 8)] + \
+               [dict(kernel=5, blocks_per_cu=1, segs_per_wave=8, nontemporal=1, xcd_chunk=c) for c in (8, 12, 16)] + \
+               [dict(kernel=5, blocks_per_cu=1, segs_per_wave=8, nontemporal=0)]
     if kind == "ragged_deep":  # deeper in-flight windows: 16-row batches, pipelined, 1-2 blocks/CU
         return ([dict(kernel=4, blocks_per_cu=2, stream_rows=8, nontemporal=1, xcd_map=4, run_segs=63)] +
                 [dict(kernel=k, blocks_per_cu=b, stream_rows=r, nontemporal=1, xcd_map=4, run_segs=63)
