@@ -116,6 +116,18 @@ int main() {
     const uint64_t n16 = fb / 16 - 64;
     for (int k = 0; k < 50; ++k) hipLaunchKernelGGL(flat_mis, dim3(cus * 4), dim3(256), 0, 0, src, dst, n16, 0u, 0u);
     (void)hipDeviceSynchronize();
+    // which side's misalignment costs: flat copies with only the source, only the destination, or both 4 B off
+    for (int bpc : {2, 4}) {
+        const int g = cus * bpc;
+        const double ab = 2.0 * n16 * 16;
+        for (uint32_t so : {0u, 4u}) {
+            for (uint32_t dof : {0u, 12u}) {
+                const float t = timeit([&] { hipLaunchKernelGGL(flat_mis, dim3(g), dim3(256), 0, 0, src, dst, n16, so, dof); });
+                printf("bpc=%d flat src+%u dst+%u %.4f ms %.0f GB/s\n", bpc, so, dof, t, ab / t / 1e6);
+            }
+        }
+    }
+    fflush(stdout);
     for (int bpc : {1, 2, 4, 8}) {
         const int g = cus * bpc;
         const float a = timeit([&] { hipLaunchKernelGGL(flat_mis, dim3(g), dim3(256), 0, 0, src, dst, n16, 0u, 0u); });
