@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPU evidence pass, part 1: parity tests, smoke, bench lines for configs 2-7,
+# GPU evidence pass, part 1: parity tests, smoke, bench lines for configs 2-9,
 # end-to-end host rate, config-1 loopback. Part 2 (profiles) is
 # tools/gpu_profiles.sh. Every GPU step has its own limit; a timeout/crash
 # (rc >= 124) ends the script.
@@ -26,6 +26,8 @@ step bench_c4 300 python bench.py --config 4 --steps 50 --cpu-seconds 5
 step bench_c5 300 python bench.py --config 5 --steps 20 --cpu-seconds 0
 step bench_c6 300 python bench.py --config 6 --steps 100 --cpu-seconds 5
 step bench_c7 300 python bench.py --config 7 --steps 100 --cpu-seconds 5
+step bench_c8 300 python bench.py --config 8 --steps 100 --cpu-seconds 5
+step bench_c9 300 python bench.py --config 9 --steps 100 --cpu-seconds 5
 step e2e_host 600 python tools/e2e_host.py
 rm -f gpurun_out/loopback.jsonl
 for m in host batch ring-host ring-gpu; do
