@@ -152,6 +152,7 @@ def test_device_calls_fail_loudly_without_gpu():
     assert L.nsx_verify_mask_dev(fake, 4, fake, None) == nsx.NSX_ENODEV
     assert L.nsx_fill_splitmix64_dev(fake, 0, 16, 1, None) == nsx.NSX_ENODEV
     assert L.nsx_ipv4_hdr_csum_dev(fake, 64, 0, 4, 0, fake, None) == nsx.NSX_ENODEV
+    assert L.nsx_ipv4_hdr_verify_mask_dev(fake, 20, 0, 4, fake, None) == nsx.NSX_ENODEV
     soa = nsx.TcpHdrSoA(*([0x1000] * 8))
     assert L.nsx_tcp_build_dev(ctypes.byref(soa), None, None, fake, fake, 16, None, 4, fake, fake, None,
                                None) == nsx.NSX_ENODEV
@@ -174,6 +175,9 @@ def test_device_calls_validate_before_device():
     assert L.nsx_csum_fixed_dev(fake, 1500, 1500, 4, None, None, None) == nsx.NSX_EINVAL
     assert L.nsx_csum_ragged_dev(fake, None, 4, None, fake, None) == nsx.NSX_EINVAL
     assert L.nsx_verify_mask_dev(None, 4, fake, None) == nsx.NSX_EINVAL
+    assert L.nsx_ipv4_hdr_verify_mask_dev(None, 20, 0, 4, fake, None) == nsx.NSX_EINVAL
+    assert L.nsx_ipv4_hdr_verify_mask_dev(fake, 20, 0, 4, None, None) == nsx.NSX_EINVAL
+    assert L.nsx_ipv4_hdr_verify_mask_dev(fake, 0, 0, 4, fake, None) == nsx.NSX_EINVAL
     assert L.nsx_verify_mask_dev(fake, 0, None, None) == 0
     assert L.nsx_pseudo_ipv6_partial_dev(fake, None, fake, 6, 4, fake, None) == nsx.NSX_EINVAL
     bad = np.array([0, 10, 5], np.uint64)
