@@ -5,10 +5,13 @@
 //   slices : wave w reads rows [w*R/W, (w+1)*R/W) in order (the ragged kernel's byte-balanced ranges)
 //   window : batch b of wave w is batch b*W + w (every wave within one W-batch window of the others)
 //   rounds : K rounds; in round k wave w reads the w-th of W slices of the k-th of K equal parts
+//   chunks : the product kernels' XCD chunk deal — chunks of 2^K batches, XCD x takes chunks x, x+8, ...,
+//            its waves walk their chunks' batches in order (K passed as the chunk log2)
 // Grid: 1 and 2 blocks of 4 waves per CU.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include <algorithm>
 #include <vector>
@@ -42,6 +45,9 @@ __global__ __launch_bounds__(256) void stream(const uint8_t* p, uint64_t nrows, 
         cnt = nbatch * (w + 1) / W - b0;
     } else if (MODE == 1) {
         cnt = w < nbatch ? (nbatch - w + W - 1) / W : 0;
+    } else if (MODE == 3) {
+        // local index i = slot*4 + wave + k*per_x over the XCD's chunks; counted by walking (cheap: exit test)
+        cnt = 0xFFFFFFFFull;
     } else {
         per = nbatch / K;  // batches per part (the tail part takes the remainder)
         cnt = 0;
@@ -59,7 +65,13 @@ __global__ __launch_bounds__(256) void stream(const uint8_t* p, uint64_t nrows, 
         e = pb + pn * (w + 1) / W;
     };
     if (MODE == 2) part_range(0, kpos, kend);
+    const uint32_t cx = b & 7, cslot = b >> 3, cper = (nb >> 3) * 4;
+    auto chunk_task = [&](uint64_t i) -> uint64_t {
+        const uint64_t li = (uint64_t)cslot * 4 + (threadIdx.x >> 6) + i * cper;
+        return ((((li >> K) << 3) + cx) << K) | (li & ((1ull << K) - 1));
+    };
     auto next_batch = [&](uint64_t i) -> uint64_t {
+        if (MODE == 3) return chunk_task(i);
         if (MODE == 0) return b0 + i;
         if (MODE == 1) return i * W + w;
         while (kpos >= kend && k + 1 < K) part_range(++k, kpos, kend);
@@ -68,6 +80,15 @@ __global__ __launch_bounds__(256) void stream(const uint8_t* p, uint64_t nrows, 
     uint32_t acc = 0;
     v4u A[kB], B[kB];
     uint64_t i = 0;
+    if (MODE == 3) {  // chunks: the sequence ends at the first batch past the end (tasks increase with i)
+        uint64_t lo = 0, hi = 1;
+        while (chunk_task(hi) < nbatch) hi <<= 1;
+        while (lo < hi) {  // first i with chunk_task(i) >= nbatch
+            const uint64_t mid = (lo + hi) / 2;
+            if (chunk_task(mid) < nbatch) lo = mid + 1; else hi = mid;
+        }
+        cnt = lo;
+    }
     if (cnt) ld_batch(p, next_batch(0) * kB, nrows, lane, A);
     while (i < cnt) {
         const bool hb = i + 1 < cnt;
@@ -107,8 +128,8 @@ float timeit(F f) {
     return t[2];
 }
 
-int main() {
-    const uint64_t bytes = 4752000000ull;  // config 3's volume
+int main(int argc, char** argv) {
+    const uint64_t bytes = argc > 1 ? strtoull(argv[1], nullptr, 10) : 4752000000ull;  // default: config 3's volume
     const uint64_t nrows = bytes / 1024;
     int cus = 0;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
@@ -128,6 +149,10 @@ int main() {
             for (uint32_t K : {4u, 16u, 64u}) {
                 const float r = timeit([&] { hipLaunchKernelGGL((stream<2>), dim3(g), dim3(256), 0, 0, buf, nrows, K, out); });
                 printf(" | rounds K=%u %.4f ms %.0f GB/s", K, r, gbs(r));
+            }
+            for (uint32_t K : {8u, 11u, 14u}) {
+                const float r = timeit([&] { hipLaunchKernelGGL((stream<3>), dim3(g), dim3(256), 0, 0, buf, nrows, K, out); });
+                printf(" | chunks 2^%u %.4f ms %.0f GB/s", K, r, gbs(r));
             }
             printf("\n");
             fflush(stdout);
