@@ -119,7 +119,8 @@ class Dist:
         if not self.on:
             return x
         import torch
-        t = torch.tensor([x], dtype=torch.float64, device=device if device is not None else "cpu")
+        on_dev = device is not None and self.dist.get_backend() == "nccl"
+        t = torch.tensor([x], dtype=torch.float64, device=device if on_dev else "cpu")
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -127,7 +128,8 @@ class Dist:
         if not self.on:
             return x
         import torch
-        t = torch.tensor([x], dtype=torch.float64, device=device if device is not None else "cpu")
+        on_dev = device is not None and self.dist.get_backend() == "nccl"
+        t = torch.tensor([x], dtype=torch.float64, device=device if on_dev else "cpu")
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
         return float(t.item())
 
@@ -448,12 +450,14 @@ def main(argv=None):
     args = parse_args(argv)
     import torch
     import nsx
-    dist = Dist("nccl")
+    # RCCL ("nccl") is the backend; NSX_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share a device
+    # round-robin), e.g. 2 ranks on a 1-GPU box
+    dist = Dist(os.environ.get("NSX_BENCH_BACKEND", "nccl"))
     if dist.world != args.gpus and dist.on:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {dist.world}; using WORLD_SIZE", file=sys.stderr)
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU: the checksum path is HIP-only (no CPU fallback)")
-    dev_id = dist.local_rank if dist.on else 0
+    dev_id = dist.local_rank % max(1, torch.cuda.device_count()) if dist.on else 0
     torch.cuda.set_device(dev_id)
     device = torch.device("cuda", dev_id)
     for kv in args.param:
