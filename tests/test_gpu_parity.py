@@ -985,3 +985,90 @@ def test_tcp_build_matches_reference_bytes_and_checksum(lead, align4):
         assert got[o:o + len(wire)].tobytes() == wire, i
         assert not got[o + len(wire):int(out_off[i + 1])].any()   # slack zero-filled
         assert O.verify(O.go_checksum(pseudos[i], wire))          # receiver accepts (tcp.go:70)
+
+
+# ------------------------------------------------------------------ re-entrancy (include/nsx_csum.h "Threading")
+
+def test_concurrent_calls_from_threads_on_separate_streams():
+    """Four host threads, each on its own HIP stream, call different device entry points
+    (fixed, ragged, TCP build with options, IPv4 verify-into-mask) 25 times each while two
+    more threads run host-resident batches; ctypes drops the GIL for every C call, so the
+    library runs them concurrently. Every result equals its single-threaded reference."""
+    import threading
+    rng = np.random.default_rng(0xC0C0)
+    # fixed
+    nf, L = 20000, 1500
+    fb = dev(rng.integers(0, 256, nf * L, dtype=np.uint8))
+    ref_f = u16(nsx.fixed_dev(fb, L, L, nf))
+    # ragged
+    lens = rng.integers(0, 9000, 5000).astype(np.uint64)
+    offs = np.zeros(lens.size + 1, np.uint64)
+    offs[1:] = np.cumsum(lens)
+    rbh = rng.integers(0, 256, int(offs[-1]) + 1, dtype=np.uint8)
+    rb, ro = dev(rbh), dev(offs.view(np.int64))
+    ref_r = u16(nsx.ragged_dev(rb, ro))
+    # TCP build with 12 B options
+    n, P, OL = 3000, 1468, 12
+    fields, data, data_off, out_off, _ = _uniform_build_case(rng, n, P, 64, pseudo=False)
+    fields["offset"][:] = 8
+    opts = rng.integers(0, 256, n * OL, dtype=np.uint8)
+    opt_off = np.arange(n + 1, dtype=np.uint64) * np.uint64(OL)
+    out_off = nsx.tcp_layout_host(data_off, opt_off)
+    dt = {np.uint16: np.int16, np.uint32: np.int32, np.uint8: np.uint8}
+    fd = {k: dev(v.view(dt[v.dtype.type])) for k, v in fields.items()}
+    dd, do, oo, od, oof = dev(data), dev(data_off.view(np.int64)), dev(out_off.view(np.int64)), dev(opts), \
+        dev(opt_off.view(np.int64))
+
+    def build(stream=None):
+        out = torch.zeros(int(out_off[-1]), dtype=torch.uint8, device="cuda")
+        raw = torch.empty(n, dtype=torch.int16, device="cuda")
+        nsx.tcp_build_dev(fd, dd, do, out, oo, opts=od, opt_off=oof, raw=raw, stream=stream)
+        return out, raw
+    ref_b = [host(t) for t in build()]
+    # IPv4 headers into a mask
+    nh = 100_000
+    hb = rng.integers(0, 256, nh * 20, dtype=np.uint8)
+    hb[::20] = 0x45
+    hd = dev(hb)
+    nsx.ipv4_hdr_csum_dev(hd, 20, nh, mode=1)
+    hd.view(nh, 20)[::7, 9] ^= 1
+    ref_m = host(nsx.ipv4_hdr_verify_mask_dev(hd, 20, nh))
+    # host-resident fixed batch
+    hh = rng.integers(0, 256, 4000 * L, dtype=np.uint8)
+    ref_h = O.c_batch(hh, 4000, stride=L, seg_len=L)
+
+    errors = []
+
+    def worker(kind):
+        try:
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                for _ in range(25):
+                    if kind == "fixed":
+                        got = nsx.fixed_dev(fb, L, L, nf, stream=s)
+                        s.synchronize()
+                        assert np.array_equal(host(got).view(np.uint16), ref_f)
+                    elif kind == "ragged":
+                        got = nsx.ragged_dev(rb, ro, stream=s)
+                        s.synchronize()
+                        assert np.array_equal(host(got).view(np.uint16), ref_r)
+                    elif kind == "build":
+                        out, raw = build(stream=s)
+                        s.synchronize()
+                        assert np.array_equal(host(out), ref_b[0]) and np.array_equal(host(raw), ref_b[1])
+                    elif kind == "mask":
+                        got = nsx.ipv4_hdr_verify_mask_dev(hd, 20, nh, stream=s)
+                        s.synchronize()
+                        assert np.array_equal(host(got), ref_m)
+                    else:
+                        assert np.array_equal(nsx.fixed_host(hh, L, L, 4000), ref_h)
+        except Exception as e:  # surfaced below
+            errors.append((kind, repr(e)))
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in ("fixed", "ragged", "build", "mask", "host", "host")]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=240)
+    assert not any(t.is_alive() for t in ts)
+    assert not errors, errors
