@@ -1072,3 +1072,51 @@ def test_concurrent_calls_from_threads_on_separate_streams():
         t.join(timeout=240)
     assert not any(t.is_alive() for t in ts)
     assert not errors, errors
+
+
+def test_entry_points_capture_into_a_hip_graph():
+    """The device entry points are plain stream-ordered launches, so a transport can
+    capture a receive/send step into a HIP graph (torch.cuda.CUDAGraph) and replay it:
+    replays over new bytes in the same buffers give the oracle's results."""
+    rng = np.random.default_rng(0x6A)
+    n, L = 4096, 1500
+    buf = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    lens = rng.integers(0, 4000, 1000).astype(np.uint64)
+    offs = np.zeros(lens.size + 1, np.uint64)
+    offs[1:] = np.cumsum(lens)
+    rb = torch.empty(int(offs[-1]), dtype=torch.uint8, device="cuda")
+    ro = dev(offs.view(np.int64))
+    nh = 50_000
+    hb = torch.empty(nh * 20, dtype=torch.uint8, device="cuda")
+    out_f = torch.empty(n, dtype=torch.int16, device="cuda")
+    out_r = torch.empty(lens.size, dtype=torch.int16, device="cuda")
+    mask = torch.empty((nh + 63) // 64, dtype=torch.int64, device="cuda")
+    nsx.fixed_dev(buf, L, L, n, out=out_f)  # first calls outside capture (library and device-info setup)
+    nsx.ragged_dev(rb, ro, out=out_r)
+    nsx.ipv4_hdr_verify_mask_dev(hb, 20, nh, mask=mask)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        nsx.fixed_dev(buf, L, L, n, out=out_f)
+        nsx.ragged_dev(rb, ro, out=out_r)
+        nsx.ipv4_hdr_verify_mask_dev(hb, 20, nh, mask=mask)
+    for rep in range(3):
+        fb = rng.integers(0, 256, n * L, dtype=np.uint8)
+        rbh = rng.integers(0, 256, int(offs[-1]), dtype=np.uint8)
+        hh = rng.integers(0, 256, nh * 20, dtype=np.uint8)
+        hh[::20] = 0x45
+        buf.copy_(torch.from_numpy(fb))
+        rb.copy_(torch.from_numpy(rbh))
+        hb.copy_(torch.from_numpy(hh))
+        nsx.ipv4_hdr_csum_dev(hb, 20, nh, mode=1)  # valid checksums, then break every 5th header
+        hb.view(nh, 20)[::5, 8] ^= 0x10
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(u16(out_f), O.c_batch(fb, n, stride=L, seg_len=L)), rep
+        assert np.array_equal(u16(out_r), O.c_batch(rbh, lens.size, offsets=offs)), rep
+        valid = np.ones(nh, bool)
+        valid[::5] = False
+        assert np.array_equal(host(mask).view(np.uint64), _mask_words(valid)), rep
