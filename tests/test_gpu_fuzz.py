@@ -1,13 +1,17 @@
 """Randomised GPU parity (seeded, bounded to a few seconds): every device entry
 point on batches whose sizes, alignments, lengths and kernel knobs are drawn at
 random, against the CPU oracle. Complements the hand-picked edge cases of
-test_gpu_parity.py with combinations nobody wrote down."""
+test_gpu_parity.py with combinations nobody wrote down. NSX_FUZZ_SCALE=k runs k times
+as many cases (new seeds; the default set is the first of them)."""
+import os
+
 import numpy as np
 import pytest
 
 from oracle import csum_oracle as O
 
 pytestmark = pytest.mark.gpu
+SCALE = max(1, int(os.environ.get("NSX_FUZZ_SCALE", "1")))
 
 torch = pytest.importorskip("torch")
 
@@ -42,7 +46,7 @@ def _u16(t):
     return t.cpu().numpy().view(np.uint16)
 
 
-@pytest.mark.parametrize("case", range(120))
+@pytest.mark.parametrize("case", range(120 * SCALE))
 def test_fuzz_fixed(case):
     rng = np.random.default_rng(1000 + case)
     seg_len = int(rng.choice([int(rng.integers(0, 64)), int(rng.integers(64, 4200)), int(rng.integers(4200, 70000))]))
@@ -62,7 +66,7 @@ def test_fuzz_fixed(case):
     assert np.array_equal(got, want), (case, knobs, seg_len, stride, n, lead)
 
 
-@pytest.mark.parametrize("case", range(90))
+@pytest.mark.parametrize("case", range(90 * SCALE))
 def test_fuzz_ragged(case):
     rng = np.random.default_rng(2000 + case)
     n = int(rng.integers(1, 30000))
@@ -87,7 +91,7 @@ def test_fuzz_ragged(case):
     assert np.array_equal(okv, want == 0xFFFF), (case, knobs)
 
 
-@pytest.mark.parametrize("case", range(60))
+@pytest.mark.parametrize("case", range(60 * SCALE))
 def test_fuzz_ipv4_headers(case):
     rng = np.random.default_rng(3000 + case)
     stride = int(rng.choice([20, 20, 24, 28, 40, 60, 64, int(rng.integers(20, 200)), 1514]))
@@ -107,7 +111,7 @@ def test_fuzz_ipv4_headers(case):
         assert got[i] == (O.c_fold_checksum(b"", buf[b0:b0 + L].tobytes()) if ok else 0), (case, stride, hdr_off, i)
 
 
-@pytest.mark.parametrize("case", range(40))
+@pytest.mark.parametrize("case", range(40 * SCALE))
 def test_fuzz_tcp_build(case):
     rng = np.random.default_rng(4000 + case)
     n = int(rng.integers(1, 3000))
@@ -139,7 +143,7 @@ def test_fuzz_tcp_build(case):
     assert np.array_equal(out.cpu().numpy(), want), (case, n, P, lead)
 
 
-@pytest.mark.parametrize("case", range(30))
+@pytest.mark.parametrize("case", range(30 * SCALE))
 def test_fuzz_tcp_build_options(case):
     """Random option lists per segment (1-byte kinds and kind-2 options with random
     lengths, tcp.go:225-231), mostly ≤ 40 bytes (group-staged in the kernel), some
