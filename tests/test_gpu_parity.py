@@ -1120,3 +1120,38 @@ def test_entry_points_capture_into_a_hip_graph():
         valid = np.ones(nh, bool)
         valid[::5] = False
         assert np.array_equal(host(mask).view(np.uint64), _mask_words(valid)), rep
+
+
+def test_f1_options_build_1M_segments_full_size_roundtrip():
+    """The bench's workload 8 at full size (1M images with 12 B of options each): every
+    image passes the receiver check (sum over pseudo ‖ image == 0xFFFF, computed by the
+    fixed-stride kernel), the reported raw sums equal an independent re-sum of the images
+    with the field zeroed, and sampled images match the options oracle byte for byte."""
+    import bench
+    cfg = bench.WORKLOADS[8]
+    w = bench.build_workload(cfg, 0, torch.device("cuda", 0))
+    w["step"]()
+    n, P, OL = cfg["n"], cfg["payload"], cfg["opt"]
+    W = P + 20 + OL
+    raw = u16(w["out"])
+    wire = w["wire"]
+    part = nsx.pseudo_ipv4_partial_dev(w["addrs"][0].reshape(-1), w["addrs"][1].reshape(-1),
+                                       torch.full((n,), W, dtype=torch.int32, device="cuda"), 6)
+    assert (u16(nsx.fixed_dev(wire, W, W, n, partial=part)) == 0xFFFF).all()
+    img = host(wire)
+    wire.view(n, W)[:, 16:18] = 0
+    assert np.array_equal(u16(nsx.fixed_dev(wire, W, W, n, partial=part)), raw)
+    sel = np.arange(0, n, 32771)
+    fields = {k: host(w["fields"][k]).view(dt)[sel] for k, dt in zip(O.TCP_FIELDS, O.TCP_FIELD_DTYPES)}
+    data, opts, addrs = host(w["data"]), host(w["opts"]), host(w["addrs"])
+    sdata = np.concatenate([data[i * P:(i + 1) * P] for i in sel])
+    sopts = np.concatenate([opts[i * OL:(i + 1) * OL] for i in sel])
+    d_off = np.arange(sel.size + 1, dtype=np.uint64) * np.uint64(P)
+    o_off = np.arange(sel.size + 1, dtype=np.uint64) * np.uint64(OL)
+    w_off = np.arange(sel.size + 1, dtype=np.uint64) * np.uint64(W)
+    pseudo = np.stack([np.concatenate([addrs[0, i], addrs[1, i], np.array([0, 6, W >> 8, W & 0xFF], np.uint8)])
+                       for i in sel])
+    want, wraw = O.c_go_tcp_build_opts(fields, sopts, o_off, sdata, d_off, w_off, pseudo)
+    for j, i in enumerate(sel):
+        assert img[i * W:(i + 1) * W].tobytes() == want[j * W:(j + 1) * W].tobytes(), i
+        assert raw[i] == wraw[j], i
