@@ -1155,3 +1155,16 @@ def test_f1_options_build_1M_segments_full_size_roundtrip():
     for j, i in enumerate(sel):
         assert img[i * W:(i + 1) * W].tobytes() == want[j * W:(j + 1) * W].tobytes(), i
         assert raw[i] == wraw[j], i
+
+
+def test_f3_mask_64M_headers_full_size():
+    """The bench's workload 9 at full size: every header's checksum was filled, then every
+    1000th header's TTL flipped; the mask has exactly those bits clear."""
+    import bench
+    cfg = bench.WORKLOADS[9]
+    w = bench.build_workload(cfg, 0, torch.device("cuda", 0))
+    w["step"]()
+    n = cfg["n"]
+    valid = np.ones(n, bool)
+    valid[::1000] = False
+    assert np.array_equal(host(w["out"]).view(np.uint64), _mask_words(valid))
