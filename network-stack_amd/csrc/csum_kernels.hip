@@ -1389,7 +1389,7 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
         // in flight through its own header/sum/store phases (tools/probes/copy_layout.hip seg_swp vs seg).
         const bool mfast = (mhdr & 3u) == 0 && (mdb & 3u) == 0 && mdb >= mhdr && (mwire & 3u) == 0 &&
                            mwire <= 2u * kRow;
-        if (pipe && (!OPT || staged) && __builtin_amdgcn_ballot_w64(!(mfast || lane >= cnt)) == 0) {
+        if (pipe == 1 && (!OPT || staged) && __builtin_amdgcn_ballot_w64(!(mfast || lane >= cnt)) == 0) {
             struct Rows {
                 u32x4 v[PS][2];
             };
@@ -1445,6 +1445,62 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
                 if (kk + PS >= cnt) break;
                 fload(kk + 2u * PS, A);
                 fdone(kk + PS, B);
+            }
+            continue;
+        }
+        // Any payload alignment, any header length, images ≤ 2 rows, at least hdr_end bytes of the data array
+        // before the payload: the same pipelining over the general composition. Image byte p comes from
+        // data + db - hdr_end + p, so one descriptor based at that address rounded down to 4 B serves both rows —
+        // a 16 B load and the next dword per lane, realigned by v_alignbyte — and the bytes under the header read
+        // from inside the data array and are masked away (build_row); no per-dword clamped head loads.
+        const bool mgen = mdb >= mhdr && mwire <= 2u * kRow;
+        if (pipe && (!OPT || staged) && __builtin_amdgcn_ballot_w64(!(mgen || lane >= cnt)) == 0) {
+            struct GRows {
+                u32x4 lo[PS][2];
+                uint32_t hi[PS][2];
+            };
+            auto gload = [&](uint32_t k0, GRows& G) {  // kk ≥ cnt: an empty descriptor, the loads move nothing
+#pragma unroll
+                for (uint32_t e = 0; e < (uint32_t)PS; ++e) {
+                    const uint32_t kk = k0 + e, kc = min(kk, cnt - 1u);
+                    const uint64_t src = readlane64(mdb, kc) - __builtin_amdgcn_readlane(mhdr, kc);
+                    const uint32_t sh = (uint32_t)src & 3u;
+                    const uint32_t nb = kk < cnt ? (sh + __builtin_amdgcn_readlane(mwire, kc) + 3u) & ~3u : 0u;
+                    const __amdgpu_buffer_rsrc_t grs = make_rsrc(data + (src & ~3ull), nb);
+#pragma unroll
+                    for (uint32_t r = 0; r < 2u; ++r) {
+                        G.lo[e][r] = bld16<LP != 0>(grs, r * kRow + lane * 16u);
+                        G.hi[e][r] = __builtin_amdgcn_raw_buffer_load_b32(grs, sh ? r * kRow + lane * 16u + 16u : kOOB,
+                                                                           0, LP);
+                    }
+                }
+            };
+            auto gdone = [&](uint32_t k0, GRows& G) {
+#pragma unroll
+                for (uint32_t e = 0; e < (uint32_t)PS; ++e)
+                    asm volatile("" : "+v"(G.lo[e][0]), "+v"(G.lo[e][1]), "+v"(G.hi[e][0]), "+v"(G.hi[e][1]));
+#pragma unroll
+                for (uint32_t e = 0; e < (uint32_t)PS; ++e) {
+                    const uint32_t kk = k0 + e;
+                    if (kk >= cnt) break;  // wave-uniform
+                    BuildSeg S;
+                    __amdgpu_buffer_rsrc_t drs, ors;
+                    seg_at(kk, S, drs, ors);
+                    u32x4 oc0{0u, 0u, 0u, 0u};
+                    if (OPT && S.optlen) oc0 = staged_opts<false>(od, kk, (S.optlen + 3u) >> 2, lane, oc0);
+                    uint32_t acc = build_row<SP>(S, ors, oc0, lane, 0, G.lo[e][0], G.hi[e][0], 0u);
+                    if (S.rows > 1) acc = build_row<SP>(S, ors, u32x4{0u, 0u, 0u, 0u}, lane, 1, G.lo[e][1], G.hi[e][1], acc);
+                    seg_done(kk, S, ors, fold32(acc));
+                }
+            };
+            GRows A, B;
+            gload(0, A);
+            for (uint32_t kk = 0; kk < cnt; kk += 2u * PS) {
+                gload(kk + PS, B);
+                gdone(kk, A);
+                if (kk + PS >= cnt) break;
+                gload(kk + 2u * PS, A);
+                gdone(kk + PS, B);
             }
             continue;
         }
@@ -2337,7 +2393,8 @@ hipError_t launch_tcp_build(const TcpHdrSoA& h, const uint8_t* opts, const uint6
                             const uint64_t* data_off, uint64_t data_bytes, const uint32_t* partial, uint64_t n,
                             uint8_t* out, const uint64_t* out_off, uint16_t* raw, uint32_t max_blocks, int policy,
                             int xchunk, int kernel, int spw, hipStream_t st) {
-    // kernel: 0 = groups of fast-path segments ≤ 2 rows software-pipelined, 2 = never pipelined;
+    // kernel: 0 = groups of ≤ 2-row segments software-pipelined (the fast composition when every segment of the
+    // group allows it, else the general one), 2 = never pipelined, 3 = the general pipelined composition always;
     // spw: segments per pipelined register set, 2 (default) or 1
     // Group size: up to 64 segments per wave task, fewer when n would leave waves idle.
     const uint64_t waves = (uint64_t)max_blocks * kWavesPerBlock;
@@ -2346,17 +2403,17 @@ hipError_t launch_tcp_build(const TcpHdrSoA& h, const uint8_t* opts, const uint6
     const uint64_t want = (tasks + kWavesPerBlock - 1) / kWavesPerBlock;
     const uint32_t grid = (uint32_t)(want < max_blocks ? want : max_blocks);
     const uint32_t clog = deal_clog(xchunk, tasks, (uint64_t)group * 3000u);  // ~payload + image per segment
+    const int pipe = kernel == 2 ? 0 : kernel == 3 ? 2 : 1;  // 3: the general pipelined path for every layout
     // policy: 0/2 = default cache policy (measured best: segment-boundary lines stay in L2 for
     // the neighbour segment's load and partial-line stores merge there), 1 = nt loads and
     // stores, 3 = nt loads + plain stores, 4 = plain loads + nt stores
 #define NSX_BUILD_PS(LP, SP, PS)                                                                                   \
     if (opt_off)                                                                                                   \
         hipLaunchKernelGGL((tcp_build_kernel<LP, SP, PS, true>), dim3(grid), dim3(kBlock), 0, st, h, opts, opt_off, \
-                           data, data_off, data_bytes, partial, n, out, out_off, raw, group, clog, kernel != 2);   \
+                           data, data_off, data_bytes, partial, n, out, out_off, raw, group, clog, pipe);         \
     else                                                                                                           \
         hipLaunchKernelGGL((tcp_build_kernel<LP, SP, PS, false>), dim3(grid), dim3(kBlock), 0, st, h, opts,        \
-                           opt_off, data, data_off, data_bytes, partial, n, out, out_off, raw, group, clog,        \
-                           kernel != 2)
+                           opt_off, data, data_off, data_bytes, partial, n, out, out_off, raw, group, clog, pipe)
 #define NSX_BUILD(LP, SP)        \
     if (spw != 1) {              \
         NSX_BUILD_PS(LP, SP, 2); \

@@ -131,7 +131,7 @@ def test_fuzz_tcp_build(case):
               "offset": np.full(n, 5, np.uint8), "control": rng.integers(0, 256, n).astype(np.uint8),
               "window": rng.integers(0, 1 << 16, n).astype(np.uint16),
               "urgent_ptr": rng.integers(0, 1 << 16, n).astype(np.uint16)}
-    _apply(dict(kernel=int(rng.choice([0, 2])), segs_per_wave=int(rng.choice([0, 1])),
+    _apply(dict(kernel=int(rng.choice([0, 2, 3])), segs_per_wave=int(rng.choice([0, 1])),
                 blocks_per_cu=int(rng.choice([0, 1, 8]))))
     want, wraw = O.c_go_tcp_build(fields, data, data_off, out_off, None)
     dt = {np.uint16: np.int16, np.uint32: np.int32, np.uint8: np.uint8}
@@ -197,7 +197,7 @@ def test_fuzz_tcp_build_options(case):
     data_off[1:] = np.cumsum([len(sg.data) for sg in segs])
     data_off += np.uint64(dlead)
     out_off = nsx.tcp_layout_host(data_off, opt_off)
-    _apply(dict(kernel=int(rng.choice([0, 2])), segs_per_wave=int(rng.choice([0, 1])),
+    _apply(dict(kernel=int(rng.choice([0, 2, 3])), segs_per_wave=int(rng.choice([0, 1])),
                 blocks_per_cu=int(rng.choice([0, 1, 8]))))
     col = lambda k, dt: _dev(np.array([getattr(sg, k) for sg in segs], dt).view(
         {np.uint16: np.int16, np.uint32: np.int32, np.uint8: np.uint8}[dt]))

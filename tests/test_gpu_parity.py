@@ -825,7 +825,7 @@ def test_tcp_build_uniform_batches(P, n, nsx_param):
     for lead in (20, 28, 0):  # lead 0: segment 0 has no 20 bytes before its payload (general path)
         fields, data, data_off, out_off, ps = _uniform_build_case(rng, n, P, lead)
         want, wraw = O.c_go_tcp_build(fields, data, data_off, out_off, ps)
-        for kern, spw in ((0, 0), (0, 1), (2, 0)):  # pipelined, 2 / 1 segments per register set; unpipelined
+        for kern, spw in ((0, 0), (0, 1), (3, 0), (2, 0)):  # pipelined 2 / 1 segs per set; general pipelined path only; unpipelined
             nsx_param(nsx.PARAM_KERNEL, kern)
             nsx_param(nsx.PARAM_SEGS_PER_WAVE, spw)
             got, raw = _run_build(fields, data, data_off, out_off, ps)
@@ -893,7 +893,7 @@ def test_tcp_build_uniform_batches_with_options(opt, P, nsx_param):
         data_off = np.arange(n + 1, dtype=np.uint64) * np.uint64(P) + np.uint64(data_lead)
         out_off = nsx.tcp_layout_host(data_off, opt_off)
         assert all(int(out_off[i + 1] - out_off[i]) >= len(want_wire[i]) for i in range(n))
-        for kern, spw in ((0, 0), (0, 1), (2, 0)):
+        for kern, spw in ((0, 0), (0, 1), (3, 0), (2, 0)):
             nsx_param(nsx.PARAM_KERNEL, kern)
             nsx_param(nsx.PARAM_SEGS_PER_WAVE, spw)
             out = torch.full((int(out_off[-1]),), 0xAB, dtype=torch.uint8, device="cuda")
