@@ -167,9 +167,13 @@ def timed_loop(step, sync, barrier, steps: int, warmup: int, ev_pair=None, every
 
 
 def result_line(*, world, steps, warmup, wall_max, bytes_per_rank_step, units_total, workload, cfg, launch_ms,
-                alg_bytes_per_launch, cpu_baseline, traffic, dtype="u16", metric=METRIC) -> dict:
+                alg_bytes_per_launch, cpu_baseline, traffic, dtype="u16", metric=METRIC, launches=1) -> dict:
     total_bytes = bytes_per_rank_step * world * steps
-    mean_launch_ms = sum(launch_ms) / len(launch_ms) if launch_ms else None
+    # launch_ms brackets one step; a step of `launches` back-to-back launches is reported per launch
+    # (alg bytes and duration divided evenly, the gaps between launches included) so that it compares
+    # with the rocprofv3 per-launch average and the PMC traffic per launch.
+    mean_launch_ms = sum(launch_ms) / len(launch_ms) / launches if launch_ms else None
+    alg_bytes_per_launch = alg_bytes_per_launch // launches
     achieved = alg_bytes_per_launch / (mean_launch_ms * 1e-3) / 1e9 if mean_launch_ms else None
     return {
         "metric": metric,
@@ -194,7 +198,7 @@ def result_line(*, world, steps, warmup, wall_max, bytes_per_rank_step, units_to
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": None if traffic is None else traffic.get("bytes_per_launch"),
             "traffic_source": None if traffic is None else traffic.get("source"),
-            "alg_bytes_per_launch": alg_bytes_per_launch},
+            "alg_bytes_per_launch": alg_bytes_per_launch, "launches_per_step": launches},
         "cpu_baseline": cpu_baseline,
     }
 
@@ -203,7 +207,18 @@ def result_line(*, world, steps, warmup, wall_max, bytes_per_rank_step, units_to
 # GPU workload
 # ---------------------------------------------------------------------------
 PARAMS = {"blocks_per_cu": 1, "segs_per_wave": 2, "nontemporal": 3, "block_mode": 4, "xcd_map": 5, "kernel": 6,
-          "stream_rows": 7, "run_segs": 8, "xcd_chunk": 9}
+          "stream_rows": 7, "run_segs": 8, "xcd_chunk": 9, "window_bytes": 10}
+
+
+def fixed_launches(n: int, stride: int, seg_len: int) -> int:
+    """Kernel launches one nsx_csum_fixed_dev call makes at the default knobs: the aligned
+    short-segment path splits batches of >= 2 x 1.6 GB into equal back-to-back windows of
+    about 1.6 GB (kAutoWindow in csum_kernels.hip)."""
+    auto_window = 1600 * 1000 * 1000
+    aligned = stride % 4 == 0 and seg_len % 4 == 0
+    if not aligned or seg_len + 3 > 4096 or n < 4 * 256 or n * stride < 2 * auto_window:
+        return 1
+    return -(-n * stride // auto_window)
 
 
 def build_workload(cfg, rank, device):
@@ -217,7 +232,7 @@ def build_workload(cfg, rank, device):
         buf = torch.empty((n - 1) * S + L, dtype=torch.uint8, device=device)
         nsx.fill_splitmix64_dev(buf, seed)
         out = torch.empty(n, dtype=torch.int16, device=device)
-        w.update(buf=buf, out=out, bytes=n * L, alg=n * L + 2 * n,
+        w.update(buf=buf, out=out, bytes=n * L, alg=n * L + 2 * n, launches=fixed_launches(n, S, L),
                  step=lambda: nsx.fixed_dev(buf, S, L, n, out=out))
     elif cfg["kind"] == "tcp_build":
         n, P, OL = cfg["n"], cfg["payload"], cfg.get("opt", 0)
@@ -490,7 +505,8 @@ def main(argv=None):
     line = result_line(world=dist.world, steps=args.steps, warmup=args.warmup, wall_max=wall_max,
                        bytes_per_rank_step=w["bytes"], units_total=cfg["n"] * dist.world, workload=cfg["name"],
                        cfg=cfg, launch_ms=launch_ms, alg_bytes_per_launch=w["alg"], cpu_baseline=cpu,
-                       traffic=load_traffic(args.config), metric=cfg.get("metric", METRIC))
+                       traffic=load_traffic(args.config), metric=cfg.get("metric", METRIC),
+                       launches=w.get("launches", 1))
     if args.param:
         line["config"]["params"] = args.param
     if dist.rank == 0:

@@ -21,7 +21,7 @@
 namespace {
 
 // ---------------------------------------------------------------- params
-constexpr int kNumParams = 10;
+constexpr int kNumParams = 11;
 std::atomic<int64_t> g_param[kNumParams];  // index = NSX_PARAM_*; 0 = default
 
 constexpr int kMaxDevices = 64;
@@ -96,6 +96,7 @@ LaunchCfg default_launch_cfg(int cus, uint64_t /*n*/) {
     c.rows = get(NSX_PARAM_STREAM_ROWS);
     c.run_segs = get(NSX_PARAM_RUN_SEGS);
     c.xcd_chunk = get(NSX_PARAM_XCD_CHUNK);
+    c.window_bytes = g_param[NSX_PARAM_WINDOW_BYTES].load();
     return c;
 }
 

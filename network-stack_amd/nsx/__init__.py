@@ -21,8 +21,8 @@ HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "
 
 NSX_OK, NSX_EIO, NSX_ENOMEM, NSX_ENODEV, NSX_EINVAL = 0, -5, -12, -19, -22
 PARAM_BLOCKS_PER_CU, PARAM_SEGS_PER_WAVE, PARAM_NONTEMPORAL, PARAM_BLOCK_MODE, PARAM_XCD_MAP = 1, 2, 3, 4, 5
-PARAM_KERNEL, PARAM_STREAM_ROWS, PARAM_RUN_SEGS, PARAM_XCD_CHUNK = 6, 7, 8, 9
-ALL_PARAMS = (1, 2, 3, 4, 5, 6, 7, 8, 9)
+PARAM_KERNEL, PARAM_STREAM_ROWS, PARAM_RUN_SEGS, PARAM_XCD_CHUNK, PARAM_WINDOW_BYTES = 6, 7, 8, 9, 10
+ALL_PARAMS = (1, 2, 3, 4, 5, 6, 7, 8, 9, 10)
 
 
 class NsxError(RuntimeError):

@@ -490,6 +490,20 @@ def test_config4_256K_x_64KiB_sampled_and_roundtrip():
     assert (ok == 0xFFFF).all()
 
 
+@pytest.mark.parametrize("window", [1_000_003, 3000, 1500, 1])
+def test_fixed_back_to_back_windows(nsx_param, window):
+    """NSX_PARAM_WINDOW_BYTES splits the aligned fixed path into back-to-back launches
+    (DESIGN.md §7 step 21): window sizes that cut the batch unevenly, down to one segment
+    per launch, with per-segment partials, against the oracle."""
+    rng = np.random.default_rng(0x21 + window)
+    L, n = 1500, 2048 if window <= 3000 else 6001
+    buf = rng.integers(0, 256, n * L, dtype=np.uint8)
+    part = rng.integers(0, 1 << 20, n, dtype=np.uint32)
+    want = O.c_batch(buf, n, stride=L, seg_len=L, partial=part)
+    nsx_param(nsx.PARAM_WINDOW_BYTES, window)
+    assert np.array_equal(run_fixed(buf, L, L, n, part), want)
+
+
 def test_config5_16M_x_1500_per_gpu_sampled():
     """Config 5's per-GPU batch (16M x 1500 B = 23.4 GiB): every
     4099th segment plus the segments either side of every 8-way shard boundary
