@@ -229,7 +229,7 @@ const char* nsx_strerror(int code);
 #define NSX_PARAM_NONTEMPORAL     3  /* 1 nt loads (default), 2 default-policy loads; nsx_tcp_build_dev: default plain, 1 nt, 3 nt loads + plain stores, 4 plain loads + nt stores */
 #define NSX_PARAM_BLOCK_MODE      4  /* 0 auto (a block per segment when n < 4*CUs), 1 never, 2 always */
 #define NSX_PARAM_XCD_MAP         5  /* task deal: 1 XCD-contiguous regions (default), 2 grid-stride, 3 one contiguous range per wave, 4 byte-balanced contiguous range per wave (ragged scan kernel; its default) */
-#define NSX_PARAM_KERNEL          6  /* 1 row-stream, 2 per-segment, 3 buffer-load, 4 prefix-scan (ragged), 5 pipelined buffer-load (fixed; the aligned default), 6 pipelined prefix-scan (ragged), 7 pipelined long segments (fixed > 4 KiB); IPv4 headers: 1 per-thread, 2 LDS-dense, 3 packed-20 B flat unpipelined; TCP build: 2 unpipelined, 3 general pipelined composition for every layout; 0 = per-path default */
+#define NSX_PARAM_KERNEL          6  /* 1 row-stream, 2 per-segment, 3 buffer-load, 4 prefix-scan (ragged), 5 pipelined buffer-load (fixed; the aligned default), 6 pipelined prefix-scan (ragged), 7 pipelined long segments (fixed > 4 KiB); IPv4 headers: 1 per-thread, 2 LDS-dense, 3 packed-20 B flat unpipelined, 4 packed-20 B with raw sums written in bursts from LDS; TCP build: 2 unpipelined, 3 general pipelined composition for every layout; 0 = per-path default */
 #define NSX_PARAM_STREAM_ROWS     7  /* row-stream / scan: 4, 8 (default) or 16 KiB in flight per wave */
 #define NSX_PARAM_RUN_SEGS        8  /* ragged scan kernel: segments per wave task, 1..63 (default 63) */
 #define NSX_PARAM_XCD_CHUNK       9  /* XCD deal (fixed-stride, long-segment, TCP build, packed IPv4 header kernels): XCD x takes chunks x, x+8, ... of 2^k wave tasks; 0 = auto (<= 24 MiB chunks, >= 64 of them), k = 1..20 fixed, any other value = contiguous eighths */

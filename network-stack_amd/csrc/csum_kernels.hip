@@ -1825,7 +1825,13 @@ constexpr uint32_t kHdr20Lds = kHdr20Task * 20u;  // bytes of LDS per wave
 // PIPE: software-pipelined — two register sets of U tasks; the loads of the next set are issued before
 // the current set goes through LDS, so every wave keeps loads in flight while it computes and stores (one
 // wave per SIMD at 1 block/CU has no other wave to cover those phases). !PIPE: one set, load then use.
-template <int MODE, int U, bool PIPE>
+// DEFER (MODE 0 only): a full task's 512 B of raw sums go to a per-wave LDS buffer of DEFER task slots instead of
+// HBM; the wave writes the buffer out when it is full and at the end, so result stores leave in bursts between
+// long read phases instead of one 512 B store per task (kernel knob 4).
+// 20 slots × 512 B × 4 waves + the 20 KiB staging slices = 60 KiB, within the default dynamic LDS limit.
+constexpr uint32_t kHdr20DeferSlots = 20;
+
+template <int MODE, int U, bool PIPE, int DEFER = 0>
 __global__ __launch_bounds__(kBlock) void ipv4_hdr20_kernel(uint8_t* __restrict__ base, uint32_t n,
                                                             uint16_t* __restrict__ out, uint32_t clog,
                                                             uint64_t* __restrict__ mask) {
@@ -1841,8 +1847,23 @@ __global__ __launch_bounds__(kBlock) void ipv4_hdr20_kernel(uint8_t* __restrict_
     const __amdgpu_buffer_rsrc_t ors = make_rsrc(out, out ? (uint64_t)n * 2 : 0);
     struct Set {
         __amdgpu_buffer_rsrc_t rs[U];
-        uint32_t cnt[U], tk[U];
+        uint32_t cnt[U], tk[U], ii[U];
         u32x4 v[U][5];
+    };
+    // Deferred raw sums: slot k holds the k-th buffered task's 64 lanes × 8 B; buffered tasks are consecutive in
+    // the wave's processing order (ii = d_first + k·step), so their task ids need no storage.
+    static_assert(DEFER == 0 || (MODE == 0 && PIPE), "deferred stores: raw-sum mode, pipelined kernel");
+    v2u* dbuf = reinterpret_cast<v2u*>(lds20 + kWavesPerBlock * (kHdr20Lds / 16u)) + (uint32_t)wave * DEFER * kWave;
+    uint32_t d_n = 0, d_first = 0;
+    auto flush = [&]() {
+        if constexpr (DEFER > 0) {
+            for (uint32_t k = 0; k < d_n; ++k) {
+                const uint32_t task = cd.task(d_first + k * step);
+                __builtin_amdgcn_raw_buffer_store_b64(dbuf[k * kWave + lane], ors, (task * kHdr20Task + lane * 4u) * 2u,
+                                                      0, 0);
+            }
+            d_n = 0;
+        }
     };
     auto live = [&](uint32_t t0) { return t0 < end && cd.task(t0) < ntasks; };
     auto issue = [&](uint32_t t0, Set& S) {
@@ -1851,6 +1872,7 @@ __global__ __launch_bounds__(kBlock) void ipv4_hdr20_kernel(uint8_t* __restrict_
             const uint32_t ii = t0 + (uint32_t)u * step;
             const uint32_t task = cd.task(ii);
             S.tk[u] = task;
+            S.ii[u] = ii;
             S.cnt[u] = (ii < end && task < ntasks) ? min(kHdr20Task, n - task * kHdr20Task) : 0u;
             S.rs[u] = make_rsrc(base + (uint64_t)min(task, ntasks - 1) * kHdr20Lds, S.cnt[u] * 20u);
 #pragma unroll
@@ -1908,10 +1930,15 @@ __global__ __launch_bounds__(kBlock) void ipv4_hdr20_kernel(uint8_t* __restrict_
                 hi += __builtin_amdgcn_update_dpp(0u, hi, 0x118, 0xF, 0xF, false);
                 const uint32_t wi = S.tk[u] * (kHdr20Task / kWave) + (lane >> 4);  // < 2^22 (n < 2^28 per launch)
                 if (j == 15u && wi * kWave < n) mask[wi] = ((uint64_t)hi << 32) | lo;
+            } else if (DEFER > 0 && S.cnt[u] == kHdr20Task) {
+                if (d_n == 0) d_first = S.ii[u];
+                dbuf[d_n * kWave + lane] = v2u{res[0] | (res[1] << 16), res[2] | (res[3] << 16)};
+                ++d_n;
             } else if (S.cnt[u] == kHdr20Task) {
                 __builtin_amdgcn_raw_buffer_store_b64(v2u{res[0] | (res[1] << 16), res[2] | (res[3] << 16)}, ors,
                                                       i0 * 2u, 0, 0);
             } else {
+                flush();  // a partial task breaks the run of consecutive buffered tasks
 #pragma unroll
                 for (int h = 0; h < 4; ++h)
                     __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res[h], ors, i0 + h < n ? (i0 + h) * 2u : kOOB, 0,
@@ -1925,6 +1952,10 @@ __global__ __launch_bounds__(kBlock) void ipv4_hdr20_kernel(uint8_t* __restrict_
             }
         }
     };
+    auto room = [&]() {
+        if constexpr (DEFER > 0)
+            if (d_n + U > (uint32_t)DEFER) flush();
+    };
     if constexpr (PIPE) {
         Set A, B;
         uint32_t t0 = (uint32_t)it.next;
@@ -1932,12 +1963,15 @@ __global__ __launch_bounds__(kBlock) void ipv4_hdr20_kernel(uint8_t* __restrict_
         while (live(t0)) {
             const uint32_t t1 = t0 + step * U;
             issue(t1, B);
+            room();
             consume(A);
             if (!live(t1)) break;
             t0 = t1 + step * U;
             issue(t0, A);
+            room();
             consume(B);
         }
+        flush();
     } else {
         for (uint32_t t0 = (uint32_t)it.next; live(t0); t0 += step * U) {
             Set A;
@@ -2459,8 +2493,9 @@ hipError_t launch_ipv4_hdr(uint8_t* base, uint64_t stride, uint32_t hdr_off, uin
             default: launch(std::integral_constant<int, 0>{}); break;
         }
     };
-    if (stride == 20 && hdr_off == 0 && ((uintptr_t)base & 3u) == 0 && (kernel == 0 || kernel == 3)) {
-        const bool pipe = kernel == 0;  // kernel 3: the unpipelined flat kernel (measured alternative)
+    if (stride == 20 && hdr_off == 0 && ((uintptr_t)base & 3u) == 0 && (kernel == 0 || kernel == 3 || kernel == 4)) {
+        const bool pipe = kernel != 3;  // kernel 3: the unpipelined flat kernel (measured alternative)
+        const bool defer = kernel == 4 && mode == 0 && out;  // kernel 4: deferred raw-sum stores (measured alternative)
         // packed option-less headers: flat-stream kernel. Default 1 block/CU with 2 tasks (10 KiB) in flight
         // per wave = 40 KiB per CU (tools/sweep.py: 0.220 ms vs 0.232 at 2 blocks/CU, 0.284 at 1 task/wave);
         // chunks keep each launch's results within one descriptor (2^28 headers = 2^22 mask words)
@@ -2474,13 +2509,16 @@ hipError_t launch_ipv4_hdr(uint8_t* base, uint64_t stride, uint32_t hdr_off, uin
             uint8_t* b = base + c0 * 20u;
             uint16_t* o = out ? out + c0 : nullptr;
             uint64_t* mk = mask ? mask + c0 / kWave : nullptr;
-            const size_t lds = (size_t)kHdr20Lds * kWavesPerBlock;
+            const size_t lds = (size_t)(kHdr20Lds + (defer ? kHdr20DeferSlots * kWave * 8u : 0u)) * kWavesPerBlock;
             const uint32_t clog = deal_clog(xchunk, tasks, kHdr20Lds + kHdr20Task * 2u);
             by_mode([&](auto m) {
                 constexpr int M = decltype(m)::value;
 #define NSX_H20(U)                                                                                              \
     do {                                                                                                        \
-        if (pipe)                                                                                               \
+        if (M == 0 && defer)                                                                                    \
+            hipLaunchKernelGGL((ipv4_hdr20_kernel<0, U, true, kHdr20DeferSlots>),                          \
+                               dim3(grid_f), dim3(kBlock), lds, st, b, cn, o, clog, mk);                        \
+        else if (pipe)                                                                                          \
             hipLaunchKernelGGL((ipv4_hdr20_kernel<M, U, true>), dim3(grid_f), dim3(kBlock), lds, st, b, cn, o,   \
                                clog, mk);                                                                       \
         else                                                                                                    \

@@ -667,7 +667,7 @@ def _ipv4_headers(rng, n, stride, hdr_off):
     return buf, ihl
 
 
-@pytest.mark.parametrize("kernel", [0, 1, 2, 3])  # 0: default (pipelined flat for packed 20 B, LDS-dense for stride <= 64), 1: per-thread, 2: LDS-dense, 3: flat
+@pytest.mark.parametrize("kernel", [0, 1, 2, 3, 4])  # 0: default (pipelined flat for packed 20 B, LDS-dense for stride <= 64), 1: per-thread, 2: LDS-dense, 3: flat, 4: pipelined flat with deferred raw stores
 @pytest.mark.parametrize("stride,hdr_off", [(64, 0), (61, 1), (1514, 14), (1500, 0), (60, 0), (40, 3), (20, 0)])
 def test_ipv4_header_checksum_verify_and_fill(stride, hdr_off, kernel, nsx_param):
     nsx_param(nsx.PARAM_KERNEL, kernel)
@@ -699,6 +699,29 @@ def test_ipv4_header_checksum_verify_and_fill(stride, hdr_off, kernel, nsx_param
     again = u16(nsx.ipv4_hdr_csum_dev(d, stride, n, hdr_off=hdr_off, mode=0))
     valid = np.array([int(ihl[i]) * 4 >= 20 and hdr_off + int(ihl[i]) * 4 <= stride for i in range(n)])
     assert (again[valid] == 0xFFFF).all()
+
+
+@pytest.mark.parametrize("n", [(8 << 20) + 77, 5_000_000])
+def test_ipv4_packed_deferred_raw_stores(n, nsx_param):
+    """Kernel knob 4 (packed 20 B headers, raw sums buffered in LDS and written in bursts):
+    enough tasks per wave to fill and flush the buffer many times, a partial last task;
+    every raw sum against a numpy restatement of the fold (RFC 1071; tcp.go:72-95) and
+    against the default kernel."""
+    rng = np.random.default_rng(n)
+    buf = rng.integers(0, 256, n * 20, dtype=np.uint8)
+    buf[::20] = 0x45
+    buf[20 * 977::20 * 1979] = 0x44  # some malformed (IHL 4): raw 0
+    w = buf.reshape(n, 10, 2).astype(np.uint32)
+    s = ((w[:, :, 0] << 8) | w[:, :, 1]).sum(axis=1)
+    s = (s & 0xFFFF) + (s >> 16)
+    s = (s & 0xFFFF) + (s >> 16)
+    want = np.where((buf[::20] & 15) == 5, s, 0).astype(np.uint16)
+    d = dev(buf)
+    nsx_param(nsx.PARAM_KERNEL, 4)
+    got = u16(nsx.ipv4_hdr_csum_dev(d, 20, n, mode=0))
+    assert np.array_equal(got, want)
+    nsx_param(nsx.PARAM_KERNEL, 0)
+    assert np.array_equal(u16(nsx.ipv4_hdr_csum_dev(d, 20, n, mode=0)), want)
 
 
 def _mask_words(valid):
