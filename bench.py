@@ -264,7 +264,8 @@ def build_workload(cfg, rank, device):
             opt_off = idx * OL
         # per segment: payload + options + 18 B of header fields + 2 (+2) offsets + partial read; wire image + raw
         # sum written
-        w.update(out=raw, wire=out, fields=fields, addrs=addrs, data=data, opts=opts, bytes=n * W,
+        w.update(out=raw, wire=out, fields=fields, addrs=addrs, data=data, opts=opts, opt_off=opt_off, part=part,
+                 data_off=data_off, out_off=out_off, bytes=n * W,
                  alg=n * (P + OL + 18 + 8 + 8 + (8 if OL else 0) + 4 + W + 2) + 16 + (8 if OL else 0),
                  step=lambda: nsx.tcp_build_dev(fields, data, data_off, out, out_off, opts=opts, opt_off=opt_off,
                                                 partial=part, raw=raw))
