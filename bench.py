@@ -210,13 +210,18 @@ PARAMS = {"blocks_per_cu": 1, "segs_per_wave": 2, "nontemporal": 3, "block_mode"
           "stream_rows": 7, "run_segs": 8, "xcd_chunk": 9, "window_bytes": 10}
 
 
-def fixed_launches(n: int, stride: int, seg_len: int) -> int:
-    """Kernel launches one nsx_csum_fixed_dev call makes at the default knobs: the aligned
-    short-segment path splits batches of >= 2 x 1.6 GB into equal back-to-back windows of
-    about 1.6 GB (kAutoWindow in csum_kernels.hip)."""
+def fixed_launches(n: int, stride: int, seg_len: int, window_bytes: int = 0, kernel: int = 0) -> int:
+    """Kernel launches one nsx_csum_fixed_dev call makes (launch_fixed in csum_kernels.hip):
+    the short-segment buffer-load path (segments <= 4 KiB, kernel knob 0, 3 or 5) splits
+    batches of >= 2 x 1.6 GB into equal back-to-back windows of about 1.6 GB (kAutoWindow;
+    DESIGN.md §7 step 21), or into windows of `window_bytes` (NSX_PARAM_WINDOW_BYTES > 0);
+    -1 = one launch. Block mode (n < 4 blocks per CU) is one launch."""
     auto_window = 1600 * 1000 * 1000
-    aligned = stride % 4 == 0 and seg_len % 4 == 0
-    if not aligned or seg_len + 3 > 4096 or n < 4 * 256 or n * stride < 2 * auto_window:
+    if kernel not in (0, 3, 5) or seg_len + 3 > 4096 or n < 4 * 256 or window_bytes < 0:
+        return 1
+    if window_bytes > 0:
+        return -(-n // max(1, min(window_bytes // stride, 1 << 28)))
+    if n * stride < 2 * auto_window:
         return 1
     return -(-n * stride // auto_window)
 
@@ -232,7 +237,7 @@ def build_workload(cfg, rank, device):
         buf = torch.empty((n - 1) * S + L, dtype=torch.uint8, device=device)
         nsx.fill_splitmix64_dev(buf, seed)
         out = torch.empty(n, dtype=torch.int16, device=device)
-        w.update(buf=buf, out=out, bytes=n * L, alg=n * L + 2 * n, launches=fixed_launches(n, S, L),
+        w.update(buf=buf, out=out, bytes=n * L, alg=n * L + 2 * n, launches=fixed_launches(n, S, L, cfg.get("window_bytes", 0), cfg.get("kernel", 0)),
                  step=lambda: nsx.fixed_dev(buf, S, L, n, out=out))
     elif cfg["kind"] == "tcp_build":
         n, P, OL = cfg["n"], cfg["payload"], cfg.get("opt", 0)
@@ -481,6 +486,8 @@ def main(argv=None):
         nsx.set_param(PARAMS[k], int(v))
 
     cfg = WORKLOADS[args.config]
+    knobs = dict(kv.split("=") for kv in args.param)
+    cfg = dict(cfg, **{k: int(knobs[k]) for k in ("window_bytes", "kernel") if k in knobs})
     w = build_workload(cfg, dist.rank, device)
     torch.cuda.synchronize()
     # Setup, not measurement: after data generation the GPU's clocks sit in an
@@ -506,7 +513,8 @@ def main(argv=None):
     line = result_line(world=dist.world, steps=args.steps, warmup=args.warmup, wall_max=wall_max,
                        bytes_per_rank_step=w["bytes"], units_total=cfg["n"] * dist.world, workload=cfg["name"],
                        cfg=cfg, launch_ms=launch_ms, alg_bytes_per_launch=w["alg"], cpu_baseline=cpu,
-                       traffic=load_traffic(args.config), metric=cfg.get("metric", METRIC),
+                       # the committed PMC traffic was profiled at the default knobs
+                       traffic=None if args.param else load_traffic(args.config), metric=cfg.get("metric", METRIC),
                        launches=w.get("launches", 1))
     if args.param:
         line["config"]["params"] = args.param

@@ -233,7 +233,7 @@ const char* nsx_strerror(int code);
 #define NSX_PARAM_STREAM_ROWS     7  /* row-stream / scan: 4, 8 (default) or 16 KiB in flight per wave */
 #define NSX_PARAM_RUN_SEGS        8  /* ragged scan kernel: segments per wave task, 1..63 (default 63) */
 #define NSX_PARAM_XCD_CHUNK       9  /* XCD deal (fixed-stride, long-segment, TCP build, packed IPv4 header kernels): XCD x takes chunks x, x+8, ... of 2^k wave tasks; 0 = auto (<= 24 MiB chunks, >= 64 of them), k = 1..20 fixed, any other value = contiguous eighths */
-#define NSX_PARAM_WINDOW_BYTES   10  /* fixed-stride aligned path: launch a batch as back-to-back windows of at most this many bytes (rounded down to whole segments); 0 = auto, -1 = one launch */
+#define NSX_PARAM_WINDOW_BYTES   10  /* fixed-stride buffer-load path (segments <= 4 KiB): launch a batch as back-to-back windows of at most this many bytes (rounded down to whole segments); 0 = auto, -1 = one launch */
 int nsx_set_param(int param, int64_t value);
 int nsx_get_param(int param, int64_t* value);
 

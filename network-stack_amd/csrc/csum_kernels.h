@@ -28,7 +28,7 @@ struct LaunchCfg {
     int rows;            // row-stream rows per batch: 4, 8, 16
     int run_segs;        // ragged scan kernel: segments per wave task, 1..63
     int xcd_chunk;       // XCD deal: interleaved chunks of 2^k tasks (0 = auto, 1..20 fixed, else contiguous eighths)
-    int64_t window_bytes = 0;  // fixed aligned path: back-to-back launches of ≤ this many bytes (0 auto, -1 one launch)
+    int64_t window_bytes = 0;  // fixed short-segment path: back-to-back launches of ≤ this many bytes (0 auto, -1 one launch)
 };
 
 // Launch configuration from the process-wide NSX_PARAM_* knobs (csum_api.cpp).

@@ -2129,7 +2129,7 @@ static Plan resolve(const LaunchCfg& c, Path p) {
     return r;
 }
 
-// Auto window of the fixed aligned path (NSX_PARAM_WINDOW_BYTES = 0): batches of at least twice this size are
+// Auto window of the fixed short-segment buffer-load path (NSX_PARAM_WINDOW_BYTES = 0): batches of at least twice this size are
 // launched as back-to-back windows of about this many bytes. One launch over config 5's 25 GB span runs ~4%
 // slower per byte than 1.5 GB windows of it.
 constexpr uint64_t kAutoWindow = 1600ull * 1000 * 1000;

@@ -32,3 +32,10 @@ def test_result_line_per_launch_with_windows():
     assert line["roofline"]["alg_bytes_per_launch"] == 1600
     assert line["roofline"]["launches_per_step"] == 16
     assert abs(line["kernel_ms_mean"] - 0.2) < 1e-9
+
+
+def test_fixed_launches_follows_the_knobs():
+    assert bench.fixed_launches(1 << 24, 1500, 1500, window_bytes=-1) == 1
+    assert bench.fixed_launches(4096, 1500, 1500, window_bytes=1500 * 1000) == 5
+    assert bench.fixed_launches(1 << 24, 1500, 1500, kernel=2) == 1  # per-segment kernel: no windows
+    assert bench.fixed_launches(1 << 24, 1501, 1501) == 16  # unaligned batches take the same path

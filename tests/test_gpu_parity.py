@@ -490,13 +490,14 @@ def test_config4_256K_x_64KiB_sampled_and_roundtrip():
     assert (ok == 0xFFFF).all()
 
 
+@pytest.mark.parametrize("L", [1500, 1501])
 @pytest.mark.parametrize("window", [1_000_003, 3000, 1500, 1])
-def test_fixed_back_to_back_windows(nsx_param, window):
-    """NSX_PARAM_WINDOW_BYTES splits the aligned fixed path into back-to-back launches
+def test_fixed_back_to_back_windows(nsx_param, window, L):
+    """NSX_PARAM_WINDOW_BYTES splits the fixed short-segment path into back-to-back launches
     (DESIGN.md §7 step 21): window sizes that cut the batch unevenly, down to one segment
-    per launch, with per-segment partials, against the oracle."""
+    per launch, aligned and odd strides, with per-segment partials, against the oracle."""
     rng = np.random.default_rng(0x21 + window)
-    L, n = 1500, 2048 if window <= 3000 else 6001
+    n = 2048 if window <= 3000 else 6001
     buf = rng.integers(0, 256, n * L, dtype=np.uint8)
     part = rng.integers(0, 1 << 20, n, dtype=np.uint32)
     want = O.c_batch(buf, n, stride=L, seg_len=L, partial=part)
