@@ -18,7 +18,7 @@ torch = pytest.importorskip("torch")
 import nsx  # noqa: E402
 
 FIXED_KNOBS = [dict(), dict(kernel=3), dict(kernel=5), dict(kernel=2), dict(kernel=7), dict(kernel=1),
-               dict(blocks_per_cu=1, segs_per_wave=8), dict(xcd_map=2), dict(xcd_chunk=99), dict(block_mode=2)]
+               dict(blocks_per_cu=1, segs_per_wave=8), dict(xcd_map=2), dict(xcd_chunk=99), dict(block_mode=2), dict(window_bytes=1_000_000), dict(window_bytes=7_777)]
 RAGGED_KNOBS = [dict(), dict(xcd_map=1), dict(kernel=6), dict(kernel=3), dict(run_segs=1), dict(stream_rows=16),
                 dict(block_mode=2)]
 
@@ -102,7 +102,7 @@ def test_fuzz_ipv4_headers(case):
     ihl[rng.random(n) < 0.6] = 5
     ihl[::53] = rng.integers(0, 5, len(ihl[::53]))
     buf[hdr_off:n * stride:stride] = (0x40 | ihl).astype(np.uint8)
-    _apply(dict(kernel=int(rng.choice([0, 0, 1, 2, 3]))))
+    _apply(dict(kernel=int(rng.choice([0, 0, 1, 2, 3, 4]))))
     got = _u16(nsx.ipv4_hdr_csum_dev(_dev(buf), stride, n, hdr_off=hdr_off, mode=0))
     for i in list(range(0, n, max(1, n // 500))) + [n - 1]:
         L = int(ihl[i]) * 4
