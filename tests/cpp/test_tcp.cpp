@@ -124,7 +124,7 @@ static void golden() {
     cases.push_back({"options_mss_noop_eol", f});
     const uint8_t src[4] = {192, 168, 0, 1}, dst[4] = {192, 168, 0, 2};
     for (auto& [name, s] : cases) {
-        s.offset = s.compute_offset();
+        if (name != "TestSegmentComputeChecksum") s.offset = s.compute_offset();  // tcp_test.go:27 leaves it 0
         const std::vector<uint8_t> bytes = s.bytes();
         const std::vector<uint8_t> pseudo = nsx::tcp::ipv4_pseudo_header(src, dst, 6, (uint16_t)bytes.size());
         std::printf("%s %u %s %u %u\n", name.c_str(), s.offset, hex(bytes).c_str(), s.compute_checksum(),
