@@ -12,6 +12,12 @@ weak. value = Σ bytes over all ranks ÷ max over ranks of the timed region.
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2-9]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
+`--gpus N` with N > 1 and no WORLD_SIZE in the environment launches the N rank
+processes itself (a torch.distributed.run child, rendezvous at 127.0.0.1) before
+anything touches a GPU, and relays rank 0's line; under a launcher that already
+set WORLD_SIZE, a WORLD_SIZE that differs from --gpus is an error (exit 2), as is
+more RCCL ranks than visible GPUs.
+
 Configs 2-5 are BASELINE.json's device-resident configurations (2 is the
 headline and the default). Configs 6 and 7 measure SURVEY.md §8's next rows to
 the same bar, each with its own metric string: 6 = the fused sender pass
@@ -26,14 +32,19 @@ Printed by rank 0: one JSON line with the contract fields plus
                  duration (HIP events on the launch stream) vs 8 TB/s HBM;
                  traffic = PMC-measured HBM bytes per launch from the committed
                  rocprofv3 summary (profiles/), or null;
-  cpu_baseline — the Go-faithful CPU restatement (oracle, 1 thread) timed on a
-                 bounded sample of the same workload (rank 0, N=1 only).
+  cpu_baseline — the Go-faithful CPU restatement (oracle) timed on a bounded
+                 sample of the same workload (rank 0, N=1 only) on every host
+                 core this process may use (`cores`), with the 1-thread rate
+                 beside it.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -88,9 +99,34 @@ def parse_args(argv=None):
     ap.add_argument("--settle-s", type=float, default=0.5, help="device clock settle time before warmup (setup)")
     ap.add_argument("--event-every", type=int, default=10,
                     help="record the per-launch HIP event pair around every N-th timed launch")
-    ap.add_argument("--param", action="append", default=[], metavar="NAME=V",
-                    help="kernel knob (include/nsx_csum.h NSX_PARAM_*): " + ", ".join(PARAMS))
+    ap.add_argument("--tune", action="append", default=[], metavar="FIELD=V",
+                    help="per-call launch override (include/nsx_tune.h nsx_tune field), e.g. blocks_per_cu=2")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: each rank's step is the CPU oracle on a small batch (exercises the launcher, "
+                         "rendezvous and the timing/reduction logic; the value is not a measurement)")
     return ap.parse_args(argv)
+
+
+# ---------------------------------------------------------------------------
+# rank launch: `--gpus N` without a launcher starts N ranks (before any GPU call)
+# ---------------------------------------------------------------------------
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(nranks: int, argv: list) -> int:
+    """Start `nranks` rank processes of this script under torch.distributed.run (one
+    process per GPU, rendezvous at 127.0.0.1) and wait for them; rank 0 prints the
+    line. The parent has not touched a GPU (no torch.cuda call, library not loaded)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nranks}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
 
 
 # ---------------------------------------------------------------------------
@@ -206,27 +242,18 @@ def result_line(*, world, steps, warmup, wall_max, bytes_per_rank_step, units_to
 # ---------------------------------------------------------------------------
 # GPU workload
 # ---------------------------------------------------------------------------
-PARAMS = {"blocks_per_cu": 1, "segs_per_wave": 2, "nontemporal": 3, "block_mode": 4, "xcd_map": 5, "kernel": 6,
-          "stream_rows": 7, "run_segs": 8, "xcd_chunk": 9, "window_bytes": 10}
+def parse_tune(items) -> dict:
+    import nsx
+    tune = {}
+    for kv in items:
+        k, v = kv.split("=", 1)
+        if k not in nsx.TUNE_FIELDS:
+            raise SystemExit(f"--tune: unknown nsx_tune field {k!r} (fields: {', '.join(nsx.TUNE_FIELDS)})")
+        tune[k] = int(v)
+    return tune
 
 
-def fixed_launches(n: int, stride: int, seg_len: int, window_bytes: int = 0, kernel: int = 0) -> int:
-    """Kernel launches one nsx_csum_fixed_dev call makes (launch_fixed in csum_kernels.hip):
-    the short-segment buffer-load path (segments <= 4 KiB, kernel knob 0, 3 or 5) splits
-    batches of >= 2 x 1.6 GB into equal back-to-back windows of about 1.6 GB (kAutoWindow;
-    DESIGN.md §7 step 21), or into windows of `window_bytes` (NSX_PARAM_WINDOW_BYTES > 0);
-    -1 = one launch. Block mode (n < 4 blocks per CU) is one launch."""
-    auto_window = 1600 * 1000 * 1000
-    if kernel not in (0, 3, 5) or seg_len + 3 > 4096 or n < 4 * 256 or window_bytes < 0:
-        return 1
-    if window_bytes > 0:
-        return -(-n // max(1, min(window_bytes // stride, 1 << 28)))
-    if n * stride < 2 * auto_window:
-        return 1
-    return -(-n * stride // auto_window)
-
-
-def build_workload(cfg, rank, device):
+def build_workload(cfg, rank, device, tune=None):
     import numpy as np
     import torch
     import nsx
@@ -237,8 +264,9 @@ def build_workload(cfg, rank, device):
         buf = torch.empty((n - 1) * S + L, dtype=torch.uint8, device=device)
         nsx.fill_splitmix64_dev(buf, seed)
         out = torch.empty(n, dtype=torch.int16, device=device)
-        w.update(buf=buf, out=out, bytes=n * L, alg=n * L + 2 * n, launches=fixed_launches(n, S, L, cfg.get("window_bytes", 0), cfg.get("kernel", 0)),
-                 step=lambda: nsx.fixed_dev(buf, S, L, n, out=out))
+        # launches per step: the library's own count of its back-to-back windows (config 5: 16)
+        w.update(buf=buf, out=out, bytes=n * L, alg=n * L + 2 * n, launches=nsx.fixed_launch_count(S, L, n, tune),
+                 step=lambda: nsx.fixed_dev(buf, S, L, n, out=out, tune=tune))
     elif cfg["kind"] == "tcp_build":
         n, P, OL = cfg["n"], cfg["payload"], cfg.get("opt", 0)
         W = P + 20 + OL  # OL ≡ 0 mod 4: tcp.go:118-121 pads nothing
@@ -273,7 +301,7 @@ def build_workload(cfg, rank, device):
                  data_off=data_off, out_off=out_off, bytes=n * W,
                  alg=n * (P + OL + 18 + 8 + 8 + (8 if OL else 0) + 4 + W + 2) + 16 + (8 if OL else 0),
                  step=lambda: nsx.tcp_build_dev(fields, data, data_off, out, out_off, opts=opts, opt_off=opt_off,
-                                                partial=part, raw=raw))
+                                                partial=part, raw=raw, tune=tune))
     elif cfg["kind"] == "ipv4_hdr":
         n, H = cfg["n"], cfg["hdr"]
         buf = torch.empty(n * H, dtype=torch.uint8, device=device)
@@ -284,11 +312,11 @@ def build_workload(cfg, rank, device):
             buf.view(n, H)[::1000, 8] ^= 1  # some invalid headers (TTL flipped after the fill)
             out = torch.empty((n + 63) // 64, dtype=torch.int64, device=device)
             w.update(buf=buf, out=out, bytes=n * H, alg=n * H + (n + 63) // 64 * 8,
-                     step=lambda: nsx.ipv4_hdr_verify_mask_dev(buf, H, n, mask=out))
+                     step=lambda: nsx.ipv4_hdr_verify_mask_dev(buf, H, n, mask=out, tune=tune))
         else:
             out = torch.empty(n, dtype=torch.int16, device=device)
             w.update(buf=buf, out=out, bytes=n * H, alg=n * (H + 2),
-                     step=lambda: nsx.ipv4_hdr_csum_dev(buf, H, n, mode=0, out=out))
+                     step=lambda: nsx.ipv4_hdr_csum_dev(buf, H, n, mode=0, out=out, tune=tune))
     else:
         rng = np.random.default_rng(cfg["seed"])  # same lengths on every rank, bytes differ by seed
         n = cfg["n"]
@@ -301,72 +329,111 @@ def build_workload(cfg, rank, device):
         d_offs = torch.from_numpy(offs.view(np.int64)).to(device)
         out = torch.empty(n, dtype=torch.int16, device=device)
         w.update(buf=buf, out=out, offsets=offs, bytes=total, alg=total + 2 * n + 8 * (n + 1),
-                 step=lambda: nsx.ragged_dev(buf, d_offs, out=out))
+                 step=lambda: nsx.ragged_dev(buf, d_offs, out=out, tune=tune))
     return w
 
 
-def cpu_baseline(cfg, w, seconds: float) -> dict:
-    """Go-faithful CPU restatement (oracle_go_batch_fixed / oracle_batch_ragged:
-    allocate + concatenate + serial compare-carry loop per segment, tcp.go:72-95),
-    one thread, over a bounded sample of this rank's own batch; its results are
-    also compared with the GPU's for the same segments (the checker role)."""
+def host_cores() -> dict:
+    """The host CPU share this process may use for the CPU baseline: its affinity set, capped by a
+    cgroup CPU quota and by OMP_NUM_THREADS when the host sets them (the GPU box declares each GPU's
+    share of its cores that way; os.cpu_count() there is the whole machine's)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = max(1, math.ceil(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or None
+    threads = min(x for x in (aff, quota, omp) if x)
+    return {"threads": threads, "affinity_cpus": aff, "cgroup_cpus": quota, "omp_num_threads": omp,
+            "host_cpus": os.cpu_count()}
+
+
+def _ptr(a, lo=0):
     import ctypes
+    return ctypes.c_void_p(a.ctypes.data + lo * a.itemsize)
+
+
+def _run_for(fn, seconds: float):
+    t0, reps = time.perf_counter(), 0
+    while True:
+        fn()
+        reps += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    return reps, time.perf_counter() - t0
+
+
+def cpu_baseline(cfg, w, seconds: float) -> dict:
+    """Go-faithful CPU restatement of the workload (allocate + concatenate + serial compare-carry loop
+    per segment, tcp.go:72-95; for f1 also segment.bytes(), tcp.go:98-128) over a bounded sample of
+    this rank's own batch, timed on every host core this process may use (contiguous shards — byte-
+    balanced for ragged batches — one thread each; ctypes releases the GIL) and on one thread. Both
+    legs' results are compared with the GPU's for the same segments (the checker role)."""
+    from concurrent.futures import ThreadPoolExecutor
     import numpy as np
     import torch
     sys.path.insert(0, ROOT)
     from oracle import csum_oracle as O
     lib = O.c_oracle()
-    torch.cuda.synchronize()
-    wire_ok = True  # workload 6 also compares the wire images
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    cores = host_cores()
+    T = cores["threads"]
     extra = None
+    check = {}
     if cfg["kind"] == "fixed":
         n, L, S = cfg["n"], cfg["seg_len"], cfg["stride"]
         m = min(n, max(1, (256 << 20) // S))  # sample: the first m segments (≤ 256 MiB)
         sample = w["buf"][: (m - 1) * S + L].cpu().numpy()
         gpu = w["out"][:m].cpu().numpy().view(np.uint16)
         out = np.empty(m, np.uint16)
-        t0, reps = time.perf_counter(), 0
-        while True:
-            lib.oracle_go_batch_fixed(sample.ctypes.data_as(ctypes.c_void_p), S, L, m, None, 0,
-                                      out.ctypes.data_as(ctypes.c_void_p))
-            reps += 1
-            if time.perf_counter() - t0 >= seconds:
-                break
-        dt = time.perf_counter() - t0
-        nbytes = reps * m * L
-        desc = f"first {m} segments x {L}B of rank 0's batch, {reps} pass(es), Go-faithful serial loop"
-        extra = cpu_extra_lines(lib, sample, S, L, m, out, max(1.0, seconds / 4))
+        bounds = [m * t // T for t in range(T + 1)]
+
+        def go(lo, hi):
+            lib.oracle_go_batch_fixed(_ptr(sample, lo * S), S, L, hi - lo, None, 0, _ptr(out, lo))
+        nbytes, desc = m * L, f"first {m} segments x {L}B of rank 0's batch"
+        check["segments"] = lambda: np.array_equal(out, gpu)
     elif cfg["kind"] == "tcp_build":
         n, P, OL = cfg["n"], cfg["payload"], cfg.get("opt", 0)
         W = P + 20 + OL
         m = min(n, 65536)  # sample: the first 64K segments (~94 MiB of wire)
-        fields = {k: v[:m].cpu().numpy().view(dt) for (k, v), dt in
-                  zip(((k, w["fields"][k]) for k in O.TCP_FIELDS), O.TCP_FIELD_DTYPES)}
+        cols = [np.ascontiguousarray(w["fields"][k][:m].cpu().numpy().view(dt))
+                for k, dt in zip(O.TCP_FIELDS, O.TCP_FIELD_DTYPES)]
         data = w["data"][: m * P].cpu().numpy()
         a = w["addrs"][:, :m].cpu().numpy()
-        pseudo = np.concatenate([a[0], a[1], np.tile(np.array([0, 6, W >> 8, W & 0xFF], np.uint8), (m, 1))], 1)
+        pseudo = np.ascontiguousarray(np.concatenate(
+            [a[0], a[1], np.tile(np.array([0, 6, W >> 8, W & 0xFF], np.uint8), (m, 1))], 1))
         data_off = np.arange(m + 1, dtype=np.uint64) * np.uint64(P)
         out_off = np.arange(m + 1, dtype=np.uint64) * np.uint64(W)
         gpu = w["out"][:m].cpu().numpy().view(np.uint16)
         gpu_wire = w["wire"][: m * W].cpu().numpy()
+        wire = np.zeros(m * W, np.uint8)
+        out = np.empty(m, np.uint16)
+        bounds = [m * t // T for t in range(T + 1)]
         if OL:
-            opts = w["opts"][: m * OL].cpu().numpy()
+            opts = np.ascontiguousarray(w["opts"][: m * OL].cpu().numpy())
             opt_off = np.arange(m + 1, dtype=np.uint64) * np.uint64(OL)
-            build = lambda: O.c_go_tcp_build_opts(fields, opts, opt_off, data, data_off, out_off, pseudo)
+
+            def go(lo, hi):
+                rc = lib.oracle_go_tcp_build_batch_opts(*[_ptr(c, lo) for c in cols], _ptr(opts), _ptr(opt_off, lo),
+                                                        _ptr(data), _ptr(data_off, lo), _ptr(pseudo, lo * 12), 12,
+                                                        hi - lo, _ptr(wire), _ptr(out_off, lo), _ptr(out, lo))
+                assert rc == 0
         else:
-            build = lambda: O.c_go_tcp_build(fields, data, data_off, out_off, pseudo)
-        t0, reps = time.perf_counter(), 0
-        while True:
-            wire, out = build()
-            reps += 1
-            if time.perf_counter() - t0 >= seconds:
-                break
-        dt = time.perf_counter() - t0
-        nbytes = reps * m * W
-        desc = (f"first {m} segments of rank 0's batch, {reps} pass(es), Go-faithful sender loop: bytes()"
+            def go(lo, hi):
+                rc = lib.oracle_go_tcp_build_batch(*[_ptr(c, lo) for c in cols], _ptr(data), _ptr(data_off, lo),
+                                                   _ptr(pseudo, lo * 12), 12, hi - lo, _ptr(wire), _ptr(out_off, lo),
+                                                   _ptr(out, lo))
+                assert rc == 0
+        nbytes = m * W
+        desc = (f"first {m} segments of rank 0's batch: the Go sender loop — bytes()"
                 f"{' with ' + str(OL) + ' B of options' if OL else ''} + computeChecksum(12B pseudo-header) + "
                 "field store per segment")
-        wire_ok = bool(np.array_equal(wire, gpu_wire))
+        check["segments"] = lambda: np.array_equal(out, gpu)
+        check["wire_images"] = lambda: np.array_equal(wire, gpu_wire)
     elif cfg["kind"] == "ipv4_hdr":
         n, H = cfg["n"], cfg["hdr"]
         m = min(n, 1 << 22)
@@ -375,85 +442,68 @@ def cpu_baseline(cfg, w, seconds: float) -> dict:
         gpu = (w["out"][: m // 64].cpu().numpy().view(np.uint64) if mask
                else w["out"][:m].cpu().numpy().view(np.uint16))
         raw = np.empty(m, np.uint16)
-        out = None
-        t0, reps = time.perf_counter(), 0
-        while True:
-            lib.oracle_go_batch_fixed(sample.ctypes.data_as(ctypes.c_void_p), H, H, m, None, 0,
-                                      raw.ctypes.data_as(ctypes.c_void_p))
-            # IHL 5 on every header of this workload, so well-formed; valid iff the sum is 0xFFFF
-            out = np.packbits(raw == 0xFFFF, bitorder="little").view(np.uint64) if mask else raw
-            reps += 1
-            if time.perf_counter() - t0 >= seconds:
-                break
-        dt = time.perf_counter() - t0
-        nbytes = reps * m * H
-        desc = (f"first {m} headers of rank 0's batch, {reps} pass(es), the reference's serial checksum loop per "
-                "header" + (" + bit packing of sum == 0xFFFF" if mask else ""))
+        bounds = [m * t // T // 64 * 64 for t in range(T)] + [m]
+
+        def go(lo, hi):
+            lib.oracle_go_batch_fixed(_ptr(sample, lo * H), H, H, hi - lo, None, 0, _ptr(raw, lo))
+        nbytes = m * H
+        desc = (f"first {m} headers of rank 0's batch, the reference's serial checksum loop per header"
+                + (" + bit packing of sum == 0xFFFF" if mask else ""))
+        # IHL 5 on every header of this workload, so well-formed; valid iff the sum is 0xFFFF
+        whole = m // 64 * 64  # mask words wholly inside the sample
+        check["headers"] = (lambda: np.array_equal(
+            np.packbits(raw[:whole] == 0xFFFF, bitorder="little").view(np.uint64), gpu)) if mask else (
+            lambda: np.array_equal(raw, gpu))
     else:
-        offs = w["offsets"]
-        m = int(min(len(offs) - 1, 50000))
-        hi = int(offs[m])
-        sample = w["buf"][:hi].cpu().numpy()
+        offs_all = w["offsets"]
+        m = int(min(len(offs_all) - 1, 50000))
+        hi_b = int(offs_all[m])
+        sample = w["buf"][:hi_b].cpu().numpy()
+        offs = np.ascontiguousarray(offs_all[: m + 1])
         gpu = w["out"][:m].cpu().numpy().view(np.uint16)
         out = np.empty(m, np.uint16)
-        so = np.ascontiguousarray(offs[: m + 1])
-        t0, reps = time.perf_counter(), 0
-        while True:
-            for i in range(m):
-                out[i] = lib.oracle_go_checksum(None, 0, sample[int(so[i]):].ctypes.data_as(ctypes.c_void_p),
-                                                int(so[i + 1] - so[i]))
-            reps += 1
-            if time.perf_counter() - t0 >= seconds:
-                break
-        dt = time.perf_counter() - t0
-        nbytes = reps * hi
-        desc = f"first {m} ragged segments of rank 0's batch, {reps} pass(es), Go-faithful serial loop"
-    return {"value": round(nbytes / dt / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
-            "sample": desc, "seconds": round(dt, 2), "sample_parity_vs_gpu": bool(np.array_equal(out, gpu)) and wire_ok,
-            "host_cpus": os.cpu_count(), "extra": extra}
+        bounds = [int(np.searchsorted(offs, hi_b * t // T)) for t in range(T)] + [m]  # byte-balanced
+
+        def go(lo, hi):
+            lib.oracle_go_batch_ragged(_ptr(sample), _ptr(offs, lo), hi - lo, None, 0, _ptr(out, lo))
+        nbytes, desc = hi_b, f"first {m} ragged segments of rank 0's batch"
+        check["segments"] = lambda: np.array_equal(out, gpu)
+    with ThreadPoolExecutor(T) as ex:
+        def all_cores():
+            list(ex.map(lambda t: go(bounds[t], bounds[t + 1]), range(T)))
+        reps_t, dt_t = _run_for(all_cores, seconds / 2)
+        ok_t = all(f() for f in check.values())
+    reps_1, dt_1 = _run_for(lambda: go(0, bounds[-1]), seconds / 2)
+    ok_1 = all(f() for f in check.values())
+    if cfg["kind"] == "fixed":
+        extra = cpu_extra_lines(sample, S, L, m, out, max(1.0, seconds / 4), T)
+    return {"value": round(reps_t * nbytes / dt_t / GIB, 4), "unit": "GiB/s", "cores": T, "kind": "port",
+            "sample": f"{desc}, {reps_t} pass(es) on {T} threads (Go-faithful loop, contiguous shards)",
+            "seconds": round(dt_t, 2),
+            "single_thread": {"value": round(reps_1 * nbytes / dt_1 / GIB, 4), "unit": "GiB/s", "cores": 1,
+                              "passes": reps_1, "seconds": round(dt_1, 2)},
+            "sample_parity_vs_gpu": bool(ok_t and ok_1), "host": cores, "extra": extra}
 
 
-CPU_THREADS = 16  # the GPU box's CPU share per GPU (nproc shows the whole machine)
-
-
-def cpu_extra_lines(lib, sample, S, L, m, want, seconds):
-    """Reference CPU lines beside the 1-thread Go-faithful value:
-    the same Go-faithful loop on CPU_THREADS threads (contiguous shards, ctypes
-    releases the GIL), and a vectorised u64-accumulate restatement
-    (oracle/csum_cpu_fast.c) on 1 and CPU_THREADS threads. Same sample; each
-    result is checked against the 1-thread output."""
-    import ctypes
-    from concurrent.futures import ThreadPoolExecutor
+def cpu_extra_lines(sample, S, L, m, want, seconds, threads):
+    """The honest best-CPU line beside the Go-faithful one: a vectorised u64-accumulate
+    restatement (oracle/csum_cpu_fast.c) on 1 and `threads` threads, same sample; each result is
+    checked against the Go-faithful output."""
     import numpy as np
     from oracle import csum_oracle as O
     fast = O.c_fast()
     out = np.empty(m, np.uint16)
     ptr = sample.ctypes.data
 
-    def go_mt():
-        def shard(t):
-            lo, hi = m * t // CPU_THREADS, m * (t + 1) // CPU_THREADS
-            lib.oracle_go_batch_fixed(ctypes.c_void_p(ptr + lo * S), S, L, hi - lo, None, 0,
-                                      out[lo:].ctypes.data_as(ctypes.c_void_p))
-        with ThreadPoolExecutor(CPU_THREADS) as ex:
-            list(ex.map(shard, range(CPU_THREADS)))
-
     def run(fn):
-        t0, reps = time.perf_counter(), 0
-        while True:
-            fn()
-            reps += 1
-            if time.perf_counter() - t0 >= seconds:
-                break
-        dt = time.perf_counter() - t0
+        reps, dt = _run_for(fn, seconds)
         return {"value": round(reps * m * L / dt / GIB, 3), "unit": "GiB/s", "parity": bool(np.array_equal(out, want))}
 
-    res = {"go_faithful_threads": dict(run(go_mt), cores=CPU_THREADS)}
-    res["optimized_1_thread"] = dict(run(lambda: fast.cpu_fast_batch_fixed(ptr, S, L, m, out.ctypes.data, 1)), cores=1)
-    res["optimized_threads"] = dict(run(lambda: fast.cpu_fast_batch_fixed(ptr, S, L, m, out.ctypes.data,
-                                                                          CPU_THREADS)), cores=CPU_THREADS)
-    res["note"] = ("optimized = oracle/csum_cpu_fast.c (8-byte loads, u64 accumulators, -O3 x86-64-v3): the best-CPU "
-                   "line; go_faithful = the reference's algorithm as written")
+    res = {"optimized_1_thread": dict(run(lambda: fast.cpu_fast_batch_fixed(ptr, S, L, m, out.ctypes.data, 1)), cores=1),
+           "optimized_threads": dict(run(lambda: fast.cpu_fast_batch_fixed(ptr, S, L, m, out.ctypes.data, threads)),
+                                     cores=threads),
+           "note": "optimized = oracle/csum_cpu_fast.c (8-byte loads, u64 accumulators, -O3 x86-64-v3): the best-CPU "
+                   "line; the baseline value is the reference's algorithm as written"}
     return res
 
 
@@ -467,28 +517,59 @@ def load_traffic(config_id: int):
     return d
 
 
-def main(argv=None):
+def dry_run(args) -> int:
+    """--dry-run: the rank/launch/timing plumbing with the CPU oracle as each rank's step (no GPU)."""
+    sys.path.insert(0, ROOT)
+    from oracle import csum_oracle as O
+    dist = Dist("gloo")
+    n, L = 256, 1500
+    buf = O.c_splitmix64(0x1071 + dist.rank, n * L)
+    wall, launch_ms = timed_loop(lambda: O.c_batch(buf, n, stride=L, seg_len=L, threads=1), lambda: None,
+                                 dist.barrier, args.steps, args.warmup)
+    wall_max = dist.max(wall)
+    line = result_line(world=dist.world, steps=args.steps, warmup=args.warmup, wall_max=wall_max,
+                       bytes_per_rank_step=n * L, units_total=n * dist.world, workload="dry run", cfg={"n": n, "seed": 0x1071},
+                       launch_ms=launch_ms, alg_bytes_per_launch=n * L + 2 * n, cpu_baseline=None, traffic=None)
+    line.update(dry_run=True, data="dry run: the CPU oracle stands in for the GPU kernel; not a measurement",
+                ranks=dist.world, backend="gloo")
+    if dist.rank == 0:
+        print(json.dumps(line), flush=True)
+    dist.close()
+    return 0
+
+
+def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else list(argv)
     args = parse_args(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args.gpus, argv)  # before anything touches a GPU
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a different GPU count",
+              file=sys.stderr)
+        return 2
+    if args.dry_run:
+        return dry_run(args)
     import torch
     import nsx
     # RCCL ("nccl") is the backend; NSX_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share a device
-    # round-robin), e.g. 2 ranks on a 1-GPU box
-    dist = Dist(os.environ.get("NSX_BENCH_BACKEND", "nccl"))
-    if dist.world != args.gpus and dist.on:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {dist.world}; using WORLD_SIZE", file=sys.stderr)
-    if not torch.cuda.is_available():
+    # round-robin, and the line says so), e.g. 2 ranks on a 1-GPU box
+    backend = os.environ.get("NSX_BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    if ndev == 0 or not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU: the checksum path is HIP-only (no CPU fallback)")
-    dev_id = dist.local_rank % max(1, torch.cuda.device_count()) if dist.on else 0
+    if world > ndev and backend == "nccl":
+        print(f"bench.py: {world} ranks but {ndev} visible GPU(s): one rank per GPU is required "
+              "(NSX_BENCH_BACKEND=gloo runs a labelled rehearsal)", file=sys.stderr)
+        return 2
+    dist = Dist(backend)
+    dev_id = dist.local_rank % ndev if dist.on else 0
     torch.cuda.set_device(dev_id)
     device = torch.device("cuda", dev_id)
-    for kv in args.param:
-        k, v = kv.split("=")
-        nsx.set_param(PARAMS[k], int(v))
+    tune = parse_tune(args.tune) or None
 
     cfg = WORKLOADS[args.config]
-    knobs = dict(kv.split("=") for kv in args.param)
-    cfg = dict(cfg, **{k: int(knobs[k]) for k in ("window_bytes", "kernel") if k in knobs})
-    w = build_workload(cfg, dist.rank, device)
+    w = build_workload(cfg, dist.rank, device, tune)
     torch.cuda.synchronize()
     # Setup, not measurement: after data generation the GPU's clocks sit in an
     # idle state and the first ~50 launches run up to 20 % slow (tools/drift.py).
@@ -513,15 +594,19 @@ def main(argv=None):
     line = result_line(world=dist.world, steps=args.steps, warmup=args.warmup, wall_max=wall_max,
                        bytes_per_rank_step=w["bytes"], units_total=cfg["n"] * dist.world, workload=cfg["name"],
                        cfg=cfg, launch_ms=launch_ms, alg_bytes_per_launch=w["alg"], cpu_baseline=cpu,
-                       # the committed PMC traffic was profiled at the default knobs
-                       traffic=None if args.param else load_traffic(args.config), metric=cfg.get("metric", METRIC),
+                       # the committed PMC traffic was profiled at the default launch shape
+                       traffic=None if tune else load_traffic(args.config), metric=cfg.get("metric", METRIC),
                        launches=w.get("launches", 1))
-    if args.param:
-        line["config"]["params"] = args.param
+    line["backend"] = backend if dist.on else None
+    if dist.on and world > ndev:
+        line.update(rehearsal=True, distinct_devices=ndev)
+    if tune:
+        line["config"]["tune"] = tune
     if dist.rank == 0:
         print(json.dumps(line), flush=True)
     dist.close()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

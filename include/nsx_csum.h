@@ -43,7 +43,7 @@ extern "C" {
 #define NSX_ENODEV (-19)  /* no usable GPU / bad device ordinal */
 #define NSX_EINVAL (-22)  /* null pointer with nonzero length, bad sizes */
 
-#define NSX_ABI_VERSION 1
+#define NSX_ABI_VERSION 2  /* 2: process-wide tuning knobs removed (nsx_tune.h) */
 
 typedef void* nsx_stream_t; /* hipStream_t, opaque to C/Go callers */
 
@@ -216,26 +216,12 @@ int nsx_fill_splitmix64_dev(void* d_buf, uint64_t byte_off, uint64_t nbytes, uin
                             nsx_stream_t stream);
 
 /* ----------------------------------------------------------------------------
- * Introspection / tuning.
+ * Introspection. (Benchmark/test launch overrides are per call, in
+ * include/nsx_tune.h — not part of this boundary.)
  */
 int nsx_abi_version(void);
 int nsx_device_count(int* out_count);        /* NSX_OK with 0 when no GPU */
 const char* nsx_strerror(int code);
-
-/* Kernel-variant knobs for benchmarking (process-wide; 0 = the default).
- * Not needed for correctness; every variant is bit-exact. */
-#define NSX_PARAM_BLOCKS_PER_CU   1  /* persistent grid, 1..8 blocks of 256 threads per CU (default per path) */
-#define NSX_PARAM_SEGS_PER_WAVE   2  /* per-segment kernels: 1, 2, 4 or 8 segments per wave pass; packed-20 B IPv4 header kernel: 1, 2 (default) or 4 tasks in flight per wave; nsx_tcp_build_dev: 1 or 2 (default) segments per pipelined register set */
-#define NSX_PARAM_NONTEMPORAL     3  /* 1 nt loads (default), 2 default-policy loads; nsx_tcp_build_dev: default plain, 1 nt, 3 nt loads + plain stores, 4 plain loads + nt stores */
-#define NSX_PARAM_BLOCK_MODE      4  /* 0 auto (a block per segment when n < 4*CUs), 1 never, 2 always */
-#define NSX_PARAM_XCD_MAP         5  /* task deal: 1 XCD-contiguous regions (default), 2 grid-stride, 3 one contiguous range per wave, 4 byte-balanced contiguous range per wave (ragged scan kernel; its default) */
-#define NSX_PARAM_KERNEL          6  /* 1 row-stream, 2 per-segment, 3 buffer-load, 4 prefix-scan (ragged), 5 pipelined buffer-load (fixed; the aligned default), 6 pipelined prefix-scan (ragged), 7 pipelined long segments (fixed > 4 KiB); IPv4 headers: 1 per-thread, 2 LDS-dense, 3 packed-20 B flat unpipelined, 4 packed-20 B with raw sums written in bursts from LDS; TCP build: 2 unpipelined, 3 general pipelined composition for every layout; 0 = per-path default */
-#define NSX_PARAM_STREAM_ROWS     7  /* row-stream / scan: 4, 8 (default) or 16 KiB in flight per wave */
-#define NSX_PARAM_RUN_SEGS        8  /* ragged scan kernel: segments per wave task, 1..63 (default 63) */
-#define NSX_PARAM_XCD_CHUNK       9  /* XCD deal (fixed-stride, long-segment, TCP build, packed IPv4 header kernels): XCD x takes chunks x, x+8, ... of 2^k wave tasks; 0 = auto (<= 24 MiB chunks, >= 64 of them), k = 1..20 fixed, any other value = contiguous eighths */
-#define NSX_PARAM_WINDOW_BYTES   10  /* fixed-stride buffer-load path (segments <= 4 KiB): launch a batch as back-to-back windows of at most this many bytes (rounded down to whole segments); 0 = auto, -1 = one launch */
-int nsx_set_param(int param, int64_t value);
-int nsx_get_param(int param, int64_t* value);
 
 /* Receiver/sender helpers (tcp.go:68-71, tcp_test.go:28-31). */
 static inline uint16_t nsx_field(uint16_t raw_sum) { return (uint16_t)~raw_sum; }

@@ -1,0 +1,75 @@
+/*
+ * nsx_tune.h — per-call launch overrides for benchmarks and tests.
+ *
+ * NOT part of the drop-in boundary (include/nsx_csum.h): a transport never
+ * needs these. Every product entry point uses the per-path defaults measured
+ * best on MI355X; the *_tuned twins below take an explicit
+ * nsx_tune per call — there is no process-wide tuning state, so concurrent
+ * callers with different settings cannot interfere. A NULL tune, or a field
+ * left 0, means the default. Every setting is bit-exact; they change only the
+ * launch shape (grid, work split, windows) or force one of the code paths the
+ * defaults pick by layout, so the parity tests can reach each path on every
+ * layout.
+ */
+#ifndef NSX_TUNE_H
+#define NSX_TUNE_H
+
+#include "nsx_csum.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NSX_TUNE_KERNEL_AUTO          0  /* the path the layout selects */
+#define NSX_TUNE_KERNEL_HDR_THREAD    1  /* IPv4 headers: one thread per header (any stride) */
+#define NSX_TUNE_KERNEL_HDR_DENSE     2  /* IPv4 headers: LDS-staged 64-header spans (stride <= 64) */
+#define NSX_TUNE_KERNEL_BUILD_PLAIN   2  /* TCP build: no software pipelining */
+#define NSX_TUNE_KERNEL_BUILD_GENERAL 3  /* TCP build: the general pipelined composition for every layout */
+
+typedef struct nsx_tune {
+    int32_t blocks_per_cu;     /* persistent grid: 1..8 blocks of 256 threads per CU */
+    int32_t segs_per_wave;     /* fixed batches of <= 4 KiB segments: segments per wave task (1, 2, 4, 8) */
+    int32_t block_mode;        /* 0 auto (a block per segment when n < 4 * CUs), 1 never, 2 always */
+    int32_t rows;              /* ragged / frame scan kernels: 1 KiB rows per load batch (4, 8, 16) */
+    int32_t run_segs;          /* ragged scan kernel: segments per wave task (1..63) */
+    int32_t xcd_chunk;         /* XCD deal: 0 auto, 1..20 = chunks of 2^k wave tasks, -1 contiguous eighths */
+    int64_t window_bytes;      /* fixed <= 4 KiB segments: back-to-back launches of <= this many bytes;
+                                  0 auto (batches >= 3.2 GB as ~1.6 GB windows), -1 one launch */
+    int32_t kernel;            /* NSX_TUNE_KERNEL_* */
+    int32_t shards_per_device; /* host batch calls: contiguous shards per GPU, each with its own host thread,
+                                  streams and staging (default 1) */
+    int32_t reserved[6];
+} nsx_tune;
+
+int nsx_csum_fixed_dev_tuned(const void* d_base, uint64_t stride, uint32_t seg_len, uint64_t n,
+                             const uint32_t* d_prefix_partial, uint16_t* d_out, nsx_stream_t stream,
+                             const nsx_tune* tune);
+int nsx_csum_ragged_dev_tuned(const void* d_base, const uint64_t* d_offsets, uint64_t n,
+                              const uint32_t* d_prefix_partial, uint16_t* d_out, nsx_stream_t stream,
+                              const nsx_tune* tune);
+int nsx_verify_ragged_dev_tuned(const void* d_base, const uint64_t* d_offsets, uint64_t n,
+                                const uint32_t* d_prefix_partial, uint8_t* d_ok, uint16_t* d_raw,
+                                nsx_stream_t stream, const nsx_tune* tune);
+int nsx_tcp_build_dev_tuned(const nsx_tcp_hdr_soa* hdr, const uint8_t* d_opts, const uint64_t* d_opt_off,
+                            const uint8_t* d_data, const uint64_t* d_data_off, uint64_t data_bytes,
+                            const uint32_t* d_prefix_partial, uint64_t n, uint8_t* d_out, const uint64_t* d_out_off,
+                            uint16_t* d_raw, nsx_stream_t stream, const nsx_tune* tune);
+int nsx_ipv4_hdr_csum_dev_tuned(void* d_base, uint64_t stride, uint32_t hdr_off, uint64_t n, int mode,
+                                uint16_t* d_out_raw, nsx_stream_t stream, const nsx_tune* tune);
+int nsx_ipv4_hdr_verify_mask_dev_tuned(const void* d_base, uint64_t stride, uint32_t hdr_off, uint64_t n,
+                                       uint64_t* d_mask, nsx_stream_t stream, const nsx_tune* tune);
+int nsx_csum_fixed_host_tuned(const uint8_t* h_base, uint64_t stride, uint32_t seg_len, uint64_t n,
+                              const uint32_t* h_prefix_partial, uint16_t* h_out, int num_gpus,
+                              const nsx_tune* tune);
+int nsx_csum_ragged_host_tuned(const uint8_t* h_base, const uint64_t* h_offsets, uint64_t n,
+                               const uint32_t* h_prefix_partial, uint16_t* h_out, int num_gpus,
+                               const nsx_tune* tune);
+
+/* Kernel launches one nsx_csum_fixed_dev(_tuned) call makes for this batch on the current device (its
+ * back-to-back windows; 1 for most batches), for per-launch timing in benchmarks. */
+int nsx_fixed_launch_count(uint64_t stride, uint32_t seg_len, uint64_t n, const nsx_tune* tune, uint64_t* out_count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NSX_TUNE_H */

@@ -8,21 +8,17 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
-#include <atomic>
 #include <cstring>
 #include <mutex>
 #include <thread>
 #include <vector>
 
 #include "../../include/nsx_csum.h"
+#include "../../include/nsx_tune.h"
 #include "csum_kernels.h"
 #include "host_csum.h"
 
 namespace {
-
-// ---------------------------------------------------------------- params
-constexpr int kNumParams = 11;
-std::atomic<int64_t> g_param[kNumParams];  // index = NSX_PARAM_*; 0 = default
 
 constexpr int kMaxDevices = 64;
 
@@ -67,9 +63,34 @@ int current_device() {
     return dev_info(d) ? d : -1;
 }
 
-nsx::LaunchCfg make_cfg(int dev, uint64_t n, bool /*segs_can_split*/) {
-    return nsx::default_launch_cfg(dev_info(dev)->cus, n);
+int map_err(hipError_t e);
+
+}  // namespace
+
+namespace nsx {
+
+// Launch configuration of one call: the device's CU count + the caller's overrides (nsx_tune.h).
+LaunchCfg launch_cfg(int cus, const nsx_tune* t) {
+    LaunchCfg c;
+    c.cus = cus;
+    if (t) {
+        c.blocks_per_cu = t->blocks_per_cu;
+        c.segs_per_wave = t->segs_per_wave;
+        c.block_mode = t->block_mode;
+        c.rows = t->rows;
+        c.run_segs = t->run_segs;
+        c.xcd_chunk = t->xcd_chunk;
+        c.window_bytes = t->window_bytes;
+        c.kernel = t->kernel;
+    }
+    return c;
 }
+
+}  // namespace nsx
+
+namespace {
+
+nsx::LaunchCfg make_cfg(int dev, const nsx_tune* t) { return nsx::launch_cfg(dev_info(dev)->cus, t); }
 
 int map_err(hipError_t e) {
     if (e == hipSuccess) return NSX_OK;
@@ -80,27 +101,6 @@ int map_err(hipError_t e) {
 }
 
 }  // namespace
-
-namespace nsx {
-
-LaunchCfg default_launch_cfg(int cus, uint64_t /*n*/) {
-    auto get = [](int p) { return (int)g_param[p].load(); };
-    LaunchCfg c;
-    c.cus = cus;
-    c.blocks_per_cu = get(NSX_PARAM_BLOCKS_PER_CU);
-    c.segs_per_wave = get(NSX_PARAM_SEGS_PER_WAVE);
-    c.nontemporal = get(NSX_PARAM_NONTEMPORAL);
-    c.block_mode = get(NSX_PARAM_BLOCK_MODE);
-    c.xcd_map = get(NSX_PARAM_XCD_MAP);
-    c.kernel = get(NSX_PARAM_KERNEL);
-    c.rows = get(NSX_PARAM_STREAM_ROWS);
-    c.run_segs = get(NSX_PARAM_RUN_SEGS);
-    c.xcd_chunk = get(NSX_PARAM_XCD_CHUNK);
-    c.window_bytes = g_param[NSX_PARAM_WINDOW_BYTES].load();
-    return c;
-}
-
-}  // namespace nsx
 
 extern "C" {
 
@@ -123,18 +123,6 @@ const char* nsx_strerror(int code) {
     }
 }
 
-int nsx_set_param(int param, int64_t value) {
-    if (param < 1 || param >= kNumParams) return NSX_EINVAL;
-    g_param[param] = value;
-    return NSX_OK;
-}
-
-int nsx_get_param(int param, int64_t* value) {
-    if (!value || param < 1 || param >= kNumParams) return NSX_EINVAL;
-    *value = g_param[param];
-    return NSX_OK;
-}
-
 // ------------------------------------------------------------ single segment
 int nsx_csum16(const uint8_t* prefix, size_t prefix_len, const uint8_t* seg, size_t seg_len,
                uint16_t* out_raw_sum) {
@@ -144,41 +132,65 @@ int nsx_csum16(const uint8_t* prefix, size_t prefix_len, const uint8_t* seg, siz
 }
 
 // ------------------------------------------------------------ device batches
+// Each product entry point is its *_tuned twin (include/nsx_tune.h) with no overrides.
 int nsx_csum_fixed_dev(const void* d_base, uint64_t stride, uint32_t seg_len, uint64_t n,
                        const uint32_t* d_prefix_partial, uint16_t* d_out, nsx_stream_t stream) {
+    return nsx_csum_fixed_dev_tuned(d_base, stride, seg_len, n, d_prefix_partial, d_out, stream, nullptr);
+}
+
+int nsx_csum_fixed_dev_tuned(const void* d_base, uint64_t stride, uint32_t seg_len, uint64_t n,
+                             const uint32_t* d_prefix_partial, uint16_t* d_out, nsx_stream_t stream,
+                             const nsx_tune* tune) {
     if (n == 0) return NSX_OK;
     if (!d_out || (seg_len && !d_base)) return NSX_EINVAL;
-    if (n > 1 && stride == 0 && seg_len) { /* every segment aliases the first: allowed */ }
+    // stride 0 with n > 1 is allowed: every segment aliases the first
     if (n > ((uint64_t)1 << 40)) return NSX_EINVAL;
     const int dev = current_device();
     if (dev < 0) return NSX_ENODEV;
-    nsx::LaunchCfg c = make_cfg(dev, n, true);
-    return map_err(nsx::launch_fixed(c, d_base, stride, seg_len, n, d_prefix_partial, d_out,
+    return map_err(nsx::launch_fixed(make_cfg(dev, tune), d_base, stride, seg_len, n, d_prefix_partial, d_out,
                                      static_cast<hipStream_t>(stream)));
+}
+
+int nsx_fixed_launch_count(uint64_t stride, uint32_t seg_len, uint64_t n, const nsx_tune* tune, uint64_t* out_count) {
+    if (!out_count) return NSX_EINVAL;
+    const int dev = current_device();
+    if (dev < 0) return NSX_ENODEV;
+    *out_count = nsx::fixed_launch_count(make_cfg(dev, tune), 0, stride, seg_len, n);
+    return NSX_OK;
 }
 
 int nsx_csum_ragged_dev(const void* d_base, const uint64_t* d_offsets, uint64_t n,
                         const uint32_t* d_prefix_partial, uint16_t* d_out, nsx_stream_t stream) {
+    return nsx_csum_ragged_dev_tuned(d_base, d_offsets, n, d_prefix_partial, d_out, stream, nullptr);
+}
+
+int nsx_csum_ragged_dev_tuned(const void* d_base, const uint64_t* d_offsets, uint64_t n,
+                              const uint32_t* d_prefix_partial, uint16_t* d_out, nsx_stream_t stream,
+                              const nsx_tune* tune) {
     if (n == 0) return NSX_OK;
     if (!d_out || !d_offsets || !d_base) return NSX_EINVAL;
     if (n > ((uint64_t)1 << 40)) return NSX_EINVAL;
     const int dev = current_device();
     if (dev < 0) return NSX_ENODEV;
-    nsx::LaunchCfg c = make_cfg(dev, n, true);
-    return map_err(nsx::launch_ragged(c, d_base, d_offsets, n, d_prefix_partial, d_out, nullptr,
+    return map_err(nsx::launch_ragged(make_cfg(dev, tune), d_base, d_offsets, n, d_prefix_partial, d_out, nullptr,
                                       static_cast<hipStream_t>(stream)));
 }
 
 int nsx_verify_ragged_dev(const void* d_base, const uint64_t* d_offsets, uint64_t n,
                           const uint32_t* d_prefix_partial, uint8_t* d_ok, uint16_t* d_raw,
                           nsx_stream_t stream) {
+    return nsx_verify_ragged_dev_tuned(d_base, d_offsets, n, d_prefix_partial, d_ok, d_raw, stream, nullptr);
+}
+
+int nsx_verify_ragged_dev_tuned(const void* d_base, const uint64_t* d_offsets, uint64_t n,
+                                const uint32_t* d_prefix_partial, uint8_t* d_ok, uint16_t* d_raw,
+                                nsx_stream_t stream, const nsx_tune* tune) {
     if (n == 0) return NSX_OK;
     if (!d_ok || !d_offsets || !d_base) return NSX_EINVAL;
     if (n > ((uint64_t)1 << 40)) return NSX_EINVAL;
     const int dev = current_device();
     if (dev < 0) return NSX_ENODEV;
-    nsx::LaunchCfg c = make_cfg(dev, n, true);
-    return map_err(nsx::launch_ragged(c, d_base, d_offsets, n, d_prefix_partial, d_raw, d_ok,
+    return map_err(nsx::launch_ragged(make_cfg(dev, tune), d_base, d_offsets, n, d_prefix_partial, d_raw, d_ok,
                                       static_cast<hipStream_t>(stream)));
 }
 
@@ -233,6 +245,14 @@ int nsx_tcp_build_dev(const nsx_tcp_hdr_soa* hdr, const uint8_t* d_opts, const u
                       const uint8_t* d_data, const uint64_t* d_data_off, uint64_t data_bytes,
                       const uint32_t* d_prefix_partial, uint64_t n, uint8_t* d_out, const uint64_t* d_out_off,
                       uint16_t* d_raw, nsx_stream_t stream) {
+    return nsx_tcp_build_dev_tuned(hdr, d_opts, d_opt_off, d_data, d_data_off, data_bytes, d_prefix_partial, n, d_out,
+                                   d_out_off, d_raw, stream, nullptr);
+}
+
+int nsx_tcp_build_dev_tuned(const nsx_tcp_hdr_soa* hdr, const uint8_t* d_opts, const uint64_t* d_opt_off,
+                            const uint8_t* d_data, const uint64_t* d_data_off, uint64_t data_bytes,
+                            const uint32_t* d_prefix_partial, uint64_t n, uint8_t* d_out, const uint64_t* d_out_off,
+                            uint16_t* d_raw, nsx_stream_t stream, const nsx_tune* tune) {
     if (n == 0) return NSX_OK;
     if (!hdr || !hdr->src_port || !hdr->dst_port || !hdr->seq_num || !hdr->ack_num || !hdr->offset ||
         !hdr->control || !hdr->window || !hdr->urgent_ptr || !d_data_off || !d_out || !d_out_off ||
@@ -240,48 +260,51 @@ int nsx_tcp_build_dev(const nsx_tcp_hdr_soa* hdr, const uint8_t* d_opts, const u
         return NSX_EINVAL;
     const int dev = current_device();
     if (dev < 0) return NSX_ENODEV;
-    const DevInfo* di = dev_info(dev);
-    const int64_t bpc = g_param[NSX_PARAM_BLOCKS_PER_CU].load();
     const nsx::TcpHdrSoA h{hdr->src_port, hdr->dst_port, hdr->seq_num, hdr->ack_num,
                            hdr->offset,   hdr->control,  hdr->window,  hdr->urgent_ptr};
-    return map_err(nsx::launch_tcp_build(h, d_opts, d_opt_off, d_data, d_data_off, data_bytes, d_prefix_partial, n,
-                                         d_out, d_out_off, d_raw, (uint32_t)di->cus * (uint32_t)(bpc >= 1 && bpc <= 8 ? bpc : 4),
-                                         (int)g_param[NSX_PARAM_NONTEMPORAL].load(),
-                                         (int)g_param[NSX_PARAM_XCD_CHUNK].load(), (int)g_param[NSX_PARAM_KERNEL].load(),
-                                         (int)g_param[NSX_PARAM_SEGS_PER_WAVE].load(), static_cast<hipStream_t>(stream)));
+    return map_err(nsx::launch_tcp_build(make_cfg(dev, tune), h, d_opts, d_opt_off, d_data, d_data_off, data_bytes,
+                                         d_prefix_partial, n, d_out, d_out_off, d_raw,
+                                         static_cast<hipStream_t>(stream)));
+}
+
+static int ipv4_args_ok(const void* d_base, uint64_t stride, uint32_t hdr_off, uint64_t n) {
+    if (!d_base) return NSX_EINVAL;
+    if (n > 1 && stride == 0) return NSX_EINVAL;
+    if (stride > ((uint64_t)1 << 22) || hdr_off > ((uint32_t)1 << 22)) return NSX_EINVAL;  // 32-bit block offsets
+    return NSX_OK;
 }
 
 int nsx_ipv4_hdr_csum_dev(void* d_base, uint64_t stride, uint32_t hdr_off, uint64_t n, int mode,
                           uint16_t* d_out_raw, nsx_stream_t stream) {
+    return nsx_ipv4_hdr_csum_dev_tuned(d_base, stride, hdr_off, n, mode, d_out_raw, stream, nullptr);
+}
+
+int nsx_ipv4_hdr_csum_dev_tuned(void* d_base, uint64_t stride, uint32_t hdr_off, uint64_t n, int mode,
+                                uint16_t* d_out_raw, nsx_stream_t stream, const nsx_tune* tune) {
     if (n == 0) return NSX_OK;
-    if (!d_base || (mode != 0 && mode != 1) || (mode == 0 && !d_out_raw)) return NSX_EINVAL;
-    if (n > 1 && stride == 0) return NSX_EINVAL;
-    if (stride > ((uint64_t)1 << 22) || hdr_off > ((uint32_t)1 << 22)) return NSX_EINVAL;  // 32-bit block offsets
+    if ((mode != 0 && mode != 1) || (mode == 0 && !d_out_raw)) return NSX_EINVAL;
+    if (int rc = ipv4_args_ok(d_base, stride, hdr_off, n)) return rc;
     const int dev = current_device();
     if (dev < 0) return NSX_ENODEV;
-    const DevInfo* di = dev_info(dev);
-    return map_err(nsx::launch_ipv4_hdr(static_cast<uint8_t*>(d_base), stride, hdr_off, n, mode, d_out_raw, nullptr,
-                                        di->cus, (int)g_param[NSX_PARAM_BLOCKS_PER_CU].load(),
-                                        (int)g_param[NSX_PARAM_KERNEL].load(),
-                                        (int)g_param[NSX_PARAM_SEGS_PER_WAVE].load(),
-                                        (int)g_param[NSX_PARAM_XCD_CHUNK].load(), static_cast<hipStream_t>(stream)));
+    return map_err(nsx::launch_ipv4_hdr(make_cfg(dev, tune), static_cast<uint8_t*>(d_base), stride, hdr_off, n, mode,
+                                        d_out_raw, nullptr, static_cast<hipStream_t>(stream)));
 }
 
 int nsx_ipv4_hdr_verify_mask_dev(const void* d_base, uint64_t stride, uint32_t hdr_off, uint64_t n, uint64_t* d_mask,
                                  nsx_stream_t stream) {
+    return nsx_ipv4_hdr_verify_mask_dev_tuned(d_base, stride, hdr_off, n, d_mask, stream, nullptr);
+}
+
+int nsx_ipv4_hdr_verify_mask_dev_tuned(const void* d_base, uint64_t stride, uint32_t hdr_off, uint64_t n,
+                                       uint64_t* d_mask, nsx_stream_t stream, const nsx_tune* tune) {
     if (n == 0) return NSX_OK;
-    if (!d_base || !d_mask) return NSX_EINVAL;
-    if (n > 1 && stride == 0) return NSX_EINVAL;
-    if (stride > ((uint64_t)1 << 22) || hdr_off > ((uint32_t)1 << 22)) return NSX_EINVAL;  // 32-bit block offsets
+    if (!d_mask) return NSX_EINVAL;
+    if (int rc = ipv4_args_ok(d_base, stride, hdr_off, n)) return rc;
     const int dev = current_device();
     if (dev < 0) return NSX_ENODEV;
-    const DevInfo* di = dev_info(dev);
     // mode 2 only reads the headers (the kernels take a non-const base for fill mode)
-    return map_err(nsx::launch_ipv4_hdr(static_cast<uint8_t*>(const_cast<void*>(d_base)), stride, hdr_off, n, 2,
-                                        nullptr, d_mask, di->cus, (int)g_param[NSX_PARAM_BLOCKS_PER_CU].load(),
-                                        (int)g_param[NSX_PARAM_KERNEL].load(),
-                                        (int)g_param[NSX_PARAM_SEGS_PER_WAVE].load(),
-                                        (int)g_param[NSX_PARAM_XCD_CHUNK].load(), static_cast<hipStream_t>(stream)));
+    return map_err(nsx::launch_ipv4_hdr(make_cfg(dev, tune), static_cast<uint8_t*>(const_cast<void*>(d_base)), stride,
+                                        hdr_off, n, 2, nullptr, d_mask, static_cast<hipStream_t>(stream)));
 }
 
 int nsx_fill_splitmix64_dev(void* d_buf, uint64_t byte_off, uint64_t nbytes, uint64_t seed,

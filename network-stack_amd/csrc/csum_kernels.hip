@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "csum_kernels.h"
@@ -126,20 +127,13 @@ struct ChunkDeal {
     }
 };
 
-// xcd_map: 1 = each XCD's blocks stream one contiguous eighth of the batch,
-// dealt round-robin inside it (kernels that take a chunk size then switch to
-// the interleaved chunks with chunk_deal); 0 = plain grid-stride; 2 = every wave
-// owns one contiguous range of tasks and walks it in order (a sequential stream
-// per wave); 3 = byte-balanced wave ranges (ragged scan kernel, its own setup).
-__device__ __forceinline__ TaskIter task_iter(uint64_t ntasks, uint32_t wave, int xcd_map) {
+// Each XCD's blocks stream one contiguous eighth of the batch, dealt round-robin inside it (kernels that
+// take a chunk size then switch to the interleaved chunks with chunk_deal); grids that are not a multiple
+// of the 8 XCDs fall back to a plain grid-stride deal.
+__device__ __forceinline__ TaskIter task_iter(uint64_t ntasks, uint32_t wave) {
     const uint32_t nb = gridDim.x, b = blockIdx.x;
     TaskIter it;
-    if (xcd_map == 2) {
-        const uint64_t waves = (uint64_t)nb * kWavesPerBlock, g = (uint64_t)b * kWavesPerBlock + wave;
-        it.next = ntasks * g / waves;
-        it.end = ntasks * (g + 1) / waves;
-        it.step = 1;
-    } else if (xcd_map == 1 && nb >= 16 && (nb & 7) == 0) {
+    if (nb >= 16 && (nb & 7) == 0) {
         // blocks b, b+8, ... share an XCD (observed round-robin dispatch; speed only).
         const uint32_t x = b & 7, slot = b >> 3, per = nb >> 3;
         const uint64_t lo = ntasks * x / 8, hi = ntasks * (x + 1) / 8;
@@ -154,14 +148,13 @@ __device__ __forceinline__ TaskIter task_iter(uint64_t ntasks, uint32_t wave, in
     return it;
 }
 
-// Switch a wave's xcd_map = 1 iteration to the XCD-interleaved chunk deal when clog > 0 and the grid
+// Switch a wave's task_iter iteration to the XCD-interleaved chunk deal when clog > 0 and the grid
 // allows it; the wave then walks i = it.next, it.next + it.step, ... < it.end with task cd.task(i),
 // stopping at the first task ≥ ntasks (task(i) increases with i). With clog = 0 nothing changes
 // (task(i) = i < it.end ≤ ntasks).
-__device__ __forceinline__ ChunkDeal chunk_deal(TaskIter& it, uint32_t wave, int xcd_map, uint32_t clog,
-                                                uint64_t ntasks) {
+__device__ __forceinline__ ChunkDeal chunk_deal(TaskIter& it, uint32_t wave, uint32_t clog, uint64_t ntasks) {
     ChunkDeal cd{0u, 0u};
-    if (clog && xcd_map == 1 && gridDim.x >= 16 && (gridDim.x & 7) == 0 && ntasks < (1ull << 31)) {
+    if (clog && gridDim.x >= 16 && (gridDim.x & 7) == 0 && ntasks < (1ull << 31)) {
         cd.x = blockIdx.x & 7;
         cd.clog = clog;
         it.next = (blockIdx.x >> 3) * kWavesPerBlock + wave;
@@ -169,74 +162,6 @@ __device__ __forceinline__ ChunkDeal chunk_deal(TaskIter& it, uint32_t wave, int
         it.end = 0xFFFFFFFFu;
     }
     return cd;
-}
-
-// ---------------------------------------------------------------------------
-// Fixed stride, U segments per wave pass, NROWS rows per segment (compile-time:
-// every load of the pass is issued before the first is consumed).
-// ---------------------------------------------------------------------------
-template <int U, int NROWS, bool NT>
-__global__ __launch_bounds__(kBlock) void csum_fixed_kernel(
-    const uint8_t* __restrict__ base, uint64_t stride, uint32_t seg_len, uint64_t n,
-    const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, const uint8_t* safe_end,
-    int xcd_map) {
-    const uint32_t lane = threadIdx.x & (kWave - 1);
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const uint64_t ntasks = (n + U - 1) / U;
-    TaskIter it = task_iter(ntasks, wave, xcd_map);
-
-    for (uint64_t t = it.next; t < it.end; t += it.step) {
-        const uint64_t s0 = t * U;
-        const uint8_t* wb[U];
-        uint32_t head[U];
-        u32x4 v[U][NROWS];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint8_t* p = base + (s0 + u) * stride;
-            head[u] = (uint32_t)((uintptr_t)p & 3u);
-            wb[u] = p - head[u];
-        }
-        // Issue phase.
-#pragma unroll
-        for (int r = 0; r < NROWS; ++r) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                v[u][r] = u32x4{0u, 0u, 0u, 0u};
-                const uint32_t q = r * kRow + lane * 16;
-                if (s0 + u < n && q < head[u] + seg_len) {
-                    const uint8_t* a = wb[u] + q;
-                    if (wb[u] + (r + 1) * kRow <= safe_end || a + 16 <= safe_end) v[u][r] = ld16<NT>(a);
-                    else v[u][r] = ld16_guarded(a, safe_end);
-                }
-            }
-        }
-        // Consume phase.
-        uint32_t tot[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            uint32_t acc = 0;
-            const int64_t lo = head[u], hi = (int64_t)head[u] + seg_len;
-#pragma unroll
-            for (int r = 0; r < NROWS; ++r) {
-                u32x4 x = v[u][r];
-                const int64_t rb = (int64_t)r * kRow;
-                if (rb < lo || rb + kRow > hi) x = mask_chunk(x, rb + lane * 16, lo, hi);
-                acc = sad4(x, acc);
-            }
-            tot[u] = wave_sum(fold32(acc));
-        }
-        // Lane u writes segment s0+u: U contiguous u16 per wave.
-        uint32_t mine = 0;
-        bool mine_even = true;
-        uint64_t my_seg = s0 + lane;
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (lane == (uint32_t)u) { mine = tot[u]; mine_even = ((uintptr_t)(wb[u] + head[u]) & 1u) == 0; }
-        if (lane < (uint32_t)U && my_seg < n) {
-            const uint32_t pp = partial ? partial[my_seg] : 0u;
-            out[my_seg] = (uint16_t)finish(mine, mine_even, pp);
-        }
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -327,37 +252,25 @@ __device__ __forceinline__ void fixed_flush(uint32_t res, uint32_t first, uint32
     __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, off, 0, 0);
 }
 
-// Fixed stride on buffer loads: a wave task = U consecutive segments × NROWS
-// rows, every load unconditional (lanes past a segment's window read 0 and
-// move no data). Results are parked one per lane and flushed with a single
-// scattered 2-byte store per 64/U tasks.
-//
-// ALIGNED (base, stride and seg_len all ≡ 0 mod 4 — e.g. config 2, 1500 B):
-// every segment starts 4-aligned and even, so there are no edge masks, the
-// descriptor size is a constant and the finish (byte swap + prefix partial) is
-// done vector-wide for the whole group at flush time; the group's partials are
-// loaded when the group starts, so their latency hides under 64/U tasks.
-template <int U, int NROWS, bool NT, bool ALIGNED>
+// Fixed stride on buffer loads, any alignment (batches whose base, stride or length is not a multiple of
+// 4; 4-aligned batches take csum_fixed_swp_kernel): a wave task = U consecutive segments × NROWS rows,
+// every load unconditional (lanes past a segment's window read 0 and move no data), only the partial
+// first and last dword of a segment masked (edge_mask). Results are parked one per lane and flushed with
+// a single scattered 2-byte store per 64/U tasks.
+template <int U, int NROWS>
 __global__ __launch_bounds__(kBlock) void csum_fixed_buf_kernel(
     const uint8_t* __restrict__ base, uint64_t stride, uint32_t seg_len, uint32_t n,
-    const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, int xcd_map, uint32_t chunk_log2) {
+    const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, uint32_t chunk_log2) {
     constexpr uint32_t G = kWave / U;
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint32_t ntasks = (n + U - 1) / U;
-    TaskIter it = task_iter(ntasks, wave, xcd_map);
-    const ChunkDeal cd = chunk_deal(it, wave, xcd_map, chunk_log2, ntasks);
+    TaskIter it = task_iter(ntasks, wave);
+    const ChunkDeal cd = chunk_deal(it, wave, chunk_log2, ntasks);
     const uint32_t end = (uint32_t)it.end, step = (uint32_t)it.step;
     const __amdgpu_buffer_rsrc_t ors = make_rsrc(out, (uint64_t)n * 2);
     const __amdgpu_buffer_rsrc_t prs = make_rsrc(partial, partial ? (uint64_t)n * 4 : 0);
-    // Lane l's segment within a group that starts at sequence index `first`.
-    auto group_seg = [&](uint32_t first) { return cd.task(first + (lane / U) * step) * U + lane % U; };
     uint32_t res = 0, k = 0, first = (uint32_t)it.next;
-    uint32_t gpart = 0;
-    if constexpr (ALIGNED) {
-        const uint32_t sg = group_seg(first);
-        gpart = __builtin_amdgcn_raw_buffer_load_b32(prs, sg < n ? sg * 4 : kOOB, 0, 0);
-    }
     for (uint32_t i = (uint32_t)it.next; i < end; i += step) {
         const uint32_t t = cd.task(i);
         if (t >= ntasks) break;
@@ -367,18 +280,12 @@ __global__ __launch_bounds__(kBlock) void csum_fixed_buf_kernel(
         const uint8_t* p = base + (uint64_t)s0 * stride;
 #pragma unroll
         for (int u = 0; u < U; ++u, p += stride) {
-            if constexpr (ALIGNED) {
-                w[u].r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p), 0,
-                                                           s0 + u < n ? (int)seg_len : 0, 0x00020000);
-            } else {
-                w[u] = seg_win(p, seg_len, s0 + u < n);
-            }
+            w[u] = seg_win(p, seg_len, s0 + u < n);
 #pragma unroll
-            for (int r = 0; r < NROWS; ++r) v[u][r] = bld16<NT>(w[u].r, r * kRow + lane * 16);
+            for (int r = 0; r < NROWS; ++r) v[u][r] = bld16<true>(w[u].r, r * kRow + lane * 16);
         }
-        uint32_t part = 0;
-        if constexpr (!ALIGNED)
-            part = __builtin_amdgcn_raw_buffer_load_b32(prs, lane < (uint32_t)U ? (s0 + lane) * 4 : kOOB, 0, 0);
+        const uint32_t part =
+            __builtin_amdgcn_raw_buffer_load_b32(prs, lane < (uint32_t)U ? (s0 + lane) * 4 : kOOB, 0, 0);
         // All U*NROWS loads are issued before the first use: LLVM would otherwise
         // sink each (invariant) load next to its consumer and serialise the wave
         // on memory. An in/out operand pins each load above this point.
@@ -390,47 +297,36 @@ __global__ __launch_bounds__(kBlock) void csum_fixed_buf_kernel(
         for (int u = 0; u < U; ++u) {
             uint32_t acc = 0;
 #pragma unroll
-            for (int r = 0; r < NROWS; ++r) {
-                if constexpr (ALIGNED) acc = sad4(v[u][r], acc);
-                else acc = sad4(edge_mask(v[u][r], w[u], r, lane), acc);
-            }
-            const uint32_t tot = wave_sum(fold32(acc));
-            uint32_t rr;
-            if constexpr (ALIGNED) rr = tot;
-            else rr = finish(tot, w[u].even, __builtin_amdgcn_readlane(part, u));
+            for (int r = 0; r < NROWS; ++r) acc = sad4(edge_mask(v[u][r], w[u], r, lane), acc);
+            const uint32_t rr = finish(wave_sum(fold32(acc)), w[u].even, __builtin_amdgcn_readlane(part, u));
             res = lane == k * U + u ? rr : res;
         }
         if (++k == G) {
-            if constexpr (ALIGNED) res = finish(res, true, gpart);
             fixed_flush<U>(res, first, step, k, n, ors, lane, cd);
             k = 0;
             first = i + step;
-            if constexpr (ALIGNED) {
-                const uint32_t sg = group_seg(first);
-                gpart = __builtin_amdgcn_raw_buffer_load_b32(prs, (first < end && sg < n) ? sg * 4 : kOOB, 0, 0);
-            }
         }
     }
-    if (k) {
-        if constexpr (ALIGNED) res = finish(res, true, gpart);
-        fixed_flush<U>(res, first, step, k, n, ors, lane, cd);
-    }
+    if (k) fixed_flush<U>(res, first, step, k, n, ors, lane, cd);
 }
 
-// Software-pipelined form of the ALIGNED csum_fixed_buf_kernel: two register sets of one task each
-// (U segments × NROWS rows); the next task's loads are issued before the current task is reduced, so a
-// wave keeps its loads in flight through its own reduce/park/flush phases instead of leaving them to
-// other waves. Same deal, parking and flush as the unpipelined kernel.
-template <int U, int NROWS, bool NT>
+// Fixed stride, 4-aligned batches (base, stride and seg_len ≡ 0 mod 4 — config 2's 1500 B): every segment
+// starts 4-aligned and even, so there are no edge masks, the descriptor size is a constant, and the finish
+// (byte swap + prefix partial) is done vector-wide for a whole group of parked results at flush time (the
+// group's partials load when the group starts, so their latency hides under 64/U tasks). Software-
+// pipelined: two register sets of one task each (U segments × NROWS rows); the next task's loads are issued
+// before the current task is reduced, so a wave keeps its loads in flight through its own reduce/park/flush
+// phases instead of leaving them to other waves.
+template <int U, int NROWS>
 __global__ __launch_bounds__(kBlock) void csum_fixed_swp_kernel(
     const uint8_t* __restrict__ base, uint64_t stride, uint32_t seg_len, uint32_t n,
-    const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, int xcd_map, uint32_t chunk_log2) {
+    const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, uint32_t chunk_log2) {
     constexpr uint32_t G = kWave / U;
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint32_t ntasks = (n + U - 1) / U;
-    TaskIter it = task_iter(ntasks, wave, xcd_map);
-    const ChunkDeal cd = chunk_deal(it, wave, xcd_map, chunk_log2, ntasks);
+    TaskIter it = task_iter(ntasks, wave);
+    const ChunkDeal cd = chunk_deal(it, wave, chunk_log2, ntasks);
     const uint32_t end = (uint32_t)it.end, step = (uint32_t)it.step;
     const __amdgpu_buffer_rsrc_t ors = make_rsrc(out, (uint64_t)n * 2);
     const __amdgpu_buffer_rsrc_t prs = make_rsrc(partial, partial ? (uint64_t)n * 4 : 0);
@@ -449,7 +345,7 @@ __global__ __launch_bounds__(kBlock) void csum_fixed_swp_kernel(
             const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
                 const_cast<uint8_t*>(p), 0, (S.ok && s0 + u < n) ? (int)seg_len : 0, 0x00020000);
 #pragma unroll
-            for (int rr = 0; rr < NROWS; ++rr) S.v[u][rr] = bld16<NT>(r, rr * kRow + lane * 16);
+            for (int rr = 0; rr < NROWS; ++rr) S.v[u][rr] = bld16<true>(r, rr * kRow + lane * 16);
         }
     };
     uint32_t res = 0, k = 0, first = (uint32_t)it.next;
@@ -499,15 +395,15 @@ __global__ __launch_bounds__(kBlock) void csum_fixed_swp_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// One segment per wave, runtime row count, rows issued R at a time. Serves the
-// ragged batch (offsets) and fixed batches with long segments.
+// One segment per wave, runtime row count, rows issued R at a time: fixed
+// batches with long segments (> 4 KiB).
 // ---------------------------------------------------------------------------
 struct SegRef {
     const uint8_t* p;
     uint64_t len;
 };
 
-template <int R, bool NT>
+template <int R>
 __device__ __forceinline__ uint32_t seg_lane_sum(const uint8_t* p, uint64_t len, uint32_t lane,
                                                  const uint8_t* safe_end, uint64_t row_first,
                                                  uint64_t row_step) {
@@ -525,7 +421,7 @@ __device__ __forceinline__ uint32_t seg_lane_sum(const uint8_t* p, uint64_t len,
             const int64_t q = (int64_t)(r * kRow) + lane * 16;
             if (q < hi) {
                 const uint8_t* a = wb + q;
-                if (wb + (r + 1) * kRow <= safe_end || a + 16 <= safe_end) v[j] = ld16<NT>(a);
+                if (wb + (r + 1) * kRow <= safe_end || a + 16 <= safe_end) v[j] = ld16<true>(a);
                 else v[j] = ld16_guarded(a, safe_end);
             }
         }
@@ -552,71 +448,22 @@ __device__ __forceinline__ SegRef seg_ref(const uint8_t* base, const uint64_t* o
     }
 }
 
-template <bool RAGGED, int R, bool NT, bool VERIFY>
-__global__ __launch_bounds__(kBlock) void csum_wave_kernel(
-    const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, uint64_t stride,
-    uint32_t seg_len, uint64_t n, const uint32_t* __restrict__ partial, uint16_t* __restrict__ out,
-    uint8_t* __restrict__ ok, const uint8_t* safe_end, int xcd_map, uint32_t clog) {
+template <int R>
+__global__ __launch_bounds__(kBlock) void csum_wave_kernel(const uint8_t* __restrict__ base, uint64_t stride,
+                                                           uint32_t seg_len, uint64_t n,
+                                                           const uint32_t* __restrict__ partial,
+                                                           uint16_t* __restrict__ out, const uint8_t* safe_end,
+                                                           uint32_t clog) {
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    if constexpr (RAGGED) safe_end = align_up4(base + offsets[n]);
-    TaskIter it = task_iter(n, wave, xcd_map);
-    const ChunkDeal cd = chunk_deal(it, wave, xcd_map, clog, n);
+    TaskIter it = task_iter(n, wave);
+    const ChunkDeal cd = chunk_deal(it, wave, clog, n);
     for (uint64_t k = it.next; k < it.end; k += it.step) {
         const uint64_t i = cd.clog ? cd.task((uint32_t)k) : k;
         if (i >= n) break;
-        const SegRef s = seg_ref<RAGGED>(base, offsets, stride, seg_len, i);
-        const uint32_t tot = wave_sum(seg_lane_sum<R, NT>(s.p, s.len, lane, safe_end, 0, 1));
-        if (lane == 0) {
-            const uint32_t res = finish(tot, ((uintptr_t)s.p & 1u) == 0, partial ? partial[i] : 0u);
-            if (out) out[i] = (uint16_t)res;
-            if constexpr (VERIFY) ok[i] = res == 0xFFFFu;
-        }
-    }
-}
-
-// Long aligned fixed-stride segments (> 4 KiB, base/stride/len ≡ 0 mod 4, len < 2^31): one wave per
-// segment through one buffer descriptor ending at the segment's last byte, rows in batches of R with two
-// register sets — batch r0 + R loads while batch r0 is summed — and no masks (the range check zero-fills
-// past the end). Segments start 4-aligned, so the finish needs no byte-swap decision per segment.
-template <int R, bool NT>
-__global__ __launch_bounds__(kBlock) void csum_long_swp_kernel(const uint8_t* __restrict__ base, uint64_t stride,
-                                                               uint32_t seg_len, uint64_t n,
-                                                               const uint32_t* __restrict__ partial,
-                                                               uint16_t* __restrict__ out, int xcd_map, uint32_t clog) {
-    const uint32_t lane = threadIdx.x & (kWave - 1);
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    TaskIter it = task_iter(n, wave, xcd_map);
-    const ChunkDeal cd = chunk_deal(it, wave, xcd_map, clog, n);
-    const uint32_t rows = (seg_len + kRow - 1) / kRow;
-    for (uint64_t k = it.next; k < it.end; k += it.step) {
-        const uint64_t i = cd.clog ? cd.task((uint32_t)k) : k;
-        if (i >= n) break;
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint8_t*>(base + i * stride), 0, (int)seg_len, 0x00020000);
-        auto issue = [&](uint32_t r0, u32x4 (&v)[R]) {
-#pragma unroll
-            for (int j = 0; j < R; ++j) v[j] = bld16<NT>(rs, r0 < rows ? (r0 + j) * kRow + lane * 16u : kOOB);
-        };
-        uint32_t acc = 0;
-        auto consume = [&](u32x4 (&v)[R]) {
-#pragma unroll
-            for (int j = 0; j < R; ++j) asm volatile("" : "+v"(v[j]));
-#pragma unroll
-            for (int j = 0; j < R; ++j) acc = sad4(v[j], acc);
-            acc = fold32(acc);
-        };
-        u32x4 A[R], B[R];
-        issue(0, A);
-        for (uint32_t r0 = 0; r0 < rows; r0 += 2 * R) {
-            issue(r0 + R, B);
-            consume(A);
-            if (r0 + R >= rows) break;
-            issue(r0 + 2 * R, A);
-            consume(B);
-        }
-        const uint32_t res = finish(wave_sum(acc), true, partial ? partial[i] : 0u);
-        if (lane == 0 && out) out[i] = (uint16_t)res;
+        const SegRef s = seg_ref<false>(base, nullptr, stride, seg_len, i);
+        const uint32_t tot = wave_sum(seg_lane_sum<R>(s.p, s.len, lane, safe_end, 0, 1));
+        if (lane == 0) out[i] = (uint16_t)finish(tot, ((uintptr_t)s.p & 1u) == 0, partial ? partial[i] : 0u);
     }
 }
 
@@ -625,7 +472,7 @@ __global__ __launch_bounds__(kBlock) void csum_long_swp_kernel(const uint8_t* __
 // w, w+4, ... so the block reads 4 KiB contiguous per step; cross-wave total
 // through LDS.
 // ---------------------------------------------------------------------------
-template <bool RAGGED, int R, bool NT, bool VERIFY>
+template <bool RAGGED, int R, bool VERIFY>
 __global__ __launch_bounds__(kBlock) void csum_block_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, uint64_t stride,
     uint32_t seg_len, uint64_t n, const uint32_t* __restrict__ partial, uint16_t* __restrict__ out,
@@ -636,7 +483,7 @@ __global__ __launch_bounds__(kBlock) void csum_block_kernel(
     if constexpr (RAGGED) safe_end = align_up4(base + offsets[n]);
     for (uint64_t i = blockIdx.x; i < n; i += gridDim.x) {
         const SegRef s = seg_ref<RAGGED>(base, offsets, stride, seg_len, i);
-        const uint32_t w = wave_sum(seg_lane_sum<R, NT>(s.p, s.len, lane, safe_end, wave, kWavesPerBlock));
+        const uint32_t w = wave_sum(seg_lane_sum<R>(s.p, s.len, lane, safe_end, wave, kWavesPerBlock));
         if (lane == 0) part[wave] = fold32(w);
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -649,274 +496,10 @@ __global__ __launch_bounds__(kBlock) void csum_block_kernel(
     }
 }
 
-// ---------------------------------------------------------------------------
-// Row-stream kernel. A wave owns a run of kRun consecutive segments and streams
-// their rows in batches of R wave-wide loads that cross segment boundaries, so
-// each batch keeps R KiB in flight whatever the segment lengths (short ragged
-// segments no longer cost a full latency round trip each). The run's offsets
-// sit one per lane in a VGPR (prefetched one run ahead) and are read with
-// v_readlane; per-segment wave totals are parked in lane (s - a) of a VGPR and
-// finished in parallel (byte-swap rule + prefix partial) at the end of the run,
-// which then stores 2·kRun contiguous bytes of results.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kRun = 32;
-
-struct SegMeta {        // wave-uniform description of one segment's window
-    const uint8_t* wb;  // 4-byte-aligned window base (segment start rounded down)
-    int64_t lo, hi;     // segment bytes are [lo, hi) of the window (lo = head <= 3)
-    uint32_t rows;      // 1 KiB rows covering [0, hi); 0 for an empty segment
-};
-
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t k) {
     const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, k);
     const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), k);
     return ((uint64_t)hi << 32) | lo;
-}
-
-template <bool RAGGED>
-__device__ __forceinline__ SegMeta seg_meta(const uint8_t* base, uint64_t my_off, uint64_t a, uint64_t s,
-                                            uint64_t stride, uint32_t seg_len) {
-    uint64_t o0, len;
-    if constexpr (RAGGED) {
-        o0 = readlane64(my_off, (uint32_t)(s - a));
-        const uint64_t o1 = readlane64(my_off, (uint32_t)(s - a + 1));
-        len = o1 > o0 ? o1 - o0 : 0;
-    } else {
-        o0 = s * stride;
-        len = seg_len;
-    }
-    const uint8_t* p = base + o0;
-    const uint32_t head = (uint32_t)((uintptr_t)p & 3u);
-    SegMeta m;
-    m.wb = p - head;
-    m.lo = head;
-    m.hi = (int64_t)head + (int64_t)len;
-    m.rows = len ? (uint32_t)((m.hi + kRow - 1) / kRow) : 0u;
-    return m;
-}
-
-template <bool RAGGED, int R, bool NT, bool VERIFY>
-__global__ __launch_bounds__(kBlock) void csum_stream_kernel(
-    const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, uint64_t stride,
-    uint32_t seg_len, uint64_t n, const uint32_t* __restrict__ partial, uint16_t* __restrict__ out,
-    uint8_t* __restrict__ ok, const uint8_t* safe_end, int xcd_map) {
-    const uint32_t lane = threadIdx.x & (kWave - 1);
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    if constexpr (RAGGED) safe_end = align_up4(base + offsets[n]);
-    const uint64_t ntasks = (n + kRun - 1) / kRun;
-    TaskIter it = task_iter(ntasks, wave, xcd_map);
-
-    uint64_t nxt_off = 0;
-    if constexpr (RAGGED) {
-        if (it.next < it.end) {
-            const uint64_t a = it.next * kRun, cnt = min((uint64_t)kRun, n - a);
-            if (lane <= cnt) nxt_off = offsets[a + lane];
-        }
-    }
-    for (uint64_t t = it.next; t < it.end; t += it.step) {
-        const uint64_t a = t * kRun, b = min(a + kRun, n);
-        const uint64_t my_off = nxt_off;
-        if constexpr (RAGGED) {  // prefetch the next run's offsets
-            const uint64_t tn = t + it.step;
-            if (tn < it.end) {
-                const uint64_t an = tn * kRun, cnt = min((uint64_t)kRun, n - an);
-                nxt_off = lane <= cnt ? offsets[an + lane] : 0;
-            }
-        }
-        const uint32_t my_part = (partial && a + lane < b) ? partial[a + lane] : 0u;
-
-        uint32_t sums = 0;  // lane k: LE half-sum total of segment a+k
-        uint32_t acc = 0;   // this lane's share of segment `cur`
-        uint64_t cur = a;
-        uint64_t ps = a;    // planning cursor: segment ps, row pr
-        uint32_t pr = 0;
-        SegMeta pm = seg_meta<RAGGED>(base, my_off, a, ps, stride, seg_len);
-        for (;;) {
-            // Plan R slots (scalar): row start address, the segment's bytes as
-            // [lo_r, hi_r) relative to that row (clamped to 32 bits), and the
-            // segment as an offset in the run (kRun = no slot).
-            const uint8_t* sra[R];
-            int32_t slo[R], shi[R];
-            uint32_t sd[R];
-#pragma unroll
-            for (int j = 0; j < R; ++j) {
-                while (ps < b && pr >= pm.rows) {
-                    ++ps;
-                    pr = 0;
-                    if (ps < b) pm = seg_meta<RAGGED>(base, my_off, a, ps, stride, seg_len);
-                }
-                const int64_t rb = (int64_t)pr * kRow;
-                sd[j] = ps < b ? (uint32_t)(ps - a) : kRun;
-                sra[j] = pm.wb + rb;
-                slo[j] = (int32_t)max(min(pm.lo - rb, (int64_t)kRow + 16), (int64_t)-16);
-                shi[j] = (int32_t)max(min(pm.hi - rb, (int64_t)kRow + 16), (int64_t)-16);
-                ++pr;
-            }
-            if (sd[0] == kRun) break;
-            // Issue all R loads.
-            u32x4 v[R];
-            const int32_t d = (int32_t)lane * 16;
-#pragma unroll
-            for (int j = 0; j < R; ++j) {
-                v[j] = u32x4{0u, 0u, 0u, 0u};
-                if (sd[j] != kRun && d < shi[j]) {
-                    const uint8_t* ad = sra[j] + d;
-                    if (sra[j] + kRow <= safe_end || ad + 16 <= safe_end) v[j] = ld16<NT>(ad);
-                    else v[j] = ld16_guarded(ad, safe_end);
-                }
-            }
-            // Consume in order; a segment change parks the finished total.
-#pragma unroll
-            for (int j = 0; j < R; ++j) {
-                if (sd[j] != kRun) {
-                    if (a + sd[j] != cur) {
-                        const uint32_t tot = wave_sum(fold32(acc));
-                        sums = lane == (uint32_t)(cur - a) ? tot : sums;
-                        acc = 0;
-                        cur = a + sd[j];
-                    }
-                    u32x4 x = v[j];
-                    if (slo[j] > 0 || shi[j] < (int32_t)kRow) {
-                        x.x &= keep_mask(slo[j], shi[j], d);
-                        x.y &= keep_mask(slo[j], shi[j], d + 4);
-                        x.z &= keep_mask(slo[j], shi[j], d + 8);
-                        x.w &= keep_mask(slo[j], shi[j], d + 12);
-                    }
-                    acc = sad4(x, acc);
-                }
-            }
-            acc = fold32(acc);
-        }
-        if (cur < b) {
-            const uint32_t tot = wave_sum(fold32(acc));
-            sums = lane == (uint32_t)(cur - a) ? tot : sums;
-        }
-        // Finish every segment of the run in parallel, one per lane.
-        if (a + lane < b) {
-            const uint64_t o = RAGGED ? my_off : (a + lane) * stride;
-            const bool even = (((uintptr_t)base + o) & 1u) == 0;
-            const uint32_t res = finish(sums, even, my_part);
-            if (out) out[a + lane] = (uint16_t)res;
-            if constexpr (VERIFY) ok[a + lane] = res == 0xFFFFu;
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Ragged row-stream on buffer loads (the default ragged kernel). Same schedule
-// as csum_stream_kernel — a wave owns kRun consecutive segments and streams
-// their 1 KiB rows in batches of R loads that cross segment boundaries — but
-// every load goes through a segment-window descriptor (csum_fixed_buf_kernel's
-// SegWin rule), so it is unconditional, pinned ahead of its use, and only the
-// partial first / last dword of a segment needs a byte mask. Per-slot state is
-// two scalars (segment slot in the run, row); descriptors are rebuilt from the
-// lane-resident offsets at issue. Segment lengths must be < 2^31 bytes.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ u32x4 edge_mask2(u32x4 x, uint32_t head, uint32_t end, uint32_t k, uint32_t lane) {
-    SegWin w;
-    w.head = head;
-    w.end = end;
-    return edge_mask(x, w, k, lane);
-}
-
-struct RunSeg {  // wave-uniform view of segment slot j of the current run
-    const uint8_t* wb;
-    uint32_t head, end, rows;
-};
-
-__device__ __forceinline__ RunSeg run_seg(const uint8_t* base, uint64_t my_off, uint32_t j) {
-    const uint64_t o0 = readlane64(my_off, j), o1 = readlane64(my_off, j + 1);
-    const uint32_t len = o1 > o0 ? (uint32_t)(o1 - o0) : 0u;
-    const uint8_t* p = base + o0;
-    RunSeg s;
-    s.head = (uint32_t)((uintptr_t)p & 3u);
-    s.wb = p - s.head;
-    s.end = s.head + len;
-    s.rows = len ? (s.end + kRow - 1) / kRow : 0u;
-    return s;
-}
-
-template <int R, bool NT, bool VERIFY>
-__global__ __launch_bounds__(kBlock) void csum_ragged_buf_kernel(
-    const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, uint32_t n,
-    const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, uint8_t* __restrict__ ok, int xcd_map) {
-    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
-    const uint32_t lane = threadIdx.x & (kWave - 1);
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const uint32_t ntasks = (n + kRun - 1) / kRun;
-    const TaskIter it = task_iter(ntasks, wave, xcd_map);
-    const uint32_t end = (uint32_t)it.end, step = (uint32_t)it.step;
-    const __amdgpu_buffer_rsrc_t ofs = make_rsrc(offsets, ((uint64_t)n + 1) * 8);
-    const __amdgpu_buffer_rsrc_t prs = make_rsrc(partial, partial ? (uint64_t)n * 4 : 0);
-    const __amdgpu_buffer_rsrc_t ors = make_rsrc(out, out ? (uint64_t)n * 2 : 0);
-    const __amdgpu_buffer_rsrc_t oks = make_rsrc(ok, VERIFY ? (uint64_t)n : 0);
-    auto load_offs = [&](uint32_t t) -> uint64_t {  // lane l: offsets[t*kRun + l], l <= run length
-        const uint32_t a = t * kRun;
-        const uint32_t voff = (t < end && lane <= kRun && a + lane <= n) ? (a + lane) * 8 : kOOB;
-        const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, voff, 0, 0);
-        return ((uint64_t)x.y << 32) | x.x;
-    };
-    uint64_t nxt_off = load_offs((uint32_t)it.next);
-    for (uint32_t t = (uint32_t)it.next; t < end; t += step) {
-        const uint32_t a = t * kRun, cnt = min(kRun, n - a);
-        const uint64_t my_off = nxt_off;
-        nxt_off = load_offs(t + step);  // prefetch the next run's offsets
-        const uint32_t my_part =
-            __builtin_amdgcn_raw_buffer_load_b32(prs, lane < cnt ? (a + lane) * 4 : kOOB, 0, 0);
-        uint32_t sums = 0, acc = 0;
-        uint32_t cur = 0;                                   // slot being accumulated
-        RunSeg cs = run_seg(base, my_off, 0);               // its window
-        uint32_t ps = 0, pr = 0, prows = cs.rows;           // planning cursor
-        for (;;) {
-            uint32_t sd[R], srow[R];
-#pragma unroll
-            for (int j = 0; j < R; ++j) {
-                while (ps < cnt && pr >= prows) {
-                    ++ps;
-                    pr = 0;
-                    if (ps < cnt) prows = run_seg(base, my_off, ps).rows;
-                }
-                sd[j] = ps < cnt ? ps : kRun;
-                srow[j] = pr++;
-            }
-            if (sd[0] == kRun) break;
-            u32x4 v[R];
-#pragma unroll
-            for (int j = 0; j < R; ++j) {
-                const bool live = sd[j] != kRun;
-                const RunSeg g = run_seg(base, my_off, live ? sd[j] : 0);
-                const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-                    const_cast<uint8_t*>(g.wb), 0, live ? (int)((g.end + 3u) & ~3u) : 0, 0x00020000);
-                v[j] = bld16<NT>(r, srow[j] * kRow + lane * 16);
-            }
-#pragma unroll
-            for (int j = 0; j < R; ++j) asm volatile("" : "+v"(v[j]));
-#pragma unroll
-            for (int j = 0; j < R; ++j) {
-                if (sd[j] != kRun) {
-                    if (sd[j] != cur) {
-                        const uint32_t tot = wave_sum(fold32(acc));
-                        sums = lane == cur ? tot : sums;
-                        acc = 0;
-                        cur = sd[j];
-                        cs = run_seg(base, my_off, cur);
-                    }
-                    acc = sad4(edge_mask2(v[j], cs.head, cs.end, srow[j], lane), acc);
-                }
-            }
-            acc = fold32(acc);
-        }
-        if (cur < cnt) {
-            const uint32_t tot = wave_sum(fold32(acc));
-            sums = lane == cur ? tot : sums;
-        }
-        const bool even = (((uintptr_t)base + my_off) & 1u) == 0;
-        const uint32_t res = finish(sums, even, my_part);
-        const bool mine = lane < cnt;
-        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, mine ? (a + lane) * 2 : kOOB, 0, 0);
-        if constexpr (VERIFY)
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(res == 0xFFFFu), oks, mine ? a + lane : kOOB, 0, 0);
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1004,11 +587,10 @@ __device__ __forceinline__ void seg_lower_bound2(__amdgpu_buffer_rsrc_t ofs, uin
         s[k] = lo[k] + (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(v[k] < t[k]));
 }
 
-template <int R, bool NT, bool VERIFY, bool PIPE>
+template <int R, bool VERIFY>
 __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, uint32_t n,
-    const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, uint8_t* __restrict__ ok, int xcd_map,
-    uint32_t run) {
+    const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t run) {
     typedef uint32_t v2u __attribute__((ext_vector_type(2)));
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -1016,13 +598,12 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
     const __amdgpu_buffer_rsrc_t prs = make_rsrc(partial, partial ? (uint64_t)n * 4 : 0);
     const __amdgpu_buffer_rsrc_t ors = make_rsrc(out, out ? (uint64_t)n * 2 : 0);
     const __amdgpu_buffer_rsrc_t oks = make_rsrc(ok, VERIFY ? (uint64_t)n : 0);
-    // The wave's tasks are runs [a, a + cnt) of ≤ run segments, a = a0, a0 + a_step, ... < a_end;
-    // a run never crosses a_end.
-    uint32_t a0, a_step, a_end;
-    if (xcd_map == 3) {
-        // Byte-balanced: wave g (XCD-contiguous numbering) owns the segments that start in
-        // the g-th of W equal byte slices of the batch, so every wave streams the same bytes
-        // (± one segment) and none is left running alone at the end of the launch.
+    // The wave's tasks are runs [a, a + cnt) of ≤ run segments, a = a0, a0 + run, ... < a_end; a run never
+    // crosses a_end. Byte-balanced: wave g (XCD-contiguous numbering) owns the segments that start in the g-th
+    // of W equal byte slices of the batch, so every wave streams the same bytes (± one segment) and none is
+    // left running alone at the end of the launch.
+    uint32_t a0, a_end;
+    {
         const uint32_t nb = gridDim.x, b = blockIdx.x, W = nb * kWavesPerBlock;
         const uint32_t g = (nb >= 16 && (nb & 7) == 0) ? ((b & 7) * (nb >> 3) + (b >> 3)) * kWavesPerBlock + wave
                                                         : b * kWavesPerBlock + wave;
@@ -1032,14 +613,8 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
         seg_lower_bound2(ofs, n, o_lo + tot * g / W, o_lo + tot * (g + 1) / W, lane, s);
         a0 = g == 0 ? 0u : s[0];
         a_end = g + 1 == W ? n : s[1];
-        a_step = run;
-    } else {
-        const uint32_t ntasks = (n + run - 1) / run;  // run ≤ kScanRun segments per wave task
-        const TaskIter it = task_iter(ntasks, wave, xcd_map);
-        a0 = (uint32_t)it.next * run;
-        a_step = (uint32_t)it.step * run;
-        a_end = (uint32_t)min((uint64_t)it.end * run, (uint64_t)n);
     }
+    const uint32_t a_step = run;
     auto load_offs = [&](uint32_t a) -> uint64_t {  // lane l ≤ run length: offsets[a + l]
         const uint32_t voff = (a < a_end && lane <= run && a + lane <= n) ? (a + lane) * 8 : kOOB;
         const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, voff, 0, 0);
@@ -1067,7 +642,7 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
             const uint64_t rem = r0 < nrows ? span - r0 * kRow : 0;
             const __amdgpu_buffer_rsrc_t rs = make_rsrc(bb, (rem + 3) & ~3ull);
 #pragma unroll
-            for (int j = 0; j < R; ++j) v[j] = bld16<NT>(rs, j * kRow + lane * 16);
+            for (int j = 0; j < R; ++j) v[j] = bld16<true>(rs, j * kRow + lane * 16);
         };
         auto process = [&](uint64_t r0, u32x4 (&v)[R]) {
 #pragma unroll
@@ -1117,23 +692,10 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
 #pragma unroll
             for (int j = 0; j < R; ++j) carry += __builtin_amdgcn_readlane(incl[j], 63);
         };
-        if constexpr (PIPE) {
-            // two register sets: batch r0 + R loads while batch r0 is reduced
-            u32x4 A[R], B[R];
-            issue(0, A);
-            for (uint64_t r0 = 0; r0 < nrows; r0 += 2 * R) {
-                issue(r0 + R, B);
-                process(r0, A);
-                if (r0 + R >= nrows) break;
-                issue(r0 + 2 * R, A);
-                process(r0 + R, B);
-            }
-        } else {
-            for (uint64_t r0 = 0; r0 < nrows; r0 += R) {
-                u32x4 v[R];
-                issue(r0, v);
-                process(r0, v);
-            }
+        for (uint64_t r0 = 0; r0 < nrows; r0 += R) {
+            u32x4 v[R];
+            issue(r0, v);
+            process(r0, v);
         }
         if (brel >= (int64_t)(nrows * kRow)) bval = carry;  // boundary at the very end of the rows
         // Segment `lane` = [boundary lane, boundary lane+1).
@@ -1314,8 +876,8 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint64_t data_end4 = (data_bytes + 3) & ~3ull;  // the last payload dword reads whole
     const uint64_t ngroups = (n + group - 1) / group;
-    TaskIter it = task_iter(ngroups, wave, 1);
-    const ChunkDeal cd = chunk_deal(it, wave, 1, clog, ngroups);
+    TaskIter it = task_iter(ngroups, wave);
+    const ChunkDeal cd = chunk_deal(it, wave, clog, ngroups);
     for (uint64_t q = it.next; q < it.end; q += it.step) {
         const uint64_t g = cd.clog ? cd.task((uint32_t)q) : q;
         if (g >= ngroups) break;
@@ -1822,16 +1384,10 @@ __global__ __launch_bounds__(kBlock) void ipv4_hdr_dense_kernel(uint8_t* __restr
 constexpr uint32_t kHdr20Task = 256;
 constexpr uint32_t kHdr20Lds = kHdr20Task * 20u;  // bytes of LDS per wave
 
-// PIPE: software-pipelined — two register sets of U tasks; the loads of the next set are issued before
-// the current set goes through LDS, so every wave keeps loads in flight while it computes and stores (one
-// wave per SIMD at 1 block/CU has no other wave to cover those phases). !PIPE: one set, load then use.
-// DEFER (MODE 0 only): a full task's 512 B of raw sums go to a per-wave LDS buffer of DEFER task slots instead of
-// HBM; the wave writes the buffer out when it is full and at the end, so result stores leave in bursts between
-// long read phases instead of one 512 B store per task (kernel knob 4).
-// 20 slots × 512 B × 4 waves + the 20 KiB staging slices = 60 KiB, within the default dynamic LDS limit.
-constexpr uint32_t kHdr20DeferSlots = 20;
-
-template <int MODE, int U, bool PIPE, int DEFER = 0>
+// Software-pipelined: two register sets of U tasks; the loads of the next set are issued before the
+// current set goes through LDS, so every wave keeps loads in flight while it computes and stores (one wave
+// per SIMD at 1 block/CU has no other wave to cover those phases).
+template <int MODE, int U>
 __global__ __launch_bounds__(kBlock) void ipv4_hdr20_kernel(uint8_t* __restrict__ base, uint32_t n,
                                                             uint16_t* __restrict__ out, uint32_t clog,
                                                             uint64_t* __restrict__ mask) {
@@ -1841,29 +1397,14 @@ __global__ __launch_bounds__(kBlock) void ipv4_hdr20_kernel(uint8_t* __restrict_
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     u32x4* my = lds20 + wave * (kHdr20Lds / 16u);
     const uint32_t ntasks = (n + kHdr20Task - 1) / kHdr20Task;
-    TaskIter it = task_iter(ntasks, wave, 1);
-    const ChunkDeal cd = chunk_deal(it, wave, 1, clog, ntasks);
+    TaskIter it = task_iter(ntasks, wave);
+    const ChunkDeal cd = chunk_deal(it, wave, clog, ntasks);
     const uint32_t end = (uint32_t)it.end, step = (uint32_t)it.step;
     const __amdgpu_buffer_rsrc_t ors = make_rsrc(out, out ? (uint64_t)n * 2 : 0);
     struct Set {
         __amdgpu_buffer_rsrc_t rs[U];
-        uint32_t cnt[U], tk[U], ii[U];
+        uint32_t cnt[U], tk[U];
         u32x4 v[U][5];
-    };
-    // Deferred raw sums: slot k holds the k-th buffered task's 64 lanes × 8 B; buffered tasks are consecutive in
-    // the wave's processing order (ii = d_first + k·step), so their task ids need no storage.
-    static_assert(DEFER == 0 || (MODE == 0 && PIPE), "deferred stores: raw-sum mode, pipelined kernel");
-    v2u* dbuf = reinterpret_cast<v2u*>(lds20 + kWavesPerBlock * (kHdr20Lds / 16u)) + (uint32_t)wave * DEFER * kWave;
-    uint32_t d_n = 0, d_first = 0;
-    auto flush = [&]() {
-        if constexpr (DEFER > 0) {
-            for (uint32_t k = 0; k < d_n; ++k) {
-                const uint32_t task = cd.task(d_first + k * step);
-                __builtin_amdgcn_raw_buffer_store_b64(dbuf[k * kWave + lane], ors, (task * kHdr20Task + lane * 4u) * 2u,
-                                                      0, 0);
-            }
-            d_n = 0;
-        }
     };
     auto live = [&](uint32_t t0) { return t0 < end && cd.task(t0) < ntasks; };
     auto issue = [&](uint32_t t0, Set& S) {
@@ -1872,7 +1413,6 @@ __global__ __launch_bounds__(kBlock) void ipv4_hdr20_kernel(uint8_t* __restrict_
             const uint32_t ii = t0 + (uint32_t)u * step;
             const uint32_t task = cd.task(ii);
             S.tk[u] = task;
-            S.ii[u] = ii;
             S.cnt[u] = (ii < end && task < ntasks) ? min(kHdr20Task, n - task * kHdr20Task) : 0u;
             S.rs[u] = make_rsrc(base + (uint64_t)min(task, ntasks - 1) * kHdr20Lds, S.cnt[u] * 20u);
 #pragma unroll
@@ -1930,15 +1470,10 @@ __global__ __launch_bounds__(kBlock) void ipv4_hdr20_kernel(uint8_t* __restrict_
                 hi += __builtin_amdgcn_update_dpp(0u, hi, 0x118, 0xF, 0xF, false);
                 const uint32_t wi = S.tk[u] * (kHdr20Task / kWave) + (lane >> 4);  // < 2^22 (n < 2^28 per launch)
                 if (j == 15u && wi * kWave < n) mask[wi] = ((uint64_t)hi << 32) | lo;
-            } else if (DEFER > 0 && S.cnt[u] == kHdr20Task) {
-                if (d_n == 0) d_first = S.ii[u];
-                dbuf[d_n * kWave + lane] = v2u{res[0] | (res[1] << 16), res[2] | (res[3] << 16)};
-                ++d_n;
             } else if (S.cnt[u] == kHdr20Task) {
                 __builtin_amdgcn_raw_buffer_store_b64(v2u{res[0] | (res[1] << 16), res[2] | (res[3] << 16)}, ors,
                                                       i0 * 2u, 0, 0);
             } else {
-                flush();  // a partial task breaks the run of consecutive buffered tasks
 #pragma unroll
                 for (int h = 0; h < 4; ++h)
                     __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res[h], ors, i0 + h < n ? (i0 + h) * 2u : kOOB, 0,
@@ -1952,32 +1487,17 @@ __global__ __launch_bounds__(kBlock) void ipv4_hdr20_kernel(uint8_t* __restrict_
             }
         }
     };
-    auto room = [&]() {
-        if constexpr (DEFER > 0)
-            if (d_n + U > (uint32_t)DEFER) flush();
-    };
-    if constexpr (PIPE) {
-        Set A, B;
-        uint32_t t0 = (uint32_t)it.next;
+    Set A, B;
+    uint32_t t0 = (uint32_t)it.next;
+    issue(t0, A);
+    while (live(t0)) {
+        const uint32_t t1 = t0 + step * U;
+        issue(t1, B);
+        consume(A);
+        if (!live(t1)) break;
+        t0 = t1 + step * U;
         issue(t0, A);
-        while (live(t0)) {
-            const uint32_t t1 = t0 + step * U;
-            issue(t1, B);
-            room();
-            consume(A);
-            if (!live(t1)) break;
-            t0 = t1 + step * U;
-            issue(t0, A);
-            room();
-            consume(B);
-        }
-        flush();
-    } else {
-        for (uint32_t t0 = (uint32_t)it.next; live(t0); t0 += step * U) {
-            Set A;
-            issue(t0, A);
-            consume(A);
-        }
+        consume(B);
     }
 }
 
@@ -2079,22 +1599,14 @@ __global__ __launch_bounds__(kBlock) void fill_bytes_kernel(uint8_t* __restrict_
 }  // namespace
 
 // ---------------------------------------------------------------------------
-// Launchers (host side of this translation unit).
+// Launchers (host side of this translation unit). Per-path defaults, measured
+// best on MI355X; a caller's nsx_tune may override them.
 // ---------------------------------------------------------------------------
-// Resolved launch parameters for one call.
-struct Plan {
-    uint32_t max_blocks;
-    int spw, rows, xcd;
-    bool nt;
-    uint32_t run;     // ragged scan kernel: segments per wave task (1..kScanRun)
-    int xcd_chunk_param;  // raw NSX_PARAM_XCD_CHUNK (deal_clog)
-};
-
-// XCD-interleaved chunk deal (chunk_deal): log2 of the tasks per chunk. param = NSX_PARAM_XCD_CHUNK:
+// XCD-interleaved chunk deal (chunk_deal): log2 of the tasks per chunk. param = nsx_tune.xcd_chunk:
 // 1..20 fixed, 0 auto, anything else off (contiguous eighths). Auto: chunks of at most 24 MiB of batch
-// (config 2: 2^12 tasks of 4 × 1500 B), but at least 64 chunks; off when that leaves < 4 tasks a chunk.
-// Contiguous eighths ran 8% slow on some allocations on some boxes; 2^10-2^14-task chunks never did
-// (tools/alloc_study.py).
+// (capped so that there are at least 64 chunks); off when that
+// leaves < 4 tasks a chunk. Contiguous eighths ran 8% slow on some allocations on some boxes; 2^10-2^14-task
+// chunks never did (tools/alloc_study.py).
 static uint32_t deal_clog(int param, uint64_t ntasks, uint64_t task_bytes) {
     if (param >= 1 && param <= 20) return (uint32_t)param;
     if (param != 0) return 0u;
@@ -2104,149 +1616,80 @@ static uint32_t deal_clog(int param, uint64_t ntasks, uint64_t task_bytes) {
     return k >= 2 ? k : 0u;
 }
 
-enum class Path { kFixedShort, kFixedLong, kRagged, kBlock };
-
-// Per-path defaults (tools/sweep.py, MI355X):
-//   fixed ≤4 rows : buffer-load kernel, 4 segments/wave, 2 blocks/CU (8 waves/CU)
-//   fixed long    : per-segment wave kernel, 2 blocks/CU (8 waves/CU, 4 KiB in flight each)
-//   ragged        : prefix-scan kernel, byte-balanced contiguous wave ranges (XCD-ordered),
-//                   63-segment runs, 8 rows/batch, 2 blocks/CU
-// nt loads everywhere; the XCD-contiguous deal on the fixed paths.
-static Plan resolve(const LaunchCfg& c, Path p) {
-    Plan r;
-    int bpc = c.blocks_per_cu;
-    if (bpc < 1 || bpc > 8) bpc = p == Path::kBlock ? 8 : 2;
-    r.max_blocks = (uint32_t)(c.cus * bpc);
-    r.spw = (c.segs_per_wave == 1 || c.segs_per_wave == 2 || c.segs_per_wave == 4 || c.segs_per_wave == 8)
-                ? c.segs_per_wave : 4;
-    r.rows = (c.rows == 4 || c.rows == 8 || c.rows == 16) ? c.rows : 8;
-    r.xcd = c.xcd_map == 2 ? 0 : (c.xcd_map == 3 ? 2 : (c.xcd_map == 4 ? 3 : 1));
-    if (c.xcd_map == 0 && p == Path::kRagged && (c.kernel == 0 || c.kernel == kKernelScan || c.kernel == kKernelScanPipe))
-        r.xcd = 3;  // byte-balanced wave ranges (scan kernel only)
-    r.nt = c.nontemporal != 2;
-    r.run = (c.run_segs >= 1 && c.run_segs <= (int)kScanRun) ? (uint32_t)c.run_segs : kScanRun;
-    r.xcd_chunk_param = c.xcd_chunk;
-    return r;
+static uint32_t grid_for(uint64_t wave_tasks, uint32_t max_blocks) {
+    const uint64_t want = (wave_tasks + kWavesPerBlock - 1) / kWavesPerBlock;
+    return (uint32_t)(want < max_blocks ? want : max_blocks);
 }
 
-// Auto window of the fixed short-segment buffer-load path (NSX_PARAM_WINDOW_BYTES = 0): batches of at least twice this size are
-// launched as back-to-back windows of about this many bytes. One launch over config 5's 25 GB span runs ~4%
-// slower per byte than 1.5 GB windows of it.
-constexpr uint64_t kAutoWindow = 1600ull * 1000 * 1000;
+static uint32_t max_blocks_of(const LaunchCfg& c, int default_bpc) {
+    const int bpc = (c.blocks_per_cu >= 1 && c.blocks_per_cu <= 8) ? c.blocks_per_cu : default_bpc;
+    return (uint32_t)(c.cus * bpc);
+}
 
 static bool use_block_mode(const LaunchCfg& c, uint64_t n) {
     return c.block_mode == 2 || (c.block_mode == 0 && n < (uint64_t)c.cus * 4);
 }
 
-static hipError_t launch_fixed_rows(const Plan& c, const uint8_t* base, uint64_t stride, uint32_t seg_len,
-                                    uint64_t n, const uint32_t* partial, uint16_t* out, const uint8_t* safe_end,
-                                    int nrows, int u, hipStream_t st) {
-    const uint64_t ntasks = (n + u - 1) / u;
-    const uint64_t want = (ntasks + kWavesPerBlock - 1) / kWavesPerBlock;
-    const uint32_t grid = (uint32_t)(want < c.max_blocks ? want : c.max_blocks);
-#define NSX_FIXED(U_, NR_)                                                                          \
-    if (u == U_ && nrows == NR_) {                                                                   \
-        if (c.nt)                                                                                    \
-            hipLaunchKernelGGL((csum_fixed_kernel<U_, NR_, true>), dim3(grid), dim3(kBlock), 0, st,  \
-                               base, stride, seg_len, n, partial, out, safe_end, c.xcd);             \
-        else                                                                                         \
-            hipLaunchKernelGGL((csum_fixed_kernel<U_, NR_, false>), dim3(grid), dim3(kBlock), 0, st, \
-                               base, stride, seg_len, n, partial, out, safe_end, c.xcd);             \
-        return hipGetLastError();                                                                    \
+// Auto window of the fixed short-segment path (window_bytes = 0): batches of at least twice this size are
+// launched as back-to-back windows of about this many bytes. One launch over config 5's 25 GB span runs
+// ~5% slower per byte than 1.6 GB windows of it.
+constexpr uint64_t kAutoWindow = 1600ull * 1000 * 1000;
+// Buffer descriptors address < 2^31 bytes of results / partials / offsets: batches are cut into launches
+// of at most this many segments.
+constexpr uint64_t kFixedChunk = 1ull << 28;
+constexpr uint64_t kRaggedChunk = 1ull << 27;
+
+static uint64_t fixed_rows(uint32_t seg_len) { return ((uint64_t)seg_len + 3 + kRow - 1) / kRow; }
+
+// Segments per launch of the fixed short-segment path.
+static uint64_t fixed_window(const LaunchCfg& c, uint64_t stride, uint64_t n) {
+    if (stride == 0) return kFixedChunk;  // every segment aliases the first: one launch per chunk
+    if (c.window_bytes > 0) {
+        const uint64_t w = (uint64_t)c.window_bytes / stride;
+        return w < 1 ? 1 : (w < kFixedChunk ? w : kFixedChunk);
     }
-    NSX_FIXED(1, 1) NSX_FIXED(2, 1) NSX_FIXED(4, 1)
-    NSX_FIXED(1, 2) NSX_FIXED(2, 2) NSX_FIXED(4, 2)
-    NSX_FIXED(1, 4) NSX_FIXED(2, 4)
+    if (c.window_bytes == 0 && n * stride >= 2 * kAutoWindow) {
+        const uint64_t nw = (n * stride + kAutoWindow - 1) / kAutoWindow;  // config 5: 16 windows of 1M segments
+        const uint64_t win = (n + nw - 1) / nw;
+        return win < kFixedChunk ? win : kFixedChunk;
+    }
+    return kFixedChunk;
+}
+
+uint64_t fixed_launch_count(const LaunchCfg& c, uintptr_t /*base*/, uint64_t stride, uint32_t seg_len, uint64_t n) {
+    if (n == 0) return 0;
+    if (use_block_mode(c, n) || fixed_rows(seg_len) > 4) return 1;
+    const uint64_t win = fixed_window(c, stride, n);
+    return (n + win - 1) / win;
+}
+
+// One launch of the short-segment fixed path: U segments per wave task, NR rows per segment.
+static hipError_t launch_fixed_short(const LaunchCfg& c, const uint8_t* base, uint64_t stride, uint32_t seg_len,
+                                     uint64_t n, const uint32_t* partial, uint16_t* out, int nrows, bool aligned,
+                                     hipStream_t st) {
+    // Aligned (config 2): the software-pipelined kernel, 8-segment tasks at one block per CU — two register
+    // sets of 8 × 2 KiB per wave, a wave per SIMD (config 2 0.2222 → 0.2184 ms, config 5 3.712 → 3.626 ms
+    // against 4-segment tasks at 2 blocks/CU, tools/alloc_study.py). Unaligned: 4-segment tasks, 2 blocks/CU.
+    int u = (c.segs_per_wave == 1 || c.segs_per_wave == 2 || c.segs_per_wave == 4 || c.segs_per_wave == 8)
+                ? c.segs_per_wave : (aligned ? 8 : 4);
+    if (nrows == 4 && u > 4) u = 4;
+    const uint64_t ntasks = (n + u - 1) / u;
+    const uint32_t grid = grid_for(ntasks, max_blocks_of(c, aligned ? 1 : 2));
+    const uint32_t clog = deal_clog(c.xcd_chunk, ntasks, (uint64_t)u * stride);
+#define NSX_FIXED(U_, NR_)                                                                                    \
+    if (u == U_ && nrows == NR_) {                                                                             \
+        if (aligned)                                                                                           \
+            hipLaunchKernelGGL((csum_fixed_swp_kernel<U_, NR_>), dim3(grid), dim3(kBlock), 0, st, base, stride, \
+                               seg_len, (uint32_t)n, partial, out, clog);                                      \
+        else                                                                                                   \
+            hipLaunchKernelGGL((csum_fixed_buf_kernel<U_, NR_>), dim3(grid), dim3(kBlock), 0, st, base, stride, \
+                               seg_len, (uint32_t)n, partial, out, clog);                                      \
+        return hipGetLastError();                                                                              \
+    }
+    NSX_FIXED(1, 1) NSX_FIXED(2, 1) NSX_FIXED(4, 1) NSX_FIXED(8, 1)
+    NSX_FIXED(1, 2) NSX_FIXED(2, 2) NSX_FIXED(4, 2) NSX_FIXED(8, 2)
+    NSX_FIXED(1, 4) NSX_FIXED(2, 4) NSX_FIXED(4, 4)
 #undef NSX_FIXED
-    return hipErrorInvalidValue;
-}
-
-static hipError_t launch_fixed_pipe(const Plan& c, const uint8_t* base, uint64_t stride, uint32_t seg_len,
-                                    uint64_t n, const uint32_t* partial, uint16_t* out, const uint8_t* safe_end,
-                                    int nrows, int u, bool swp, hipStream_t st) {
-    const uint64_t ntasks = (n + u - 1) / u;
-    const uint64_t want = (ntasks + kWavesPerBlock - 1) / kWavesPerBlock;
-    const uint32_t grid = (uint32_t)(want < c.max_blocks ? want : c.max_blocks);
-    const bool aligned = ((uintptr_t)base & 3u) == 0 && (stride & 3u) == 0 && (seg_len & 3u) == 0;
-    const uint32_t clog = deal_clog(c.xcd_chunk_param, ntasks, (uint64_t)u * stride);
-#define NSX_PIPE(U_, NR_)                                                                                  \
-    if (u == U_ && nrows == NR_) {                                                                          \
-        if (aligned && swp) {                                                                               \
-            if (c.nt)                                                                                       \
-                hipLaunchKernelGGL((csum_fixed_swp_kernel<U_, NR_, true>), dim3(grid), dim3(kBlock), 0, st,    \
-                                   base, stride, seg_len, (uint32_t)n, partial, out, c.xcd, clog);          \
-            else                                                                                            \
-                hipLaunchKernelGGL((csum_fixed_swp_kernel<U_, NR_, false>), dim3(grid), dim3(kBlock), 0, st,   \
-                                   base, stride, seg_len, (uint32_t)n, partial, out, c.xcd, clog);          \
-        } else if (aligned) {                                                                               \
-            if (c.nt)                                                                                       \
-                hipLaunchKernelGGL((csum_fixed_buf_kernel<U_, NR_, true, true>), dim3(grid), dim3(kBlock), 0, st, \
-                                   base, stride, seg_len, (uint32_t)n, partial, out, c.xcd, clog);          \
-            else                                                                                            \
-                hipLaunchKernelGGL((csum_fixed_buf_kernel<U_, NR_, false, true>), dim3(grid), dim3(kBlock), 0, \
-                                   st, base, stride, seg_len, (uint32_t)n, partial, out, c.xcd, clog);      \
-        } else {                                                                                            \
-            if (c.nt)                                                                                       \
-                hipLaunchKernelGGL((csum_fixed_buf_kernel<U_, NR_, true, false>), dim3(grid), dim3(kBlock), 0, \
-                                   st, base, stride, seg_len, (uint32_t)n, partial, out, c.xcd, clog);      \
-            else                                                                                            \
-                hipLaunchKernelGGL((csum_fixed_buf_kernel<U_, NR_, false, false>), dim3(grid), dim3(kBlock), 0, \
-                                   st, base, stride, seg_len, (uint32_t)n, partial, out, c.xcd, clog);      \
-        }                                                                                                   \
-        return hipGetLastError();                                                                           \
-    }
-    NSX_PIPE(1, 1) NSX_PIPE(2, 1) NSX_PIPE(4, 1) NSX_PIPE(8, 1)
-    NSX_PIPE(1, 2) NSX_PIPE(2, 2) NSX_PIPE(4, 2) NSX_PIPE(8, 2)
-    NSX_PIPE(1, 4) NSX_PIPE(2, 4) NSX_PIPE(4, 4)
-#undef NSX_PIPE
-    return hipErrorInvalidValue;
-}
-
-template <bool RAGGED, bool VERIFY>
-static hipError_t launch_seg(const Plan& c, const uint8_t* base, const uint64_t* offsets, uint64_t stride,
-                             uint32_t seg_len, uint64_t n, const uint32_t* partial, uint16_t* out, uint8_t* ok,
-                             const uint8_t* safe_end, bool block_mode, hipStream_t st) {
-    if (block_mode) {
-        const uint32_t grid = (uint32_t)(n < c.max_blocks ? n : c.max_blocks);
-        if (c.nt)
-            hipLaunchKernelGGL((csum_block_kernel<RAGGED, 4, true, VERIFY>), dim3(grid), dim3(kBlock), 0, st, base,
-                               offsets, stride, seg_len, n, partial, out, ok, safe_end);
-        else
-            hipLaunchKernelGGL((csum_block_kernel<RAGGED, 4, false, VERIFY>), dim3(grid), dim3(kBlock), 0, st, base,
-                               offsets, stride, seg_len, n, partial, out, ok, safe_end);
-    } else {
-        const uint64_t want = (n + kWavesPerBlock - 1) / kWavesPerBlock;
-        const uint32_t grid = (uint32_t)(want < c.max_blocks ? want : c.max_blocks);
-        const uint32_t clog = RAGGED ? 0u : deal_clog(c.xcd_chunk_param, n, std::max<uint64_t>(stride, 1));
-        if (c.nt)
-            hipLaunchKernelGGL((csum_wave_kernel<RAGGED, 4, true, VERIFY>), dim3(grid), dim3(kBlock), 0, st, base,
-                               offsets, stride, seg_len, n, partial, out, ok, safe_end, c.xcd, clog);
-        else
-            hipLaunchKernelGGL((csum_wave_kernel<RAGGED, 4, false, VERIFY>), dim3(grid), dim3(kBlock), 0, st, base,
-                               offsets, stride, seg_len, n, partial, out, ok, safe_end, c.xcd, clog);
-    }
-    return hipGetLastError();
-}
-
-template <bool RAGGED, bool VERIFY>
-static hipError_t launch_stream(const Plan& c, const uint8_t* base, const uint64_t* offsets, uint64_t stride,
-                                uint32_t seg_len, uint64_t n, const uint32_t* partial, uint16_t* out, uint8_t* ok,
-                                const uint8_t* safe_end, hipStream_t st) {
-    const uint64_t ntasks = (n + kRun - 1) / kRun;
-    const uint64_t want = (ntasks + kWavesPerBlock - 1) / kWavesPerBlock;
-    const uint32_t grid = (uint32_t)(want < c.max_blocks ? want : c.max_blocks);
-#define NSX_STREAM(R_)                                                                                      \
-    if (c.rows == R_) {                                                                                      \
-        if (c.nt)                                                                                            \
-            hipLaunchKernelGGL((csum_stream_kernel<RAGGED, R_, true, VERIFY>), dim3(grid), dim3(kBlock), 0, st, \
-                               base, offsets, stride, seg_len, n, partial, out, ok, safe_end, c.xcd);        \
-        else                                                                                                 \
-            hipLaunchKernelGGL((csum_stream_kernel<RAGGED, R_, false, VERIFY>), dim3(grid), dim3(kBlock), 0,  \
-                               st, base, offsets, stride, seg_len, n, partial, out, ok, safe_end, c.xcd);     \
-        return hipGetLastError();                                                                            \
-    }
-    NSX_STREAM(4) NSX_STREAM(8) NSX_STREAM(16)
-#undef NSX_STREAM
     return hipErrorInvalidValue;
 }
 
@@ -2255,132 +1698,53 @@ hipError_t launch_fixed(const LaunchCfg& c, const void* d_base, uint64_t stride,
     const uint8_t* base = static_cast<const uint8_t*>(d_base);
     const uint8_t* end = base + (n - 1) * stride + seg_len;
     const uint8_t* safe_end = reinterpret_cast<const uint8_t*>(((uintptr_t)end + 3) & ~(uintptr_t)3);
-    if (use_block_mode(c, n))
-        return launch_seg<false, false>(resolve(c, Path::kBlock), base, nullptr, stride, seg_len, n, partial, out,
-                                        nullptr, safe_end, true, st);
-    // Rows a segment window can span (the window starts up to 3 bytes early).
-    const uint64_t rows = ((uint64_t)seg_len + 3 + kRow - 1) / kRow;
-    const Path path = rows <= 4 ? Path::kFixedShort : Path::kFixedLong;
-    Plan p = resolve(c, path);
-    if (c.kernel == kKernelRowStream)
-        return launch_stream<false, false>(p, base, nullptr, stride, seg_len, n, partial, out, nullptr, safe_end, st);
-    if (path == Path::kFixedShort) {
+    if (use_block_mode(c, n)) {
+        const uint32_t grid = (uint32_t)std::min<uint64_t>(n, max_blocks_of(c, 8));
+        hipLaunchKernelGGL((csum_block_kernel<false, 4, false>), dim3(grid), dim3(kBlock), 0, st, base, nullptr, stride,
+                           seg_len, n, partial, out, nullptr, safe_end);
+        return hipGetLastError();
+    }
+    const uint64_t rows = fixed_rows(seg_len);  // a segment window starts up to 3 bytes early
+    if (rows <= 4) {
         const int nrows = rows <= 1 ? 1 : (rows <= 2 ? 2 : 4);
         const bool aligned = ((uintptr_t)base & 3u) == 0 && (stride & 3u) == 0 && (seg_len & 3u) == 0;
-        // Default for aligned batches (config 2): the software-pipelined kernel with 8-segment tasks at one
-        // block per CU — two register sets of 8 × 2 KiB per wave, a wave per SIMD (tools/alloc_study.py:
-        // config 2 0.2222 → 0.2184 ms, config 5 3.712 → 3.626 ms against the unpipelined 4 × 2 blocks/CU).
-        const bool swp = c.kernel == kKernelSwPipe || (c.kernel == 0 && aligned);
-        if (c.kernel == 0 && aligned) {
-            if (c.blocks_per_cu == 0) p.max_blocks = (uint32_t)c.cus;
-            if (c.segs_per_wave == 0) p.spw = 8;
+        const uint64_t win = fixed_window(c, stride, n);
+        for (uint64_t c0 = 0; c0 < n; c0 += win) {
+            const uint64_t cn = n - c0 < win ? n - c0 : win;
+            const hipError_t e = launch_fixed_short(c, base + c0 * stride, stride, seg_len, cn,
+                                                    partial ? partial + c0 : nullptr, out + c0, nrows, aligned, st);
+            if (e != hipSuccess) return e;
         }
-        if (c.kernel == kKernelPipelined || c.kernel == kKernelSwPipe || c.kernel == 0) {
-            const int u = (nrows == 4 && p.spw > 4) ? 4 : p.spw;
-            // Buffer descriptors address ≤ 2^31 bytes of results/partials: chunk huge batches. A launch
-            // may also be split into back-to-back windows (NSX_PARAM_WINDOW_BYTES).
-            constexpr uint64_t kChunk = 1ull << 28;
-            uint64_t win = kChunk;
-            if (c.window_bytes > 0) {
-                const uint64_t w = (uint64_t)c.window_bytes / stride;
-                win = w < 1 ? 1 : (w < kChunk ? w : kChunk);
-            } else if (c.window_bytes == 0 && n * stride >= 2 * kAutoWindow) {
-                // Auto: equal windows of about kAutoWindow bytes (config 5: 16 of 1M segments).
-                const uint64_t nw = (n * stride + kAutoWindow - 1) / kAutoWindow;
-                win = (n + nw - 1) / nw;
-                if (win > kChunk) win = kChunk;
-            }
-            for (uint64_t c0 = 0; c0 < n; c0 += win) {
-                const uint64_t cn = n - c0 < win ? n - c0 : win;
-                hipError_t e = launch_fixed_pipe(p, base + c0 * stride, stride, seg_len, cn,
-                                                 partial ? partial + c0 : nullptr, out + c0, safe_end, nrows, u,
-                                                 swp, st);
-                if (e != hipSuccess) return e;
-            }
-            return hipSuccess;
-        }
-        const int u = (nrows == 4 && p.spw > 2) ? 2 : (p.spw > 4 ? 4 : p.spw);
-        return launch_fixed_rows(p, base, stride, seg_len, n, partial, out, safe_end, nrows, u, st);
+        return hipSuccess;
     }
-    const bool aligned = ((uintptr_t)base & 3u) == 0 && (stride & 3u) == 0 && (seg_len & 3u) == 0;
-    if (aligned && seg_len < (1u << 31) && (c.kernel == kKernelSwPipe || c.kernel == kKernelLongSwp)) {
-        const uint64_t want = (n + kWavesPerBlock - 1) / kWavesPerBlock;
-        const uint32_t grid = (uint32_t)(want < p.max_blocks ? want : p.max_blocks);
-        const uint32_t clog = deal_clog(p.xcd_chunk_param, n, stride);
-#define NSX_LONG(R_)                                                                                            \
-        if (p.rows == R_) {                                                                                      \
-            if (p.nt)                                                                                            \
-                hipLaunchKernelGGL((csum_long_swp_kernel<R_, true>), dim3(grid), dim3(kBlock), 0, st, base, stride, \
-                                   seg_len, n, partial, out, p.xcd, clog);                                       \
-            else                                                                                                 \
-                hipLaunchKernelGGL((csum_long_swp_kernel<R_, false>), dim3(grid), dim3(kBlock), 0, st, base,      \
-                                   stride, seg_len, n, partial, out, p.xcd, clog);                               \
-            return hipGetLastError();                                                                            \
-        }
-        NSX_LONG(4) NSX_LONG(8) NSX_LONG(16)
-#undef NSX_LONG
-    }
-    return launch_seg<false, false>(p, base, nullptr, stride, seg_len, n, partial, out, nullptr, safe_end, false, st);
+    // Long segments (config 4's 64 KiB): one wave per segment, rows 4 at a time, 2 blocks/CU.
+    const uint32_t grid = grid_for(n, max_blocks_of(c, 2));
+    const uint32_t clog = deal_clog(c.xcd_chunk, n, std::max<uint64_t>(stride, 1));
+    hipLaunchKernelGGL((csum_wave_kernel<4>), dim3(grid), dim3(kBlock), 0, st, base, stride, seg_len, n, partial, out,
+                       safe_end, clog);
+    return hipGetLastError();
 }
 
 template <bool VERIFY>
-static hipError_t launch_ragged_buf(const Plan& c, const uint8_t* base, const uint64_t* offsets, uint64_t n,
-                                    const uint32_t* partial, uint16_t* out, uint8_t* ok, hipStream_t st) {
-    // Buffer descriptors address ≤ 2^31 bytes of offsets/results: chunk huge batches.
-    constexpr uint64_t kChunk = 1ull << 27;
-    for (uint64_t c0 = 0; c0 < n; c0 += kChunk) {
-        const uint32_t cn = (uint32_t)(n - c0 < kChunk ? n - c0 : kChunk);
-        const uint64_t ntasks = (cn + kRun - 1) / kRun;
-        const uint64_t want = (ntasks + kWavesPerBlock - 1) / kWavesPerBlock;
-        const uint32_t grid = (uint32_t)(want < c.max_blocks ? want : c.max_blocks);
+static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, const uint64_t* offsets, uint64_t n,
+                                     const uint32_t* partial, uint16_t* out, uint8_t* ok, hipStream_t st) {
+    // Default: 8 rows per batch, 63-segment runs, 2 blocks/CU (tools/c3_sweep.sh).
+    const int rows = (c.rows == 4 || c.rows == 8 || c.rows == 16) ? c.rows : 8;
+    const uint32_t run = (c.run_segs >= 1 && c.run_segs <= (int)kScanRun) ? (uint32_t)c.run_segs : kScanRun;
+    const uint32_t mb = max_blocks_of(c, 2);
+    for (uint64_t c0 = 0; c0 < n; c0 += kRaggedChunk) {
+        const uint32_t cn = (uint32_t)(n - c0 < kRaggedChunk ? n - c0 : kRaggedChunk);
+        const uint32_t grid = grid_for((cn + run - 1) / run, mb);
         const uint32_t* pc = partial ? partial + c0 : nullptr;
         uint16_t* oc = out ? out + c0 : nullptr;
         uint8_t* kc = ok ? ok + c0 : nullptr;
-#define NSX_RBUF(R_)                                                                                             \
-        if (c.rows == R_) {                                                                                       \
-            if (c.nt)                                                                                             \
-                hipLaunchKernelGGL((csum_ragged_buf_kernel<R_, true, VERIFY>), dim3(grid), dim3(kBlock), 0, st,   \
-                                   base, offsets + c0, cn, pc, oc, kc, c.xcd);                                    \
-            else                                                                                                  \
-                hipLaunchKernelGGL((csum_ragged_buf_kernel<R_, false, VERIFY>), dim3(grid), dim3(kBlock), 0, st,  \
-                                   base, offsets + c0, cn, pc, oc, kc, c.xcd);                                    \
-        }
-        NSX_RBUF(4) NSX_RBUF(8) NSX_RBUF(16)
-#undef NSX_RBUF
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
-}
-
-template <bool VERIFY>
-static hipError_t launch_ragged_scan(const Plan& c, const uint8_t* base, const uint64_t* offsets, uint64_t n,
-                                     const uint32_t* partial, uint16_t* out, uint8_t* ok, bool pipe,
-                                     hipStream_t st) {
-    constexpr uint64_t kChunk = 1ull << 27;
-    for (uint64_t c0 = 0; c0 < n; c0 += kChunk) {
-        const uint32_t cn = (uint32_t)(n - c0 < kChunk ? n - c0 : kChunk);
-        const uint64_t ntasks = (cn + c.run - 1) / c.run;
-        const uint64_t want = (ntasks + kWavesPerBlock - 1) / kWavesPerBlock;
-        const uint32_t grid = (uint32_t)(want < c.max_blocks ? want : c.max_blocks);
-        const uint32_t* pc = partial ? partial + c0 : nullptr;
-        uint16_t* oc = out ? out + c0 : nullptr;
-        uint8_t* kc = ok ? ok + c0 : nullptr;
-#define NSX_RSCAN(R_)                                                                                             \
-        if (c.rows == R_) {                                                                                        \
-            if (pipe)                                                                                              \
-                hipLaunchKernelGGL((csum_ragged_scan_kernel<R_, true, VERIFY, true>), dim3(grid), dim3(kBlock), 0, \
-                                   st, base, offsets + c0, cn, pc, oc, kc, c.xcd, c.run);                          \
-            else if (c.nt)                                                                                         \
-                hipLaunchKernelGGL((csum_ragged_scan_kernel<R_, true, VERIFY, false>), dim3(grid), dim3(kBlock), 0, \
-                                   st, base, offsets + c0, cn, pc, oc, kc, c.xcd, c.run);                          \
-            else                                                                                                   \
-                hipLaunchKernelGGL((csum_ragged_scan_kernel<R_, false, VERIFY, false>), dim3(grid), dim3(kBlock), 0, \
-                                   st, base, offsets + c0, cn, pc, oc, kc, c.xcd, c.run);                          \
-        }
+#define NSX_RSCAN(R_)                                                                                          \
+        if (rows == R_)                                                                                         \
+            hipLaunchKernelGGL((csum_ragged_scan_kernel<R_, VERIFY>), dim3(grid), dim3(kBlock), 0, st, base,    \
+                               offsets + c0, cn, pc, oc, kc, run);
         NSX_RSCAN(4) NSX_RSCAN(8) NSX_RSCAN(16)
 #undef NSX_RSCAN
-        hipError_t e = hipGetLastError();
+        const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
@@ -2389,27 +1753,18 @@ static hipError_t launch_ragged_scan(const Plan& c, const uint8_t* base, const u
 hipError_t launch_ragged(const LaunchCfg& c, const void* d_base, const uint64_t* d_offsets, uint64_t n,
                          const uint32_t* partial, uint16_t* out, uint8_t* ok, hipStream_t st) {
     const uint8_t* base = static_cast<const uint8_t*>(d_base);
-    if (use_block_mode(c, n)) {
-        const Plan p = resolve(c, Path::kBlock);
-        if (ok) return launch_seg<true, true>(p, base, d_offsets, 0, 0, n, partial, out, ok, nullptr, true, st);
-        return launch_seg<true, false>(p, base, d_offsets, 0, 0, n, partial, out, nullptr, nullptr, true, st);
+    if (use_block_mode(c, n)) {  // few segments: a block per segment
+        const uint32_t grid = (uint32_t)std::min<uint64_t>(n, max_blocks_of(c, 8));
+        if (ok)
+            hipLaunchKernelGGL((csum_block_kernel<true, 4, true>), dim3(grid), dim3(kBlock), 0, st, base, d_offsets,
+                               0, 0, n, partial, out, ok, nullptr);
+        else
+            hipLaunchKernelGGL((csum_block_kernel<true, 4, false>), dim3(grid), dim3(kBlock), 0, st, base, d_offsets,
+                               0, 0, n, partial, out, nullptr, nullptr);
+        return hipGetLastError();
     }
-    const Plan p = resolve(c, Path::kRagged);
-    if (c.kernel == 0 || c.kernel == kKernelScan || c.kernel == kKernelScanPipe) {
-        const bool pipe = c.kernel == kKernelScanPipe;
-        if (ok) return launch_ragged_scan<true>(p, base, d_offsets, n, partial, out, ok, pipe, st);
-        return launch_ragged_scan<false>(p, base, d_offsets, n, partial, out, nullptr, pipe, st);
-    }
-    if (c.kernel == kKernelPipelined) {
-        if (ok) return launch_ragged_buf<true>(p, base, d_offsets, n, partial, out, ok, st);
-        return launch_ragged_buf<false>(p, base, d_offsets, n, partial, out, nullptr, st);
-    }
-    if (c.kernel == kKernelRowStream) {
-        if (ok) return launch_stream<true, true>(p, base, d_offsets, 0, 0, n, partial, out, ok, nullptr, st);
-        return launch_stream<true, false>(p, base, d_offsets, 0, 0, n, partial, out, nullptr, nullptr, st);
-    }
-    if (ok) return launch_seg<true, true>(p, base, d_offsets, 0, 0, n, partial, out, ok, nullptr, false, st);
-    return launch_seg<true, false>(p, base, d_offsets, 0, 0, n, partial, out, nullptr, nullptr, false, st);
+    if (ok) return launch_ragged_scan<true>(c, base, d_offsets, n, partial, out, ok, st);
+    return launch_ragged_scan<false>(c, base, d_offsets, n, partial, out, nullptr, st);
 }
 
 hipError_t launch_pseudo_ipv4(const uint8_t* src, const uint8_t* dst, const uint32_t* len, uint8_t proto,
@@ -2439,52 +1794,34 @@ hipError_t launch_verify_mask(const uint16_t* raw, uint64_t n, uint64_t* mask, u
     return hipGetLastError();
 }
 
-hipError_t launch_tcp_build(const TcpHdrSoA& h, const uint8_t* opts, const uint64_t* opt_off, const uint8_t* data,
-                            const uint64_t* data_off, uint64_t data_bytes, const uint32_t* partial, uint64_t n,
-                            uint8_t* out, const uint64_t* out_off, uint16_t* raw, uint32_t max_blocks, int policy,
-                            int xchunk, int kernel, int spw, hipStream_t st) {
-    // kernel: 0 = groups of ≤ 2-row segments software-pipelined (the fast composition when every segment of the
-    // group allows it, else the general one), 2 = never pipelined, 3 = the general pipelined composition always;
-    // spw: segments per pipelined register set, 2 (default) or 1
-    // Group size: up to 64 segments per wave task, fewer when n would leave waves idle.
+hipError_t launch_tcp_build(const LaunchCfg& c, const TcpHdrSoA& h, const uint8_t* opts, const uint64_t* opt_off,
+                            const uint8_t* data, const uint64_t* data_off, uint64_t data_bytes,
+                            const uint32_t* partial, uint64_t n, uint8_t* out, const uint64_t* out_off,
+                            uint16_t* raw, hipStream_t st) {
+    // Path by layout: groups of ≤ 2-row images software-pipelined (the fast composition when every segment of
+    // the group allows it, else the general one); longer images unpipelined. kernel 2 forces the unpipelined
+    // path, kernel 3 the general pipelined composition (test coverage of those paths on every layout).
+    // Group size: up to 64 segments per wave task, fewer when n would leave waves idle. 4 blocks/CU.
+    const uint32_t max_blocks = max_blocks_of(c, 4);
     const uint64_t waves = (uint64_t)max_blocks * kWavesPerBlock;
     const uint32_t group = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, (n + waves - 1) / waves));
     const uint64_t tasks = (n + group - 1) / group;
-    const uint64_t want = (tasks + kWavesPerBlock - 1) / kWavesPerBlock;
-    const uint32_t grid = (uint32_t)(want < max_blocks ? want : max_blocks);
-    const uint32_t clog = deal_clog(xchunk, tasks, (uint64_t)group * 3000u);  // ~payload + image per segment
-    const int pipe = kernel == 2 ? 0 : kernel == 3 ? 2 : 1;  // 3: the general pipelined path for every layout
-    // policy: 0/2 = default cache policy (measured best: segment-boundary lines stay in L2 for
-    // the neighbour segment's load and partial-line stores merge there), 1 = nt loads and
-    // stores, 3 = nt loads + plain stores, 4 = plain loads + nt stores
-#define NSX_BUILD_PS(LP, SP, PS)                                                                                   \
-    if (opt_off)                                                                                                   \
-        hipLaunchKernelGGL((tcp_build_kernel<LP, SP, PS, true>), dim3(grid), dim3(kBlock), 0, st, h, opts, opt_off, \
-                           data, data_off, data_bytes, partial, n, out, out_off, raw, group, clog, pipe);         \
-    else                                                                                                           \
-        hipLaunchKernelGGL((tcp_build_kernel<LP, SP, PS, false>), dim3(grid), dim3(kBlock), 0, st, h, opts,        \
-                           opt_off, data, data_off, data_bytes, partial, n, out, out_off, raw, group, clog, pipe)
-#define NSX_BUILD(LP, SP)        \
-    if (spw != 1) {              \
-        NSX_BUILD_PS(LP, SP, 2); \
-    } else {                     \
-        NSX_BUILD_PS(LP, SP, 1); \
-    }
-    switch (policy) {
-        case 1: NSX_BUILD(2, 2); break;
-        case 3: NSX_BUILD(2, 0); break;
-        case 4: NSX_BUILD(0, 2); break;
-        default: NSX_BUILD(0, 0); break;
-    }
-#undef NSX_BUILD
-#undef NSX_BUILD_PS
+    const uint32_t grid = grid_for(tasks, max_blocks);
+    const uint32_t clog = deal_clog(c.xcd_chunk, tasks, (uint64_t)group * 3000u);  // ~payload + image per segment
+    const int pipe = c.kernel == 2 ? 0 : c.kernel == 3 ? 2 : 1;
+    if (opt_off)
+        hipLaunchKernelGGL((tcp_build_kernel<0, 0, 2, true>), dim3(grid), dim3(kBlock), 0, st, h, opts, opt_off, data,
+                           data_off, data_bytes, partial, n, out, out_off, raw, group, clog, pipe);
+    else
+        hipLaunchKernelGGL((tcp_build_kernel<0, 0, 2, false>), dim3(grid), dim3(kBlock), 0, st, h, opts, opt_off, data,
+                           data_off, data_bytes, partial, n, out, out_off, raw, group, clog, pipe);
     return hipGetLastError();
 }
 
-hipError_t launch_ipv4_hdr(uint8_t* base, uint64_t stride, uint32_t hdr_off, uint64_t n, int mode, uint16_t* out,
-                           uint64_t* mask, int cus, int bpc, int kernel, int unroll, int xchunk, hipStream_t st) {
-    // kernel: 0 = auto (pipelined flat kernel for packed 20 B headers, else LDS-dense for stride ≤ 64, else
-    // per-thread), 1 = per-thread, 2 = LDS-dense (stride ≤ 64), 3 = flat without pipelining.
+hipError_t launch_ipv4_hdr(const LaunchCfg& c, uint8_t* base, uint64_t stride, uint32_t hdr_off, uint64_t n,
+                           int mode, uint16_t* out, uint64_t* mask, hipStream_t st) {
+    // Kernel by layout: packed 20 B headers (stride 20, hdr_off 0, 4-aligned base) → the pipelined flat
+    // kernel; other strides ≤ 64 → LDS-dense; else per-thread. kernel 1 forces per-thread, 2 LDS-dense.
     // mode: 0 verify (raw sums), 1 fill in place, 2 verify into the bitmask `mask`.
     auto by_mode = [&](auto launch) {
         switch (mode) {
@@ -2493,64 +1830,39 @@ hipError_t launch_ipv4_hdr(uint8_t* base, uint64_t stride, uint32_t hdr_off, uin
             default: launch(std::integral_constant<int, 0>{}); break;
         }
     };
-    if (stride == 20 && hdr_off == 0 && ((uintptr_t)base & 3u) == 0 && (kernel == 0 || kernel == 3 || kernel == 4)) {
-        const bool pipe = kernel != 3;  // kernel 3: the unpipelined flat kernel (measured alternative)
-        const bool defer = kernel == 4 && mode == 0 && out;  // kernel 4: deferred raw-sum stores (measured alternative)
-        // packed option-less headers: flat-stream kernel. Default 1 block/CU with 2 tasks (10 KiB) in flight
-        // per wave = 40 KiB per CU (tools/sweep.py: 0.220 ms vs 0.232 at 2 blocks/CU, 0.284 at 1 task/wave);
-        // chunks keep each launch's results within one descriptor (2^28 headers = 2^22 mask words)
-        const uint32_t mb = (uint32_t)cus * (uint32_t)(bpc >= 1 && bpc <= 8 ? bpc : 1);
-        constexpr uint64_t kChunk = 1ull << 28;
-        for (uint64_t c0 = 0; c0 < n; c0 += kChunk) {
-            const uint32_t cn = (uint32_t)std::min<uint64_t>(kChunk, n - c0);
+    if (stride == 20 && hdr_off == 0 && ((uintptr_t)base & 3u) == 0 && c.kernel == 0) {
+        // 1 block/CU with 2 tasks (10 KiB) in flight per wave = 40 KiB per CU (tools/sweep.py: 0.220 ms vs
+        // 0.232 at 2 blocks/CU, 0.284 at 1 task/wave); chunks keep each launch's results within one
+        // descriptor (2^28 headers = 2^22 mask words)
+        const uint32_t mb = max_blocks_of(c, 1);
+        for (uint64_t c0 = 0; c0 < n; c0 += kFixedChunk) {
+            const uint32_t cn = (uint32_t)std::min<uint64_t>(kFixedChunk, n - c0);
             const uint64_t tasks = (cn + kHdr20Task - 1) / kHdr20Task;
-            const uint64_t want_f = (tasks + kWavesPerBlock - 1) / kWavesPerBlock;
-            const uint32_t grid_f = (uint32_t)(want_f < mb ? want_f : mb);
+            const uint32_t grid = grid_for(tasks, mb);
             uint8_t* b = base + c0 * 20u;
             uint16_t* o = out ? out + c0 : nullptr;
             uint64_t* mk = mask ? mask + c0 / kWave : nullptr;
-            const size_t lds = (size_t)(kHdr20Lds + (defer ? kHdr20DeferSlots * kWave * 8u : 0u)) * kWavesPerBlock;
-            const uint32_t clog = deal_clog(xchunk, tasks, kHdr20Lds + kHdr20Task * 2u);
+            const size_t lds = (size_t)kHdr20Lds * kWavesPerBlock;
+            const uint32_t clog = deal_clog(c.xcd_chunk, tasks, kHdr20Lds + kHdr20Task * 2u);
             by_mode([&](auto m) {
                 constexpr int M = decltype(m)::value;
-#define NSX_H20(U)                                                                                              \
-    do {                                                                                                        \
-        if (M == 0 && defer)                                                                                    \
-            hipLaunchKernelGGL((ipv4_hdr20_kernel<0, U, true, kHdr20DeferSlots>),                          \
-                               dim3(grid_f), dim3(kBlock), lds, st, b, cn, o, clog, mk);                        \
-        else if (pipe)                                                                                          \
-            hipLaunchKernelGGL((ipv4_hdr20_kernel<M, U, true>), dim3(grid_f), dim3(kBlock), lds, st, b, cn, o,   \
-                               clog, mk);                                                                       \
-        else                                                                                                    \
-            hipLaunchKernelGGL((ipv4_hdr20_kernel<M, U, false>), dim3(grid_f), dim3(kBlock), lds, st, b, cn, o,  \
-                               clog, mk);                                                                       \
-    } while (0)
-                switch (unroll) {
-                    case 1: NSX_H20(1); break;
-                    case 4: NSX_H20(4); break;
-                    default: NSX_H20(2); break;
-                }
-#undef NSX_H20
+                hipLaunchKernelGGL((ipv4_hdr20_kernel<M, 2>), dim3(grid), dim3(kBlock), lds, st, b, cn, o, clog, mk);
             });
-            hipError_t e = hipGetLastError();
+            const hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
         return hipSuccess;
     }
-    const uint32_t max_blocks = (uint32_t)cus * (uint32_t)(bpc >= 1 && bpc <= 8 ? bpc : 8);
-    const uint64_t want = (n + (uint64_t)kBlock * kHdrUnroll - 1) / ((uint64_t)kBlock * kHdrUnroll);
-    const uint32_t grid = (uint32_t)(want < max_blocks ? want : max_blocks);
-    if (stride >= 1 && stride <= kHdrDenseMaxStride && (kernel == 0 || kernel == 2)) {
+    const uint32_t max_blocks = max_blocks_of(c, 8);
+    if (stride >= 1 && stride <= kHdrDenseMaxStride && (c.kernel == 0 || c.kernel == 2)) {
         // a wave's 64 headers span ≤ 63·stride + 3 + 20 bytes: ROWS 1 KiB rows per task in registers,
         // U tasks per iteration, an LDS slice of U·ROWS KiB per wave
         const uint32_t rows = (63u * (uint32_t)stride + 3u + 20u + 3u + kRow - 1) / kRow;
-        const uint64_t tasks = (n + kWave - 1) / kWave;
-        const uint64_t want_d = (tasks + kWavesPerBlock - 1) / kWavesPerBlock;
-        const uint32_t grid_d = (uint32_t)(want_d < max_blocks ? want_d : max_blocks);
+        const uint32_t grid = grid_for((n + kWave - 1) / kWave, max_blocks);
         by_mode([&](auto m) {
             constexpr int M = decltype(m)::value;
 #define NSX_HDR(R, U)                                                                                              \
-    hipLaunchKernelGGL((ipv4_hdr_dense_kernel<M, R, U>), dim3(grid_d), dim3(kBlock),                               \
+    hipLaunchKernelGGL((ipv4_hdr_dense_kernel<M, R, U>), dim3(grid), dim3(kBlock),                                 \
                        (size_t)(R) * (U) * kRow * kWavesPerBlock, st, base, (uint32_t)stride, hdr_off, n, out, mask)
             switch (rows) {
                 case 1: NSX_HDR(1, 4); break;
@@ -2563,6 +1875,8 @@ hipError_t launch_ipv4_hdr(uint8_t* base, uint64_t stride, uint32_t hdr_off, uin
         });
         return hipGetLastError();
     }
+    const uint64_t want = (n + (uint64_t)kBlock * kHdrUnroll - 1) / ((uint64_t)kBlock * kHdrUnroll);
+    const uint32_t grid = (uint32_t)(want < max_blocks ? want : max_blocks);
     by_mode([&](auto m) {
         constexpr int M = decltype(m)::value;
         hipLaunchKernelGGL(ipv4_hdr_kernel<M>, dim3(grid), dim3(kBlock), 0, st, base, stride, hdr_off, n, out, mask);

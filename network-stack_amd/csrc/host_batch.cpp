@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "../../include/nsx_csum.h"
+#include "../../include/nsx_tune.h"
 #include "csum_kernels.h"
 #include "host_csum.h"
 
@@ -84,13 +85,13 @@ int map_err(hipError_t e) {
         }                                      \
     } while (0)
 
-nsx::LaunchCfg default_cfg(int dev, uint64_t n) {
+nsx::LaunchCfg cfg_for(int dev, const nsx_tune* tune) {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) {
         (void)hipGetLastError();
         cus = 256;
     }
-    return nsx::default_launch_cfg(cus, n);
+    return nsx::launch_cfg(cus, tune);
 }
 
 // One chunk = segments [c0, c1) of the shard.
@@ -109,6 +110,8 @@ struct Job {
     const uint32_t* h_partial;
     uint16_t* h_out;
     int dev;
+    int slot;  // shard slot on the device (its own DevCtx: streams + staging)
+    const nsx_tune* tune;
     int rc;
 };
 
@@ -180,14 +183,15 @@ struct DevCtx {
 };
 
 constexpr int kMaxDevices = 64;
+constexpr int kMaxSlots = 8;  // nsx_tune.shards_per_device ≤ this
 std::mutex g_ctx_mu;
-DevCtx* g_ctx[kMaxDevices] = {};  // never destroyed: HIP may be torn down before static destructors run
+DevCtx* g_ctx[kMaxDevices][kMaxSlots] = {};  // never destroyed: HIP may be torn down before static destructors run
 
-DevCtx* dev_ctx(int dev) {
-    if (dev < 0 || dev >= kMaxDevices) return nullptr;
+DevCtx* dev_ctx(int dev, int slot) {
+    if (dev < 0 || dev >= kMaxDevices || slot < 0 || slot >= kMaxSlots) return nullptr;
     std::lock_guard<std::mutex> g(g_ctx_mu);
-    if (!g_ctx[dev]) g_ctx[dev] = new DevCtx;
-    return g_ctx[dev];
+    if (!g_ctx[dev][slot]) g_ctx[dev][slot] = new DevCtx;
+    return g_ctx[dev][slot];
 }
 
 void run_job(Job* j) {
@@ -202,7 +206,7 @@ void run_job(Job* j) {
     const bool out_pinned = is_pinned(j->h_out);
     const bool ragged = j->h_offsets != nullptr;
     const int nslots = chunks.size() > 1 ? 2 : 1;
-    DevCtx* ctx = dev_ctx(j->dev);
+    DevCtx* ctx = dev_ctx(j->dev, j->slot);
     if (!ctx) {
         j->rc = NSX_EINVAL;
         return;
@@ -213,7 +217,7 @@ void run_job(Job* j) {
     const Chunk* pending[2] = {nullptr, nullptr};
 
     NSX_TRY(hipSetDevice(j->dev));
-    cfg = default_cfg(j->dev, max_segs);
+    cfg = cfg_for(j->dev, j->tune);
     for (int s = 0; s < nslots; ++s) {
         if (!st[s]) NSX_TRY(hipStreamCreateWithFlags(&st[s], hipStreamNonBlocking));
         NSX_TRY(ctx->d_data[s].ensure(std::max<uint64_t>(max_span, 16)));
@@ -285,8 +289,10 @@ done:
     j->rc = rc;
 }
 
+// Shards: num_gpus × shards_per_device contiguous ranges (byte-balanced for ragged batches); shard g runs on
+// device g / shards_per_device in slot g % shards_per_device, one host thread per shard.
 int run_sharded(const uint8_t* h_base, uint64_t stride, uint32_t seg_len, const uint64_t* h_offsets, uint64_t n,
-                const uint32_t* h_partial, uint16_t* h_out, int num_gpus) {
+                const uint32_t* h_partial, uint16_t* h_out, int num_gpus, const nsx_tune* tune) {
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess) {
         (void)hipGetLastError();
@@ -299,16 +305,18 @@ int run_sharded(const uint8_t* h_base, uint64_t stride, uint32_t seg_len, const 
         num_gpus = (int)std::min<uint64_t>(want, (uint64_t)count);
     }
     if (num_gpus > count) return NSX_ENODEV;
+    const int spd = (tune && tune->shards_per_device > 1) ? std::min(tune->shards_per_device, kMaxSlots) : 1;
     int caller_dev = 0;
     (void)hipGetDevice(&caller_dev);
-    if ((uint64_t)num_gpus > n) num_gpus = (int)n;
-    std::vector<uint64_t> bounds(num_gpus + 1);
-    nsx::shard_plan(h_offsets, n, num_gpus, bounds.data());
-    std::vector<Job> jobs(num_gpus);
-    for (int g = 0; g < num_gpus; ++g)
-        jobs[g] = Job{h_base, stride, seg_len, h_offsets, bounds[g], bounds[g + 1], h_partial, h_out, g, NSX_OK};
+    const int parts = (int)std::min<uint64_t>((uint64_t)num_gpus * spd, n);
+    std::vector<uint64_t> bounds(parts + 1);
+    nsx::shard_plan(h_offsets, n, parts, bounds.data());
+    std::vector<Job> jobs(parts);
+    for (int g = 0; g < parts; ++g)
+        jobs[g] = Job{h_base, stride, seg_len, h_offsets, bounds[g], bounds[g + 1], h_partial, h_out, g / spd, g % spd,
+                      tune, NSX_OK};
     std::vector<std::thread> th;
-    for (int g = 1; g < num_gpus; ++g)
+    for (int g = 1; g < parts; ++g)
         if (jobs[g].hi > jobs[g].lo) th.emplace_back(run_job, &jobs[g]);
     if (jobs[0].hi > jobs[0].lo) run_job(&jobs[0]);
     for (auto& t : th) t.join();
@@ -324,18 +332,30 @@ extern "C" {
 
 int nsx_csum_fixed_host(const uint8_t* h_base, uint64_t stride, uint32_t seg_len, uint64_t n,
                         const uint32_t* h_prefix_partial, uint16_t* h_out, int num_gpus) {
+    return nsx_csum_fixed_host_tuned(h_base, stride, seg_len, n, h_prefix_partial, h_out, num_gpus, nullptr);
+}
+
+int nsx_csum_fixed_host_tuned(const uint8_t* h_base, uint64_t stride, uint32_t seg_len, uint64_t n,
+                              const uint32_t* h_prefix_partial, uint16_t* h_out, int num_gpus,
+                              const nsx_tune* tune) {
     if (n == 0) return NSX_OK;
     if (!h_out || (seg_len && !h_base)) return NSX_EINVAL;
-    return run_sharded(h_base, stride, seg_len, nullptr, n, h_prefix_partial, h_out, num_gpus);
+    return run_sharded(h_base, stride, seg_len, nullptr, n, h_prefix_partial, h_out, num_gpus, tune);
 }
 
 int nsx_csum_ragged_host(const uint8_t* h_base, const uint64_t* h_offsets, uint64_t n,
                          const uint32_t* h_prefix_partial, uint16_t* h_out, int num_gpus) {
+    return nsx_csum_ragged_host_tuned(h_base, h_offsets, n, h_prefix_partial, h_out, num_gpus, nullptr);
+}
+
+int nsx_csum_ragged_host_tuned(const uint8_t* h_base, const uint64_t* h_offsets, uint64_t n,
+                               const uint32_t* h_prefix_partial, uint16_t* h_out, int num_gpus,
+                               const nsx_tune* tune) {
     if (n == 0) return NSX_OK;
     if (!h_out || !h_offsets || !h_base) return NSX_EINVAL;
     for (uint64_t i = 0; i < n; ++i)
         if (h_offsets[i + 1] < h_offsets[i]) return NSX_EINVAL;
-    return run_sharded(h_base, 0, 0, h_offsets, n, h_prefix_partial, h_out, num_gpus);
+    return run_sharded(h_base, 0, 0, h_offsets, n, h_prefix_partial, h_out, num_gpus, tune);
 }
 
 int nsx_host_cache_release(void) {
@@ -343,13 +363,15 @@ int nsx_host_cache_release(void) {
     int dev0 = 0;
     const bool restore = hipGetDevice(&dev0) == hipSuccess;
     for (int d = 0; d < kMaxDevices; ++d) {
-        if (!g_ctx[d]) continue;
-        std::lock_guard<std::mutex> hold(g_ctx[d]->mu);
-        if (hipSetDevice(d) != hipSuccess) {
-            (void)hipGetLastError();
-            continue;
+        for (int s = 0; s < kMaxSlots; ++s) {
+            if (!g_ctx[d][s]) continue;
+            std::lock_guard<std::mutex> hold(g_ctx[d][s]->mu);
+            if (hipSetDevice(d) != hipSuccess) {
+                (void)hipGetLastError();
+                continue;
+            }
+            g_ctx[d][s]->release();  // streams stay: they are cheap and reused
         }
-        g_ctx[d]->release();  // streams stay: they are cheap and reused
     }
     if (restore) (void)hipSetDevice(dev0);
     return NSX_OK;

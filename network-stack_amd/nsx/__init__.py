@@ -20,9 +20,29 @@ LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libnsx_csum.so")
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "nsx_csum.h")
 
 NSX_OK, NSX_EIO, NSX_ENOMEM, NSX_ENODEV, NSX_EINVAL = 0, -5, -12, -19, -22
-PARAM_BLOCKS_PER_CU, PARAM_SEGS_PER_WAVE, PARAM_NONTEMPORAL, PARAM_BLOCK_MODE, PARAM_XCD_MAP = 1, 2, 3, 4, 5
-PARAM_KERNEL, PARAM_STREAM_ROWS, PARAM_RUN_SEGS, PARAM_XCD_CHUNK, PARAM_WINDOW_BYTES = 6, 7, 8, 9, 10
-ALL_PARAMS = (1, 2, 3, 4, 5, 6, 7, 8, 9, 10)
+# nsx_tune.kernel (include/nsx_tune.h)
+KERNEL_HDR_THREAD, KERNEL_HDR_DENSE, KERNEL_BUILD_PLAIN, KERNEL_BUILD_GENERAL = 1, 2, 2, 3
+
+
+class Tune(ctypes.Structure):
+    """include/nsx_tune.h: per-call launch overrides (0 = default). Benchmarks and tests only."""
+    _fields_ = [("blocks_per_cu", ctypes.c_int32), ("segs_per_wave", ctypes.c_int32),
+                ("block_mode", ctypes.c_int32), ("rows", ctypes.c_int32), ("run_segs", ctypes.c_int32),
+                ("xcd_chunk", ctypes.c_int32), ("window_bytes", ctypes.c_int64), ("kernel", ctypes.c_int32),
+                ("shards_per_device", ctypes.c_int32), ("reserved", ctypes.c_int32 * 6)]
+
+
+TUNE_FIELDS = tuple(f for f, _ in Tune._fields_ if f != "reserved")
+
+
+def _tune(tune):
+    """dict (or Tune, or None) → ctypes pointer argument (None = defaults)."""
+    if tune is None or isinstance(tune, Tune):
+        return None if tune is None else ctypes.byref(tune)
+    bad = set(tune) - set(TUNE_FIELDS)
+    if bad:
+        raise ValueError(f"unknown nsx_tune field(s): {sorted(bad)}")
+    return ctypes.byref(Tune(**{k: int(v) for k, v in tune.items()}))
 
 
 class NsxError(RuntimeError):
@@ -65,8 +85,16 @@ def lib() -> ctypes.CDLL:
             "nsx_tcp_layout_host": [vp, vp, u64, vp],
             "nsx_abi_version": [],
             "nsx_device_count": [ctypes.POINTER(i32)],
-            "nsx_set_param": [i32, ctypes.c_int64],
-            "nsx_get_param": [i32, ctypes.POINTER(ctypes.c_int64)],
+            # include/nsx_tune.h (per-call overrides)
+            "nsx_csum_fixed_dev_tuned": [vp, u64, u32, u64, vp, vp, vp, vp],
+            "nsx_csum_ragged_dev_tuned": [vp, vp, u64, vp, vp, vp, vp],
+            "nsx_verify_ragged_dev_tuned": [vp, vp, u64, vp, vp, vp, vp, vp],
+            "nsx_tcp_build_dev_tuned": [vp, vp, vp, vp, vp, u64, vp, u64, vp, vp, vp, vp, vp],
+            "nsx_ipv4_hdr_csum_dev_tuned": [vp, u64, u32, u64, i32, vp, vp, vp],
+            "nsx_ipv4_hdr_verify_mask_dev_tuned": [vp, u64, u32, u64, vp, vp, vp],
+            "nsx_csum_fixed_host_tuned": [vp, u64, u32, u64, vp, vp, i32, vp],
+            "nsx_csum_ragged_host_tuned": [vp, vp, u64, vp, vp, i32, vp],
+            "nsx_fixed_launch_count": [u64, u32, u64, vp, ctypes.POINTER(u64)],
         }
         for name, args in sig.items():
             f = getattr(L, name)
@@ -136,35 +164,32 @@ def shard_plan(n: int, parts: int, offsets: np.ndarray | None = None) -> np.ndar
     return b
 
 
-def set_param(param: int, value: int) -> None:
-    _check(lib().nsx_set_param(param, value), "nsx_set_param")
-
-
-def get_param(param: int) -> int:
-    v = ctypes.c_int64(0)
-    _check(lib().nsx_get_param(param, ctypes.byref(v)), "nsx_get_param")
-    return v.value
+def fixed_launch_count(stride: int, seg_len: int, n: int, tune=None) -> int:
+    """Kernel launches one fixed_dev call makes for this batch on the current device."""
+    c = ctypes.c_uint64(0)
+    _check(lib().nsx_fixed_launch_count(stride, seg_len, n, _tune(tune), ctypes.byref(c)), "nsx_fixed_launch_count")
+    return c.value
 
 
 def fixed_host(buf: np.ndarray, stride: int, seg_len: int, n: int, partial: np.ndarray | None = None,
-               num_gpus: int = 0) -> np.ndarray:
+               num_gpus: int = 0, tune=None) -> np.ndarray:
     buf = np.ascontiguousarray(buf, np.uint8)
     out = np.empty(n, np.uint16)
     part = None if partial is None else np.ascontiguousarray(partial, np.uint32)
-    _check(lib().nsx_csum_fixed_host(_np_ptr(buf), stride, seg_len, n, _np_ptr(part), _np_ptr(out), num_gpus),
-           "nsx_csum_fixed_host")
+    _check(lib().nsx_csum_fixed_host_tuned(_np_ptr(buf), stride, seg_len, n, _np_ptr(part), _np_ptr(out), num_gpus,
+                                           _tune(tune)), "nsx_csum_fixed_host")
     return out
 
 
 def ragged_host(buf: np.ndarray, offsets: np.ndarray, partial: np.ndarray | None = None,
-                num_gpus: int = 0) -> np.ndarray:
+                num_gpus: int = 0, tune=None) -> np.ndarray:
     buf = np.ascontiguousarray(buf, np.uint8)
     offsets = np.ascontiguousarray(offsets, np.uint64)
     n = offsets.size - 1
     out = np.empty(max(n, 0), np.uint16)
     part = None if partial is None else np.ascontiguousarray(partial, np.uint32)
-    _check(lib().nsx_csum_ragged_host(_np_ptr(buf), _np_ptr(offsets), n, _np_ptr(part), _np_ptr(out), num_gpus),
-           "nsx_csum_ragged_host")
+    _check(lib().nsx_csum_ragged_host_tuned(_np_ptr(buf), _np_ptr(offsets), n, _np_ptr(part), _np_ptr(out), num_gpus,
+                                            _tune(tune)), "nsx_csum_ragged_host")
     return out
 
 
@@ -194,31 +219,31 @@ class PinnedBuffer:
 # ---------------------------------------------------------------------------
 # device-side API (torch tensors as HBM buffers)
 # ---------------------------------------------------------------------------
-def fixed_dev(buf, stride: int, seg_len: int, n: int, partial=None, out=None, stream=None):
+def fixed_dev(buf, stride: int, seg_len: int, n: int, partial=None, out=None, stream=None, tune=None):
     import torch
     if out is None:
         out = torch.empty(n, dtype=torch.int16, device=buf.device)  # u16 bits
-    _check(lib().nsx_csum_fixed_dev(_dev_ptr(buf), stride, seg_len, n, _dev_ptr(partial), _dev_ptr(out),
-                                    _stream(stream)), "nsx_csum_fixed_dev")
+    _check(lib().nsx_csum_fixed_dev_tuned(_dev_ptr(buf), stride, seg_len, n, _dev_ptr(partial), _dev_ptr(out),
+                                          _stream(stream), _tune(tune)), "nsx_csum_fixed_dev")
     return out
 
 
-def ragged_dev(buf, offsets, partial=None, out=None, stream=None):
+def ragged_dev(buf, offsets, partial=None, out=None, stream=None, tune=None):
     import torch
     n = offsets.numel() - 1
     if out is None:
         out = torch.empty(max(n, 0), dtype=torch.int16, device=offsets.device)  # u16 bits
-    _check(lib().nsx_csum_ragged_dev(_dev_ptr(buf), _dev_ptr(offsets), n, _dev_ptr(partial), _dev_ptr(out),
-                                     _stream(stream)), "nsx_csum_ragged_dev")
+    _check(lib().nsx_csum_ragged_dev_tuned(_dev_ptr(buf), _dev_ptr(offsets), n, _dev_ptr(partial), _dev_ptr(out),
+                                           _stream(stream), _tune(tune)), "nsx_csum_ragged_dev")
     return out
 
 
-def verify_ragged_dev(buf, offsets, partial=None, raw=None, stream=None):
+def verify_ragged_dev(buf, offsets, partial=None, raw=None, stream=None, tune=None):
     import torch
     n = offsets.numel() - 1
     ok = torch.empty(max(n, 0), dtype=torch.uint8, device=offsets.device)
-    _check(lib().nsx_verify_ragged_dev(_dev_ptr(buf), _dev_ptr(offsets), n, _dev_ptr(partial), _dev_ptr(ok),
-                                       _dev_ptr(raw), _stream(stream)), "nsx_verify_ragged_dev")
+    _check(lib().nsx_verify_ragged_dev_tuned(_dev_ptr(buf), _dev_ptr(offsets), n, _dev_ptr(partial), _dev_ptr(ok),
+                                             _dev_ptr(raw), _stream(stream), _tune(tune)), "nsx_verify_ragged_dev")
     return ok
 
 
@@ -252,23 +277,23 @@ def verify_mask_dev(raw, out=None, stream=None):
     return out
 
 
-def ipv4_hdr_csum_dev(buf, stride: int, n: int, hdr_off: int = 0, mode: int = 0, out=None, stream=None):
+def ipv4_hdr_csum_dev(buf, stride: int, n: int, hdr_off: int = 0, mode: int = 0, out=None, stream=None, tune=None):
     """RFC 791 header checksums of n packets at a fixed stride (mode 0 verify, 1 fill in place)."""
     import torch
     if out is None and mode == 0:
         out = torch.empty(n, dtype=torch.int16, device=buf.device)  # u16 bits
-    _check(lib().nsx_ipv4_hdr_csum_dev(_dev_ptr(buf), stride, hdr_off, n, mode, _dev_ptr(out), _stream(stream)),
-           "nsx_ipv4_hdr_csum_dev")
+    _check(lib().nsx_ipv4_hdr_csum_dev_tuned(_dev_ptr(buf), stride, hdr_off, n, mode, _dev_ptr(out), _stream(stream),
+                                             _tune(tune)), "nsx_ipv4_hdr_csum_dev")
     return out
 
 
-def ipv4_hdr_verify_mask_dev(buf, stride: int, n: int, hdr_off: int = 0, mask=None, stream=None):
+def ipv4_hdr_verify_mask_dev(buf, stride: int, n: int, hdr_off: int = 0, mask=None, stream=None, tune=None):
     """Fused IPv4 header verify into a bitmask: bit i%64 of mask[i//64] iff header i is valid."""
     import torch
     if mask is None:
         mask = torch.empty((n + 63) // 64, dtype=torch.int64, device=buf.device)  # u64 bits
-    _check(lib().nsx_ipv4_hdr_verify_mask_dev(_dev_ptr(buf), stride, hdr_off, n, _dev_ptr(mask), _stream(stream)),
-           "nsx_ipv4_hdr_verify_mask_dev")
+    _check(lib().nsx_ipv4_hdr_verify_mask_dev_tuned(_dev_ptr(buf), stride, hdr_off, n, _dev_ptr(mask),
+                                                    _stream(stream), _tune(tune)), "nsx_ipv4_hdr_verify_mask_dev")
     return mask
 
 
@@ -291,14 +316,15 @@ def tcp_layout_host(data_off: np.ndarray, opt_off: np.ndarray | None = None) -> 
 
 
 def tcp_build_dev(fields: dict, data, data_off, out, out_off, opts=None, opt_off=None, partial=None, raw=None,
-                  stream=None):
+                  stream=None, tune=None):
     """Fused segment.bytes() + checksum + field write (fields: dict of device tensors)."""
     soa = TcpHdrSoA(*[fields[k].data_ptr() for k in
                       ("src_port", "dst_port", "seq_num", "ack_num", "offset", "control", "window", "urgent_ptr")])
     n = data_off.numel() - 1
-    _check(lib().nsx_tcp_build_dev(ctypes.byref(soa), _dev_ptr(opts), _dev_ptr(opt_off), _dev_ptr(data),
-                                   _dev_ptr(data_off), data.numel(), _dev_ptr(partial), n, _dev_ptr(out),
-                                   _dev_ptr(out_off), _dev_ptr(raw), _stream(stream)), "nsx_tcp_build_dev")
+    _check(lib().nsx_tcp_build_dev_tuned(ctypes.byref(soa), _dev_ptr(opts), _dev_ptr(opt_off), _dev_ptr(data),
+                                         _dev_ptr(data_off), data.numel(), _dev_ptr(partial), n, _dev_ptr(out),
+                                         _dev_ptr(out_off), _dev_ptr(raw), _stream(stream), _tune(tune)),
+           "nsx_tcp_build_dev")
     return out
 
 

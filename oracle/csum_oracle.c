@@ -114,6 +114,14 @@ ORACLE_EXPORT void oracle_go_batch_fixed(const uint8_t* base, uint64_t stride, u
         out[i] = (uint16_t)oracle_go_checksum(prefix, prefix_len, base + i * stride, seg_len);
 }
 
+/* The same over a ragged batch: segment i = base[offsets[i], offsets[i+1]). */
+ORACLE_EXPORT void oracle_go_batch_ragged(const uint8_t* base, const uint64_t* offsets, uint64_t n,
+                                          const uint8_t* prefix, size_t prefix_len, uint16_t* out) {
+    for (uint64_t i = 0; i < n; i++)
+        out[i] = (uint16_t)oracle_go_checksum(prefix, prefix_len, base + offsets[i],
+                                              (size_t)(offsets[i + 1] - offsets[i]));
+}
+
 /* Multi-threaded variant of oracle_batch_fixed / _ragged for full-size checks
  * in the GPU tests (contiguous index shards, one pthread each). */
 typedef struct {

@@ -245,6 +245,7 @@ def c_oracle():
                                         u8p, u8p, ctypes.c_int]
         lib.oracle_go_batch_fixed.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
                                               u8p, ctypes.c_size_t, u8p]
+        lib.oracle_go_batch_ragged.argtypes = [u8p, u8p, ctypes.c_uint64, u8p, ctypes.c_size_t, u8p]
         lib.oracle_splitmix64_fill.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]
         lib.oracle_go_tcp_build_batch.argtypes = [u8p] * 10 + [u8p, ctypes.c_size_t, ctypes.c_uint64, u8p, u8p, u8p]
         lib.oracle_go_tcp_build_batch.restype = ctypes.c_int

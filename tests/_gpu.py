@@ -1,0 +1,50 @@
+"""Shared helpers of the -m gpu tests: numpy <-> device tensors and the two batch
+entry points with numpy inputs (the results come back as uint16 arrays)."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import nsx  # noqa: E402
+
+
+def setup_gpu():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X; the HIP path has no CPU fallback"
+    assert nsx.device_count() > 0
+    torch.cuda.set_device(0)
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def u16(t):
+    return host(t.view(torch.int16)).view(np.uint16)
+
+
+def run_fixed(buf_np, stride, seg_len, n, partial=None, start=0, tune=None):
+    d = dev(buf_np)
+    p = None if partial is None else dev(np.asarray(partial, np.uint32).view(np.int32))
+    out = torch.empty(n, dtype=torch.int16, device="cuda")
+    nsx.fixed_dev(d[start:], stride, seg_len, n, partial=p, out=out, tune=tune)
+    return u16(out)
+
+
+def run_ragged(buf_np, offsets, partial=None, tune=None):
+    d = dev(buf_np)
+    o = dev(np.asarray(offsets, np.uint64).view(np.int64))
+    p = None if partial is None else dev(np.asarray(partial, np.uint32).view(np.int32))
+    n = len(offsets) - 1
+    out = torch.empty(n, dtype=torch.int16, device="cuda")
+    nsx.ragged_dev(d, o, partial=p, out=out, tune=tune)
+    return u16(out)
+
+
+def mask_words(valid):
+    pad = np.zeros((valid.size + 63) // 64 * 64, np.uint8)
+    pad[:valid.size] = valid
+    return np.packbits(pad, bitorder="little").view(np.uint64)

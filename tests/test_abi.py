@@ -1,7 +1,8 @@
 """C-ABI boundary tests that need no GPU: the library loads, exports every
-function include/nsx_csum.h declares, the single-segment host entry point
-(computeChecksum, tcp.go:72-95) matches the oracle, host logic (shard plan,
-params) behaves, and device entry points refuse loudly without a GPU."""
+function include/nsx_csum.h (the drop-in boundary) and include/nsx_tune.h (per-call
+bench/test overrides) declare, the single-segment host entry point
+(computeChecksum, tcp.go:72-95) matches the oracle, host logic (shard plan, layout)
+behaves, and device entry points refuse loudly without a GPU."""
 import ctypes
 import json
 import os
@@ -16,10 +17,11 @@ from conftest import GOLDEN, ROOT
 from oracle import csum_oracle as O
 
 HEADER = os.path.join(ROOT, "include", "nsx_csum.h")
+TUNE_HEADER = os.path.join(ROOT, "include", "nsx_tune.h")
 
 
-def declared_functions():
-    src = open(HEADER).read()
+def declared_functions(header=HEADER):
+    src = open(header).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     names = re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(nsx_[a-z_0-9]+)\s*\(", src, flags=re.M)
     inline = set(re.findall(r"static inline [a-z_0-9]+ (nsx_[a-z_0-9]+)\(", src))
@@ -35,11 +37,46 @@ def test_header_declares_the_boundary():
 
 def test_library_exports_every_declared_symbol():
     L = nsx.lib()
-    missing = [n for n in declared_functions() if not hasattr(L, n)]
+    declared = declared_functions() + declared_functions(TUNE_HEADER)
+    assert len(declared_functions(TUNE_HEADER)) == 9
+    missing = [n for n in declared if not hasattr(L, n)]
     assert not missing, missing
     out = subprocess.run(["nm", "-D", "--defined-only", nsx.LIB_PATH], capture_output=True, text=True).stdout
     exported = set(re.findall(r" T (nsx_\w+)", out))
-    assert set(declared_functions()) <= exported
+    assert set(declared) <= exported
+
+
+def test_no_process_wide_tuning_state_in_the_boundary():
+    """ADVICE/VERDICT r1: the product header holds no global knobs; overrides travel per call."""
+    src = open(HEADER).read()
+    assert "NSX_PARAM_" not in src and "set_param" not in src
+    out = subprocess.run(["nm", "-D", "--defined-only", nsx.LIB_PATH], capture_output=True, text=True).stdout
+    assert "nsx_set_param" not in out and "nsx_get_param" not in out
+
+
+def test_tune_struct_layout_matches_header():
+    """nsx_tune as the C compiler lays it out (what a cgo or C caller sees) == the ctypes mirror."""
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        src = os.path.join(td, "t.c")
+        open(src, "w").write(r'''
+#include <stddef.h>
+#include <stdio.h>
+#include "nsx_tune.h"
+int main(void) {
+    printf("%zu %zu %zu %zu %zu\n", sizeof(nsx_tune), offsetof(nsx_tune, window_bytes),
+           offsetof(nsx_tune, kernel), offsetof(nsx_tune, shards_per_device), offsetof(nsx_tune, reserved));
+    return 0;
+}
+''')
+        exe = os.path.join(td, "t")
+        subprocess.check_call(["gcc", "-std=c11", "-Wall", "-Werror", src, "-I", os.path.join(ROOT, "include"), "-o", exe])
+        got = [int(x) for x in subprocess.run([exe], capture_output=True, text=True).stdout.split()]
+    T = nsx.Tune
+    assert got == [ctypes.sizeof(T), T.window_bytes.offset, T.kernel.offset, T.shards_per_device.offset,
+                   T.reserved.offset]
+    with pytest.raises(ValueError):
+        nsx._tune(dict(no_such_knob=1))
 
 
 def test_library_has_gfx950_code_object():
@@ -51,7 +88,7 @@ def test_library_has_gfx950_code_object():
 
 
 def test_abi_version():
-    assert nsx.abi_version() == 1
+    assert nsx.abi_version() == 2
 
 
 @pytest.mark.parametrize("case", json.load(open(os.path.join(GOLDEN, "kat.json"))), ids=lambda c: c["name"])
@@ -126,17 +163,6 @@ def test_shard_plan_ragged_byte_balanced():
     assert sum(per) == int(offs[-1])
 
 
-def test_params_roundtrip():
-    for p in (nsx.PARAM_BLOCKS_PER_CU, nsx.PARAM_SEGS_PER_WAVE, nsx.PARAM_NONTEMPORAL, nsx.PARAM_BLOCK_MODE,
-              nsx.PARAM_XCD_MAP):
-        old = nsx.get_param(p)
-        nsx.set_param(p, 1)
-        assert nsx.get_param(p) == 1
-        nsx.set_param(p, old)
-    with pytest.raises(nsx.NsxError):
-        nsx.set_param(99, 1)
-
-
 def test_device_calls_fail_loudly_without_gpu():
     """No CPU fallback: on a GPU-less host every device/batch entry point reports
     NSX_ENODEV (never a silently computed result)."""
@@ -156,12 +182,25 @@ def test_device_calls_fail_loudly_without_gpu():
     soa = nsx.TcpHdrSoA(*([0x1000] * 8))
     assert L.nsx_tcp_build_dev(ctypes.byref(soa), None, None, fake, fake, 16, None, 4, fake, fake, None,
                                None) == nsx.NSX_ENODEV
+    tune = ctypes.byref(nsx.Tune(blocks_per_cu=2))
+    assert L.nsx_csum_fixed_dev_tuned(fake, 1500, 1500, 4, None, fake, None, tune) == nsx.NSX_ENODEV
+    assert L.nsx_csum_ragged_dev_tuned(fake, fake, 4, None, fake, None, tune) == nsx.NSX_ENODEV
+    assert L.nsx_verify_ragged_dev_tuned(fake, fake, 4, None, fake, None, None, tune) == nsx.NSX_ENODEV
+    assert L.nsx_ipv4_hdr_csum_dev_tuned(fake, 64, 0, 4, 0, fake, None, tune) == nsx.NSX_ENODEV
+    assert L.nsx_ipv4_hdr_verify_mask_dev_tuned(fake, 20, 0, 4, fake, None, tune) == nsx.NSX_ENODEV
+    assert L.nsx_tcp_build_dev_tuned(ctypes.byref(soa), None, None, fake, fake, 16, None, 4, fake, fake, None,
+                                     None, tune) == nsx.NSX_ENODEV
+    cnt = ctypes.c_uint64(7)
+    assert L.nsx_fixed_launch_count(1500, 1500, 4, None, ctypes.byref(cnt)) == nsx.NSX_ENODEV
     buf = np.zeros(3000, np.uint8)
     with pytest.raises(nsx.NsxError) as e:
         nsx.fixed_host(buf, 1500, 1500, 2)
     assert e.value.code == nsx.NSX_ENODEV
     with pytest.raises(nsx.NsxError):
         nsx.ragged_host(buf, np.array([0, 10, 3000], np.uint64))
+    with pytest.raises(nsx.NsxError) as e:
+        nsx.fixed_host(buf, 1500, 1500, 2, tune=dict(shards_per_device=3))
+    assert e.value.code == nsx.NSX_ENODEV
     p = ctypes.c_void_p()
     assert L.nsx_alloc_pinned(64, ctypes.byref(p)) == nsx.NSX_ENODEV
     assert L.nsx_host_cache_release() == 0  # nothing cached, nothing to do

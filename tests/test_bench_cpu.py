@@ -1,28 +1,99 @@
-"""bench.py's CPU reference lines run without a GPU: the multi-thread
-Go-faithful and vectorised restatements agree with the 1-thread oracle output
-on the same sample (their `parity` flags), and report positive rates."""
+"""bench.py without a GPU: the rank launcher (`--gpus 2` starts two gloo ranks itself
+and reports n_gpus 2; a WORLD_SIZE that disagrees with --gpus is an error), the CPU
+baseline leg on every host core with its 1-thread rate beside it (checked against
+known-correct outputs standing in for the GPU's), the best-CPU extra lines, and
+the per-launch reporting of windowed steps."""
+import json
+import os
+import subprocess
+import sys
+
 import numpy as np
+import pytest
 
 import bench
+from conftest import ROOT
 from oracle import csum_oracle as O
 
-
-def test_cpu_extra_lines_parity():
-    L = S = 1500
-    m = 4096
-    sample = O.c_splitmix64(0x1071, m * S)
-    want = O.c_batch(sample, m, stride=S, seg_len=L)
-    res = bench.cpu_extra_lines(O.c_oracle(), sample, S, L, m, want, 0.05)
-    for k in ("go_faithful_threads", "optimized_1_thread", "optimized_threads"):
-        assert res[k]["parity"] and res[k]["value"] > 0, k
+torch = pytest.importorskip("torch")
 
 
-def test_fixed_launches_mirrors_the_auto_window():
-    """Config 5's 25 GB batch runs as 16 windows of 1M segments; configs 2 and 4 in one launch."""
-    assert bench.fixed_launches(1 << 24, 1500, 1500) == 16
-    assert bench.fixed_launches(1 << 20, 1500, 1500) == 1
-    assert bench.fixed_launches(1 << 18, 65536, 65536) == 1  # long-segment path: never windowed
-    assert bench.fixed_launches(1 << 22, 1500, 1500) == 4
+def _bench(*args, env_extra=None, timeout=240):
+    env = dict(os.environ, **(env_extra or {}))
+    env.pop("WORLD_SIZE", None) if not (env_extra and "WORLD_SIZE" in env_extra) else None
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                          timeout=timeout, env=env, cwd=ROOT)
+
+
+def test_gpus_2_launches_two_ranks_itself():
+    """`bench.py --gpus N` with no launcher must run N ranks, not one rank on GPU 0."""
+    r = _bench("--gpus", "2", "--dry-run", "--steps", "3", "--warmup", "1")
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    line = lines[0]
+    assert line["n_gpus"] == 2 and line["ranks"] == 2 and line["dry_run"]
+    assert line["config"]["units_per_step_all_gpus"] == 2 * line["config"]["units_per_gpu"]
+
+
+def test_world_size_disagreeing_with_gpus_is_an_error():
+    r = _bench("--gpus", "2", "--dry-run", "--steps", "1", "--warmup", "0", env_extra={"WORLD_SIZE": "1"})
+    assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr
+
+
+def test_host_cores_share():
+    c = bench.host_cores()
+    assert 1 <= c["threads"] <= c["affinity_cpus"] <= c["host_cpus"]
+
+
+def _fixed_case(n=4096, L=1500):
+    buf = O.c_splitmix64(0x1071, n * L)
+    out = O.c_batch(buf, n, stride=L, seg_len=L)
+    cfg = dict(kind="fixed", n=n, seg_len=L, stride=L, seed=0x1071)
+    return cfg, {"buf": torch.from_numpy(buf), "out": torch.from_numpy(out.view(np.int16))}
+
+
+def test_cpu_baseline_fixed_all_cores_and_single_thread():
+    cfg, w = _fixed_case()
+    res = bench.cpu_baseline(cfg, w, 0.2)
+    assert res["sample_parity_vs_gpu"] and res["value"] > 0 and res["cores"] == bench.host_cores()["threads"]
+    assert res["single_thread"]["cores"] == 1 and res["single_thread"]["value"] > 0
+    for k in ("optimized_1_thread", "optimized_threads"):
+        assert res["extra"][k]["parity"] and res["extra"][k]["value"] > 0, k
+    w["out"][5] ^= 1  # a wrong "GPU" result is caught
+    assert not bench.cpu_baseline(cfg, w, 0.05)["sample_parity_vs_gpu"]
+
+
+def test_cpu_baseline_ragged_byte_balanced():
+    rng = np.random.default_rng(0x1072)
+    n = 3000
+    lens = rng.integers(64, 9001, n).astype(np.uint64)
+    offs = np.zeros(n + 1, np.uint64)
+    offs[1:] = np.cumsum(lens)
+    buf = O.c_splitmix64(0x1072, int(offs[-1]))
+    out = O.c_batch(buf, n, offsets=offs)
+    cfg = dict(kind="ragged", n=n, seed=0x1072)
+    res = bench.cpu_baseline(cfg, {"buf": torch.from_numpy(buf), "out": torch.from_numpy(out.view(np.int16)),
+                                   "offsets": offs}, 0.2)
+    assert res["sample_parity_vs_gpu"] and res["value"] > 0
+
+
+@pytest.mark.parametrize("mask", [False, True])
+def test_cpu_baseline_ipv4_headers(mask):
+    n, H = 64 * 500 + 7, 20
+    buf = O.c_splitmix64(0x1075, n * H)
+    buf[::H] = 0x45
+    raw = O.c_batch(buf, n, stride=H, seg_len=H)
+    # make about half valid: any header whose sum is 0xFFFF is valid; force some by setting the field
+    if mask:
+        valid = raw == 0xFFFF
+        out = np.packbits(np.concatenate([valid, np.zeros(-n % 64, bool)]), bitorder="little").view(np.uint64)
+        outt = torch.from_numpy(out.view(np.int64))
+    else:
+        outt = torch.from_numpy(raw.view(np.int16))
+    cfg = dict(kind="ipv4_hdr", n=n, hdr=H, mask=mask, seed=0x1075)
+    res = bench.cpu_baseline(cfg, {"buf": torch.from_numpy(buf), "out": outt}, 0.1)
+    assert res["sample_parity_vs_gpu"] and res["value"] > 0
 
 
 def test_result_line_per_launch_with_windows():
@@ -32,10 +103,3 @@ def test_result_line_per_launch_with_windows():
     assert line["roofline"]["alg_bytes_per_launch"] == 1600
     assert line["roofline"]["launches_per_step"] == 16
     assert abs(line["kernel_ms_mean"] - 0.2) < 1e-9
-
-
-def test_fixed_launches_follows_the_knobs():
-    assert bench.fixed_launches(1 << 24, 1500, 1500, window_bytes=-1) == 1
-    assert bench.fixed_launches(4096, 1500, 1500, window_bytes=1500 * 1000) == 5
-    assert bench.fixed_launches(1 << 24, 1500, 1500, kernel=2) == 1  # per-segment kernel: no windows
-    assert bench.fixed_launches(1 << 24, 1501, 1501) == 16  # unaligned batches take the same path

@@ -1,0 +1,160 @@
+"""GPU parity first in line (collected before every other -m gpu file, so that
+`pytest -x` can never stop ahead of them): the committed golden fixtures and the
+reference's own test (transport/tcp/tcp_test.go:26-32) through the device entry
+points, then BASELINE.json's device-resident configurations at full size —
+config 2 (1M x 1500 B) and config 3 (1M ragged 64-9000 B) against the oracle on
+every segment, config 4 (256K x 64 KiB) and config 5 (16M x 1500 B per GPU)
+sampled against the oracle plus size-independent properties on every segment.
+Bit-exact throughout (integer work)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from _gpu import dev, host, run_fixed, run_ragged, setup_gpu, torch, u16
+from conftest import GOLDEN
+from oracle import csum_oracle as O
+
+import nsx  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu():
+    setup_gpu()
+
+
+# ------------------------------------------------------------------ golden fixtures
+
+def test_golden_vectors_fixed_and_ragged():
+    """tests/golden/vectors.*: 86 cases (lengths 0-65536, start misalignment 0-7, no / IPv4 / IPv6
+    prefix) through the fixed entry point (with and without the prefix partial) and the ragged one."""
+    idx = json.load(open(os.path.join(GOLDEN, "vectors.json")))
+    blob = np.fromfile(os.path.join(GOLDEN, "vectors.bin"), np.uint8)
+    d = dev(blob)
+    for c in idx:
+        out = torch.empty(1, dtype=torch.int16, device="cuda")
+        part = dev(np.array([c["prefix_partial"]], np.uint32).view(np.int32))
+        nsx.fixed_dev(d[c["offset"]:], 0, c["length"], 1, partial=part, out=out)
+        assert u16(out)[0] == c["raw"], c
+        nsx.fixed_dev(d[c["offset"]:], 0, c["length"], 1, out=out)
+        assert u16(out)[0] == c["raw_no_prefix"], c
+        r = run_ragged(blob, [c["offset"], c["offset"] + c["length"]])
+        assert r[0] == c["raw_no_prefix"], c
+
+
+def test_golden_ragged_batch():
+    meta = json.load(open(os.path.join(GOLDEN, "ragged.json")))
+    blob = np.fromfile(os.path.join(GOLDEN, "ragged.bin"), np.uint8)
+    assert run_ragged(blob, meta["offsets"]).tolist() == meta["raw"]
+    assert run_ragged(blob, meta["offsets"], meta["partial"]).tolist() == meta["raw_with_partial"]
+
+
+def test_golden_kat_and_reference_test():
+    for c in json.load(open(os.path.join(GOLDEN, "kat.json"))):
+        seg = np.frombuffer(bytes.fromhex(c["segment"]) or b"\0", np.uint8)
+        L = len(bytes.fromhex(c["segment"]))
+        partial = [O.be_word_sum(bytes.fromhex(c["prefix"]))]
+        if len(bytes.fromhex(c["prefix"])) % 2:
+            continue  # the device API's prefix partial requires an even-length prefix
+        assert run_fixed(seg, 0, L, 1, partial)[0] == c["raw"], c["name"]
+
+
+def test_reference_TestSegmentComputeChecksum_on_device():
+    """tcp_test.go:26-32 on the device: segment{data:"hello"} (offset 0, every header field 0;
+    tests/golden/segments.json) → raw 0x43D2; store ^sum at bytes 16-17, the re-sum is 0xFFFF."""
+    case = next(c for c in json.load(open(os.path.join(GOLDEN, "segments.json")))
+                if c["name"] == "TestSegmentComputeChecksum")
+    b = np.frombuffer(bytes.fromhex(case["bytes"]), np.uint8).copy()
+    assert b.size == 25 and b[12] == 0 and case["raw"] == 0x43D2
+    raw = run_fixed(b, 0, len(b), 1)[0]
+    assert raw == case["raw"]
+    b[16], b[17] = (~raw & 0xFFFF) >> 8, (~raw) & 0xFF
+    assert run_fixed(b, 0, len(b), 1)[0] == 0xFFFF
+    # the same through the ragged entry point at an odd start
+    pad = np.concatenate([np.zeros(1, np.uint8), b])
+    assert run_ragged(pad, [1, 26])[0] == 0xFFFF
+
+
+# ------------------------------------------------------------------ BASELINE configs at full size
+
+def test_config2_1M_x_1500_full():
+    n, L = 1 << 20, 1500
+    t = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    nsx.fill_splitmix64_dev(t, 0x1071)
+    h = host(t)
+    assert np.array_equal(h[:4096], O.c_splitmix64(0x1071, 4096))
+    assert np.array_equal(h[-4096:], O.c_splitmix64(0x1071, 4096, n * L - 4096))
+    out = nsx.fixed_dev(t, L, L, n, out=torch.empty(n, dtype=torch.int16, device="cuda"))
+    got = u16(out)
+    assert np.array_equal(got, O.c_batch(h, n, stride=L, seg_len=L, threads=16))
+    out2 = nsx.fixed_dev(t, L, L, n, out=torch.empty(n, dtype=torch.int16, device="cuda"))
+    assert np.array_equal(u16(out2), got)  # idempotent
+
+
+def test_config3_1M_ragged_full():
+    n = 1 << 20
+    rng = np.random.default_rng(0x1072)
+    lens = rng.integers(64, 9001, n).astype(np.uint64)
+    offs = np.zeros(n + 1, np.uint64)
+    offs[1:] = np.cumsum(lens)
+    t = torch.empty(int(offs[-1]), dtype=torch.uint8, device="cuda")
+    nsx.fill_splitmix64_dev(t, 0x1072)
+    want = O.c_batch(host(t), n, offsets=offs, threads=16)
+    d_offs = dev(offs.view(np.int64))
+    for tune in (None, dict(rows=16, run_segs=16), dict(blocks_per_cu=1)):
+        out = nsx.ragged_dev(t, d_offs, out=torch.empty(n, dtype=torch.int16, device="cuda"), tune=tune)
+        assert np.array_equal(u16(out), want), tune
+
+
+def test_config4_256K_x_64KiB_sampled_and_roundtrip():
+    n, L = 1 << 18, 65536
+    t = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    nsx.fill_splitmix64_dev(t, 0x1073)
+    out = nsx.fixed_dev(t, L, L, n, out=torch.empty(n, dtype=torch.int16, device="cuda"))
+    got = u16(out)
+    idx = sorted(set(range(0, n, 4099)) | {0, 1, n // 2, n - 2, n - 1})
+    for i in idx:
+        seg = O.c_splitmix64(0x1073, L, i * L)
+        assert got[i] == O.c_fold_checksum(b"", seg.tobytes()), i
+    # size-independent property: block-per-segment mode agrees with wave mode on every segment
+    out_b = nsx.fixed_dev(t, L, L, n, out=torch.empty(n, dtype=torch.int16, device="cuda"), tune=dict(block_mode=2))
+    assert np.array_equal(u16(out_b), got)
+    # sender/receiver round trip on every segment: the field words are zeroed before the sum
+    # (tcp.go:68), ^raw goes into bytes 16-17, and every re-sum is 0xFFFF
+    del out
+    v = t.view(n, L)
+    v[:, 16:18] = 0
+    raw0 = u16(nsx.fixed_dev(t, L, L, n, out=torch.empty(n, dtype=torch.int16, device="cuda")))
+    fld = torch.from_numpy(((~raw0) & 0xFFFF).astype(np.int32)).cuda()
+    v[:, 16] = (fld >> 8).to(torch.uint8)
+    v[:, 17] = (fld & 0xFF).to(torch.uint8)
+    ok = u16(nsx.fixed_dev(t, L, L, n, out=torch.empty(n, dtype=torch.int16, device="cuda")))
+    assert (ok == 0xFFFF).all()
+
+
+def test_config5_16M_x_1500_per_gpu_sampled():
+    """Config 5's per-GPU batch (16M x 1500 B = 23.4 GiB, SURVEY.md §8d, run as 16 back-to-back
+    windows): every 4099th segment plus the segments either side of every 8-way shard boundary
+    and of every window boundary against the oracle (bytes regenerated on the CPU from the
+    counter-based stream); every segment re-checked as one launch and by the block-per-segment
+    kernel."""
+    n, L, seed = 1 << 24, 1500, 0x1071 + 3  # the rank-3 seed
+    t = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    nsx.fill_splitmix64_dev(t, seed)
+    assert nsx.fixed_launch_count(L, L, n) == 16
+    got = u16(nsx.fixed_dev(t, L, L, n, out=torch.empty(n, dtype=torch.int16, device="cuda")))
+    idx = set(range(0, n, 4099)) | {n - 1}
+    for b in list(nsx.shard_plan(n, 8)[1:-1]) + [k * (n // 16) for k in range(1, 16)]:
+        idx |= {int(b) - 1, int(b)}
+    for i in sorted(idx):
+        seg = O.c_splitmix64(seed, L, i * L)
+        assert got[i] == O.c_fold_checksum(b"", seg.tobytes()), i
+    one = u16(nsx.fixed_dev(t, L, L, n, out=torch.empty(n, dtype=torch.int16, device="cuda"),
+                            tune=dict(window_bytes=-1)))
+    assert np.array_equal(one, got)
+    alt = u16(nsx.fixed_dev(t, L, L, n, out=torch.empty(n, dtype=torch.int16, device="cuda"),
+                            tune=dict(block_mode=2)))
+    assert np.array_equal(alt, got)

@@ -1,115 +1,24 @@
 """GPU parity: the gfx950 kernels (through the C ABI) against the oracle on the
-same inputs — bit-exact, as integer work must be. Golden fixtures, edge cases
-the reference's arithmetic has (odd lengths, zero/0xFFFF sums, odd starts,
-empty segments, end-of-allocation tails), every kernel variant, and the
-BASELINE.json configurations at full size (full compare where the oracle is
-fast enough, sampled + round-trip properties for the 16 GiB config)."""
-import json
-import os
-
+same inputs — bit-exact, as integer work must be. Edge cases the reference's
+arithmetic has (odd lengths, zero/0xFFFF sums, odd starts, empty segments,
+end-of-allocation tails), every launch shape the per-call overrides of
+include/nsx_tune.h allow, the SURVEY §8 f-rows (verify, pseudo-headers, TCP build,
+IPv4 headers), the host batch path and re-entrancy. The golden fixtures and the
+BASELINE configs at full size run first, in test_gpu_00_baseline.py."""
 import numpy as np
 import pytest
 
-from conftest import GOLDEN
+from _gpu import dev, host, mask_words, run_fixed, run_ragged, setup_gpu, torch, u16
 from oracle import csum_oracle as O
 
-pytestmark = pytest.mark.gpu
-
-torch = pytest.importorskip("torch")
 import nsx  # noqa: E402
+
+pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(scope="module", autouse=True)
 def gpu():
-    assert torch.cuda.is_available(), "GPU tests need an MI355X; the HIP path has no CPU fallback"
-    assert nsx.device_count() > 0
-    torch.cuda.set_device(0)
-    yield
-    for p in nsx.ALL_PARAMS:
-        nsx.set_param(p, 0)
-
-
-@pytest.fixture
-def nsx_param():
-    """Set kernel knobs for one test; all reset to defaults afterwards."""
-    yield nsx.set_param
-    for p in nsx.ALL_PARAMS:
-        nsx.set_param(p, 0)
-
-
-def dev(a):
-    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
-
-
-def host(t):
-    torch.cuda.synchronize()
-    return t.cpu().numpy()
-
-
-def u16(t):
-    return host(t.view(torch.int16)).view(np.uint16)
-
-
-def run_fixed(buf_np, stride, seg_len, n, partial=None, start=0):
-    d = dev(buf_np)
-    p = None if partial is None else dev(np.asarray(partial, np.uint32).view(np.int32))
-    out = torch.empty(n, dtype=torch.int16, device="cuda")
-    nsx.fixed_dev(d[start:], stride, seg_len, n, partial=p, out=out)
-    return u16(out)
-
-
-def run_ragged(buf_np, offsets, partial=None):
-    d = dev(buf_np)
-    o = dev(np.asarray(offsets, np.uint64).view(np.int64))
-    p = None if partial is None else dev(np.asarray(partial, np.uint32).view(np.int32))
-    n = len(offsets) - 1
-    out = torch.empty(n, dtype=torch.int16, device="cuda")
-    nsx.ragged_dev(d, o, partial=p, out=out)
-    return u16(out)
-
-
-# ------------------------------------------------------------------ golden
-
-def test_golden_vectors_fixed_and_ragged():
-    idx = json.load(open(os.path.join(GOLDEN, "vectors.json")))
-    blob = np.fromfile(os.path.join(GOLDEN, "vectors.bin"), np.uint8)
-    d = dev(blob)
-    for c in idx:
-        out = torch.empty(1, dtype=torch.int16, device="cuda")
-        part = dev(np.array([c["prefix_partial"]], np.uint32).view(np.int32))
-        nsx.fixed_dev(d[c["offset"]:], 0, c["length"], 1, partial=part, out=out)
-        assert u16(out)[0] == c["raw"], c
-        nsx.fixed_dev(d[c["offset"]:], 0, c["length"], 1, out=out)
-        assert u16(out)[0] == c["raw_no_prefix"], c
-    offs = [c["offset"] for c in idx]
-    # as one ragged batch over the blob (segments separated by filler → use per-seg offsets)
-    for c in idx:
-        r = run_ragged(blob, [c["offset"], c["offset"] + c["length"]])
-        assert r[0] == c["raw_no_prefix"]
-    assert offs
-
-
-def test_golden_ragged_batch():
-    meta = json.load(open(os.path.join(GOLDEN, "ragged.json")))
-    blob = np.fromfile(os.path.join(GOLDEN, "ragged.bin"), np.uint8)
-    assert run_ragged(blob, meta["offsets"]).tolist() == meta["raw"]
-    assert run_ragged(blob, meta["offsets"], meta["partial"]).tolist() == meta["raw_with_partial"]
-
-
-def test_golden_kat_and_reference_test():
-    for c in json.load(open(os.path.join(GOLDEN, "kat.json"))):
-        seg = np.frombuffer(bytes.fromhex(c["segment"]) or b"\0", np.uint8)
-        L = len(bytes.fromhex(c["segment"]))
-        partial = [O.be_word_sum(bytes.fromhex(c["prefix"]))]
-        if len(bytes.fromhex(c["prefix"])) % 2:
-            continue  # the device API's prefix partial requires an even-length prefix
-        assert run_fixed(seg, 0, L, 1, partial)[0] == c["raw"], c["name"]
-    # tcp_test.go:26-32 on the device: store ^sum at bytes 16-17, re-sum is 0xFFFF
-    s = O.Segment(data=b"hello")
-    b = np.frombuffer(s.bytes(), np.uint8).copy()
-    raw = run_fixed(b, 0, len(b), 1)[0]
-    b[16], b[17] = (~raw & 0xFFFF) >> 8, (~raw) & 0xFF
-    assert run_fixed(b, 0, len(b), 1)[0] == 0xFFFF
+    setup_gpu()
 
 
 # ------------------------------------------------------------------ edges
@@ -182,64 +91,36 @@ def test_zero_segments_is_noop():
 
 # ------------------------------------------------------------------ variants
 
-VARIANTS = ([dict(kernel=2, spw=s, nt=nt, xcd=x, bpc=b, rows=0) for s in (1, 2, 4) for nt in (1, 2) for x in (1, 2)
-             for b in (8, 3)] +
-            [dict(kernel=1, spw=0, nt=nt, xcd=x, bpc=b, rows=r) for r in (4, 8, 16) for nt in (1, 2) for x in (1, 2)
-             for b in (8, 3)] +
-            [dict(kernel=3, spw=s, nt=nt, xcd=x, bpc=b, rows=0) for s in (1, 2, 4, 8) for nt in (1, 2)
-             for x in (1, 2, 3) for b in (8, 3)] +
-            [dict(kernel=3, spw=s, nt=1, xcd=1, bpc=b, rows=0, chunk=c) for s in (1, 4) for b in (8, 2)
-             for c in (1, 3, 6, 10, 99)] +
-            [dict(kernel=2, spw=1, nt=1, xcd=1, bpc=b, rows=0, chunk=c) for b in (8, 2) for c in (2, 5, 99)] +
-            [dict(kernel=5, spw=s, nt=nt, xcd=x, bpc=b, rows=0, chunk=c) for s in (1, 2, 4, 8) for nt in (1, 2)
-             for x in (1, 2) for b in (8, 1) for c in (0, 99)] +
-            [dict(kernel=7, spw=0, nt=nt, xcd=x, bpc=b, rows=r, chunk=c) for nt in (1, 2) for x in (1, 2)
-             for b in (8, 1) for r in (4, 8, 16) for c in (0, 99)])
+FIXED_TUNES = [dict(segs_per_wave=s, blocks_per_cu=b, xcd_chunk=c) for s in (0, 1, 2, 4, 8) for b in (0, 1, 3, 8)
+               for c in (0, -1, 3)]
 
 
-def set_variant(v, block_mode=0):
-    nsx.set_param(nsx.PARAM_RUN_SEGS, v.get("run", 0))
-    nsx.set_param(nsx.PARAM_XCD_CHUNK, v.get("chunk", 0))
-    nsx.set_param(nsx.PARAM_KERNEL, v["kernel"])
-    nsx.set_param(nsx.PARAM_STREAM_ROWS, v["rows"])
-    nsx.set_param(nsx.PARAM_SEGS_PER_WAVE, v["spw"])
-    nsx.set_param(nsx.PARAM_NONTEMPORAL, v["nt"])
-    nsx.set_param(nsx.PARAM_XCD_MAP, v["xcd"])
-    nsx.set_param(nsx.PARAM_BLOCKS_PER_CU, v["bpc"])
-    nsx.set_param(nsx.PARAM_BLOCK_MODE, block_mode)
-
-
-def test_all_variants_bit_exact():
+def test_all_launch_shapes_bit_exact():
+    """Every segments-per-task / grid / XCD-deal shape, each in auto, wave and block mode, over
+    aligned short (config 2's pipelined kernel), unaligned short (edge-masked buffer kernel) and
+    long (wave kernel) batches."""
     buf = O.c_splitmix64(0x1071, 1500 * 50001 + 64)
     d = dev(buf)
     want = {}
-    for L, stride, n in ((1500, 1500, 50001), (1400, 1500, 50001), (700, 700, 9999), (3000, 3001, 20000),
-                         (9000, 9000, 5000), (65536, 65536, 500)):
+    for L, stride, n in ((1500, 1500, 50001), (1400, 1500, 50001), (700, 700, 9999), (1499, 1501, 30001),
+                         (3000, 3001, 20000), (9000, 9000, 5000), (65536, 65536, 500)):
         want[(L, stride, n)] = O.c_batch(buf, n, stride=stride, seg_len=L)
-    try:
-        for v in VARIANTS:
-            for bm in (0, 1, 2):
-                set_variant(v, bm)
-                for (L, stride, n), w in want.items():
-                    out = torch.empty(n, dtype=torch.int16, device="cuda")
-                    nsx.fixed_dev(d, stride, L, n, out=out)
-                    assert np.array_equal(u16(out), w), (v, bm, L, stride, n)
-    finally:
-        set_variant(dict(kernel=0, rows=0, spw=0, nt=0, xcd=0, bpc=0), 0)
+    for t in FIXED_TUNES:
+        for bm in (0, 1, 2):
+            if bm == 2 and t["segs_per_wave"] not in (0, 8):
+                continue  # block mode ignores the task shape
+            tune = dict(t, block_mode=bm)
+            for (L, stride, n), w in want.items():
+                out = torch.empty(n, dtype=torch.int16, device="cuda")
+                nsx.fixed_dev(d, stride, L, n, out=out, tune=tune)
+                assert np.array_equal(u16(out), w), (tune, L, stride, n)
 
 
-RAGGED_VARIANTS = ([dict(kernel=k, rows=r, nt=nt, xcd=x, bpc=b, spw=0) for k in (3, 4) for r in (4, 8, 16)
-                    for nt in (1, 2) for x in (1, 2, 3) for b in (8, 2)] +
-                   [dict(kernel=1, rows=r, nt=1, xcd=1, bpc=4, spw=0) for r in (4, 8, 16)] +
-                   [dict(kernel=4, rows=8, nt=1, xcd=1, bpc=8, spw=0, run=rs) for rs in (1, 2, 7, 16, 33, 63)] +
-                   [dict(kernel=2, rows=0, nt=1, xcd=x, bpc=4, spw=0) for x in (1, 3)] +
-                   [dict(kernel=4, rows=r, nt=1, xcd=4, bpc=b, spw=0, run=rs) for r in (4, 8, 16) for b in (1, 2, 8)
-                    for rs in (1, 16, 63)] +
-                   [dict(kernel=6, rows=r, nt=1, xcd=x, bpc=b, spw=0, run=rs) for r in (4, 8, 16) for x in (1, 4)
-                    for b in (2, 8) for rs in (1, 63)])
+RAGGED_TUNES = [dict(rows=r, run_segs=rs, blocks_per_cu=b) for r in (0, 4, 16) for rs in (0, 1, 16, 63)
+                for b in (0, 1, 8)]
 
 
-def test_ragged_variants_bit_exact():
+def test_ragged_launch_shapes_bit_exact():
     rng = np.random.default_rng(1234)
     lens = rng.integers(0, 9001, 20000).astype(np.uint64)
     lens[rng.integers(0, 20000, 300)] = 0
@@ -253,24 +134,20 @@ def test_ragged_variants_bit_exact():
     want = O.c_batch(buf, lens.size, offsets=offs)
     want_p = O.c_batch(buf, lens.size, offsets=offs, partial=part)
     d, o, p = dev(buf), dev(offs.view(np.int64)), dev(part.view(np.int32))
-    try:
-        for v in RAGGED_VARIANTS:
-            for bm in (0, 1):
-                set_variant(v, bm)
-                out = torch.empty(lens.size, dtype=torch.int16, device="cuda")
-                nsx.ragged_dev(d, o, out=out)
-                assert np.array_equal(u16(out), want), (v, bm)
-                nsx.ragged_dev(d, o, partial=p, out=out)
-                assert np.array_equal(u16(out), want_p), (v, bm)
-                okv = host(nsx.verify_ragged_dev(d, o, partial=p))
-                assert np.array_equal(okv.astype(bool), want_p == 0xFFFF), (v, bm)
-    finally:
-        set_variant(dict(kernel=0, rows=0, spw=0, nt=0, xcd=0, bpc=0), 0)
+    for t in RAGGED_TUNES + [dict(block_mode=2)]:
+        tune = dict(t, block_mode=t.get("block_mode", 1))
+        out = torch.empty(lens.size, dtype=torch.int16, device="cuda")
+        nsx.ragged_dev(d, o, out=out, tune=tune)
+        assert np.array_equal(u16(out), want), tune
+        nsx.ragged_dev(d, o, partial=p, out=out, tune=tune)
+        assert np.array_equal(u16(out), want_p), tune
+        okv = host(nsx.verify_ragged_dev(d, o, partial=p, tune=tune))
+        assert np.array_equal(okv.astype(bool), want_p == 0xFFFF), tune
 
 
 def test_ragged_byte_balanced_partition_edges():
-    """XCD_MAP=4 (byte-balanced wave ranges found by an in-kernel 64-ary search over
-    the offsets): skewed, sorted, all-empty and tiny batches, more waves than segments."""
+    """Byte-balanced wave ranges (found by an in-kernel 64-ary search over the offsets):
+    skewed, sorted, all-empty and tiny batches, more waves than segments."""
     rng = np.random.default_rng(77)
     cases = {
         "sorted": np.sort(rng.integers(0, 20000, 6000)).astype(np.uint64),
@@ -280,22 +157,18 @@ def test_ragged_byte_balanced_partition_edges():
         "all_empty": np.zeros(4000, np.uint64),
         "few": rng.integers(0, 5000, 1030).astype(np.uint64),
     }
-    try:
-        for name, lens in cases.items():
-            offs = np.zeros(lens.size + 1, np.uint64)
-            offs[1:] = np.cumsum(lens)
-            offs += np.uint64(3)
-            buf = O.c_splitmix64(0x1099, int(offs[-1]) + 8)
-            want = O.c_batch(buf, lens.size, offsets=offs)
-            d, o = dev(buf), dev(offs.view(np.int64))
-            for b in (1, 8):
-                for rs in (1, 16, 63):
-                    set_variant(dict(kernel=4, rows=8, nt=1, xcd=4, bpc=b, spw=0, run=rs), 1)
-                    out = torch.empty(lens.size, dtype=torch.int16, device="cuda")
-                    nsx.ragged_dev(d, o, out=out)
-                    assert np.array_equal(u16(out), want), (name, b, rs)
-    finally:
-        set_variant(dict(kernel=0, rows=0, spw=0, nt=0, xcd=0, bpc=0), 0)
+    for name, lens in cases.items():
+        offs = np.zeros(lens.size + 1, np.uint64)
+        offs[1:] = np.cumsum(lens)
+        offs += np.uint64(3)
+        buf = O.c_splitmix64(0x1099, int(offs[-1]) + 8)
+        want = O.c_batch(buf, lens.size, offsets=offs)
+        d, o = dev(buf), dev(offs.view(np.int64))
+        for b in (1, 8):
+            for rs in (1, 16, 63):
+                out = torch.empty(lens.size, dtype=torch.int16, device="cuda")
+                nsx.ragged_dev(d, o, out=out, tune=dict(blocks_per_cu=b, run_segs=rs, block_mode=1))
+                assert np.array_equal(u16(out), want), (name, b, rs)
 
 
 # ------------------------------------------------------------------ verify / pseudo-header
@@ -425,108 +298,74 @@ def test_host_batch_paths_pageable_and_pinned():
     pin.free()
 
 
-# ------------------------------------------------------------------ BASELINE configs at full size
-
-def test_config2_1M_x_1500_full():
-    n, L = 1 << 20, 1500
-    t = torch.empty(n * L, dtype=torch.uint8, device="cuda")
-    nsx.fill_splitmix64_dev(t, 0x1071)
-    h = host(t)
-    assert np.array_equal(h[:4096], O.c_splitmix64(0x1071, 4096))
-    assert np.array_equal(h[-4096:], O.c_splitmix64(0x1071, 4096, n * L - 4096))
-    out = nsx.fixed_dev(t, L, L, n, out=torch.empty(n, dtype=torch.int16, device="cuda"))
-    got = u16(out)
-    assert np.array_equal(got, O.c_batch(h, n, stride=L, seg_len=L, threads=16))
-    out2 = nsx.fixed_dev(t, L, L, n, out=torch.empty(n, dtype=torch.int16, device="cuda"))
-    assert np.array_equal(u16(out2), got)  # idempotent
-
-
-def test_config3_1M_ragged_full():
-    n = 1 << 20
-    rng = np.random.default_rng(0x1072)
-    lens = rng.integers(64, 9001, n).astype(np.uint64)
-    offs = np.zeros(n + 1, np.uint64)
-    offs[1:] = np.cumsum(lens)
-    t = torch.empty(int(offs[-1]), dtype=torch.uint8, device="cuda")
-    nsx.fill_splitmix64_dev(t, 0x1072)
-    want = O.c_batch(host(t), n, offsets=offs, threads=16)
-    try:
-        for xcd in (0, 1, 4):  # default, XCD deal, byte-balanced wave ranges
-            nsx.set_param(nsx.PARAM_XCD_MAP, xcd)
-            out = nsx.ragged_dev(t, dev(offs.view(np.int64)), out=torch.empty(n, dtype=torch.int16, device="cuda"))
-            assert np.array_equal(u16(out), want), xcd
-    finally:
-        nsx.set_param(nsx.PARAM_XCD_MAP, 0)
+@pytest.mark.parametrize("shards", [2, 3, 8])
+def test_host_batch_sharded_threads_on_one_device(shards):
+    """The multi-GPU host path's shard-and-stitch logic (run_sharded: contiguous shards, byte-balanced
+    for ragged batches, one host thread + its own streams and staging per shard) on the one GPU:
+    nsx_tune.shards_per_device = K splits the batch into K shards on device 0. Fixed and ragged
+    host batches, pageable and with partials, against the oracle; more shards than segments too.
+    (The host path starts in transport buffers: transport/pipe/pipe.go:73-124.)"""
+    rng = np.random.default_rng(0x5A + shards)
+    tune = dict(shards_per_device=shards)
+    L = 1500
+    for n in (1, shards - 1 or 1, 5000, 70_001):
+        buf = rng.integers(0, 256, n * L + 3, dtype=np.uint8)
+        part = rng.integers(0, 1 << 20, n, dtype=np.uint64).astype(np.uint32)
+        got = nsx.fixed_host(buf[3:], L, L, n, partial=part, tune=tune)
+        assert np.array_equal(got, O.c_batch(buf[3:], n, stride=L, seg_len=L, partial=part)), (shards, n)
+        lens = rng.integers(0, 9001, n).astype(np.uint64)
+        offs = np.zeros(n + 1, np.uint64)
+        offs[1:] = np.cumsum(lens)
+        offs += np.uint64(1)
+        rb = rng.integers(0, 256, int(offs[-1]) + 2, dtype=np.uint8)
+        assert np.array_equal(nsx.ragged_host(rb, offs, partial=part, tune=tune),
+                              O.c_batch(rb, n, offsets=offs, partial=part)), (shards, n)
 
 
-def test_config4_256K_x_64KiB_sampled_and_roundtrip():
-    n, L = 1 << 18, 65536
-    t = torch.empty(n * L, dtype=torch.uint8, device="cuda")
-    nsx.fill_splitmix64_dev(t, 0x1073)
-    out = nsx.fixed_dev(t, L, L, n, out=torch.empty(n, dtype=torch.int16, device="cuda"))
-    got = u16(out)
-    idx = sorted(set(range(0, n, 4099)) | {0, 1, n // 2, n - 2, n - 1})
-    for i in idx:
-        seg = O.c_splitmix64(0x1073, L, i * L)
-        assert got[i] == O.c_fold_checksum(b"", seg.tobytes()), i
-    # size-independent property: block-per-segment mode agrees with wave mode on every segment
-    nsx.set_param(nsx.PARAM_BLOCK_MODE, 2)
-    try:
-        out_b = nsx.fixed_dev(t, L, L, n, out=torch.empty(n, dtype=torch.int16, device="cuda"))
-        assert np.array_equal(u16(out_b), got)
-    finally:
-        nsx.set_param(nsx.PARAM_BLOCK_MODE, 0)
-    # sender/receiver round trip on every segment: write ^raw into bytes 16-17, re-sum == 0xFFFF
-    del out
-    v = t.view(n, L)
-    fld = torch.from_numpy(((~got) & 0xFFFF).astype(np.int32)).cuda()
-    # the field words must be zero before the sum is taken (tcp.go:68): recompute with them zeroed
-    v[:, 16:18] = 0
-    raw0 = u16(nsx.fixed_dev(t, L, L, n, out=torch.empty(n, dtype=torch.int16, device="cuda")))
-    fld = torch.from_numpy(((~raw0) & 0xFFFF).astype(np.int32)).cuda()
-    v[:, 16] = (fld >> 8).to(torch.uint8)
-    v[:, 17] = (fld & 0xFF).to(torch.uint8)
-    ok = u16(nsx.fixed_dev(t, L, L, n, out=torch.empty(n, dtype=torch.int16, device="cuda")))
-    assert (ok == 0xFFFF).all()
+def test_host_batch_more_gpus_than_present_is_enodev():
+    """num_gpus > device count: NSX_ENODEV, nothing computed, the caller's current device unchanged."""
+    before = torch.cuda.current_device()
+    buf = np.zeros(3000, np.uint8)
+    with pytest.raises(nsx.NsxError) as e:
+        nsx.fixed_host(buf, 1500, 1500, 2, num_gpus=nsx.device_count() + 1)
+    assert e.value.code == nsx.NSX_ENODEV
+    with pytest.raises(nsx.NsxError) as e:
+        nsx.ragged_host(buf, np.array([0, 1000, 3000], np.uint64), num_gpus=nsx.device_count() + 1)
+    assert e.value.code == nsx.NSX_ENODEV
+    assert torch.cuda.current_device() == before
+    assert np.array_equal(nsx.fixed_host(buf, 1500, 1500, 2, num_gpus=nsx.device_count()), [0, 0])
 
+
+# ------------------------------------------------------------------ large batches
 
 @pytest.mark.parametrize("L", [1500, 1501])
 @pytest.mark.parametrize("window", [1_000_003, 3000, 1500, 1])
-def test_fixed_back_to_back_windows(nsx_param, window, L):
-    """NSX_PARAM_WINDOW_BYTES splits the fixed short-segment path into back-to-back launches
+def test_fixed_back_to_back_windows(window, L):
+    """nsx_tune.window_bytes splits the fixed short-segment path into back-to-back launches
     (DESIGN.md §7 step 21): window sizes that cut the batch unevenly, down to one segment
-    per launch, aligned and odd strides, with per-segment partials, against the oracle."""
+    per launch, aligned and odd strides, with per-segment partials, against the oracle; the
+    library's launch count says how many launches that is."""
     rng = np.random.default_rng(0x21 + window)
     n = 2048 if window <= 3000 else 6001
     buf = rng.integers(0, 256, n * L, dtype=np.uint8)
     part = rng.integers(0, 1 << 20, n, dtype=np.uint32)
     want = O.c_batch(buf, n, stride=L, seg_len=L, partial=part)
-    nsx_param(nsx.PARAM_WINDOW_BYTES, window)
-    assert np.array_equal(run_fixed(buf, L, L, n, part), want)
+    tune = dict(window_bytes=window)
+    assert np.array_equal(run_fixed(buf, L, L, n, part, tune=tune), want)
+    assert nsx.fixed_launch_count(L, L, n, tune) == -(-n // max(1, window // L))
 
 
-def test_config5_16M_x_1500_per_gpu_sampled():
-    """Config 5's per-GPU batch (16M x 1500 B = 23.4 GiB): every
-    4099th segment plus the segments either side of every 8-way shard boundary
-    against the oracle (bytes regenerated on the CPU from the counter-based
-    stream); every segment re-checked by the block-per-segment kernel."""
-    n, L, seed = 1 << 24, 1500, 0x1071 + 3  # the rank-3 seed
-    t = torch.empty(n * L, dtype=torch.uint8, device="cuda")
-    nsx.fill_splitmix64_dev(t, seed)
-    got = u16(nsx.fixed_dev(t, L, L, n, out=torch.empty(n, dtype=torch.int16, device="cuda")))
-    bounds = nsx.shard_plan(n, 8)
-    idx = set(range(0, n, 4099)) | {n - 1}
-    for b in bounds[1:-1]:
-        idx |= {int(b) - 1, int(b)}
-    for i in sorted(idx):
-        seg = O.c_splitmix64(seed, L, i * L)
-        assert got[i] == O.c_fold_checksum(b"", seg.tobytes()), i
-    nsx.set_param(nsx.PARAM_BLOCK_MODE, 2)
-    try:
-        alt = u16(nsx.fixed_dev(t, L, L, n, out=torch.empty(n, dtype=torch.int16, device="cuda")))
-    finally:
-        nsx.set_param(nsx.PARAM_BLOCK_MODE, 0)
-    assert np.array_equal(alt, got)
+@pytest.mark.parametrize("window", [0, 1, 3000, -1])
+def test_fixed_stride_zero_aliases_first_segment(window):
+    """stride 0 (every segment aliases the first — allowed by nsx_csum_fixed_dev) with and without
+    windows: one launch, every result equal (window_bytes / stride divided by zero)."""
+    rng = np.random.default_rng(7)
+    for L in (1500, 1497, 64, 8):
+        buf = rng.integers(0, 256, L + 8, dtype=np.uint8)
+        n = 5000
+        got = run_fixed(buf, 0, L, n, tune=dict(window_bytes=window))
+        assert (got == O.c_go_checksum(b"", buf[:L].tobytes())).all(), (L, window)
+        assert nsx.fixed_launch_count(0, L, n, dict(window_bytes=window)) == 1
 
 
 def test_fixed_batch_past_the_launch_chunk():
@@ -541,11 +380,8 @@ def test_fixed_batch_past_the_launch_chunk():
     idx = sorted(set(range(0, n, 1_000_003)) | set(range((1 << 28) - 5, (1 << 28) + 5)) | {n - 1})
     for i in idx:
         assert got[i] == O.c_fold_checksum(b"", O.c_splitmix64(seed, L, i * L).tobytes()), i
-    nsx.set_param(nsx.PARAM_XCD_MAP, 2)
-    try:
-        alt = u16(nsx.fixed_dev(t, L, L, n, out=torch.empty(n, dtype=torch.int16, device="cuda")))
-    finally:
-        nsx.set_param(nsx.PARAM_XCD_MAP, 0)
+    alt = u16(nsx.fixed_dev(t, L, L, n, out=torch.empty(n, dtype=torch.int16, device="cuda"),
+                            tune=dict(xcd_chunk=-1, segs_per_wave=2, blocks_per_cu=8)))
     assert np.array_equal(alt, got)
 
 
@@ -668,15 +504,15 @@ def _ipv4_headers(rng, n, stride, hdr_off):
     return buf, ihl
 
 
-@pytest.mark.parametrize("kernel", [0, 1, 2, 3, 4])  # 0: default (pipelined flat for packed 20 B, LDS-dense for stride <= 64), 1: per-thread, 2: LDS-dense, 3: flat, 4: pipelined flat with deferred raw stores
+@pytest.mark.parametrize("kernel", [0, 1, 2])  # 0: by layout (packed 20 B flat, LDS-dense for stride <= 64), 1: per-thread, 2: LDS-dense
 @pytest.mark.parametrize("stride,hdr_off", [(64, 0), (61, 1), (1514, 14), (1500, 0), (60, 0), (40, 3), (20, 0)])
-def test_ipv4_header_checksum_verify_and_fill(stride, hdr_off, kernel, nsx_param):
-    nsx_param(nsx.PARAM_KERNEL, kernel)
+def test_ipv4_header_checksum_verify_and_fill(stride, hdr_off, kernel):
+    tune = dict(kernel=kernel)
     rng = np.random.default_rng(stride * 31 + hdr_off)
     n = 3000
     buf, ihl = _ipv4_headers(rng, n, stride, hdr_off)
     d = dev(buf)
-    raw = u16(nsx.ipv4_hdr_csum_dev(d, stride, n, hdr_off=hdr_off, mode=0))
+    raw = u16(nsx.ipv4_hdr_csum_dev(d, stride, n, hdr_off=hdr_off, mode=0, tune=tune))
     for i in range(n):
         L = int(ihl[i]) * 4
         ok = L >= 20 and hdr_off + L <= stride
@@ -684,7 +520,7 @@ def test_ipv4_header_checksum_verify_and_fill(stride, hdr_off, kernel, nsx_param
         assert raw[i] == (O.go_checksum(b"", h) if ok else 0), i
     # fill mode: field written in place, then every valid header verifies
     out = torch.empty(n, dtype=torch.int16, device="cuda")
-    nsx.ipv4_hdr_csum_dev(d, stride, n, hdr_off=hdr_off, mode=1, out=out)
+    nsx.ipv4_hdr_csum_dev(d, stride, n, hdr_off=hdr_off, mode=1, out=out, tune=tune)
     filled = host(d)
     raw_fill = u16(out)
     for i in range(0, n, 7):
@@ -697,49 +533,20 @@ def test_ipv4_header_checksum_verify_and_fill(stride, hdr_off, kernel, nsx_param
             assert (int(filled[b0 + 10]) << 8 | int(filled[b0 + 11])) == (~raw_fill[i]) & 0xFFFF
         else:
             assert np.array_equal(filled[b0:b0 + 12], buf[b0:b0 + 12])  # malformed: untouched
-    again = u16(nsx.ipv4_hdr_csum_dev(d, stride, n, hdr_off=hdr_off, mode=0))
+    again = u16(nsx.ipv4_hdr_csum_dev(d, stride, n, hdr_off=hdr_off, mode=0, tune=tune))
     valid = np.array([int(ihl[i]) * 4 >= 20 and hdr_off + int(ihl[i]) * 4 <= stride for i in range(n)])
     assert (again[valid] == 0xFFFF).all()
 
 
-@pytest.mark.parametrize("n", [(8 << 20) + 77, 5_000_000])
-def test_ipv4_packed_deferred_raw_stores(n, nsx_param):
-    """Kernel knob 4 (packed 20 B headers, raw sums buffered in LDS and written in bursts):
-    enough tasks per wave to fill and flush the buffer many times, a partial last task;
-    every raw sum against a numpy restatement of the fold (RFC 1071; tcp.go:72-95) and
-    against the default kernel."""
-    rng = np.random.default_rng(n)
-    buf = rng.integers(0, 256, n * 20, dtype=np.uint8)
-    buf[::20] = 0x45
-    buf[20 * 977::20 * 1979] = 0x44  # some malformed (IHL 4): raw 0
-    w = buf.reshape(n, 10, 2).astype(np.uint32)
-    s = ((w[:, :, 0] << 8) | w[:, :, 1]).sum(axis=1)
-    s = (s & 0xFFFF) + (s >> 16)
-    s = (s & 0xFFFF) + (s >> 16)
-    want = np.where((buf[::20] & 15) == 5, s, 0).astype(np.uint16)
-    d = dev(buf)
-    nsx_param(nsx.PARAM_KERNEL, 4)
-    got = u16(nsx.ipv4_hdr_csum_dev(d, 20, n, mode=0))
-    assert np.array_equal(got, want)
-    nsx_param(nsx.PARAM_KERNEL, 0)
-    assert np.array_equal(u16(nsx.ipv4_hdr_csum_dev(d, 20, n, mode=0)), want)
-
-
-def _mask_words(valid):
-    pad = np.zeros((valid.size + 63) // 64 * 64, np.uint8)
-    pad[:valid.size] = valid
-    return np.packbits(pad, bitorder="little").view(np.uint64)
-
-
-@pytest.mark.parametrize("kernel", [0, 1, 2, 3])
+@pytest.mark.parametrize("kernel", [0, 1, 2])
 @pytest.mark.parametrize("stride,hdr_off", [(20, 0), (22, 2), (60, 0), (61, 1), (1514, 14)])
 @pytest.mark.parametrize("n", [1, 63, 64, 65, 255, 256, 257, 3001])
-def test_ipv4_header_verify_mask(n, stride, hdr_off, kernel, nsx_param):
+def test_ipv4_header_verify_mask(n, stride, hdr_off, kernel):
     """nsx_ipv4_hdr_verify_mask_dev: bit i set iff header i is well-formed and sums to
     0xFFFF — the oracle's go_checksum over the header (RFC 791 §3.1 with tcp.go:72-95's
     sum) on about half the headers made valid, the rest corrupted or malformed; every
-    mask word written (garbage before), bits past n zero; all four kernels."""
-    nsx_param(nsx.PARAM_KERNEL, kernel)
+    mask word written (garbage before), bits past n zero; all three kernels."""
+    tune = dict(kernel=kernel)
     rng = np.random.default_rng(n * 7 + stride)
     buf, ihl = _ipv4_headers(rng, n, stride, hdr_off)
     valid = np.zeros(n, bool)
@@ -754,26 +561,26 @@ def test_ipv4_header_verify_mask(n, stride, hdr_off, kernel, nsx_param):
             buf[b0 + 10], buf[b0 + 11] = f >> 8, f & 0xFF
         valid[i] = O.go_checksum(b"", buf[b0:b0 + L].tobytes()) == 0xFFFF
     mask = torch.full(((n + 63) // 64,), 0x5A5A5A5A5A5A5A5A, dtype=torch.int64, device="cuda")
-    nsx.ipv4_hdr_verify_mask_dev(dev(buf), stride, n, hdr_off=hdr_off, mask=mask)
+    nsx.ipv4_hdr_verify_mask_dev(dev(buf), stride, n, hdr_off=hdr_off, mask=mask, tune=tune)
     got = host(mask).view(np.uint64)
-    assert np.array_equal(got, _mask_words(valid)), (n, stride, kernel)
+    assert np.array_equal(got, mask_words(valid)), (n, stride, kernel)
     # the same answer as verify-into-raw-sums followed by the f2 mask kernel
-    raw = nsx.ipv4_hdr_csum_dev(dev(buf), stride, n, hdr_off=hdr_off, mode=0)
+    raw = nsx.ipv4_hdr_csum_dev(dev(buf), stride, n, hdr_off=hdr_off, mode=0, tune=tune)
     assert np.array_equal(host(nsx.verify_mask_dev(raw)).view(np.uint64), got)
 
 
-@pytest.mark.parametrize("kernel", [0, 1, 2, 3])
+@pytest.mark.parametrize("kernel", [0, 1, 2])
 @pytest.mark.parametrize("stride,hdr_off", [(20, 0), (22, 2), (23, 3)])
-def test_ipv4_dense_headers_end_at_allocation_end(stride, hdr_off, kernel, nsx_param):
+def test_ipv4_dense_headers_end_at_allocation_end(stride, hdr_off, kernel):
     """Packed IHL=5 headers (header-split ring), the last one ending exactly at
     the allocation's last byte: no read past a header's own 20 bytes."""
-    nsx_param(nsx.PARAM_KERNEL, kernel)
+    tune = dict(kernel=kernel)
     rng = np.random.default_rng(stride)
     n = 70_001
     buf = rng.integers(0, 256, n * stride, dtype=np.uint8)
     buf[hdr_off::stride] = 0x45
     d = dev(buf[: (n - 1) * stride + hdr_off + 20])
-    nsx.ipv4_hdr_csum_dev(d, stride, n, hdr_off=hdr_off, mode=1)
+    nsx.ipv4_hdr_csum_dev(d, stride, n, hdr_off=hdr_off, mode=1, tune=tune)
     got = host(d)
     want = buf[: (n - 1) * stride + hdr_off + 20].copy()
     for i in list(range(0, n, 1013)) + [n - 1]:
@@ -782,11 +589,11 @@ def test_ipv4_dense_headers_end_at_allocation_end(stride, hdr_off, kernel, nsx_p
         h[10:12] = b"\0\0"
         f = O.field_value(O.go_checksum(b"", bytes(h)))
         assert got[b0 + 10] == f >> 8 and got[b0 + 11] == f & 0xFF, i
-    raw = u16(nsx.ipv4_hdr_csum_dev(d, stride, n, hdr_off=hdr_off, mode=0))
+    raw = u16(nsx.ipv4_hdr_csum_dev(d, stride, n, hdr_off=hdr_off, mode=0, tune=tune))
     assert (raw == 0xFFFF).all()
 
 
-def test_xcd_deal_variants_agree_build_and_headers(nsx_param):
+def test_xcd_deal_variants_agree_build_and_headers():
     """The XCD deal (auto interleaved chunks, fixed small chunks, contiguous eighths)
     changes only which wave takes which task: TCP build images and IPv4 header sums
     are identical under every deal."""
@@ -798,11 +605,11 @@ def test_xcd_deal_variants_agree_build_and_headers(nsx_param):
     hb = rng.integers(0, 256, nh * 20, dtype=np.uint8)
     hb[::20] = 0x45
     want_h = O.c_batch(hb, nh, stride=20, seg_len=20)
-    for chunk in (0, 2, 4, 99):
-        nsx_param(nsx.PARAM_XCD_CHUNK, chunk)
-        img, raw = _run_build(fields, data, data_off, out_off, ps)
+    for chunk in (0, 2, 4, -1):
+        tune = dict(xcd_chunk=chunk)
+        img, raw = _run_build(fields, data, data_off, out_off, ps, tune=tune)
         assert np.array_equal(raw, ref_raw) and np.array_equal(img, ref_img), chunk
-        got = u16(nsx.ipv4_hdr_csum_dev(dev(hb), 20, nh, mode=0))
+        got = u16(nsx.ipv4_hdr_csum_dev(dev(hb), 20, nh, mode=0, tune=tune))
         assert np.array_equal(got, want_h), chunk
 
 
@@ -838,7 +645,7 @@ def _uniform_build_case(rng, n, P, lead, pseudo=True):
     return fields, data, data_off, out_off, ps
 
 
-def _run_build(fields, data, data_off, out_off, ps):
+def _run_build(fields, data, data_off, out_off, ps, tune=None):
     n = data_off.size - 1
     dt = {np.uint16: np.int16, np.uint32: np.int32, np.uint8: np.uint8}
     f = {k: dev(v.view(dt[v.dtype.type])) for k, v in fields.items()}
@@ -846,29 +653,28 @@ def _run_build(fields, data, data_off, out_off, ps):
     out = torch.full((int(out_off[-1]),), 0xAB, dtype=torch.uint8, device="cuda")
     raw = torch.empty(n, dtype=torch.int16, device="cuda")
     nsx.tcp_build_dev(f, dev(data), dev(data_off.view(np.int64)), out, dev(out_off.view(np.int64)), partial=part,
-                      raw=raw)
+                      raw=raw, tune=tune)
     return host(out), u16(raw)
 
 
 @pytest.mark.parametrize("P", [0, 4, 8, 12, 16, 100, 1004, 1480, 4096, 8996, 65536])
 @pytest.mark.parametrize("n", [1, 63, 64, 65, 300])
-def test_tcp_build_uniform_batches(P, n, nsx_param):
+def test_tcp_build_uniform_batches(P, n):
     """Packed option-less batches (same payload length, payloads and images back to
     back — the bench's f1 layout): images and raw sums equal the Go-faithful oracle's
     for tiny, row-sized and 64 KiB payloads, with the pipelined fast-group path
-    (kernel 0, images ≤ 2 KiB) and without it (kernel 2)."""
+    (kernel 0, images ≤ 2 KiB), the general pipelined composition (kernel 3) and the
+    unpipelined path (kernel 2)."""
     if n * (P + 20) > 40 << 20:
         n = 65
     rng = np.random.default_rng(P * 1000 + n)
     for lead in (20, 28, 0):  # lead 0: segment 0 has no 20 bytes before its payload (general path)
         fields, data, data_off, out_off, ps = _uniform_build_case(rng, n, P, lead)
         want, wraw = O.c_go_tcp_build(fields, data, data_off, out_off, ps)
-        for kern, spw in ((0, 0), (0, 1), (3, 0), (2, 0)):  # pipelined 2 / 1 segs per set; general pipelined path only; unpipelined
-            nsx_param(nsx.PARAM_KERNEL, kern)
-            nsx_param(nsx.PARAM_SEGS_PER_WAVE, spw)
-            got, raw = _run_build(fields, data, data_off, out_off, ps)
-            assert np.array_equal(raw, wraw), (P, n, lead, kern, spw)
-            assert np.array_equal(got, want), (P, n, lead, kern, spw)
+        for kern in (0, nsx.KERNEL_BUILD_GENERAL, nsx.KERNEL_BUILD_PLAIN):
+            got, raw = _run_build(fields, data, data_off, out_off, ps, tune=dict(kernel=kern))
+            assert np.array_equal(raw, wraw), (P, n, lead, kern)
+            assert np.array_equal(got, want), (P, n, lead, kern)
 
 
 _OPT_SETS = {  # option lists as the reference serialises them (tcp.go:225-231: kind 2 carries length + data)
@@ -887,7 +693,7 @@ _OPT_SETS = {  # option lists as the reference serialises them (tcp.go:225-231: 
 
 @pytest.mark.parametrize("P", [0, 12, 1468, 3000])
 @pytest.mark.parametrize("opt", sorted(_OPT_SETS))
-def test_tcp_build_uniform_batches_with_options(opt, P, nsx_param):
+def test_tcp_build_uniform_batches_with_options(opt, P):
     """Packed batches whose every segment carries the same option list (the bench's
     config 8 layout): images and raw sums equal the Python oracle's Segment.bytes() /
     computeChecksum (tcp.go:98-128, :72-95) with the options at image byte 20, the
@@ -931,15 +737,14 @@ def test_tcp_build_uniform_batches_with_options(opt, P, nsx_param):
         data_off = np.arange(n + 1, dtype=np.uint64) * np.uint64(P) + np.uint64(data_lead)
         out_off = nsx.tcp_layout_host(data_off, opt_off)
         assert all(int(out_off[i + 1] - out_off[i]) >= len(want_wire[i]) for i in range(n))
-        for kern, spw in ((0, 0), (0, 1), (3, 0), (2, 0)):
-            nsx_param(nsx.PARAM_KERNEL, kern)
-            nsx_param(nsx.PARAM_SEGS_PER_WAVE, spw)
+        for kern in (0, nsx.KERNEL_BUILD_GENERAL, nsx.KERNEL_BUILD_PLAIN):
             out = torch.full((int(out_off[-1]),), 0xAB, dtype=torch.uint8, device="cuda")
             raw = torch.empty(n, dtype=torch.int16, device="cuda")
             nsx.tcp_build_dev(fields, dev(data), dev(data_off.view(np.int64)), out, dev(out_off.view(np.int64)),
-                              opts=dev(opts), opt_off=dev(opt_off.view(np.int64)), partial=part, raw=raw)
+                              opts=dev(opts), opt_off=dev(opt_off.view(np.int64)), partial=part, raw=raw,
+                              tune=dict(kernel=kern))
             got, raw_h = host(out), u16(raw)
-            key = (opt, P, opt_lead, data_lead, kern, spw)
+            key = (opt, P, opt_lead, data_lead, kern)
             assert np.array_equal(raw_h, want_raw), key
             for i in range(n):
                 o = int(out_off[i])
@@ -1157,7 +962,7 @@ def test_entry_points_capture_into_a_hip_graph():
         assert np.array_equal(u16(out_r), O.c_batch(rbh, lens.size, offsets=offs)), rep
         valid = np.ones(nh, bool)
         valid[::5] = False
-        assert np.array_equal(host(mask).view(np.uint64), _mask_words(valid)), rep
+        assert np.array_equal(host(mask).view(np.uint64), mask_words(valid)), rep
 
 
 def test_f1_options_build_1M_segments_full_size_roundtrip():
@@ -1205,4 +1010,4 @@ def test_f3_mask_64M_headers_full_size():
     n = cfg["n"]
     valid = np.ones(n, bool)
     valid[::1000] = False
-    assert np.array_equal(host(w["out"]).view(np.uint64), _mask_words(valid))
+    assert np.array_equal(host(w["out"]).view(np.uint64), mask_words(valid))

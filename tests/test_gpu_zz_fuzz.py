@@ -1,8 +1,10 @@
 """Randomised GPU parity (seeded, bounded to a few seconds): every device entry
 point on batches whose sizes, alignments, lengths and kernel knobs are drawn at
 random, against the CPU oracle. Complements the hand-picked edge cases of
-test_gpu_parity.py with combinations nobody wrote down. NSX_FUZZ_SCALE=k runs k times
-as many cases (new seeds; the default set is the first of them)."""
+test_gpu_parity.py with combinations nobody wrote down, and collects after it (and
+after the BASELINE configs of test_gpu_00_baseline.py) so that under -x a fuzz failure
+never hides those. NSX_FUZZ_SCALE=k runs k times as many cases (new seeds; the default
+set is the first of them). Launch overrides (include/nsx_tune.h) are drawn per case."""
 import os
 
 import numpy as np
@@ -17,25 +19,11 @@ torch = pytest.importorskip("torch")
 
 import nsx  # noqa: E402
 
-FIXED_KNOBS = [dict(), dict(kernel=3), dict(kernel=5), dict(kernel=2), dict(kernel=7), dict(kernel=1),
-               dict(blocks_per_cu=1, segs_per_wave=8), dict(xcd_map=2), dict(xcd_chunk=99), dict(block_mode=2), dict(window_bytes=1_000_000), dict(window_bytes=7_777)]
-RAGGED_KNOBS = [dict(), dict(xcd_map=1), dict(kernel=6), dict(kernel=3), dict(run_segs=1), dict(stream_rows=16),
-                dict(block_mode=2)]
-
-
-def _apply(knobs):
-    import bench
-    for p in nsx.ALL_PARAMS:
-        nsx.set_param(p, 0)
-    for k, v in knobs.items():
-        nsx.set_param(bench.PARAMS[k], v)
-
-
-@pytest.fixture(autouse=True)
-def _reset_knobs():
-    yield
-    for p in nsx.ALL_PARAMS:
-        nsx.set_param(p, 0)
+FIXED_KNOBS = [dict(), dict(segs_per_wave=4, blocks_per_cu=2), dict(segs_per_wave=1), dict(segs_per_wave=2),
+               dict(blocks_per_cu=8), dict(blocks_per_cu=1, segs_per_wave=8), dict(xcd_chunk=-1), dict(xcd_chunk=3),
+               dict(block_mode=2), dict(block_mode=1), dict(window_bytes=1_000_000), dict(window_bytes=7_777)]
+RAGGED_KNOBS = [dict(), dict(rows=4), dict(rows=16), dict(run_segs=1), dict(run_segs=17, blocks_per_cu=1),
+                dict(blocks_per_cu=8), dict(block_mode=2), dict(block_mode=1)]
 
 
 def _dev(a):
@@ -59,10 +47,10 @@ def test_fuzz_fixed(case):
         buf[:] = 0xFF
     part = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32) if case % 3 == 0 else None
     knobs = FIXED_KNOBS[case % len(FIXED_KNOBS)]
-    _apply(knobs)
     d = _dev(buf)[lead:]
     want = O.c_batch(buf[lead:], n, stride=stride, seg_len=seg_len, partial=part)
-    got = _u16(nsx.fixed_dev(d, stride, seg_len, n, partial=None if part is None else _dev(part.view(np.int32))))
+    got = _u16(nsx.fixed_dev(d, stride, seg_len, n, partial=None if part is None else _dev(part.view(np.int32)),
+                             tune=knobs))
     assert np.array_equal(got, want), (case, knobs, seg_len, stride, n, lead)
 
 
@@ -81,13 +69,12 @@ def test_fuzz_ragged(case):
     buf = rng.integers(0, 256, int(offs[-1]) + int(rng.integers(0, 5)), dtype=np.uint8)
     part = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32) if case % 2 else None
     knobs = RAGGED_KNOBS[case % len(RAGGED_KNOBS)]
-    _apply(knobs)
     want = O.c_batch(buf, n, offsets=offs, partial=part)
     d, o = _dev(buf), _dev(offs.view(np.int64))
     p = None if part is None else _dev(part.view(np.int32))
-    got = _u16(nsx.ragged_dev(d, o, partial=p))
+    got = _u16(nsx.ragged_dev(d, o, partial=p, tune=knobs))
     assert np.array_equal(got, want), (case, knobs, n, hi, lead)
-    okv = nsx.verify_ragged_dev(d, o, partial=p).cpu().numpy().astype(bool)
+    okv = nsx.verify_ragged_dev(d, o, partial=p, tune=knobs).cpu().numpy().astype(bool)
     assert np.array_equal(okv, want == 0xFFFF), (case, knobs)
 
 
@@ -102,8 +89,8 @@ def test_fuzz_ipv4_headers(case):
     ihl[rng.random(n) < 0.6] = 5
     ihl[::53] = rng.integers(0, 5, len(ihl[::53]))
     buf[hdr_off:n * stride:stride] = (0x40 | ihl).astype(np.uint8)
-    _apply(dict(kernel=int(rng.choice([0, 0, 1, 2, 3, 4]))))
-    got = _u16(nsx.ipv4_hdr_csum_dev(_dev(buf), stride, n, hdr_off=hdr_off, mode=0))
+    tune = dict(kernel=int(rng.choice([0, 0, nsx.KERNEL_HDR_THREAD, nsx.KERNEL_HDR_DENSE])))
+    got = _u16(nsx.ipv4_hdr_csum_dev(_dev(buf), stride, n, hdr_off=hdr_off, mode=0, tune=tune))
     for i in list(range(0, n, max(1, n // 500))) + [n - 1]:
         L = int(ihl[i]) * 4
         ok = L >= 20 and hdr_off + L <= stride
@@ -131,14 +118,15 @@ def test_fuzz_tcp_build(case):
               "offset": np.full(n, 5, np.uint8), "control": rng.integers(0, 256, n).astype(np.uint8),
               "window": rng.integers(0, 1 << 16, n).astype(np.uint16),
               "urgent_ptr": rng.integers(0, 1 << 16, n).astype(np.uint16)}
-    _apply(dict(kernel=int(rng.choice([0, 2, 3])), segs_per_wave=int(rng.choice([0, 1])),
-                blocks_per_cu=int(rng.choice([0, 1, 8]))))
+    tune = dict(kernel=int(rng.choice([0, nsx.KERNEL_BUILD_PLAIN, nsx.KERNEL_BUILD_GENERAL])),
+                blocks_per_cu=int(rng.choice([0, 1, 8])))
     want, wraw = O.c_go_tcp_build(fields, data, data_off, out_off, None)
     dt = {np.uint16: np.int16, np.uint32: np.int32, np.uint8: np.uint8}
     f = {k: _dev(v.view(dt[v.dtype.type])) for k, v in fields.items()}
     out = torch.full((int(out_off[-1]),), 0xAB, dtype=torch.uint8, device="cuda")
     raw = torch.empty(n, dtype=torch.int16, device="cuda")
-    nsx.tcp_build_dev(f, _dev(data), _dev(data_off.view(np.int64)), out, _dev(out_off.view(np.int64)), raw=raw)
+    nsx.tcp_build_dev(f, _dev(data), _dev(data_off.view(np.int64)), out, _dev(out_off.view(np.int64)), raw=raw,
+                      tune=tune)
     assert np.array_equal(_u16(raw), wraw), (case, n, P, lead)
     assert np.array_equal(out.cpu().numpy(), want), (case, n, P, lead)
 
@@ -197,8 +185,8 @@ def test_fuzz_tcp_build_options(case):
     data_off[1:] = np.cumsum([len(sg.data) for sg in segs])
     data_off += np.uint64(dlead)
     out_off = nsx.tcp_layout_host(data_off, opt_off)
-    _apply(dict(kernel=int(rng.choice([0, 2, 3])), segs_per_wave=int(rng.choice([0, 1])),
-                blocks_per_cu=int(rng.choice([0, 1, 8]))))
+    tune = dict(kernel=int(rng.choice([0, nsx.KERNEL_BUILD_PLAIN, nsx.KERNEL_BUILD_GENERAL])),
+                blocks_per_cu=int(rng.choice([0, 1, 8])))
     col = lambda k, dt: _dev(np.array([getattr(sg, k) for sg in segs], dt).view(
         {np.uint16: np.int16, np.uint32: np.int32, np.uint8: np.uint8}[dt]))
     f = {"src_port": col("src_port", np.uint16), "dst_port": col("dst_port", np.uint16),
@@ -210,7 +198,7 @@ def test_fuzz_tcp_build_options(case):
     out = torch.full((int(out_off[-1]),), 0xAB, dtype=torch.uint8, device="cuda")
     raw = torch.empty(n, dtype=torch.int16, device="cuda")
     nsx.tcp_build_dev(f, _dev(data), _dev(data_off.view(np.int64)), out, _dev(out_off.view(np.int64)),
-                      opts=_dev(optarr), opt_off=_dev(opt_off.view(np.int64)), partial=part, raw=raw)
+                      opts=_dev(optarr), opt_off=_dev(opt_off.view(np.int64)), partial=part, raw=raw, tune=tune)
     got = out.cpu().numpy()
     assert np.array_equal(_u16(raw), want_raw), (case, n, P)
     for i in range(n):

@@ -48,13 +48,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--launches", type=int, default=600)
-    ap.add_argument("--param", action="append", default=[])
+    ap.add_argument("--tune", action="append", default=[])
     a = ap.parse_args()
     torch.cuda.set_device(0)
-    for kv in a.param:
-        k, v = kv.split("=")
-        nsx.set_param(bench.PARAMS[k], int(v))
-    w = bench.build_workload(bench.WORKLOADS[a.config], 0, torch.device("cuda", 0))
+    w = bench.build_workload(bench.WORKLOADS[a.config], 0, torch.device("cuda", 0), bench.parse_tune(a.tune) or None)
     alg = w["alg"]
     for rep in range(2):
         d = per_launch(w, a.launches)
