@@ -833,10 +833,9 @@ __device__ __forceinline__ u32x4 staged_opts(const uint32_t (&od)[kOptDw], uint3
     return x;
 }
 
-// Compose, sum and store row r of the wire image; oc = the chunk's option bytes (opt_fin, 0 when none).
-template <int SP>
-__device__ __forceinline__ uint32_t build_row(const BuildSeg& S, __amdgpu_buffer_rsrc_t ors, u32x4 oc, uint32_t lane,
-                                              uint32_t r, u32x4 lo, uint32_t hi, uint32_t acc) {
+// Compose row r of the wire image (general composition); oc = the chunk's option bytes (opt_fin, 0 when none).
+__device__ __forceinline__ u32x4 compose_row(const BuildSeg& S, u32x4 oc, uint32_t lane, uint32_t r, u32x4 lo,
+                                             uint32_t hi) {
     const uint32_t pos0 = r * kRow + lane * 16u;
     u32x4 x = S.sh ? realign(lo, hi, S.sh) : lo;
     if (r * kRow < S.hdr_end || (r + 1) * kRow > S.wire)  // keep payload bytes [hdr_end, wire) only
@@ -849,6 +848,16 @@ __device__ __forceinline__ uint32_t build_row(const BuildSeg& S, __amdgpu_buffer
         x.w |= lane == 0 ? S.D3 : 0u;
     }
     x.x |= oc.x, x.y |= oc.y, x.z |= oc.z, x.w |= oc.w;  // option bytes [20, 20 + optlen)
+    return x;
+}
+
+// Images of more than 2 rows (unpipelined path): compose, sum and store row r as it goes; dword 4 (urgent
+// pointer + checksum field) is held back and written with the field once the sum is known.
+template <int SP>
+__device__ __forceinline__ uint32_t build_row(const BuildSeg& S, __amdgpu_buffer_rsrc_t ors, u32x4 oc, uint32_t lane,
+                                              uint32_t r, u32x4 lo, uint32_t hi, uint32_t acc) {
+    const uint32_t pos0 = r * kRow + lane * 16u;
+    const u32x4 x = compose_row(S, oc, lane, r, lo, hi);
     acc = sad4(x, acc);
     typedef uint32_t v4u __attribute__((ext_vector_type(4)));
     typedef uint32_t v3u __attribute__((ext_vector_type(3)));
@@ -940,11 +949,21 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
             drs = make_rsrc(data + dbase, data_end4 - dbase);
             ors = make_rsrc(out + readlane64(moo, k), S.nb4);
         };
+        // Raw sums are parked one per lane (lane k = segment g0 + k) and leave as one 2-byte store per lane
+        // when the group is done.
+        uint32_t raws = 0;
+        auto seg_raw = [&](uint32_t k, uint32_t acc) {
+            const uint32_t raw = finish(wave_sum(acc), true, __builtin_amdgcn_readlane(mpart, k));  // images 4-aligned
+            raws = lane == k ? raw : raws;
+            return raw;
+        };
         auto seg_done = [&](uint32_t k, const BuildSeg& S, __amdgpu_buffer_rsrc_t ors, uint32_t acc) {
-            const uint32_t tot = wave_sum(acc);
-            const uint32_t raw = finish(tot, true, __builtin_amdgcn_readlane(mpart, k));  // images are 4-aligned
+            const uint32_t raw = seg_raw(k, acc);
             __builtin_amdgcn_raw_buffer_store_b32(S.D4 | bswap16u(~raw & 0xFFFFu), ors, lane == 0 ? 16u : kOOB, 0, SP);
-            if (raw_out && lane == 0) raw_out[g0 + k] = (uint16_t)raw;
+        };
+        auto flush_raws = [&]() {
+            const __amdgpu_buffer_rsrc_t rrs = make_rsrc(raw_out + g0, raw_out ? (uint64_t)cnt * 2u : 0u);
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)raws, rrs, lane < cnt ? lane * 2u : kOOB, 0, 0);
         };
         // Every segment of the group on the fast path and at most 2 rows long (the bench layouts): software-
         // pipelined — segment k+1's two rows are loaded before segment k is built, so the wave keeps its loads
@@ -988,15 +1007,13 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
                     x.y = lane == 0 ? S.D1 : x.y;
                     x.z = lane == 0 ? S.D2 : x.z;
                     x.w = lane == 0 ? S.D3 : x.w;
-                    uint32_t acc = sad4(x, 0u);
-                    const bool d4 = lane == 1;  // dword 4 waits for the field
-                    __builtin_amdgcn_raw_buffer_store_b128(v4u{x.x, x.y, x.z, x.w}, ors, d4 ? kOOB : lane * 16u, 0,
-                                                           SP);
-                    __builtin_amdgcn_raw_buffer_store_b96(v3u{x.y, x.z, x.w}, ors, d4 ? 20u : kOOB, 0, SP);
                     const u32x4 y = F.v[e][1];  // row 1: zeros past the image (range check), stores clipped likewise
-                    acc = sad4(y, acc);
+                    const uint32_t raw = seg_raw(kk, fold32(sad4(y, sad4(x, 0u))));
+                    // both rows leave once the sum is known, one store each: dword 4 (lane 1's first) carries the
+                    // field (tcp.go:110, ^sum) — no separate partial-chunk or field stores
+                    x.x = lane == 1 ? S.D4 | bswap16u(~raw & 0xFFFFu) : x.x;
+                    __builtin_amdgcn_raw_buffer_store_b128(v4u{x.x, x.y, x.z, x.w}, ors, lane * 16u, 0, SP);
                     __builtin_amdgcn_raw_buffer_store_b128(v4u{y.x, y.y, y.z, y.w}, ors, kRow + lane * 16u, 0, SP);
-                    seg_done(kk, S, ors, fold32(acc));
                 }
             };
             Rows A, B;
@@ -1008,6 +1025,7 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
                 fload(kk + 2u * PS, A);
                 fdone(kk + PS, B);
             }
+            flush_raws();
             continue;
         }
         // Any payload alignment, any header length, images ≤ 2 rows, at least hdr_end bytes of the data array
@@ -1050,9 +1068,12 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
                     seg_at(kk, S, drs, ors);
                     u32x4 oc0{0u, 0u, 0u, 0u};
                     if (OPT && S.optlen) oc0 = staged_opts<false>(od, kk, (S.optlen + 3u) >> 2, lane, oc0);
-                    uint32_t acc = build_row<SP>(S, ors, oc0, lane, 0, G.lo[e][0], G.hi[e][0], 0u);
-                    if (S.rows > 1) acc = build_row<SP>(S, ors, u32x4{0u, 0u, 0u, 0u}, lane, 1, G.lo[e][1], G.hi[e][1], acc);
-                    seg_done(kk, S, ors, fold32(acc));
+                    u32x4 x = compose_row(S, oc0, lane, 0, G.lo[e][0], G.hi[e][0]);
+                    const u32x4 y = compose_row(S, u32x4{0u, 0u, 0u, 0u}, lane, 1, G.lo[e][1], G.hi[e][1]);
+                    const uint32_t raw = seg_raw(kk, fold32(sad4(y, sad4(x, 0u))));  // row 1 is 0 past the image
+                    x.x = lane == 1 ? S.D4 | bswap16u(~raw & 0xFFFFu) : x.x;  // the field, dword 4
+                    __builtin_amdgcn_raw_buffer_store_b128(v4u{x.x, x.y, x.z, x.w}, ors, lane * 16u, 0, SP);
+                    __builtin_amdgcn_raw_buffer_store_b128(v4u{y.x, y.y, y.z, y.w}, ors, kRow + lane * 16u, 0, SP);
                 }
             };
             GRows A, B;
@@ -1064,6 +1085,7 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
                 gload(kk + 2u * PS, A);
                 gdone(kk + PS, B);
             }
+            flush_raws();
             continue;
         }
         uint32_t k = 0;
@@ -1168,6 +1190,7 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
             seg_done(k, S, ors, acc);
             k += 1;
         }
+        flush_raws();
     }
 }
 
