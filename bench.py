@@ -84,6 +84,11 @@ WORKLOADS = {
     7: dict(kind="ipv4_hdr", n=1 << 26, hdr=20, seed=0x1075,
             metric="GiB/s IPv4 header checksum verify, header bytes",
             name="f3: 64M packed 20B IPv4 headers per GPU (header-split ring), verify, device-resident"),
+    # not a BASELINE config: the receive side of f2 + f3 fused into one pass over received datagrams
+    10: dict(kind="rx", n=1 << 20, lo=40, hi=1500, seed=0x1079,
+             metric="GiB/s fused receive verify (IPv4 header + pseudo-header + TCP checksum into a bitmask), frame bytes",
+             name="f2+f3 rx: 1M IPv4/TCP datagrams per GPU, 40-1500B (uniform), densely packed (odd starts), "
+                  "1 in 1000 corrupted, verified into a validity bitmask, device-resident"),
 }
 
 
@@ -94,7 +99,7 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", type=int, default=2, choices=sorted(WORKLOADS),
                     help="2-5: BASELINE configs (2 = headline); 6: f1 fused TCP build; 7: f3 IPv4 header verify; "
-                         "8: f1 with 12 B options; 9: f3 verify into a bitmask")
+                         "8: f1 with 12 B options; 9: f3 verify into a bitmask; 10: fused receive pass (f2+f3)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--settle-s", type=float, default=0.5, help="device clock settle time before warmup (setup)")
     ap.add_argument("--event-every", type=int, default=10,
@@ -266,7 +271,7 @@ def build_workload(cfg, rank, device, tune=None):
         out = torch.empty(n, dtype=torch.int16, device=device)
         # launches per step: the library's own count of its back-to-back windows (config 5: 16)
         w.update(buf=buf, out=out, bytes=n * L, alg=n * L + 2 * n, launches=nsx.fixed_launch_count(S, L, n, tune),
-                 step=lambda: nsx.fixed_dev(buf, S, L, n, out=out, tune=tune))
+                 step_for=lambda t: lambda: nsx.fixed_dev(buf, S, L, n, out=out, tune=t))
     elif cfg["kind"] == "tcp_build":
         n, P, OL = cfg["n"], cfg["payload"], cfg.get("opt", 0)
         W = P + 20 + OL  # OL ≡ 0 mod 4: tcp.go:118-121 pads nothing
@@ -300,8 +305,8 @@ def build_workload(cfg, rank, device, tune=None):
         w.update(out=raw, wire=out, fields=fields, addrs=addrs, data=data, opts=opts, opt_off=opt_off, part=part,
                  data_off=data_off, out_off=out_off, bytes=n * W,
                  alg=n * (P + OL + 18 + 8 + 8 + (8 if OL else 0) + 4 + W + 2) + 16 + (8 if OL else 0),
-                 step=lambda: nsx.tcp_build_dev(fields, data, data_off, out, out_off, opts=opts, opt_off=opt_off,
-                                                partial=part, raw=raw, tune=tune))
+                 step_for=lambda t: lambda: nsx.tcp_build_dev(fields, data, data_off, out, out_off, opts=opts,
+                                                              opt_off=opt_off, partial=part, raw=raw, tune=t))
     elif cfg["kind"] == "ipv4_hdr":
         n, H = cfg["n"], cfg["hdr"]
         buf = torch.empty(n * H, dtype=torch.uint8, device=device)
@@ -312,11 +317,17 @@ def build_workload(cfg, rank, device, tune=None):
             buf.view(n, H)[::1000, 8] ^= 1  # some invalid headers (TTL flipped after the fill)
             out = torch.empty((n + 63) // 64, dtype=torch.int64, device=device)
             w.update(buf=buf, out=out, bytes=n * H, alg=n * H + (n + 63) // 64 * 8,
-                     step=lambda: nsx.ipv4_hdr_verify_mask_dev(buf, H, n, mask=out, tune=tune))
+                     step_for=lambda t: lambda: nsx.ipv4_hdr_verify_mask_dev(buf, H, n, mask=out, tune=t))
         else:
             out = torch.empty(n, dtype=torch.int16, device=device)
             w.update(buf=buf, out=out, bytes=n * H, alg=n * (H + 2),
-                     step=lambda: nsx.ipv4_hdr_csum_dev(buf, H, n, mode=0, out=out, tune=tune))
+                     step_for=lambda t: lambda: nsx.ipv4_hdr_csum_dev(buf, H, n, mode=0, out=out, tune=t))
+    elif cfg["kind"] == "rx":
+        w.update(build_rx_frames(cfg, seed, device))
+        n, buf, d_offs, total = cfg["n"], w["buf"], w["d_offs"], w["bytes"]
+        out = torch.empty((n + 63) // 64, dtype=torch.int64, device=device)
+        w.update(out=out, alg=total + 8 * (n + 1) + (n + 63) // 64 * 8,
+                 step_for=lambda t: lambda: nsx.rx_ipv4_tcp_verify_dev(buf, d_offs, mask=out, tune=t))
     else:
         rng = np.random.default_rng(cfg["seed"])  # same lengths on every rank, bytes differ by seed
         n = cfg["n"]
@@ -329,7 +340,8 @@ def build_workload(cfg, rank, device, tune=None):
         d_offs = torch.from_numpy(offs.view(np.int64)).to(device)
         out = torch.empty(n, dtype=torch.int16, device=device)
         w.update(buf=buf, out=out, offsets=offs, bytes=total, alg=total + 2 * n + 8 * (n + 1),
-                 step=lambda: nsx.ragged_dev(buf, d_offs, out=out, tune=tune))
+                 step_for=lambda t: lambda: nsx.ragged_dev(buf, d_offs, out=out, tune=t))
+    w["step"] = w["step_for"](tune)  # one pass of the hot path; step_for(t) = the same with other overrides
     return w
 
 
@@ -364,6 +376,58 @@ def _run_for(fn, seconds: float):
         if time.perf_counter() - t0 >= seconds:
             break
     return reps, time.perf_counter() - t0
+
+
+def build_rx_frames(cfg, seed, device) -> dict:
+    """Workload 10's received datagrams, built on the device: frame lengths uniform on [lo, hi] (same on every
+    rank), densely packed; splitmix64 bytes, then per frame an IPv4 header (version 4, IHL 5, total length =
+    frame length, DF, protocol 6; the random bytes stay as id / TTL / addresses) and a TCP segment of the
+    rest. Both checksum fields are filled with this library's own ragged kernel over the 2n header /
+    segment spans (the TCP spans with their pseudo-header partials, RFC 9293 §3.1), then every 1000th frame
+    gets one bit flipped in its TCP header (setup; the parity test checks the outcome against the oracle)."""
+    import numpy as np
+    import torch
+    import nsx
+    n = cfg["n"]
+    rng = np.random.default_rng(cfg["seed"])
+    lens = rng.integers(cfg["lo"], cfg["hi"] + 1, n).astype(np.uint64)
+    offs = np.zeros(n + 1, np.uint64)
+    offs[1:] = np.cumsum(lens)
+    total = int(offs[-1])
+    buf = torch.empty(total, dtype=torch.uint8, device=device)
+    nsx.fill_splitmix64_dev(buf, seed)
+    d_offs = torch.from_numpy(offs.view(np.int64)).to(device)
+    st = d_offs[:-1]
+    ln = (d_offs[1:] - st)
+    put = lambda k, v: buf.index_put_((st + k,), v if torch.is_tensor(v) else torch.full_like(st, v, dtype=torch.uint8))
+    put(0, 0x45)
+    put(1, 0)
+    put(2, (ln >> 8).to(torch.uint8))
+    put(3, (ln & 0xFF).to(torch.uint8))
+    put(6, 0x40)
+    put(7, 0)
+    put(9, 6)
+    for k in (10, 11, 36, 37):  # checksum fields zero while the sums are taken
+        put(k, 0)
+    idx4 = torch.arange(4, device=device)
+    src = buf[(st[:, None] + 12 + idx4).reshape(-1)]
+    dst = buf[(st[:, None] + 16 + idx4).reshape(-1)]
+    tcp_len = (ln - 20).to(torch.int32)
+    pseudo = nsx.pseudo_ipv4_partial_dev(src, dst, tcp_len, 6)
+    spans = torch.stack([st, st + 20], 1).reshape(-1)
+    spans = torch.cat([spans, d_offs[-1:]])
+    part2 = torch.stack([torch.zeros_like(pseudo), pseudo], 1).reshape(-1)
+    raw2 = nsx.ragged_dev(buf, spans, partial=part2).to(torch.int32) & 0xFFFF
+    fld = (~raw2) & 0xFFFF
+    ip_f, tcp_f = fld[0::2], fld[1::2]
+    put(10, (ip_f >> 8).to(torch.uint8))
+    put(11, (ip_f & 0xFF).to(torch.uint8))
+    put(36, (tcp_f >> 8).to(torch.uint8))
+    put(37, (tcp_f & 0xFF).to(torch.uint8))
+    bad = st[::1000] + 30
+    buf[bad] ^= 1
+    torch.cuda.synchronize()
+    return {"buf": buf, "d_offs": d_offs, "offsets": offs, "bytes": total}
 
 
 def cpu_baseline(cfg, w, seconds: float) -> dict:
@@ -454,6 +518,22 @@ def cpu_baseline(cfg, w, seconds: float) -> dict:
         check["headers"] = (lambda: np.array_equal(
             np.packbits(raw[:whole] == 0xFFFF, bitorder="little").view(np.uint64), gpu)) if mask else (
             lambda: np.array_equal(raw, gpu))
+    elif cfg["kind"] == "rx":
+        offs_all = w["offsets"]
+        m = int(min(len(offs_all) - 1, np.searchsorted(offs_all, 256 << 20))) // 64 * 64  # ≤ 256 MiB, whole words
+        hi_b = int(offs_all[m])
+        sample = w["buf"][:hi_b].cpu().numpy()
+        offs = np.ascontiguousarray(offs_all[: m + 1])
+        gpu = w["out"][: m // 64].cpu().numpy().view(np.uint64)
+        cmask = np.zeros(m // 64, np.uint64)
+        bounds = [int(np.searchsorted(offs, hi_b * t // T)) // 64 * 64 for t in range(T)] + [m]  # byte-balanced
+
+        def go(lo, hi):
+            lib.oracle_go_rx_ipv4_tcp(_ptr(sample), _ptr(offs, lo), hi - lo, _ptr(cmask, lo // 64), None, None)
+        nbytes = hi_b
+        desc = (f"first {m} frames of rank 0's batch: per frame the reference's checksum loop over the IPv4 header "
+                "and over pseudo-header ‖ TCP segment (allocate + concatenate + serial loop) + bit packing")
+        check["mask"] = lambda: np.array_equal(cmask, gpu)
     else:
         offs_all = w["offsets"]
         m = int(min(len(offs_all) - 1, 50000))

@@ -173,6 +173,29 @@ int nsx_ipv4_hdr_csum_dev(void* d_base, uint64_t stride, uint32_t hdr_off, uint6
 int nsx_ipv4_hdr_verify_mask_dev(const void* d_base, uint64_t stride, uint32_t hdr_off, uint64_t n,
                                  uint64_t* d_mask, nsx_stream_t stream);
 
+/* Fused receive pass (SURVEY.md §8 f2 + f3 in one launch): n received IPv4
+ * datagrams carrying TCP, densely packed — frame i = d_base[d_offsets[i],
+ * d_offsets[i+1]), any alignment, d_offsets as for nsx_csum_ragged_dev. Bit
+ * (i % 64) of d_mask[i / 64] is set iff frame i
+ *   - is a well-formed, unfragmented IPv4 datagram carrying TCP: version 4,
+ *     IHL >= 5, IHL*4 <= frame length, total length (bytes 2-3) == frame
+ *     length, MF clear and fragment offset 0 (a fragment's TCP checksum covers
+ *     bytes it does not hold), protocol 6 (ip.NextProtoTCP,
+ *     network/ip/protocols.go:8), and a TCP segment (total − IHL*4 bytes) of at
+ *     least 20 bytes (tcp.go:131, minSegmentLength);
+ *   - has a valid header checksum: the raw sum over its IHL*4 header bytes is
+ *     0xFFFF (RFC 791 §3.1);
+ *   - has a valid TCP checksum: the raw sum over the pseudo-header built from
+ *     the header's own source and destination (ip.Addr.Raw(),
+ *     network/ip/v4/ipv4.go:15), 0, 6, TCP length ‖ the segment is 0xFFFF
+ *     (tcp.go:70 receiver rule over computeChecksum, tcp.go:72-95).
+ * Bits past n in the last word are 0; d_mask holds ceil(n/64) words.
+ * d_ip_raw (nullable): the header's raw sum (0 when IHL < 5 or IHL*4 exceeds the
+ * frame). d_tcp_raw (nullable): the raw sum over pseudo-header ‖ segment (0
+ * unless the frame is well-formed as above). One pass over the frame bytes. */
+int nsx_rx_ipv4_tcp_verify_dev(const void* d_base, const uint64_t* d_offsets, uint64_t n, uint64_t* d_mask,
+                               uint16_t* d_ip_raw, uint16_t* d_tcp_raw, nsx_stream_t stream);
+
 /* ----------------------------------------------------------------------------
  * Host-resident batches: pinned staging, H2D → kernel → D2H double-buffered
  * over two streams per GPU, segments sharded contiguously across num_gpus

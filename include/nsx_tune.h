@@ -30,8 +30,8 @@ typedef struct nsx_tune {
     int32_t blocks_per_cu;     /* persistent grid: 1..8 blocks of 256 threads per CU */
     int32_t segs_per_wave;     /* fixed batches of <= 4 KiB segments: segments per wave task (1, 2, 4, 8) */
     int32_t block_mode;        /* 0 auto (a block per segment when n < 4 * CUs), 1 never, 2 always */
-    int32_t rows;              /* ragged / frame scan kernels: 1 KiB rows per load batch (4, 8, 16) */
-    int32_t run_segs;          /* ragged scan kernel: segments per wave task (1..63) */
+    int32_t rows;              /* ragged scan / receive kernels: 1 KiB rows per load batch (4, 8, 16) */
+    int32_t run_segs;          /* segments per wave task: ragged scan kernel 1..63, TCP build 1..64 */
     int32_t xcd_chunk;         /* XCD deal: 0 auto, 1..20 = chunks of 2^k wave tasks, -1 contiguous eighths */
     int64_t window_bytes;      /* fixed <= 4 KiB segments: back-to-back launches of <= this many bytes;
                                   0 auto (batches >= 3.2 GB as ~1.6 GB windows), -1 one launch */
@@ -58,6 +58,9 @@ int nsx_ipv4_hdr_csum_dev_tuned(void* d_base, uint64_t stride, uint32_t hdr_off,
                                 uint16_t* d_out_raw, nsx_stream_t stream, const nsx_tune* tune);
 int nsx_ipv4_hdr_verify_mask_dev_tuned(const void* d_base, uint64_t stride, uint32_t hdr_off, uint64_t n,
                                        uint64_t* d_mask, nsx_stream_t stream, const nsx_tune* tune);
+int nsx_rx_ipv4_tcp_verify_dev_tuned(const void* d_base, const uint64_t* d_offsets, uint64_t n, uint64_t* d_mask,
+                                     uint16_t* d_ip_raw, uint16_t* d_tcp_raw, nsx_stream_t stream,
+                                     const nsx_tune* tune);
 int nsx_csum_fixed_host_tuned(const uint8_t* h_base, uint64_t stride, uint32_t seg_len, uint64_t n,
                               const uint32_t* h_prefix_partial, uint16_t* h_out, int num_gpus,
                               const nsx_tune* tune);

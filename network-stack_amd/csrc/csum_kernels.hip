@@ -587,6 +587,78 @@ __device__ __forceinline__ void seg_lower_bound2(__amdgpu_buffer_rsrc_t ofs, uin
         s[k] = lo[k] + (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(v[k] < t[k]));
 }
 
+// Stream the bytes [rbase + head, rbase + span) as 1 KiB rows of one wave (rbase 128-byte aligned, so a row
+// touches exactly 8 lines), R rows per load batch, and sample S (the weighted byte sum of the ragged scan
+// kernel, relative to rbase) at every lane's boundary brel (−1: none): bval = S(brel). A boundary at or past
+// the last row gets the total; carry = S(span) on return. Bytes before head and past span count as 0.
+template <int R>
+__device__ __forceinline__ void scan_span(const uint8_t* rbase, uint64_t span, uint32_t head, int64_t brel,
+                                          uint32_t lane, uint64_t& bval, uint64_t& carry) {
+    const uint64_t nrows = (span + kRow - 1) / kRow;
+    // Batch r0 = rows [r0, r0 + R), one descriptor based at its first row (rows past the run read 0).
+    auto issue = [&](uint64_t r0, u32x4 (&v)[R]) {
+        const uint8_t* bb = rbase + r0 * kRow;
+        const uint64_t rem = r0 < nrows ? span - r0 * kRow : 0;
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(bb, (rem + 3) & ~3ull);
+#pragma unroll
+        for (int j = 0; j < R; ++j) v[j] = bld16<true>(rs, j * kRow + lane * 16);
+    };
+    auto process = [&](uint64_t r0, u32x4 (&v)[R]) {
+#pragma unroll
+        for (int j = 0; j < R; ++j) asm volatile("" : "+v"(v[j]));
+        // Phase 1: edge masks (first/last row of the run only), lane half-sums
+        // and the R row scans as independent chains (ILP across rows).
+        uint32_t sl[R], incl[R];
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const uint64_t r = r0 + j;
+            const int64_t rowrel = (int64_t)(r * kRow);
+            if (r == 0 && head) {  // bytes before the run's first segment
+                const int32_t h = (int32_t)head - (int32_t)lane * 16;
+                v[j] = keep_bytes(v[j], min(max(h, 0), 16), 16);
+            }
+            if (r < nrows && rowrel + (int64_t)kRow > (int64_t)span) {  // bytes past the run's end
+                const int32_t e = (int32_t)((int64_t)span - rowrel) - (int32_t)lane * 16;
+                v[j] = keep_bytes(v[j], 0, min(max(e, 0), 16));
+            }
+            sl[j] = sad4(v[j], 0u);
+        }
+#pragma unroll
+        for (int j = 0; j < R; ++j) incl[j] = wave_incl_scan(sl[j]);
+        // Phase 2: boundaries that fall in this batch (rows past nrows hold zeros).
+        const int64_t qb = brel - (int64_t)(r0 * kRow);
+        const bool in_batch = qb >= 0 && qb < (int64_t)R * kRow;
+        if (__builtin_amdgcn_ballot_w64(in_batch)) {
+            uint64_t c = carry;
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                const int64_t q = qb - (int64_t)j * kRow;  // boundary position inside row j
+                const bool here = q >= 0 && q < (int64_t)kRow;
+                if (__builtin_amdgcn_ballot_w64(here)) {
+                    const uint32_t src = here ? (uint32_t)(q >> 4) : lane;
+                    const uint32_t pre = bperm(incl[j] - sl[j], src);
+                    u32x4 y;
+                    y.x = bperm(v[j].x, src);
+                    y.y = bperm(v[j].y, src);
+                    y.z = bperm(v[j].z, src);
+                    y.w = bperm(v[j].w, src);
+                    const uint32_t part = sad4(keep_bytes(y, 0, (int32_t)(q & 15)), 0u);
+                    if (here) bval = c + pre + part;
+                }
+                c += __builtin_amdgcn_readlane(incl[j], 63);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < R; ++j) carry += __builtin_amdgcn_readlane(incl[j], 63);
+    };
+    for (uint64_t r0 = 0; r0 < nrows; r0 += R) {
+        u32x4 v[R];
+        issue(r0, v);
+        process(r0, v);
+    }
+    if (brel >= (int64_t)(nrows * kRow)) bval = carry;  // boundary at the very end of the rows
+}
+
 template <int R, bool VERIFY>
 __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, uint32_t n,
@@ -631,73 +703,10 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
         const uint8_t* rbase = reinterpret_cast<const uint8_t*>(((uintptr_t)(base + lo)) & ~(uintptr_t)127);
         const uint64_t span = (uint64_t)((base + hi) - rbase);           // bytes from rbase to the run's end
         const uint32_t head = (uint32_t)((uintptr_t)(base + lo) & 127u);  // bytes before the run in row 0
-        const uint64_t nrows = (span + kRow - 1) / kRow;
         // Boundary lane state: its position relative to rbase, and S there.
         const int64_t brel = lane <= cnt ? (int64_t)((base + my_off) - rbase) : -1;
-        uint64_t bval = 0;
-        uint64_t carry = 0;  // S over all rows before the current one
-        // Batch r0 = rows [r0, r0 + R), one descriptor based at its first row (rows past the run read 0).
-        auto issue = [&](uint64_t r0, u32x4 (&v)[R]) {
-            const uint8_t* bb = rbase + r0 * kRow;
-            const uint64_t rem = r0 < nrows ? span - r0 * kRow : 0;
-            const __amdgpu_buffer_rsrc_t rs = make_rsrc(bb, (rem + 3) & ~3ull);
-#pragma unroll
-            for (int j = 0; j < R; ++j) v[j] = bld16<true>(rs, j * kRow + lane * 16);
-        };
-        auto process = [&](uint64_t r0, u32x4 (&v)[R]) {
-#pragma unroll
-            for (int j = 0; j < R; ++j) asm volatile("" : "+v"(v[j]));
-            // Phase 1: edge masks (first/last row of the run only), lane half-sums
-            // and the R row scans as independent chains (ILP across rows).
-            uint32_t sl[R], incl[R];
-#pragma unroll
-            for (int j = 0; j < R; ++j) {
-                const uint64_t r = r0 + j;
-                const int64_t rowrel = (int64_t)(r * kRow);
-                if (r == 0 && head) {  // bytes before the run's first segment
-                    const int32_t h = (int32_t)head - (int32_t)lane * 16;
-                    v[j] = keep_bytes(v[j], min(max(h, 0), 16), 16);
-                }
-                if (r < nrows && rowrel + (int64_t)kRow > (int64_t)span) {  // bytes past the run's end
-                    const int32_t e = (int32_t)((int64_t)span - rowrel) - (int32_t)lane * 16;
-                    v[j] = keep_bytes(v[j], 0, min(max(e, 0), 16));
-                }
-                sl[j] = sad4(v[j], 0u);
-            }
-#pragma unroll
-            for (int j = 0; j < R; ++j) incl[j] = wave_incl_scan(sl[j]);
-            // Phase 2: boundaries that fall in this batch (rows past nrows hold zeros).
-            const int64_t qb = brel - (int64_t)(r0 * kRow);
-            const bool in_batch = qb >= 0 && qb < (int64_t)R * kRow;
-            if (__builtin_amdgcn_ballot_w64(in_batch)) {
-                uint64_t c = carry;
-#pragma unroll
-                for (int j = 0; j < R; ++j) {
-                    const int64_t q = qb - (int64_t)j * kRow;  // boundary position inside row j
-                    const bool here = q >= 0 && q < (int64_t)kRow;
-                    if (__builtin_amdgcn_ballot_w64(here)) {
-                        const uint32_t src = here ? (uint32_t)(q >> 4) : lane;
-                        const uint32_t pre = bperm(incl[j] - sl[j], src);
-                        u32x4 y;
-                        y.x = bperm(v[j].x, src);
-                        y.y = bperm(v[j].y, src);
-                        y.z = bperm(v[j].z, src);
-                        y.w = bperm(v[j].w, src);
-                        const uint32_t part = sad4(keep_bytes(y, 0, (int32_t)(q & 15)), 0u);
-                        if (here) bval = c + pre + part;
-                    }
-                    c += __builtin_amdgcn_readlane(incl[j], 63);
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < R; ++j) carry += __builtin_amdgcn_readlane(incl[j], 63);
-        };
-        for (uint64_t r0 = 0; r0 < nrows; r0 += R) {
-            u32x4 v[R];
-            issue(r0, v);
-            process(r0, v);
-        }
-        if (brel >= (int64_t)(nrows * kRow)) bval = carry;  // boundary at the very end of the rows
+        uint64_t bval = 0, carry = 0;
+        scan_span<R>(rbase, span, head, brel, lane, bval, carry);
         // Segment `lane` = [boundary lane, boundary lane+1).
         const uint64_t nb = ((uint64_t)__shfl_down((unsigned long long)bval, 1));
         const uint64_t d = nb - bval;
@@ -712,6 +721,153 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Fused receive pass (SURVEY.md §8 f2 + f3 in one launch): a batch of received
+// IPv4 datagrams carrying TCP, densely packed (frame i = base[offsets[i],
+// offsets[i+1]), any alignment). Per frame: the IPv4 header checksum (RFC 791),
+// the TCP pseudo-header built from that header's own src/dst (ip.Addr.Raw(),
+// network/ip/v4/ipv4.go:15; protocol ip.NextProtoTCP = 6, network/ip/
+// protocols.go:8; TCP length = total length − IHL·4) and the TCP checksum over
+// pseudo ‖ segment with the receiver rule raw == 0xFFFF (tcp.go:70, :72-95),
+// into one validity bit per frame.
+//
+// The frames of a run stream exactly like the ragged scan kernel's segments
+// (scan_span: one pass over the bytes, S sampled at every frame start), so a
+// frame's weighted sum is F = S(end) − S(start). Each lane also loads its own
+// frame's first 20 header bytes (plus the option dwords when some lane has
+// IHL > 5): H = the header's weighted sum, computed in registers — those lines
+// are the run's own first bytes, read again from cache — and the TCP segment's
+// sum is F − H, exact. Runs are 64 frames aligned to 64, so each run's ballot is
+// one whole mask word.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t bswap16u(uint32_t v) { return ((v & 0xFFu) << 8) | ((v >> 8) & 0xFFu); }
+
+constexpr uint32_t kRxRun = 64;
+
+template <int R>
+__global__ __launch_bounds__(kBlock) void rx_ipv4_tcp_kernel(const uint8_t* __restrict__ base,
+                                                             const uint64_t* __restrict__ offsets, uint32_t n,
+                                                             uint64_t* __restrict__ mask,
+                                                             uint16_t* __restrict__ ip_raw,
+                                                             uint16_t* __restrict__ tcp_raw) {
+    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const __amdgpu_buffer_rsrc_t ofs = make_rsrc(offsets, ((uint64_t)n + 1) * 8);
+    const __amdgpu_buffer_rsrc_t mrs = make_rsrc(mask, (((uint64_t)n + 63) / 64) * 8);
+    const __amdgpu_buffer_rsrc_t irs = make_rsrc(ip_raw, ip_raw ? (uint64_t)n * 2 : 0);
+    const __amdgpu_buffer_rsrc_t trs = make_rsrc(tcp_raw, tcp_raw ? (uint64_t)n * 2 : 0);
+    // Byte-balanced wave ranges (as csum_ragged_scan_kernel), cut at multiples of 64 frames.
+    uint32_t a0, a_end;
+    {
+        const uint32_t nb = gridDim.x, b = blockIdx.x, W = nb * kWavesPerBlock;
+        const uint32_t g = (nb >= 16 && (nb & 7) == 0) ? ((b & 7) * (nb >> 3) + (b >> 3)) * kWavesPerBlock + wave
+                                                        : b * kWavesPerBlock + wave;
+        const uint64_t o_lo = ld_off(ofs, 0), o_hi = ld_off(ofs, n);
+        const uint64_t tot = o_hi - o_lo;
+        uint32_t s[2];
+        seg_lower_bound2(ofs, n, o_lo + tot * g / W, o_lo + tot * (g + 1) / W, lane, s);
+        a0 = g == 0 ? 0u : min((s[0] + 63u) & ~63u, n);
+        a_end = g + 1 == W ? n : min((s[1] + 63u) & ~63u, n);
+    }
+    auto load_off = [&](uint32_t i, bool live) -> uint64_t {
+        const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, live ? i * 8 : kOOB, 0, 0);
+        return ((uint64_t)x.y << 32) | x.x;
+    };
+    // lane l: offsets[a + l] and offsets[a + l + 1] of the next run, prefetched one run ahead
+    uint64_t nxt_off = load_off(a0 + lane, a0 < a_end && a0 + lane <= n);
+    uint64_t nxt_end = load_off(a0 + lane + 1, a0 < a_end && a0 + lane + 1 <= n);
+    for (uint32_t a = a0; a < a_end; a += kRxRun) {
+        const uint32_t cnt = min(kRxRun, a_end - a);
+        const uint64_t my_off = nxt_off, my_end = nxt_end;  // frame a + lane = [my_off, my_end) for lane < cnt
+        const uint32_t an = a + kRxRun;
+        nxt_off = load_off(an + lane, an < a_end && an + lane <= n);
+        nxt_end = load_off(an + lane + 1, an < a_end && an + lane + 1 <= n);
+        const bool live = lane < cnt;
+        const uint64_t lo = readlane64(my_off, 0), hi = readlane64(my_end, cnt - 1);
+        const uint8_t* fp = base + (live ? my_off : lo);
+        const uint32_t hd = (uint32_t)((uintptr_t)fp & 3u);
+        const uint8_t* rbase = reinterpret_cast<const uint8_t*>(((uintptr_t)(base + lo)) & ~(uintptr_t)127);
+        const uint64_t span = (uint64_t)((base + hi) - rbase);
+        const uint32_t head = (uint32_t)((uintptr_t)(base + lo) & 127u);
+        const int64_t brel = live ? (int64_t)((base + my_off) - rbase) : -1;
+        // Header window: the 4-aligned dwords from the frame start, 24 bytes (a 16 B and an 8 B load per lane)
+        // through one descriptor over the run (rbase is 128-aligned, so window offset = brel & ~3); dwords past
+        // the run read 0, bytes past the frame or the header are masked below. Issued ahead of the stream:
+        // nothing waits for them until the run's last header step. A run wider than a descriptor (2 GiB of
+        // frames — only possible behind frames longer than any IPv4 datagram) loads per lane instead.
+        uint32_t d[16];
+        const bool narrow = span < (1ull << 31);
+        const __amdgpu_buffer_rsrc_t hrs = make_rsrc(rbase, narrow ? ((span + 3) & ~3ull) : 0);
+        const uint32_t hwo = live && narrow ? (uint32_t)brel & ~3u : kOOB;
+        {
+            typedef uint32_t v2x __attribute__((ext_vector_type(2)));
+            const u32x4 q = bld16<false>(hrs, hwo);
+            const v2x r = __builtin_amdgcn_raw_buffer_load_b64(hrs, hwo == kOOB ? kOOB : hwo + 16u, 0, 0);
+            d[0] = q.x, d[1] = q.y, d[2] = q.z, d[3] = q.w, d[4] = r.x, d[5] = r.y;
+        }
+        const uint32_t* hw = reinterpret_cast<const uint32_t*>(fp - hd);
+        const uint32_t* last_dw = reinterpret_cast<const uint32_t*>((uintptr_t)(base + (hi > lo ? hi - 1 : lo)) & ~(uintptr_t)3);
+        if (!narrow && hi > lo) {  // clamped to the run's last readable dword: every lane loads unconditionally
+#pragma unroll
+            for (int k = 0; k < 6; ++k) d[k] = hw + k < last_dw ? hw[k] : *last_dw;
+        }
+        // The run's bytes, S sampled at every frame start.
+        uint64_t bval = 0, carry = 0;
+        scan_span<R>(rbase, span, head, brel, lane, bval, carry);
+        const uint64_t nbv = (uint64_t)__shfl_down((unsigned long long)bval, 1);
+        const uint64_t F = (lane == cnt - 1 ? carry : nbv) - bval;  // the frame's weighted sum (exact)
+        // IPv4 header fields (RFC 791 §3.1): header dword m = bytes 4m..4m+3, little-endian view.
+        const uint64_t flen = my_end - my_off;
+        const uint32_t H0 = __builtin_amdgcn_alignbyte(d[1], d[0], hd);
+        const uint32_t H1 = __builtin_amdgcn_alignbyte(d[2], d[1], hd);
+        const uint32_t H2 = __builtin_amdgcn_alignbyte(d[3], d[2], hd);
+        const uint32_t H3 = __builtin_amdgcn_alignbyte(d[4], d[3], hd);
+        const uint32_t H4 = __builtin_amdgcn_alignbyte(d[5], d[4], hd);
+        const uint32_t ihl = H0 & 15u, hlen = ihl * 4u;
+        const uint32_t total = bswap16u(H0 >> 16);
+        const uint32_t frag = bswap16u(H1 >> 16);        // flags + fragment offset
+        const uint32_t proto = (H2 >> 8) & 0xFFu;
+        const bool hdr_ok = live && flen >= 20u && ihl >= 5u && hlen <= flen;
+        const bool well = hdr_ok && (H0 & 0xF0u) == 0x40u && total == flen && (frag & 0x3FFFu) == 0u &&
+                          proto == 6u && total - hlen >= 20u;  // tcp.go:131: a segment is at least 20 bytes
+        // Header sum over window bytes [hd, hd + hlen): dwords 0..5 always, 6..15 when some lane has options.
+        uint32_t hs = 0;
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+            hs = __builtin_amdgcn_sad_u16(d[k] & keep_mask((int32_t)hd, (int32_t)(hd + hlen), 4 * k), 0u, hs);
+        if (__builtin_amdgcn_ballot_w64(hdr_ok && ihl > 5u)) {  // option dwords 6..15
+            if (narrow) {
+                typedef uint32_t v2x __attribute__((ext_vector_type(2)));
+                const uint32_t o = hwo == kOOB ? kOOB : hwo + 24u;
+                const u32x4 q0 = bld16<false>(hrs, o), q1 = bld16<false>(hrs, o == kOOB ? kOOB : o + 16u);
+                const v2x r = __builtin_amdgcn_raw_buffer_load_b64(hrs, o == kOOB ? kOOB : o + 32u, 0, 0);
+                d[6] = q0.x, d[7] = q0.y, d[8] = q0.z, d[9] = q0.w, d[10] = q1.x, d[11] = q1.y, d[12] = q1.z;
+                d[13] = q1.w, d[14] = r.x, d[15] = r.y;
+            } else {
+#pragma unroll
+                for (int k = 6; k < 16; ++k) d[k] = hw + k < last_dw ? hw[k] : *last_dw;
+            }
+#pragma unroll
+            for (int k = 6; k < 16; ++k)
+                hs = __builtin_amdgcn_sad_u16(d[k] & keep_mask((int32_t)hd, (int32_t)(hd + hlen), 4 * k), 0u, hs);
+        }
+        const bool even = ((uintptr_t)fp & 1u) == 0;  // frame start parity = TCP segment start parity (IHL·4 even)
+        const uint32_t ipr = hdr_ok ? finish(hs, even, 0u) : 0u;
+        const uint64_t T = F - (hdr_ok ? hs : 0u);     // the TCP segment's weighted sum
+        const uint32_t tle = fold32((uint32_t)T) + fold32((uint32_t)(T >> 32));
+        const uint32_t pseudo = bswap16u(H3 & 0xFFFFu) + bswap16u(H3 >> 16) + bswap16u(H4 & 0xFFFFu) +
+                                bswap16u(H4 >> 16) + 6u + ((total - hlen) & 0xFFFFu);
+        const uint32_t tcpr = well ? finish(tle, even, pseudo) : 0u;
+        const uint64_t bits = __builtin_amdgcn_ballot_w64(well && ipr == 0xFFFFu && tcpr == 0xFFFFu);
+        typedef uint32_t v2w __attribute__((ext_vector_type(2)));
+        __builtin_amdgcn_raw_buffer_store_b64(v2w{(uint32_t)bits, (uint32_t)(bits >> 32)}, mrs,
+                                              lane == 0 ? (a / 64u) * 8u : kOOB, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ipr, irs, live ? (a + lane) * 2u : kOOB, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)tcpr, trs, live ? (a + lane) * 2u : kOOB, 0, 0);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Fused sender path: segment.bytes() + computeChecksum +
 // field write in one pass (transport/tcp/tcp.go:98-128 and :68-71). Each wire
 // image — the 20-byte BE header built from SoA fields, options, the
@@ -720,7 +876,6 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
 // image are zero-filled) while its dwords are summed with the checksum field
 // at 0; ~raw then goes into bytes 16-17.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t bswap16u(uint32_t v) { return ((v & 0xFFu) << 8) | ((v >> 8) & 0xFFu); }
 __device__ __forceinline__ uint32_t bswap32u(uint32_t v) {
     return (v >> 24) | ((v >> 8) & 0xFF00u) | ((v << 8) & 0xFF0000u) | (v << 24);
 }
@@ -1790,6 +1945,31 @@ hipError_t launch_ragged(const LaunchCfg& c, const void* d_base, const uint64_t*
     return launch_ragged_scan<false>(c, base, d_offsets, n, partial, out, nullptr, st);
 }
 
+hipError_t launch_rx_ipv4_tcp(const LaunchCfg& c, const void* d_base, const uint64_t* d_offsets, uint64_t n,
+                              uint64_t* mask, uint16_t* ip_raw, uint16_t* tcp_raw, hipStream_t st) {
+    // 8 rows per batch, 3 blocks/CU (tools/ab.py --config 10: 0.135 ms against 0.157 at 2 blocks/CU and 0.144
+    // at 4; the plain ragged scan over the same frames 0.138); launches of ≤ 2^27 frames (a multiple of 64,
+    // so every launch starts on a mask word)
+    const int rows = (c.rows == 4 || c.rows == 8 || c.rows == 16) ? c.rows : 8;
+    const uint32_t mb = max_blocks_of(c, 3);
+    const uint8_t* base = static_cast<const uint8_t*>(d_base);
+    for (uint64_t c0 = 0; c0 < n; c0 += kRaggedChunk) {
+        const uint32_t cn = (uint32_t)(n - c0 < kRaggedChunk ? n - c0 : kRaggedChunk);
+        const uint32_t grid = grid_for((cn + kRxRun - 1) / kRxRun, mb);
+        uint16_t* ic = ip_raw ? ip_raw + c0 : nullptr;
+        uint16_t* tc = tcp_raw ? tcp_raw + c0 : nullptr;
+#define NSX_RX(R_)                                                                                                \
+        if (rows == R_)                                                                                            \
+            hipLaunchKernelGGL((rx_ipv4_tcp_kernel<R_>), dim3(grid), dim3(kBlock), 0, st, base, d_offsets + c0, cn,  \
+                               mask + c0 / 64, ic, tc);
+        NSX_RX(4) NSX_RX(8) NSX_RX(16)
+#undef NSX_RX
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
 hipError_t launch_pseudo_ipv4(const uint8_t* src, const uint8_t* dst, const uint32_t* len, uint8_t proto,
                               uint64_t n, uint32_t* partial, uint32_t max_blocks, hipStream_t st) {
     const uint64_t want = (n + kBlock - 1) / kBlock;
@@ -1827,7 +2007,8 @@ hipError_t launch_tcp_build(const LaunchCfg& c, const TcpHdrSoA& h, const uint8_
     // Group size: up to 64 segments per wave task, fewer when n would leave waves idle. 4 blocks/CU.
     const uint32_t max_blocks = max_blocks_of(c, 4);
     const uint64_t waves = (uint64_t)max_blocks * kWavesPerBlock;
-    const uint32_t group = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, (n + waves - 1) / waves));
+    uint32_t group = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, (n + waves - 1) / waves));
+    if (c.run_segs >= 1 && c.run_segs <= 64) group = (uint32_t)c.run_segs;
     const uint64_t tasks = (n + group - 1) / group;
     const uint32_t grid = grid_for(tasks, max_blocks);
     const uint32_t clog = deal_clog(c.xcd_chunk, tasks, (uint64_t)group * 3000u);  // ~payload + image per segment

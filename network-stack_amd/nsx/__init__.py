@@ -81,6 +81,8 @@ def lib() -> ctypes.CDLL:
             "nsx_fill_splitmix64_dev": [vp, u64, u64, u64, vp],
             "nsx_ipv4_hdr_csum_dev": [vp, u64, u32, u64, i32, vp, vp],
             "nsx_ipv4_hdr_verify_mask_dev": [vp, u64, u32, u64, vp, vp],
+            "nsx_rx_ipv4_tcp_verify_dev": [vp, vp, u64, vp, vp, vp, vp],
+            "nsx_rx_ipv4_tcp_verify_dev_tuned": [vp, vp, u64, vp, vp, vp, vp, vp],
             "nsx_tcp_build_dev": [vp, vp, vp, vp, vp, u64, vp, u64, vp, vp, vp, vp],
             "nsx_tcp_layout_host": [vp, vp, u64, vp],
             "nsx_abi_version": [],
@@ -294,6 +296,18 @@ def ipv4_hdr_verify_mask_dev(buf, stride: int, n: int, hdr_off: int = 0, mask=No
         mask = torch.empty((n + 63) // 64, dtype=torch.int64, device=buf.device)  # u64 bits
     _check(lib().nsx_ipv4_hdr_verify_mask_dev_tuned(_dev_ptr(buf), stride, hdr_off, n, _dev_ptr(mask),
                                                     _stream(stream), _tune(tune)), "nsx_ipv4_hdr_verify_mask_dev")
+    return mask
+
+
+def rx_ipv4_tcp_verify_dev(buf, offsets, mask=None, ip_raw=None, tcp_raw=None, stream=None, tune=None):
+    """Fused receive pass over packed IPv4/TCP frames: validity bitmask (+ optional raw sums)."""
+    import torch
+    n = offsets.numel() - 1
+    if mask is None:
+        mask = torch.empty((max(n, 0) + 63) // 64, dtype=torch.int64, device=offsets.device)  # u64 bits
+    _check(lib().nsx_rx_ipv4_tcp_verify_dev_tuned(_dev_ptr(buf), _dev_ptr(offsets), n, _dev_ptr(mask),
+                                                  _dev_ptr(ip_raw), _dev_ptr(tcp_raw), _stream(stream), _tune(tune)),
+           "nsx_rx_ipv4_tcp_verify_dev")
     return mask
 
 

@@ -322,6 +322,54 @@ ORACLE_EXPORT int oracle_go_tcp_build_batch_opts(const uint16_t* src_port, const
     return 0;
 }
 
+/* ---- fused receive check (SURVEY.md §8 f2 + f3), frame by frame ----
+ * Frame i = base[offsets[i], offsets[i+1]): an IPv4 datagram carrying TCP. The
+ * checks of nsx_rx_ipv4_tcp_verify_dev (include/nsx_csum.h), each sum through
+ * oracle_go_checksum (tcp.go:72-95: allocate, concatenate, serial loop):
+ *   ip_raw  = computeChecksum over the IHL*4 header bytes (RFC 791 §3.1), when
+ *             the frame holds >= 20 bytes, IHL >= 5 and IHL*4 <= its length; else 0;
+ *   tcp_raw = computeChecksum(pseudo) over the segment, pseudo = src(4) dst(4)
+ *             0 6 len(2) from the header's own addresses (ip.Addr.Raw(),
+ *             network/ip/v4/ipv4.go:15; ip.NextProtoTCP = 6, protocols.go:8),
+ *             when the frame is also version 4, total length == frame length,
+ *             unfragmented, protocol 6 and the segment >= 20 bytes (tcp.go:131);
+ *             else 0;
+ *   bit i   = both checks apply and both sums are 0xFFFF (tcp.go:70).
+ * mask holds ceil(n/64) words; ip_raw / tcp_raw nullable. */
+ORACLE_EXPORT void oracle_go_rx_ipv4_tcp(const uint8_t* base, const uint64_t* offsets, uint64_t n, uint64_t* mask,
+                                         uint16_t* ip_raw, uint16_t* tcp_raw) {
+    memset(mask, 0, (size_t)((n + 63) / 64) * 8);
+    for (uint64_t i = 0; i < n; i++) {
+        const uint8_t* p = base + offsets[i];
+        const uint64_t len = offsets[i + 1] - offsets[i];
+        uint32_t ipr = 0, tcpr = 0;
+        int valid = 0;
+        if (len >= 20) {
+            const uint32_t ihl = p[0] & 15u, hlen = ihl * 4u;
+            if (ihl >= 5 && hlen <= len) {
+                ipr = oracle_go_checksum(NULL, 0, p, hlen);
+                const uint32_t total = ((uint32_t)p[2] << 8) | p[3];
+                const uint32_t frag = (((uint32_t)p[6] << 8) | p[7]) & 0x3FFFu;
+                if ((p[0] >> 4) == 4 && total == len && frag == 0 && p[9] == 6 && total - hlen >= 20) {
+                    const uint32_t tlen = total - hlen;
+                    uint8_t pseudo[12];
+                    memcpy(pseudo, p + 12, 4);      /* src: ip.Addr.Raw() */
+                    memcpy(pseudo + 4, p + 16, 4);  /* dst */
+                    pseudo[8] = 0;
+                    pseudo[9] = 6;                  /* ip.NextProtoTCP */
+                    pseudo[10] = (uint8_t)(tlen >> 8);
+                    pseudo[11] = (uint8_t)tlen;
+                    tcpr = oracle_go_checksum(pseudo, 12, p + hlen, tlen);
+                    valid = ipr == 0xFFFFu && tcpr == 0xFFFFu;
+                }
+            }
+        }
+        if (ip_raw) ip_raw[i] = (uint16_t)ipr;
+        if (tcp_raw) tcp_raw[i] = (uint16_t)tcpr;
+        if (valid) mask[i / 64] |= 1ull << (i % 64);
+    }
+}
+
 /* ---- synthetic data: splitmix64 stream, counter-based ---- */
 static inline uint64_t splitmix64_at(uint64_t seed, uint64_t i) {
     uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;

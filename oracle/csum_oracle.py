@@ -215,6 +215,45 @@ def ipv6_pseudo_header(src: bytes, dst: bytes, next_header: int, length: int) ->
     return bytes(src) + bytes(dst) + (length & 0xFFFFFFFF).to_bytes(4, "big") + bytes(3) + bytes([next_header & 0xFF])
 
 
+def rx_ipv4_tcp(frame: bytes) -> tuple:
+    """One received frame through the fused receive check (nsx_rx_ipv4_tcp_verify_dev), pure Python:
+    (ip_raw, tcp_raw, valid). Every sum is go_checksum (tcp.go:72-95); the pseudo-header is built from the
+    frame's own addresses (ipv4.go:15 Raw) and ip.NextProtoTCP = 6 (protocols.go:8); a segment is at least
+    minSegmentLength = 20 bytes (tcp.go:131); the receiver accepts iff the sum is 0xFFFF (tcp.go:70)."""
+    f = bytes(frame)
+    if len(f) < 20:
+        return 0, 0, False
+    ihl = f[0] & 15
+    hlen = ihl * 4
+    if ihl < 5 or hlen > len(f):
+        return 0, 0, False
+    ipr = go_checksum(b"", f[:hlen])
+    total = int.from_bytes(f[2:4], "big")
+    frag = int.from_bytes(f[6:8], "big") & 0x3FFF
+    if f[0] >> 4 != 4 or total != len(f) or frag or f[9] != 6 or total - hlen < 20:
+        return ipr, 0, False
+    tcpr = go_checksum(ipv4_pseudo_header(f[12:16], f[16:20], 6, total - hlen), f[hlen:total])
+    return ipr, tcpr, ipr == 0xFFFF and tcpr == 0xFFFF
+
+
+def ipv4_tcp_frame(seg: bytes, src: bytes, dst: bytes, ident: int = 0, ttl: int = 64, options: bytes = b"",
+                   fix_tcp: bool = True) -> bytes:
+    """An IPv4 datagram carrying the TCP segment `seg` (RFC 791 header, IHL = 5 + len(options)/4, DF set,
+    protocol 6), with a valid header checksum and — when fix_tcp — the segment's checksum field (bytes 16-17)
+    set to ^computeChecksum(pseudo) over the segment with the field zeroed (tcp.go:68-71, :110)."""
+    assert len(options) % 4 == 0 and len(options) <= 40
+    seg = bytearray(seg)
+    if fix_tcp and len(seg) >= 18:
+        seg[16:18] = b"\0\0"
+        raw = go_checksum(ipv4_pseudo_header(src, dst, 6, len(seg)), bytes(seg))
+        seg[16:18] = field_value(raw).to_bytes(2, "big")
+    hlen = 20 + len(options)
+    h = bytearray([0x40 | (hlen // 4), 0]) + (hlen + len(seg)).to_bytes(2, "big") + ident.to_bytes(2, "big") + \
+        b"\x40\x00" + bytes([ttl, 6]) + b"\0\0" + bytes(src) + bytes(dst) + bytes(options)
+    h[10:12] = field_value(go_checksum(b"", bytes(h))).to_bytes(2, "big")
+    return bytes(h) + bytes(seg)
+
+
 # ---------------------------------------------------------------------------
 # C restatement (oracle/csum_oracle.c) via ctypes
 # ---------------------------------------------------------------------------
@@ -246,6 +285,7 @@ def c_oracle():
         lib.oracle_go_batch_fixed.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
                                               u8p, ctypes.c_size_t, u8p]
         lib.oracle_go_batch_ragged.argtypes = [u8p, u8p, ctypes.c_uint64, u8p, ctypes.c_size_t, u8p]
+        lib.oracle_go_rx_ipv4_tcp.argtypes = [u8p, u8p, ctypes.c_uint64, u8p, u8p, u8p]
         lib.oracle_splitmix64_fill.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]
         lib.oracle_go_tcp_build_batch.argtypes = [u8p] * 10 + [u8p, ctypes.c_size_t, ctypes.c_uint64, u8p, u8p, u8p]
         lib.oracle_go_tcp_build_batch.restype = ctypes.c_int
@@ -350,6 +390,18 @@ def c_batch(buf: np.ndarray, n: int, stride: int = 0, seg_len: int = 0, offsets:
         partial = np.ascontiguousarray(partial, dtype=np.uint32)
     c_oracle().oracle_batch_mt(_ptr(buf), stride, seg_len, _ptr(offsets), n, _ptr(partial), _ptr(out), threads)
     return out
+
+
+def c_rx_ipv4_tcp(buf: np.ndarray, offsets: np.ndarray):
+    """oracle_go_rx_ipv4_tcp over a packed frame batch: (mask u64[ceil(n/64)], ip_raw u16[n], tcp_raw u16[n])."""
+    buf = np.ascontiguousarray(buf, np.uint8)
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    n = offsets.size - 1
+    mask = np.zeros((n + 63) // 64, np.uint64)
+    ipr, tcpr = np.empty(n, np.uint16), np.empty(n, np.uint16)
+    c_oracle().oracle_go_rx_ipv4_tcp(_ptr(buf if buf.size else np.zeros(1, np.uint8)), _ptr(offsets), n, _ptr(mask),
+                                     _ptr(ipr), _ptr(tcpr))
+    return mask, ipr, tcpr
 
 
 def c_splitmix64(seed: int, nbytes: int, byte_off: int = 0) -> np.ndarray:

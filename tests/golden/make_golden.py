@@ -10,7 +10,9 @@ test (transport/tcp/tcp_test.go:26-32) and the RFC 1071 §3 example (kat.json).
 
 Run from the repo root:  python tests/golden/make_golden.py
 Outputs (small, committed): kat.json, vectors.json + vectors.bin,
-ragged.json + ragged.bin, segments.json.
+ragged.json + ragged.bin, segments.json, rx.json + rx.bin (received IPv4/TCP
+frames for the fused receive pass: expected bitmask and raw sums, written only if
+the Python and C restatements of the receive check agree).
 """
 from __future__ import annotations
 
@@ -156,6 +158,37 @@ def segments() -> list:
     return out
 
 
+def rx(rng):
+    """Received IPv4/TCP frames of every kind tests/_rx.py builds (valid, broken sums, malformed, fragments,
+    non-TCP, short), plus the RFC 791 example header as a frame of its own (a UDP datagram: header valid,
+    not TCP), packed behind an odd lead. Expected per-frame (ip_raw, tcp_raw, valid) from O.rx_ipv4_tcp,
+    checked against the C restatement."""
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE)))
+    import _rx
+    frames = []
+    for k in _rx.KINDS:
+        frames += [_rx.frame(rng, k, max_payload=300) for _ in range(12)]
+    rfc = bytes.fromhex("450000730000400040110000c0a80001c0a800c7")
+    rfc = rfc[:10] + O.field_value(O.go_checksum(b"", rfc)).to_bytes(2, "big") + rfc[12:]
+    frames.append(rfc + bytes(0x73 - 20))  # RFC 791-style header; total length 0x73 = the frame
+    order = rng.permutation(len(frames))
+    frames = [frames[i] for i in order]
+    lead = 3
+    offs = np.zeros(len(frames) + 1, np.uint64)
+    offs[1:] = np.cumsum([len(f) for f in frames])
+    offs += np.uint64(lead)
+    blob = bytes(range(lead)) + b"".join(frames)
+    res = [O.rx_ipv4_tcp(f) for f in frames]
+    mask, ipr, tcpr = O.c_rx_ipv4_tcp(np.frombuffer(blob, np.uint8), offs)
+    valid = np.array([v for _, _, v in res])
+    pad = np.zeros((len(frames) + 63) // 64 * 64, np.uint8)
+    pad[:len(frames)] = valid
+    assert np.array_equal(mask, np.packbits(pad, bitorder="little").view(np.uint64))
+    assert ipr.tolist() == [a for a, _, _ in res] and tcpr.tolist() == [b for _, b, _ in res]
+    return blob, {"offsets": [int(x) for x in offs], "ip_raw": ipr.tolist(), "tcp_raw": tcpr.tolist(),
+                  "valid": [bool(v) for v in valid], "mask": [int(x) for x in mask]}
+
+
 def main():
     rng = np.random.default_rng(0x1071)
     with open(os.path.join(HERE, "kat.json"), "w") as f:
@@ -172,7 +205,13 @@ def main():
         json.dump(rmeta, f)
     with open(os.path.join(HERE, "segments.json"), "w") as f:
         json.dump(segments(), f, indent=1)
-    print(f"vectors: {len(idx)} cases, {len(blob)} B; ragged: {len(rmeta['raw'])} segments, {len(rblob)} B")
+    xblob, xmeta = rx(np.random.default_rng(0x1078))
+    with open(os.path.join(HERE, "rx.bin"), "wb") as f:
+        f.write(xblob)
+    with open(os.path.join(HERE, "rx.json"), "w") as f:
+        json.dump(xmeta, f)
+    print(f"vectors: {len(idx)} cases, {len(blob)} B; ragged: {len(rmeta['raw'])} segments, {len(rblob)} B; "
+          f"rx: {len(xmeta['valid'])} frames ({sum(xmeta['valid'])} valid), {len(xblob)} B")
 
 
 if __name__ == "__main__":

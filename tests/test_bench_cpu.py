@@ -103,3 +103,18 @@ def test_result_line_per_launch_with_windows():
     assert line["roofline"]["alg_bytes_per_launch"] == 1600
     assert line["roofline"]["launches_per_step"] == 16
     assert abs(line["kernel_ms_mean"] - 0.2) < 1e-9
+
+
+def test_cpu_baseline_rx_frames():
+    """Workload 10's CPU leg: the Go-faithful per-frame receive check on every host core, byte-balanced in
+    whole 64-frame mask words, against a known-correct mask standing in for the GPU's."""
+    import _rx
+    rng = np.random.default_rng(0x10)
+    buf, offs, _ = _rx.batch(rng, 64 * 40 + 17, lead=0, max_payload=600)
+    mask, _, _ = O.c_rx_ipv4_tcp(buf, offs)
+    cfg = dict(kind="rx", n=offs.size - 1, seed=1)
+    w = {"buf": torch.from_numpy(buf), "out": torch.from_numpy(mask.view(np.int64)), "offsets": offs}
+    res = bench.cpu_baseline(cfg, w, 0.2)
+    assert res["sample_parity_vs_gpu"] and res["value"] > 0
+    w["out"][3] ^= 1 << 5
+    assert not bench.cpu_baseline(cfg, w, 0.05)["sample_parity_vs_gpu"]

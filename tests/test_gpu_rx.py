@@ -1,0 +1,110 @@
+"""GPU parity of the fused receive pass (nsx_rx_ipv4_tcp_verify_dev, SURVEY.md §8 f2 + f3 in one launch):
+validity bitmask and both raw sums per frame against the oracle (oracle_go_rx_ipv4_tcp: every sum through
+the reference's computeChecksum loop, tcp.go:72-95; pseudo-header from the frame's own addresses,
+ipv4.go:15, protocol 6, protocols.go:8; receiver rule tcp.go:70) — the committed golden frames, every kind
+of valid / broken / malformed frame at every start alignment and batch size around the 64-frame mask
+words, every launch shape, maximum-size datagrams, and the bench's workload 10 at full size."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import _rx
+from _gpu import dev, host, setup_gpu, torch, u16
+from conftest import GOLDEN
+from oracle import csum_oracle as O
+
+import nsx  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu():
+    setup_gpu()
+
+
+def run_rx(buf, offs, tune=None):
+    n = offs.size - 1
+    mask = torch.full(((n + 63) // 64,), 0x5A5A5A5A5A5A5A5A, dtype=torch.int64, device="cuda")  # garbage before
+    ipr = torch.empty(n, dtype=torch.int16, device="cuda")
+    tcpr = torch.empty(n, dtype=torch.int16, device="cuda")
+    nsx.rx_ipv4_tcp_verify_dev(dev(buf), dev(offs.view(np.int64)), mask=mask, ip_raw=ipr, tcp_raw=tcpr, tune=tune)
+    return host(mask).view(np.uint64), u16(ipr), u16(tcpr)
+
+
+def test_rx_golden_frames():
+    meta = json.load(open(os.path.join(GOLDEN, "rx.json")))
+    blob = np.fromfile(os.path.join(GOLDEN, "rx.bin"), np.uint8)
+    mask, ipr, tcpr = run_rx(blob, np.array(meta["offsets"], np.uint64))
+    assert mask.tolist() == meta["mask"]
+    assert ipr.tolist() == meta["ip_raw"] and tcpr.tolist() == meta["tcp_raw"]
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 127, 128, 129, 1000, 4099])
+@pytest.mark.parametrize("lead", [0, 1, 2, 3])
+def test_rx_mixed_batches(n, lead):
+    rng = np.random.default_rng(n * 4 + lead)
+    buf, offs, kinds = _rx.batch(rng, n, lead=lead, max_payload=1460)
+    want = O.c_rx_ipv4_tcp(buf, offs)
+    got = run_rx(buf, offs)
+    for w, g, what in zip(want, got, ("mask", "ip_raw", "tcp_raw")):
+        assert np.array_equal(w, g), (what, n, lead)
+
+
+TUNES = [dict(rows=4), dict(rows=16), dict(blocks_per_cu=1), dict(blocks_per_cu=8), dict(rows=16, blocks_per_cu=1)]
+
+
+@pytest.mark.parametrize("tune", TUNES, ids=lambda t: ",".join(f"{k}={v}" for k, v in t.items()))
+def test_rx_launch_shapes(tune):
+    rng = np.random.default_rng(0x7E)
+    buf, offs, _ = _rx.batch(rng, 20_000, lead=1, max_payload=1460)
+    want = O.c_rx_ipv4_tcp(buf, offs)
+    got = run_rx(buf, offs, tune)
+    for w, g in zip(want, got):
+        assert np.array_equal(w, g), tune
+
+
+def test_rx_mostly_valid_large_frames_and_junk():
+    """Maximum-size datagrams (total length 65535 − header), jumbo-ish frames, runs of empty frames, and a
+    4 MB junk frame (not IPv4, longer than any datagram) in the middle: its neighbours still verify."""
+    rng = np.random.default_rng(0x7F)
+    frames = []
+    for i in range(700):
+        r = i % 7
+        if r == 0:
+            seg_len = 65535 - 20 - 20 * (i % 3)
+            frames.append(O.ipv4_tcp_frame(_rx._segment(rng, seg_len - 20), rng.bytes(4), rng.bytes(4)))
+        elif r == 1:
+            frames.append(b"")
+        else:
+            frames.append(_rx.frame(rng, "valid", max_payload=9000))
+    frames.insert(350, rng.integers(0, 256, 4 << 20, dtype=np.uint8).tobytes())
+    offs = np.zeros(len(frames) + 1, np.uint64)
+    offs[1:] = np.cumsum([len(f) for f in frames])
+    buf = np.frombuffer(b"".join(frames) + bytes(3), np.uint8)
+    want = O.c_rx_ipv4_tcp(buf, offs)
+    got = run_rx(buf, offs)
+    for w, g in zip(want, got):
+        assert np.array_equal(w, g)
+    bits = np.unpackbits(want[0].view(np.uint8), bitorder="little")
+    assert bits[:len(frames)].sum() == sum(1 for i, f in enumerate(frames) if len(f) and i != 350)
+
+
+def test_rx_bench_workload_full_size():
+    """The bench's workload 10 at full size (1M frames of 40-1500 B, 1 in 1000 corrupted after the fill):
+    the device mask equals the oracle's on every frame, and exactly the corrupted frames fail."""
+    import bench
+    cfg = bench.WORKLOADS[10]
+    w = bench.build_workload(cfg, 0, torch.device("cuda", 0))
+    w["step"]()
+    got = host(w["out"]).view(np.uint64)
+    want, _, _ = O.c_rx_ipv4_tcp(host(w["buf"]), w["offsets"])
+    assert np.array_equal(got, want)
+    n = cfg["n"]
+    valid = np.ones(n, bool)
+    valid[::1000] = False
+    pad = np.zeros((n + 63) // 64 * 64, np.uint8)
+    pad[:n] = valid
+    assert np.array_equal(got, np.packbits(pad, bitorder="little").view(np.uint64))

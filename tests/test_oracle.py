@@ -242,3 +242,54 @@ def test_cpu_fast_line_matches_go_checksum():
         for i in range(n):
             seg = buf[1 + i * (L + 3):1 + i * (L + 3) + L].tobytes()
             assert out[i] == O.c_go_checksum(b"", seg), (L, i)
+
+
+# --- fused receive check (SURVEY.md §8 f2 + f3): Python vs C restatement, fixtures, per-kind rules ---
+
+def test_rx_golden_fixture_both_restatements():
+    meta = load("rx.json")
+    blob = np.fromfile(os.path.join(GOLDEN, "rx.bin"), np.uint8)
+    offs = np.array(meta["offsets"], np.uint64)
+    mask, ipr, tcpr = O.c_rx_ipv4_tcp(blob, offs)
+    assert mask.tolist() == meta["mask"] and ipr.tolist() == meta["ip_raw"] and tcpr.tolist() == meta["tcp_raw"]
+    for i in range(offs.size - 1):
+        f = blob[int(offs[i]):int(offs[i + 1])].tobytes()
+        assert O.rx_ipv4_tcp(f) == (meta["ip_raw"][i], meta["tcp_raw"][i], meta["valid"][i]), i
+    assert 0 < sum(meta["valid"]) < len(meta["valid"])
+
+
+def test_rx_rules_per_kind():
+    """Every kind of frame tests/_rx.py builds lands on the side of the check it should: the valid kinds
+    pass (and their TCP segments re-verify through computeChecksum with the pseudo-header, tcp.go:70), every
+    broken or malformed kind fails, with the raw sums zeroed exactly where the rules say."""
+    import _rx
+    rng = np.random.default_rng(0x78)
+    for kind in _rx.KINDS:
+        for _ in range(20):
+            f = _rx.frame(rng, kind, max_payload=200)
+            ipr, tcpr, ok = O.rx_ipv4_tcp(f)
+            assert ok == (kind in ("valid", "valid_options", "header_only", "odd_payload")), (kind, f.hex())
+            if kind in ("short", "empty", "ihl_lt5", "ihl_past_end"):
+                assert ipr == 0 and tcpr == 0, kind
+            if kind in ("udp", "fragment_mf", "fragment_off", "version6", "total_mismatch", "tcp_lt20"):
+                assert tcpr == 0 and (kind == "total_mismatch" or ipr == 0xFFFF), kind
+
+
+def test_rx_rfc791_header_is_not_tcp():
+    h = bytearray.fromhex("45000073000040004011b861c0a80001c0a800c7")  # RFC 791 §3.1 example: UDP
+    f = bytes(h) + bytes(0x73 - 20)
+    assert O.rx_ipv4_tcp(f) == (0xFFFF, 0, False)
+    h[9] = 6  # as TCP the header sum breaks
+    assert O.rx_ipv4_tcp(bytes(h) + bytes(0x73 - 20))[2] is False
+
+
+def test_rx_c_matches_python_random_batches():
+    import _rx
+    rng = np.random.default_rng(0x79)
+    for lead in (0, 1, 2, 3):
+        buf, offs, kinds = _rx.batch(rng, 300, lead=lead, max_payload=400)
+        mask, ipr, tcpr = O.c_rx_ipv4_tcp(buf, offs)
+        bits = np.unpackbits(mask.view(np.uint8), bitorder="little")[:300]
+        for i in range(300):
+            a, b, v = O.rx_ipv4_tcp(buf[int(offs[i]):int(offs[i + 1])].tobytes())
+            assert (ipr[i], tcpr[i], bool(bits[i])) == (a, b, v), (i, kinds[i])

@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Same-process A/B of launch overrides (include/nsx_tune.h) on one bench workload.
+
+    python tools/ab.py --config 6 --variants "def:;b3:blocks_per_cu=3;b8:blocks_per_cu=8" [--rounds 7]
+
+For config 10 (fused receive pass), a variant named scan* runs the plain ragged
+checksum (nsx_csum_ragged_dev) over the same frames instead: the receive pass's
+own cost against the one-pass checksum it is built on.
+
+Builds the workload once (bench.build_workload), settles the clocks, then runs
+the variants in interleaved rounds (each round: every variant, `--launches`
+back-to-back launches bracketed by HIP events on the launch stream) and prints
+the median per-launch time and roofline fraction per variant. Box-to-box and
+allocation effects cancel because every variant sees the same buffers in the
+same process.
+"""
+import argparse
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "network-stack_amd")]
+
+
+def main():
+    import bench
+    import torch
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--variants", required=True, help="name:field=v,field=v;name2:...")
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--launches", type=int, default=50)
+    a = ap.parse_args()
+    torch.cuda.set_device(0)
+    cfg = bench.WORKLOADS[a.config]
+    w = bench.build_workload(cfg, 0, torch.device("cuda", 0))
+    variants = []
+    for item in a.variants.split(";"):
+        name, _, kv = item.partition(":")
+        tune = bench.parse_tune([x for x in kv.split(",") if x]) or None
+        step = w["step_for"](tune)
+        if cfg["kind"] == "rx" and name.startswith("scan"):
+            import nsx
+            rout = torch.empty(cfg["n"], dtype=torch.int16, device="cuda")
+            step = (lambda t: lambda: nsx.ragged_dev(w["buf"], w["d_offs"], out=rout, tune=t))(tune)
+        variants.append((name, step, __import__("nsx").fixed_launch_count(
+            cfg["stride"], cfg["seg_len"], cfg["n"], tune) if cfg["kind"] == "fixed" else 1))
+    t_end = time.perf_counter() + 1.0
+    while time.perf_counter() < t_end:  # settle
+        for _, step, _ in variants:
+            step()
+        torch.cuda.synchronize()
+    res = {name: [] for name, _, _ in variants}
+    for r in range(a.rounds):
+        for name, step, launches in variants:
+            for _ in range(3):
+                step()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.launches):
+                step()
+            e1.record()
+            torch.cuda.synchronize()
+            res[name].append(e0.elapsed_time(e1) / a.launches / launches)
+    base = None
+    for name, _, launches in variants:
+        med = statistics.median(res[name])
+        frac = w["alg"] / launches / (med * 1e-3) / 1e9 / bench.HBM_PEAK_GBPS
+        base = base or med
+        print(f"AB config{a.config} {name:16s} median {med:.5f} ms/launch  frac {frac:.4f}  vs first {med / base:.4f}  "
+              f"min {min(res[name]):.5f} max {max(res[name]):.5f}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
