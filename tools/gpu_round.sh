@@ -4,7 +4,7 @@
 # tools/gpu_profiles.sh. Every GPU step has its own limit; a timeout/crash
 # (rc >= 124) ends the script.
 set -u
-tag=${1:-r01}
+tag=${1:-r02}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 SKIP_TESTS=${SKIP_TESTS:-0}
@@ -17,8 +17,10 @@ step() {  # step <name> <timeout> cmd...
   if [ $rc -ge 124 ]; then echo "fatal rc=$rc, stopping"; exit $rc; fi
   return 0
 }
-nproc > gpurun_out/host.txt; lscpu | grep -E "Model name|^CPU\(s\)|Thread|Core|Socket" >> gpurun_out/host.txt
-[ "$SKIP_TESTS" = 1 ] || step pytest_gpu 900 python -m pytest tests -q -m gpu
+{ nproc; python3 -c "import os; print('affinity', len(os.sched_getaffinity(0)), 'cpu_count', os.cpu_count())";
+  cat /sys/fs/cgroup/cpu.max 2>/dev/null; echo "OMP_NUM_THREADS=${OMP_NUM_THREADS:-}";
+  lscpu | grep -E "Model name|^CPU\(s\)|Thread|Core|Socket"; } > gpurun_out/host.txt 2>&1
+[ "$SKIP_TESTS" = 1 ] || step pytest_gpu 900 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench_c2 300 python bench.py
 step bench_c3 300 python bench.py --config 3 --cpu-seconds 5
@@ -28,6 +30,7 @@ step bench_c6 300 python bench.py --config 6 --steps 100 --cpu-seconds 5
 step bench_c7 300 python bench.py --config 7 --steps 100 --cpu-seconds 5
 step bench_c8 300 python bench.py --config 8 --steps 100 --cpu-seconds 5
 step bench_c9 300 python bench.py --config 9 --steps 100 --cpu-seconds 5
+step bench_c10 300 python bench.py --config 10 --steps 100 --cpu-seconds 5
 step e2e_host 600 python tools/e2e_host.py
 rm -f gpurun_out/loopback.jsonl
 for m in host batch ring-host ring-gpu; do

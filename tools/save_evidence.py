@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def main(tag):
     src, dst = os.path.join(ROOT, "gpurun_out"), os.path.join(ROOT, "profiles")
-    for c in range(2, 10):
+    for c in range(2, 11):
         p = os.path.join(src, f"bench_c{c}.log")
         if not os.path.exists(p):
             continue
@@ -35,4 +35,4 @@ def main(tag):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
+    main(sys.argv[1] if len(sys.argv) > 1 else "r02")
