@@ -591,7 +591,8 @@ __device__ __forceinline__ void seg_lower_bound2(__amdgpu_buffer_rsrc_t ofs, uin
 // touches exactly 8 lines), R rows per load batch, and sample S (the weighted byte sum of the ragged scan
 // kernel, relative to rbase) at every lane's boundary brel (−1: none): bval = S(brel). A boundary at or past
 // the last row gets the total; carry = S(span) on return. Bytes before head and past span count as 0.
-template <int R>
+// PIPE: two register sets — batch r0 + R loads while batch r0 is scanned.
+template <int R, bool PIPE = false>
 __device__ __forceinline__ void scan_span(const uint8_t* rbase, uint64_t span, uint32_t head, int64_t brel,
                                           uint32_t lane, uint64_t& bval, uint64_t& carry) {
     const uint64_t nrows = (span + kRow - 1) / kRow;
@@ -651,10 +652,22 @@ __device__ __forceinline__ void scan_span(const uint8_t* rbase, uint64_t span, u
 #pragma unroll
         for (int j = 0; j < R; ++j) carry += __builtin_amdgcn_readlane(incl[j], 63);
     };
-    for (uint64_t r0 = 0; r0 < nrows; r0 += R) {
-        u32x4 v[R];
-        issue(r0, v);
-        process(r0, v);
+    if constexpr (PIPE) {
+        u32x4 A[R], B[R];
+        issue(0, A);
+        for (uint64_t r0 = 0; r0 < nrows; r0 += 2 * R) {
+            issue(r0 + R, B);  // past the rows: an empty descriptor, the loads move nothing
+            process(r0, A);
+            if (r0 + R >= nrows) break;
+            issue(r0 + 2 * R, A);
+            process(r0 + R, B);
+        }
+    } else {
+        for (uint64_t r0 = 0; r0 < nrows; r0 += R) {
+            u32x4 v[R];
+            issue(r0, v);
+            process(r0, v);
+        }
     }
     if (brel >= (int64_t)(nrows * kRow)) bval = carry;  // boundary at the very end of the rows
 }
@@ -732,7 +745,11 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
 //
 // The frames of a run stream exactly like the ragged scan kernel's segments
 // (scan_span: one pass over the bytes, S sampled at every frame start), so a
-// frame's weighted sum is F = S(end) − S(start). Each lane also loads its own
+// frame's weighted sum is F = S(end) − S(start) — with double-buffered row
+// batches (scan_span<R, true>): frames of a few hundred bytes put a boundary in
+// nearly every row, and the extra scan work per row needs the next batch
+// already in flight (a pipelined ragged scan over config 3's 4.5 KB segments
+// measured 3.7% slower). Each lane also loads its own
 // frame's first 20 header bytes (plus the option dwords when some lane has
 // IHL > 5): H = the header's weighted sum, computed in registers — those lines
 // are the run's own first bytes, read again from cache — and the TCP segment's
@@ -813,7 +830,7 @@ __global__ __launch_bounds__(kBlock) void rx_ipv4_tcp_kernel(const uint8_t* __re
         }
         // The run's bytes, S sampled at every frame start.
         uint64_t bval = 0, carry = 0;
-        scan_span<R>(rbase, span, head, brel, lane, bval, carry);
+        scan_span<R, true>(rbase, span, head, brel, lane, bval, carry);
         const uint64_t nbv = (uint64_t)__shfl_down((unsigned long long)bval, 1);
         const uint64_t F = (lane == cnt - 1 ? carry : nbv) - bval;  // the frame's weighted sum (exact)
         // IPv4 header fields (RFC 791 §3.1): header dword m = bytes 4m..4m+3, little-endian view.
@@ -1947,10 +1964,10 @@ hipError_t launch_ragged(const LaunchCfg& c, const void* d_base, const uint64_t*
 
 hipError_t launch_rx_ipv4_tcp(const LaunchCfg& c, const void* d_base, const uint64_t* d_offsets, uint64_t n,
                               uint64_t* mask, uint16_t* ip_raw, uint16_t* tcp_raw, hipStream_t st) {
-    // 8 rows per batch, 3 blocks/CU (tools/ab.py --config 10: 0.135 ms against 0.157 at 2 blocks/CU and 0.144
-    // at 4; the plain ragged scan over the same frames 0.138); launches of ≤ 2^27 frames (a multiple of 64,
-    // so every launch starts on a mask word)
-    const int rows = (c.rows == 4 || c.rows == 8 || c.rows == 16) ? c.rows : 8;
+    // Double-buffered batches of 4 rows, 3 blocks/CU (tools/ab.py --config 10, same process: 0.1305 ms against
+    // 0.1348 for single batches of 8 rows, 0.157 at 2 blocks/CU, 0.144 at 4; the plain ragged scan over the
+    // same frames 0.138); launches of ≤ 2^27 frames (a multiple of 64, so every launch starts on a mask word)
+    const int rows = (c.rows == 4 || c.rows == 8 || c.rows == 16) ? c.rows : 4;
     const uint32_t mb = max_blocks_of(c, 3);
     const uint8_t* base = static_cast<const uint8_t*>(d_base);
     for (uint64_t c0 = 0; c0 < n; c0 += kRaggedChunk) {
