@@ -2021,10 +2021,13 @@ hipError_t launch_tcp_build(const LaunchCfg& c, const TcpHdrSoA& h, const uint8_
     // Path by layout: groups of ≤ 2-row images software-pipelined (the fast composition when every segment of
     // the group allows it, else the general one); longer images unpipelined. kernel 2 forces the unpipelined
     // path, kernel 3 the general pipelined composition (test coverage of those paths on every layout).
-    // Group size: up to 64 segments per wave task, fewer when n would leave waves idle. 4 blocks/CU.
-    const uint32_t max_blocks = max_blocks_of(c, 4);
+    // Group size: up to 16 segments per wave task (fewer when n would leave waves idle) at 2 blocks/CU — the
+    // chip's waves then hold a compact window of the batch (2048 × 16 segments in flight instead of 4096 × 64):
+    // same process, three boxes, workloads 6 / 8: 0.602 / 0.609 ms against 0.633 / 0.640 for 64-segment groups
+    // at 4 blocks/CU (tools/ab.py).
+    const uint32_t max_blocks = max_blocks_of(c, 2);
     const uint64_t waves = (uint64_t)max_blocks * kWavesPerBlock;
-    uint32_t group = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, (n + waves - 1) / waves));
+    uint32_t group = (uint32_t)std::min<uint64_t>(16, std::max<uint64_t>(1, (n + waves - 1) / waves));
     if (c.run_segs >= 1 && c.run_segs <= 64) group = (uint32_t)c.run_segs;
     const uint64_t tasks = (n + group - 1) / group;
     const uint32_t grid = grid_for(tasks, max_blocks);
