@@ -209,6 +209,12 @@ int nsx_csum_fixed_host(const uint8_t* h_base, uint64_t stride, uint32_t seg_len
 int nsx_csum_ragged_host(const uint8_t* h_base, const uint64_t* h_offsets, uint64_t n,
                          const uint32_t* h_prefix_partial, uint16_t* h_out, int num_gpus);
 
+/* The fused receive pass (nsx_rx_ipv4_tcp_verify_dev) over host-resident
+ * datagrams: h_mask receives ceil(n/64) words. Shards and chunks start on
+ * 64-frame mask words. */
+int nsx_rx_ipv4_tcp_verify_host(const uint8_t* h_base, const uint64_t* h_offsets, uint64_t n, uint64_t* h_mask,
+                                int num_gpus);
+
 /* The host batch calls keep per-device streams and grow-only device/pinned
  * staging buffers across calls (a transport calls them once per batch). This
  * frees the cached buffers; the next call re-allocates. Safe to call at any

@@ -67,6 +67,8 @@ int nsx_csum_fixed_host_tuned(const uint8_t* h_base, uint64_t stride, uint32_t s
 int nsx_csum_ragged_host_tuned(const uint8_t* h_base, const uint64_t* h_offsets, uint64_t n,
                                const uint32_t* h_prefix_partial, uint16_t* h_out, int num_gpus,
                                const nsx_tune* tune);
+int nsx_rx_ipv4_tcp_verify_host_tuned(const uint8_t* h_base, const uint64_t* h_offsets, uint64_t n, uint64_t* h_mask,
+                                      int num_gpus, const nsx_tune* tune);
 
 /* Kernel launches one nsx_csum_fixed_dev(_tuned) call makes for this batch on the current device (its
  * back-to-back windows; 1 for most batches), for per-launch timing in benchmarks. */

@@ -108,7 +108,8 @@ struct Job {
     const uint64_t* h_offsets;  // null → fixed stride; else absolute offsets into h_base
     uint64_t lo, hi;            // segment index range of the shard
     const uint32_t* h_partial;
-    uint16_t* h_out;
+    uint16_t* h_out;            // checksum mode: one raw sum per segment
+    uint64_t* h_mask;           // receive mode (nsx_rx_ipv4_tcp_verify_host): one validity bit per frame
     int dev;
     int slot;  // shard slot on the device (its own DevCtx: streams + staging)
     const nsx_tune* tune;
@@ -117,7 +118,16 @@ struct Job {
 
 std::vector<Chunk> plan_chunks(const Job& j) {
     std::vector<Chunk> v;
-    if (!j.h_offsets) {
+    if (j.h_mask) {  // receive mode: chunks of whole 64-frame mask words (the shard starts on one)
+        uint64_t c0 = j.lo;
+        while (c0 < j.hi) {
+            uint64_t c1 = c0 + 1;
+            while (c1 < j.hi && j.h_offsets[c1 + 1] - j.h_offsets[c0] <= kChunkBytes) ++c1;
+            if (c1 < j.hi) c1 = std::min(j.hi, c0 + std::max<uint64_t>(64, (c1 - c0) / 64 * 64));
+            v.push_back({c0, c1, j.h_offsets[c0], j.h_offsets[c1]});
+            c0 = c1;
+        }
+    } else if (!j.h_offsets) {
         const uint64_t span = std::max<uint64_t>(std::max<uint64_t>(j.stride, j.seg_len), 1);
         const uint64_t per = std::max<uint64_t>(1, kChunkBytes / span);
         for (uint64_t c0 = j.lo; c0 < j.hi; c0 += per) {
@@ -202,8 +212,14 @@ void run_job(Job* j) {
         max_span = std::max(max_span, c.byte_hi - c.byte_lo);
         max_segs = std::max(max_segs, c.c1 - c.c0);
     }
+    const bool rx = j->h_mask != nullptr;
+    // results of chunk segments [c0, c1): raw sums, or mask words (receive mode; c0 is a multiple of 64)
+    auto out_bytes = [rx](uint64_t cn) { return rx ? (cn + 63) / 64 * 8 : cn * sizeof(uint16_t); };
+    auto out_host = [j, rx](uint64_t c0) {
+        return rx ? reinterpret_cast<uint8_t*>(j->h_mask + c0 / 64) : reinterpret_cast<uint8_t*>(j->h_out + c0);
+    };
     const bool in_pinned = is_pinned(j->h_base);
-    const bool out_pinned = is_pinned(j->h_out);
+    const bool out_pinned = is_pinned(out_host(j->lo));
     const bool ragged = j->h_offsets != nullptr;
     const int nslots = chunks.size() > 1 ? 2 : 1;
     DevCtx* ctx = dev_ctx(j->dev, j->slot);
@@ -221,7 +237,7 @@ void run_job(Job* j) {
     for (int s = 0; s < nslots; ++s) {
         if (!st[s]) NSX_TRY(hipStreamCreateWithFlags(&st[s], hipStreamNonBlocking));
         NSX_TRY(ctx->d_data[s].ensure(std::max<uint64_t>(max_span, 16)));
-        NSX_TRY(ctx->d_out[s].ensure(max_segs * sizeof(uint16_t)));
+        NSX_TRY(ctx->d_out[s].ensure(std::max<uint64_t>(out_bytes(max_segs), 8)));
         if (j->h_partial) {
             NSX_TRY(ctx->d_part[s].ensure(max_segs * sizeof(uint32_t)));
             NSX_TRY(ctx->h_pstage[s].ensure(max_segs * sizeof(uint32_t)));
@@ -231,7 +247,7 @@ void run_job(Job* j) {
             NSX_TRY(ctx->h_offstage[s].ensure((max_segs + 1) * sizeof(uint64_t)));
         }
         if (!in_pinned) NSX_TRY(ctx->h_stage[s].ensure(std::max<uint64_t>(max_span, 16)));
-        if (!out_pinned) NSX_TRY(ctx->h_ostage[s].ensure(max_segs * sizeof(uint16_t)));
+        if (!out_pinned) NSX_TRY(ctx->h_ostage[s].ensure(std::max<uint64_t>(out_bytes(max_segs), 8)));
     }
 
     for (size_t k = 0; k < chunks.size(); ++k) {
@@ -241,11 +257,11 @@ void run_job(Job* j) {
         uint8_t* d_data = ctx->d_data[s].as<uint8_t>();
         uint16_t* d_out = ctx->d_out[s].as<uint16_t>();
         uint32_t* d_part = j->h_partial ? ctx->d_part[s].as<uint32_t>() : nullptr;
-        uint16_t* h_ostage = ctx->h_ostage[s].as<uint16_t>();
+        uint8_t* h_ostage = ctx->h_ostage[s].as<uint8_t>();
         if (pending[s]) {  // slot reuse: finish chunk k-2
             NSX_TRY(hipStreamSynchronize(st[s]));
             if (!out_pinned)
-                std::memcpy(j->h_out + pending[s]->c0, h_ostage, (pending[s]->c1 - pending[s]->c0) * sizeof(uint16_t));
+                std::memcpy(out_host(pending[s]->c0), h_ostage, out_bytes(pending[s]->c1 - pending[s]->c0));
             pending[s] = nullptr;
         }
         const uint8_t* src = j->h_base + c.byte_lo;
@@ -259,26 +275,27 @@ void run_job(Job* j) {
             std::memcpy(h_pstage, j->h_partial + c.c0, cn * sizeof(uint32_t));
             NSX_TRY(hipMemcpyAsync(d_part, h_pstage, cn * sizeof(uint32_t), hipMemcpyHostToDevice, st[s]));
         }
-        uint16_t* out_dst = out_pinned ? j->h_out + c.c0 : h_ostage;
+        uint8_t* out_dst = out_pinned ? out_host(c.c0) : h_ostage;
         hipError_t e;
         if (ragged) {
             uint64_t* h_offstage = ctx->h_offstage[s].as<uint64_t>();
             uint64_t* d_off = ctx->d_off[s].as<uint64_t>();
             for (uint64_t i = 0; i <= cn; ++i) h_offstage[i] = j->h_offsets[c.c0 + i] - c.byte_lo;
             NSX_TRY(hipMemcpyAsync(d_off, h_offstage, (cn + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st[s]));
-            e = nsx::launch_ragged(cfg, d_data, d_off, cn, d_part, d_out, nullptr, st[s]);
+            e = rx ? nsx::launch_rx_ipv4_tcp(cfg, d_data, d_off, cn, reinterpret_cast<uint64_t*>(d_out), nullptr,
+                                             nullptr, st[s])
+                   : nsx::launch_ragged(cfg, d_data, d_off, cn, d_part, d_out, nullptr, st[s]);
         } else {
             e = nsx::launch_fixed(cfg, d_data, j->stride, j->seg_len, cn, d_part, d_out, st[s]);
         }
         NSX_TRY(e);
-        NSX_TRY(hipMemcpyAsync(out_dst, d_out, cn * sizeof(uint16_t), hipMemcpyDeviceToHost, st[s]));
+        NSX_TRY(hipMemcpyAsync(out_dst, d_out, out_bytes(cn), hipMemcpyDeviceToHost, st[s]));
         pending[s] = &c;
     }
     for (int s = 0; s < nslots; ++s) {
         NSX_TRY(hipStreamSynchronize(st[s]));
         if (pending[s] && !out_pinned)
-            std::memcpy(j->h_out + pending[s]->c0, ctx->h_ostage[s].p,
-                        (pending[s]->c1 - pending[s]->c0) * sizeof(uint16_t));
+            std::memcpy(out_host(pending[s]->c0), ctx->h_ostage[s].p, out_bytes(pending[s]->c1 - pending[s]->c0));
         pending[s] = nullptr;
     }
 
@@ -292,7 +309,7 @@ done:
 // Shards: num_gpus × shards_per_device contiguous ranges (byte-balanced for ragged batches); shard g runs on
 // device g / shards_per_device in slot g % shards_per_device, one host thread per shard.
 int run_sharded(const uint8_t* h_base, uint64_t stride, uint32_t seg_len, const uint64_t* h_offsets, uint64_t n,
-                const uint32_t* h_partial, uint16_t* h_out, int num_gpus, const nsx_tune* tune) {
+                const uint32_t* h_partial, uint16_t* h_out, uint64_t* h_mask, int num_gpus, const nsx_tune* tune) {
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess) {
         (void)hipGetLastError();
@@ -311,10 +328,12 @@ int run_sharded(const uint8_t* h_base, uint64_t stride, uint32_t seg_len, const 
     const int parts = (int)std::min<uint64_t>((uint64_t)num_gpus * spd, n);
     std::vector<uint64_t> bounds(parts + 1);
     nsx::shard_plan(h_offsets, n, parts, bounds.data());
+    if (h_mask)  // receive mode: every shard starts on a 64-frame mask word
+        for (int g = 1; g < parts; ++g) bounds[g] = std::min<uint64_t>(n, (bounds[g] + 63) / 64 * 64);
     std::vector<Job> jobs(parts);
     for (int g = 0; g < parts; ++g)
-        jobs[g] = Job{h_base, stride, seg_len, h_offsets, bounds[g], bounds[g + 1], h_partial, h_out, g / spd, g % spd,
-                      tune, NSX_OK};
+        jobs[g] = Job{h_base, stride, seg_len, h_offsets, bounds[g], bounds[g + 1], h_partial, h_out, h_mask, g / spd,
+                      g % spd, tune, NSX_OK};
     std::vector<std::thread> th;
     for (int g = 1; g < parts; ++g)
         if (jobs[g].hi > jobs[g].lo) th.emplace_back(run_job, &jobs[g]);
@@ -340,7 +359,7 @@ int nsx_csum_fixed_host_tuned(const uint8_t* h_base, uint64_t stride, uint32_t s
                               const nsx_tune* tune) {
     if (n == 0) return NSX_OK;
     if (!h_out || (seg_len && !h_base)) return NSX_EINVAL;
-    return run_sharded(h_base, stride, seg_len, nullptr, n, h_prefix_partial, h_out, num_gpus, tune);
+    return run_sharded(h_base, stride, seg_len, nullptr, n, h_prefix_partial, h_out, nullptr, num_gpus, tune);
 }
 
 int nsx_csum_ragged_host(const uint8_t* h_base, const uint64_t* h_offsets, uint64_t n,
@@ -355,7 +374,21 @@ int nsx_csum_ragged_host_tuned(const uint8_t* h_base, const uint64_t* h_offsets,
     if (!h_out || !h_offsets || !h_base) return NSX_EINVAL;
     for (uint64_t i = 0; i < n; ++i)
         if (h_offsets[i + 1] < h_offsets[i]) return NSX_EINVAL;
-    return run_sharded(h_base, 0, 0, h_offsets, n, h_prefix_partial, h_out, num_gpus, tune);
+    return run_sharded(h_base, 0, 0, h_offsets, n, h_prefix_partial, h_out, nullptr, num_gpus, tune);
+}
+
+int nsx_rx_ipv4_tcp_verify_host(const uint8_t* h_base, const uint64_t* h_offsets, uint64_t n, uint64_t* h_mask,
+                                int num_gpus) {
+    return nsx_rx_ipv4_tcp_verify_host_tuned(h_base, h_offsets, n, h_mask, num_gpus, nullptr);
+}
+
+int nsx_rx_ipv4_tcp_verify_host_tuned(const uint8_t* h_base, const uint64_t* h_offsets, uint64_t n, uint64_t* h_mask,
+                                      int num_gpus, const nsx_tune* tune) {
+    if (n == 0) return NSX_OK;
+    if (!h_mask || !h_offsets || !h_base) return NSX_EINVAL;
+    for (uint64_t i = 0; i < n; ++i)
+        if (h_offsets[i + 1] < h_offsets[i]) return NSX_EINVAL;
+    return run_sharded(h_base, 0, 0, h_offsets, n, nullptr, nullptr, h_mask, num_gpus, tune);
 }
 
 int nsx_host_cache_release(void) {

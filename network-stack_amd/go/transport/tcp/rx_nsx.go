@@ -1,0 +1,55 @@
+//go:build nsx
+
+// Receive-side batch verification over the MI355X library: received IPv4
+// datagrams carrying TCP are packed into pinned staging and checked in one
+// GPU pass (nsx_rx_ipv4_tcp_verify_host): the IPv4 header checksum, the
+// pseudo-header built from the header's own addresses (ip.Addr.Raw(),
+// network/ip/v4/ipv4.go:15; ip.NextProtoTCP, network/ip/protocols.go:8), and
+// computeChecksum(pseudo) == 0xFFFF over the segment (tcp.go:70, :72-95).
+package tcp
+
+/*
+#include "nsx_csum.h"
+*/
+import "C"
+
+import (
+	"fmt"
+	"unsafe"
+)
+
+// VerifyDatagrams reports, per received datagram, whether it is a well-formed
+// unfragmented IPv4 datagram carrying a TCP segment of at least
+// minSegmentLength bytes (tcp.go:131) whose header and TCP checksums both
+// verify. numGPUs 0 = all visible GPUs.
+func VerifyDatagrams(frames [][]byte, numGPUs int) ([]bool, error) {
+	total := 0
+	for _, f := range frames {
+		total += len(f)
+	}
+	b, err := NewPinnedBatch(total + 1)
+	if err != nil {
+		return nil, err
+	}
+	defer b.Free()
+	for _, f := range frames {
+		if err := b.Append(f); err != nil {
+			return nil, err
+		}
+	}
+	n := len(frames)
+	ok := make([]bool, n)
+	if n == 0 {
+		return ok, nil
+	}
+	mask := make([]uint64, (n+63)/64)
+	rc := C.nsx_rx_ipv4_tcp_verify_host((*C.uint8_t)(b.base), (*C.uint64_t)(unsafe.Pointer(&b.offsets[0])),
+		C.uint64_t(n), (*C.uint64_t)(unsafe.Pointer(&mask[0])), C.int(numGPUs))
+	if rc != C.NSX_OK {
+		return nil, fmt.Errorf("nsx_rx_ipv4_tcp_verify_host: %s", C.GoString(C.nsx_strerror(rc)))
+	}
+	for i := range ok {
+		ok[i] = mask[i/64]>>(uint(i)%64)&1 == 1
+	}
+	return ok, nil
+}

@@ -83,6 +83,8 @@ def lib() -> ctypes.CDLL:
             "nsx_ipv4_hdr_verify_mask_dev": [vp, u64, u32, u64, vp, vp],
             "nsx_rx_ipv4_tcp_verify_dev": [vp, vp, u64, vp, vp, vp, vp],
             "nsx_rx_ipv4_tcp_verify_dev_tuned": [vp, vp, u64, vp, vp, vp, vp, vp],
+            "nsx_rx_ipv4_tcp_verify_host": [vp, vp, u64, vp, i32],
+            "nsx_rx_ipv4_tcp_verify_host_tuned": [vp, vp, u64, vp, i32, vp],
             "nsx_tcp_build_dev": [vp, vp, vp, vp, vp, u64, vp, u64, vp, vp, vp, vp],
             "nsx_tcp_layout_host": [vp, vp, u64, vp],
             "nsx_abi_version": [],
@@ -193,6 +195,17 @@ def ragged_host(buf: np.ndarray, offsets: np.ndarray, partial: np.ndarray | None
     _check(lib().nsx_csum_ragged_host_tuned(_np_ptr(buf), _np_ptr(offsets), n, _np_ptr(part), _np_ptr(out), num_gpus,
                                             _tune(tune)), "nsx_csum_ragged_host")
     return out
+
+
+def rx_ipv4_tcp_verify_host(buf: np.ndarray, offsets: np.ndarray, num_gpus: int = 0, tune=None) -> np.ndarray:
+    """Fused receive pass over host-resident datagrams: the validity bitmask (uint64[ceil(n/64)])."""
+    buf = np.ascontiguousarray(buf, np.uint8)
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    n = offsets.size - 1
+    mask = np.zeros((max(n, 0) + 63) // 64, np.uint64)
+    _check(lib().nsx_rx_ipv4_tcp_verify_host_tuned(_np_ptr(buf), _np_ptr(offsets), n, _np_ptr(mask), num_gpus,
+                                                   _tune(tune)), "nsx_rx_ipv4_tcp_verify_host")
+    return mask
 
 
 class PinnedBuffer:

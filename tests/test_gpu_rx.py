@@ -108,3 +108,21 @@ def test_rx_bench_workload_full_size():
     pad = np.zeros((n + 63) // 64 * 64, np.uint8)
     pad[:n] = valid
     assert np.array_equal(got, np.packbits(pad, bitorder="little").view(np.uint64))
+
+
+@pytest.mark.parametrize("shards", [1, 2, 3, 8])
+def test_rx_host_batches_sharded(shards):
+    """nsx_rx_ipv4_tcp_verify_host: the receive pass from host memory (pinned staging, H2D → kernel → D2H of
+    mask words), the batch split into `shards` shards on the one device and into 64 MiB chunks, every shard and
+    chunk starting on a 64-frame mask word; ~200 MB of frames (a tiled mixed batch), pageable input."""
+    rng = np.random.default_rng(0x80 + shards)
+    buf0, offs0, _ = _rx.batch(rng, 4999, lead=0, max_payload=1460)
+    reps = 40
+    span = int(offs0[-1])
+    buf = np.concatenate([buf0[:span]] * reps + [np.zeros(3, np.uint8)])
+    offs = np.concatenate([offs0[:-1] + np.uint64(k * span) for k in range(reps)] + [np.array([reps * span], np.uint64)])
+    want, _, _ = O.c_rx_ipv4_tcp(buf, offs)
+    got = nsx.rx_ipv4_tcp_verify_host(buf, offs, tune=dict(shards_per_device=shards))
+    assert np.array_equal(got, want), shards
+    small = nsx.rx_ipv4_tcp_verify_host(buf0, offs0, tune=dict(shards_per_device=shards))
+    assert np.array_equal(small, O.c_rx_ipv4_tcp(buf0, offs0)[0])
