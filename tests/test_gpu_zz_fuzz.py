@@ -205,3 +205,26 @@ def test_fuzz_tcp_build_options(case):
         o = int(out_off[i])
         assert got[o:o + len(want[i])].tobytes() == want[i], (case, i)
         assert not got[o + len(want[i]):int(out_off[i + 1])].any(), (case, i)
+
+
+@pytest.mark.parametrize("case", range(40 * SCALE))
+def test_fuzz_rx(case):
+    """Random received-datagram batches (every frame kind of tests/_rx.py in random proportions, random start
+    alignment, sizes from tiny to a few thousand frames, random launch shape) through the fused receive pass,
+    device and host entry points, against oracle_go_rx_ipv4_tcp."""
+    import _rx
+    rng = np.random.default_rng(6000 + case)
+    n = int(rng.choice([int(rng.integers(1, 70)), int(rng.integers(60, 700)), int(rng.integers(500, 3000))]))
+    w = rng.random(len(_rx.KINDS)) ** 3
+    buf, offs, _ = _rx.batch(rng, n, weights=w / w.sum(), lead=int(rng.integers(0, 8)),
+                             max_payload=int(rng.choice([64, 600, 1460, 9000])))
+    want_m, want_i, want_t = O.c_rx_ipv4_tcp(buf, offs)
+    tune = dict(rows=int(rng.choice([0, 4, 8, 16])), blocks_per_cu=int(rng.choice([0, 1, 2, 8])))
+    mask = torch.empty((n + 63) // 64, dtype=torch.int64, device="cuda")
+    ipr, tcpr = torch.empty(n, dtype=torch.int16, device="cuda"), torch.empty(n, dtype=torch.int16, device="cuda")
+    nsx.rx_ipv4_tcp_verify_dev(_dev(buf), _dev(offs.view(np.int64)), mask=mask, ip_raw=ipr, tcp_raw=tcpr, tune=tune)
+    assert np.array_equal(mask.cpu().numpy().view(np.uint64), want_m), (case, n, tune)
+    assert np.array_equal(_u16(ipr), want_i) and np.array_equal(_u16(tcpr), want_t), (case, n, tune)
+    if case % 4 == 0:
+        assert np.array_equal(nsx.rx_ipv4_tcp_verify_host(buf, offs, tune=dict(shards_per_device=1 + case % 3)),
+                              want_m), case

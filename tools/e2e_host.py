@@ -3,7 +3,9 @@
 from and return to the transport's host buffers). Times nsx_csum_fixed_host /
 nsx_csum_ragged_host — pinned H2D → kernel → D2H, double-buffered over two
 streams per GPU — on config 2 (1M x 1500 B) and config 3 (1M ragged) batches
-held in pinned memory (nsx_alloc_pinned) and in pageable numpy memory.
+held in pinned memory (nsx_alloc_pinned) and in pageable numpy memory, and the
+fused receive pass from host memory (nsx_rx_ipv4_tcp_verify_host) over ~770 MB of
+received datagrams (a mixed batch of tests/_rx.py tiled 200 times).
 Results are spot-checked against the oracle (tools are test infrastructure).
 
     python tools/e2e_host.py [--reps 5] [--gpus 0]
@@ -70,6 +72,23 @@ def main():
         res[name] = {"seconds": t, "GB_per_s": total / t / 1e9, "GiB_per_s": total / t / (1 << 30)}
         print(name, json.dumps(res[name]), flush=True)
     rpin.free()
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _rx
+    buf0, offs0, _ = _rx.batch(np.random.default_rng(0x1079), 4992, max_payload=1460)
+    span, reps = int(offs0[-1]), 200
+    xbuf = np.concatenate([buf0[:span]] * reps)
+    xoffs = np.concatenate([offs0[:-1] + np.uint64(k * span) for k in range(reps)] +
+                           [np.array([reps * span], np.uint64)])
+    want = O.c_rx_ipv4_tcp(buf0, offs0)[0]
+    xpin = nsx.PinnedBuffer(xbuf.nbytes)
+    xpin.array[:] = xbuf
+    for name, arr in (("rx_pinned", xpin.array), ("rx_pageable", xbuf)):
+        t, out = timed(lambda: nsx.rx_ipv4_tcp_verify_host(arr, xoffs, num_gpus=a.gpus), a.reps)
+        assert np.array_equal(out.reshape(reps, -1), np.tile(want, (reps, 1))), name  # 4992 frames = 78 words a tile
+        res[name] = {"seconds": t, "GB_per_s": xbuf.nbytes / t / 1e9, "GiB_per_s": xbuf.nbytes / t / (1 << 30),
+                     "frames": int(xoffs.size - 1)}
+        print(name, json.dumps(res[name]), flush=True)
+    xpin.free()
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "e2e_host.json"), "w") as f:
         json.dump(res, f, indent=1)
