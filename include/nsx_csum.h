@@ -123,7 +123,9 @@ int nsx_verify_mask_dev(const uint16_t* d_raw, uint64_t n, uint64_t* d_mask, nsx
  * each image are zero-filled (use nsx_tcp_layout_host). d_opt_off nullable (no
  * options); data_bytes = size of the d_data buffer. d_raw (nullable) receives
  * the raw sums. All nsx_tcp_hdr_soa members are device arrays of n entries;
- * `offset` is the whole byte 12, as the reference stores it (tcp.go:106).
+ * `offset` is the whole byte 12, as the reference stores it (tcp.go:106); a
+ * NULL `offset` computes it on the device as computeOffset() does (tcp.go:59-66):
+ * uint8((20 + option bytes + 3) / 4).
  * Each wire image must be shorter than 2^31 bytes (TCP segments are ≤ 64 KiB;
  * TSO super-segments ≤ 256 KiB). */
 typedef struct {

@@ -271,7 +271,7 @@ int nsx_tcp_build_dev_tuned(const nsx_tcp_hdr_soa* hdr, const uint8_t* d_opts, c
                             const uint32_t* d_prefix_partial, uint64_t n, uint8_t* d_out, const uint64_t* d_out_off,
                             uint16_t* d_raw, nsx_stream_t stream, const nsx_tune* tune) {
     if (n == 0) return NSX_OK;
-    if (!hdr || !hdr->src_port || !hdr->dst_port || !hdr->seq_num || !hdr->ack_num || !hdr->offset ||
+    if (!hdr || !hdr->src_port || !hdr->dst_port || !hdr->seq_num || !hdr->ack_num ||
         !hdr->control || !hdr->window || !hdr->urgent_ptr || !d_data_off || !d_out || !d_out_off ||
         (d_opt_off && !d_opts) || (data_bytes && !d_data))
         return NSX_EINVAL;

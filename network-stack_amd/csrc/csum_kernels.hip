@@ -1068,12 +1068,14 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
         const uint64_t i = g0 + min(lane, cnt - 1);
         const uint32_t mD0 = bswap16u(h.src_port[i]) | (bswap16u(h.dst_port[i]) << 16);
         const uint32_t mD1 = bswap32u(h.seq[i]), mD2 = bswap32u(h.ack[i]);
-        const uint32_t mD3 = (uint32_t)h.offset[i] | ((uint32_t)h.ctl[i] << 8) | (bswap16u(h.window[i]) << 16);
+        const uint64_t mob = OPT ? opt_off[i] : 0;
+        const uint32_t moptlen = OPT ? (uint32_t)(opt_off[i + 1] - mob) : 0u;
+        // byte 12: the caller's, or computeOffset() (tcp.go:59-66) over the serialized option bytes
+        const uint32_t moff = h.offset ? (uint32_t)h.offset[i] : ((23u + moptlen) >> 2) & 0xFFu;
+        const uint32_t mD3 = moff | ((uint32_t)h.ctl[i] << 8) | (bswap16u(h.window[i]) << 16);
         const uint32_t mD4 = bswap16u(h.urgent[i]) << 16;  // checksum field (bytes 16-17) = 0 for the sum
         const uint64_t mdb = data_off[i], mde = data_off[i + 1], moo = out_off[i];
         const uint32_t mpart = partial ? partial[i] : 0u;
-        const uint64_t mob = OPT ? opt_off[i] : 0;
-        const uint32_t moptlen = OPT ? (uint32_t)(opt_off[i + 1] - mob) : 0u;
         const uint32_t mhdr = 20u + moptlen + (moptlen ? (20u + moptlen) % 4u : 0u);  // tcp.go:118-121
         const uint32_t mwire = mhdr + (uint32_t)(mde - mdb);                             // < 2^31
         uint32_t od[kOptDw];

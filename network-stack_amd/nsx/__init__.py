@@ -344,8 +344,9 @@ def tcp_layout_host(data_off: np.ndarray, opt_off: np.ndarray | None = None) -> 
 
 def tcp_build_dev(fields: dict, data, data_off, out, out_off, opts=None, opt_off=None, partial=None, raw=None,
                   stream=None, tune=None):
-    """Fused segment.bytes() + checksum + field write (fields: dict of device tensors)."""
-    soa = TcpHdrSoA(*[fields[k].data_ptr() for k in
+    """Fused segment.bytes() + checksum + field write (fields: dict of device tensors; a missing or None
+    "offset" computes byte 12 on the device as computeOffset() does, tcp.go:59-66)."""
+    soa = TcpHdrSoA(*[_dev_ptr(fields.get(k)) for k in
                       ("src_port", "dst_port", "seq_num", "ack_num", "offset", "control", "window", "urgent_ptr")])
     n = data_off.numel() - 1
     _check(lib().nsx_tcp_build_dev_tuned(ctypes.byref(soa), _dev_ptr(opts), _dev_ptr(opt_off), _dev_ptr(data),

@@ -737,14 +737,16 @@ def test_tcp_build_uniform_batches_with_options(opt, P):
         data_off = np.arange(n + 1, dtype=np.uint64) * np.uint64(P) + np.uint64(data_lead)
         out_off = nsx.tcp_layout_host(data_off, opt_off)
         assert all(int(out_off[i + 1] - out_off[i]) >= len(want_wire[i]) for i in range(n))
-        for kern in (0, nsx.KERNEL_BUILD_GENERAL, nsx.KERNEL_BUILD_PLAIN):
+        # offset=None: byte 12 computed on the device (computeOffset, tcp.go:59-66) from the option bytes
+        for kern, comp in ((0, False), (nsx.KERNEL_BUILD_GENERAL, False), (nsx.KERNEL_BUILD_PLAIN, False),
+                           (0, True), (nsx.KERNEL_BUILD_PLAIN, True)):
             out = torch.full((int(out_off[-1]),), 0xAB, dtype=torch.uint8, device="cuda")
             raw = torch.empty(n, dtype=torch.int16, device="cuda")
-            nsx.tcp_build_dev(fields, dev(data), dev(data_off.view(np.int64)), out, dev(out_off.view(np.int64)),
-                              opts=dev(opts), opt_off=dev(opt_off.view(np.int64)), partial=part, raw=raw,
-                              tune=dict(kernel=kern))
+            nsx.tcp_build_dev(dict(fields, offset=None) if comp else fields, dev(data), dev(data_off.view(np.int64)),
+                              out, dev(out_off.view(np.int64)), opts=dev(opts), opt_off=dev(opt_off.view(np.int64)),
+                              partial=part, raw=raw, tune=dict(kernel=kern))
             got, raw_h = host(out), u16(raw)
-            key = (opt, P, opt_lead, data_lead, kern)
+            key = (opt, P, opt_lead, data_lead, kern, comp)
             assert np.array_equal(raw_h, want_raw), key
             for i in range(n):
                 o = int(out_off[i])
@@ -812,12 +814,16 @@ def test_tcp_build_matches_reference_bytes_and_checksum(lead, align4):
               "offset": u([s.offset for s in segs], np.uint8), "control": u([s.control.byte() for s in segs], np.uint8),
               "window": u([s.window for s in segs], np.uint16), "urgent_ptr": u([s.urgent_ptr for s in segs], np.uint16)}
     part = np.array([O.be_word_sum(p) for p in pseudos], np.uint32)
-    out = torch.full((int(out_off[-1]),), 0xAB, dtype=torch.uint8, device="cuda")
-    raw = torch.empty(n, dtype=torch.int16, device="cuda")
-    nsx.tcp_build_dev(fields, dev(np.frombuffer(data, np.uint8)), dev(data_off.view(np.int64)), out,
-                      dev(out_off.view(np.int64)), opts=dev(np.frombuffer(opts, np.uint8)),
-                      opt_off=dev(opt_off.view(np.int64)), partial=dev(part.view(np.int32)), raw=raw)
-    got, raw_h = host(out), u16(raw)
+    outs = []
+    for f in (fields, dict(fields, offset=None)):  # the caller's byte 12, then computeOffset on the device
+        out = torch.full((int(out_off[-1]),), 0xAB, dtype=torch.uint8, device="cuda")
+        raw = torch.empty(n, dtype=torch.int16, device="cuda")
+        nsx.tcp_build_dev(f, dev(np.frombuffer(data, np.uint8)), dev(data_off.view(np.int64)), out,
+                          dev(out_off.view(np.int64)), opts=dev(np.frombuffer(opts, np.uint8)),
+                          opt_off=dev(opt_off.view(np.int64)), partial=dev(part.view(np.int32)), raw=raw)
+        outs.append((host(out), u16(raw)))
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+    got, raw_h = outs[0]
     for i, s in enumerate(segs):
         s.checksum = 0
         r = s.compute_checksum(pseudos[i])
