@@ -672,7 +672,7 @@ __device__ __forceinline__ void scan_span(const uint8_t* rbase, uint64_t span, u
     if (brel >= (int64_t)(nrows * kRow)) bval = carry;  // boundary at the very end of the rows
 }
 
-template <int R, bool VERIFY>
+template <int R, bool VERIFY, bool PIPE>
 __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, uint32_t n,
     const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t run) {
@@ -719,7 +719,7 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
         // Boundary lane state: its position relative to rbase, and S there.
         const int64_t brel = lane <= cnt ? (int64_t)((base + my_off) - rbase) : -1;
         uint64_t bval = 0, carry = 0;
-        scan_span<R>(rbase, span, head, brel, lane, bval, carry);
+        scan_span<R, PIPE>(rbase, span, head, brel, lane, bval, carry);
         // Segment `lane` = [boundary lane, boundary lane+1).
         const uint64_t nb = ((uint64_t)__shfl_down((unsigned long long)bval, 1));
         const uint64_t d = nb - bval;
@@ -1925,8 +1925,13 @@ hipError_t launch_fixed(const LaunchCfg& c, const void* d_base, uint64_t stride,
 template <bool VERIFY>
 static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, const uint64_t* offsets, uint64_t n,
                                      const uint32_t* partial, uint16_t* out, uint8_t* ok, hipStream_t st) {
-    // Default: 8 rows per batch, 63-segment runs, 2 blocks/CU (tools/c3_sweep.sh).
-    const int rows = (c.rows == 4 || c.rows == 8 || c.rows == 16) ? c.rows : 8;
+    // Default: double-buffered batches of 2 rows, 63-segment runs, 2 blocks/CU (tools/ab.py --config 3, same
+    // process on three boxes: 0.680 ms against 0.691 for single batches of 8 rows, 0.702-0.713 for pipelined
+    // batches of 3 or 4 rows, 0.93 for 1 row). kernel 2 (NSX_TUNE_KERNEL_SCAN_PLAIN):
+    // single batches of 4, 8 (default) or 16 rows.
+    const bool pipe = c.kernel != 2;
+    const int rows = pipe ? (c.rows == 2 || c.rows == 4 || c.rows == 8 ? c.rows : 2)
+                          : (c.rows == 4 || c.rows == 8 || c.rows == 16 ? c.rows : 8);
     const uint32_t run = (c.run_segs >= 1 && c.run_segs <= (int)kScanRun) ? (uint32_t)c.run_segs : kScanRun;
     const uint32_t mb = max_blocks_of(c, 2);
     for (uint64_t c0 = 0; c0 < n; c0 += kRaggedChunk) {
@@ -1935,11 +1940,12 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
         const uint32_t* pc = partial ? partial + c0 : nullptr;
         uint16_t* oc = out ? out + c0 : nullptr;
         uint8_t* kc = ok ? ok + c0 : nullptr;
-#define NSX_RSCAN(R_)                                                                                          \
-        if (rows == R_)                                                                                         \
-            hipLaunchKernelGGL((csum_ragged_scan_kernel<R_, VERIFY>), dim3(grid), dim3(kBlock), 0, st, base,    \
+#define NSX_RSCAN(R_, P_)                                                                                      \
+        if (rows == R_ && pipe == P_)                                                                           \
+            hipLaunchKernelGGL((csum_ragged_scan_kernel<R_, VERIFY, P_>), dim3(grid), dim3(kBlock), 0, st, base, \
                                offsets + c0, cn, pc, oc, kc, run);
-        NSX_RSCAN(4) NSX_RSCAN(8) NSX_RSCAN(16)
+        NSX_RSCAN(2, true) NSX_RSCAN(4, true) NSX_RSCAN(8, true)
+        NSX_RSCAN(4, false) NSX_RSCAN(8, false) NSX_RSCAN(16, false)
 #undef NSX_RSCAN
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
@@ -1966,10 +1972,10 @@ hipError_t launch_ragged(const LaunchCfg& c, const void* d_base, const uint64_t*
 
 hipError_t launch_rx_ipv4_tcp(const LaunchCfg& c, const void* d_base, const uint64_t* d_offsets, uint64_t n,
                               uint64_t* mask, uint16_t* ip_raw, uint16_t* tcp_raw, hipStream_t st) {
-    // Double-buffered batches of 4 rows, 3 blocks/CU (tools/ab.py --config 10, same process: 0.1305 ms against
-    // 0.1348 for single batches of 8 rows, 0.157 at 2 blocks/CU, 0.144 at 4; the plain ragged scan over the
-    // same frames 0.138); launches of ≤ 2^27 frames (a multiple of 64, so every launch starts on a mask word)
-    const int rows = (c.rows == 4 || c.rows == 8 || c.rows == 16) ? c.rows : 4;
+    // Double-buffered batches of 2 rows, 3 blocks/CU (tools/ab.py --config 10, same process: 0.1294 ms against
+    // 0.1305 for batches of 4 rows, 0.1348 for single batches of 8 rows, 0.145 for 2 rows at 2 blocks/CU, 0.136
+    // at 4); launches of ≤ 2^27 frames (a multiple of 64, so every launch starts on a mask word)
+    const int rows = (c.rows == 2 || c.rows == 4 || c.rows == 8 || c.rows == 16) ? c.rows : 2;
     const uint32_t mb = max_blocks_of(c, 3);
     const uint8_t* base = static_cast<const uint8_t*>(d_base);
     for (uint64_t c0 = 0; c0 < n; c0 += kRaggedChunk) {
@@ -1981,7 +1987,7 @@ hipError_t launch_rx_ipv4_tcp(const LaunchCfg& c, const void* d_base, const uint
         if (rows == R_)                                                                                            \
             hipLaunchKernelGGL((rx_ipv4_tcp_kernel<R_>), dim3(grid), dim3(kBlock), 0, st, base, d_offsets + c0, cn,  \
                                mask + c0 / 64, ic, tc);
-        NSX_RX(4) NSX_RX(8) NSX_RX(16)
+        NSX_RX(2) NSX_RX(4) NSX_RX(8) NSX_RX(16)
 #undef NSX_RX
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;

@@ -104,7 +104,7 @@ def test_config3_1M_ragged_full():
     nsx.fill_splitmix64_dev(t, 0x1072)
     want = O.c_batch(host(t), n, offsets=offs, threads=16)
     d_offs = dev(offs.view(np.int64))
-    for tune in (None, dict(rows=16, run_segs=16), dict(blocks_per_cu=1)):
+    for tune in (None, dict(kernel=nsx.KERNEL_SCAN_PLAIN, rows=16, run_segs=16), dict(blocks_per_cu=1, rows=8)):
         out = nsx.ragged_dev(t, d_offs, out=torch.empty(n, dtype=torch.int16, device="cuda"), tune=tune)
         assert np.array_equal(u16(out), want), tune
 

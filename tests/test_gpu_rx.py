@@ -53,7 +53,7 @@ def test_rx_mixed_batches(n, lead):
         assert np.array_equal(w, g), (what, n, lead)
 
 
-TUNES = [dict(rows=4), dict(rows=16), dict(blocks_per_cu=1), dict(blocks_per_cu=8), dict(rows=16, blocks_per_cu=1)]
+TUNES = [dict(rows=2), dict(rows=4), dict(rows=16), dict(blocks_per_cu=1), dict(blocks_per_cu=8), dict(rows=16, blocks_per_cu=1)]
 
 
 @pytest.mark.parametrize("tune", TUNES, ids=lambda t: ",".join(f"{k}={v}" for k, v in t.items()))
