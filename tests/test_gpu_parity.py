@@ -678,6 +678,41 @@ def test_tcp_build_uniform_batches(P, n):
             assert np.array_equal(got, want), (P, n, lead, kern)
 
 
+@pytest.mark.parametrize("P", [0, 4, 12, 1004, 1480, 2012, 2016, 2028])
+@pytest.mark.parametrize("out_base", [0, 4, 8, 12])
+@pytest.mark.parametrize("gaps", ["none", "some", "all"])
+def test_tcp_build_output_bases_and_gaps(P, out_base, gaps):
+    """The fast path's descriptor-clipped stores: output arrays at every 4 B offset from a 16 B boundary, images
+    back to back or with gaps of 4-60 bytes between some or all of them, group edges (n = 211, 16-segment
+    groups) and images at the 2-row limit (P 2012-2028: 2032-2048 B images). Every image equals the oracle's,
+    and no byte outside the images (gaps, the array's lead and tail) changes."""
+    rng = np.random.default_rng(P * 31 + out_base * 7 + len(gaps))
+    n = 211
+    fields, data, data_off, out_off, ps = _uniform_build_case(rng, n, P, 20)
+    wire = 20 + P
+    gap = {"none": np.zeros(n, np.uint64), "all": 4 * rng.integers(1, 16, n).astype(np.uint64),
+           "some": 4 * rng.integers(1, 16, n).astype(np.uint64) * (rng.random(n) < 0.2)}[gaps]
+    out_off = np.zeros(n + 1, np.uint64)
+    out_off[1:] = np.cumsum(np.uint64((wire + 3) & ~3) + gap)
+    want, wraw = O.c_go_tcp_build(fields, data, data_off, out_off, ps)
+    dt = {np.uint16: np.int16, np.uint32: np.int32, np.uint8: np.uint8}
+    f = {k: dev(v.view(dt[v.dtype.type])) for k, v in fields.items()}
+    part = dev(np.array([O.be_word_sum(p.tobytes()) for p in ps], np.uint32).view(np.int32))
+    full = torch.full((out_base + int(out_off[-1]) + 32,), 0xAB, dtype=torch.uint8, device="cuda")
+    out = full[out_base:]
+    raw = torch.empty(n, dtype=torch.int16, device="cuda")
+    nsx.tcp_build_dev(f, dev(data), dev(data_off.view(np.int64)), out, dev(out_off.view(np.int64)), partial=part,
+                      raw=raw)
+    got = host(full)
+    exp = np.full(got.size, 0xAB, np.uint8)
+    for i in range(n):
+        o = int(out_off[i])
+        exp[out_base + o:out_base + o + ((wire + 3) & ~3)] = want[o:o + ((wire + 3) & ~3)]
+    assert np.array_equal(u16(raw), wraw)
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, (bad[:8], got[bad[:8]], exp[bad[:8]])
+
+
 _OPT_SETS = {  # option lists as the reference serialises them (tcp.go:225-231: kind 2 carries length + data)
     "nop_nop_k2len10": lambda r: [O.Option(kind=1), O.Option(kind=1), O.Option(kind=2, length=10, data=r(8))],
     "mss": lambda r: [O.Option(kind=2, length=4, data=r(2))],
