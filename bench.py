@@ -89,6 +89,11 @@ WORKLOADS = {
              metric="GiB/s fused receive verify (IPv4 header + pseudo-header + TCP checksum into a bitmask), frame bytes",
              name="f2+f3 rx: 1M IPv4/TCP datagrams per GPU, 40-1500B (uniform), densely packed (odd starts), "
                   "1 in 1000 corrupted, verified into a validity bitmask, device-resident"),
+    # not a BASELINE config: the same receive pass over IPv6 packets (RFC 8200 pseudo-header, no header checksum)
+    11: dict(kind="rx", ipver=6, n=1 << 20, lo=60, hi=1500, seed=0x107A,
+             metric="GiB/s fused receive verify (IPv6 pseudo-header + TCP checksum into a bitmask), packet bytes",
+             name="f2 rx6: 1M IPv6/TCP packets per GPU, 60-1500B (uniform), densely packed (odd starts), "
+                  "1 in 1000 corrupted, verified into a validity bitmask, device-resident"),
 }
 
 
@@ -99,7 +104,8 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", type=int, default=2, choices=sorted(WORKLOADS),
                     help="2-5: BASELINE configs (2 = headline); 6: f1 fused TCP build; 7: f3 IPv4 header verify; "
-                         "8: f1 with 12 B options; 9: f3 verify into a bitmask; 10: fused receive pass (f2+f3)")
+                         "8: f1 with 12 B options; 9: f3 verify into a bitmask; 10: fused receive pass (f2+f3); "
+                         "11: the receive pass over IPv6")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--settle-s", type=float, default=0.5, help="device clock settle time before warmup (setup)")
     ap.add_argument("--event-every", type=int, default=10,
@@ -326,8 +332,9 @@ def build_workload(cfg, rank, device, tune=None):
         w.update(build_rx_frames(cfg, seed, device))
         n, buf, d_offs, total = cfg["n"], w["buf"], w["d_offs"], w["bytes"]
         out = torch.empty((n + 63) // 64, dtype=torch.int64, device=device)
+        rx = nsx.rx_ipv6_tcp_verify_dev if cfg.get("ipver") == 6 else nsx.rx_ipv4_tcp_verify_dev
         w.update(out=out, alg=total + 8 * (n + 1) + (n + 63) // 64 * 8,
-                 step_for=lambda t: lambda: nsx.rx_ipv4_tcp_verify_dev(buf, d_offs, mask=out, tune=t))
+                 step_for=lambda t: lambda: rx(buf, d_offs, mask=out, tune=t))
     else:
         rng = np.random.default_rng(cfg["seed"])  # same lengths on every rank, bytes differ by seed
         n = cfg["n"]
@@ -384,7 +391,10 @@ def build_rx_frames(cfg, seed, device) -> dict:
     frame length, DF, protocol 6; the random bytes stay as id / TTL / addresses) and a TCP segment of the
     rest. Both checksum fields are filled with this library's own ragged kernel over the 2n header /
     segment spans (the TCP spans with their pseudo-header partials, RFC 9293 §3.1), then every 1000th frame
-    gets one bit flipped in its TCP header (setup; the parity test checks the outcome against the oracle)."""
+    gets one bit flipped in its TCP header (setup; the parity test checks the outcome against the oracle).
+    Workload 11 (ipver 6): an IPv6 header instead (version 6, payload length = frame length − 40, Next
+    Header 6; the random bytes stay as class / flow / hop limit / addresses), the TCP field filled over the
+    RFC 8200 §8.1 pseudo-header."""
     import numpy as np
     import torch
     import nsx
@@ -400,6 +410,25 @@ def build_rx_frames(cfg, seed, device) -> dict:
     st = d_offs[:-1]
     ln = (d_offs[1:] - st)
     put = lambda k, v: buf.index_put_((st + k,), v if torch.is_tensor(v) else torch.full_like(st, v, dtype=torch.uint8))
+    if cfg.get("ipver") == 6:
+        put(0, ((buf[st] & 0x0F) | 0x60).to(torch.uint8))
+        put(4, ((ln - 40) >> 8).to(torch.uint8))
+        put(5, ((ln - 40) & 0xFF).to(torch.uint8))
+        put(6, 6)
+        put(56, 0)
+        put(57, 0)
+        idx16 = torch.arange(16, device=device)
+        src = buf[(st[:, None] + 8 + idx16).reshape(-1)]
+        dst = buf[(st[:, None] + 24 + idx16).reshape(-1)]
+        pseudo = nsx.pseudo_ipv6_partial_dev(src, dst, (ln - 40).to(torch.int32), 6)
+        spans = torch.cat([torch.stack([st, st + 40], 1).reshape(-1), d_offs[-1:]])
+        part2 = torch.stack([torch.zeros_like(pseudo), pseudo], 1).reshape(-1)
+        tcp_f = (~(nsx.ragged_dev(buf, spans, partial=part2).to(torch.int32) & 0xFFFF))[1::2] & 0xFFFF
+        put(56, (tcp_f >> 8).to(torch.uint8))
+        put(57, (tcp_f & 0xFF).to(torch.uint8))
+        buf[st[::1000] + 50] ^= 1
+        torch.cuda.synchronize()
+        return {"buf": buf, "d_offs": d_offs, "offsets": offs, "bytes": total}
     put(0, 0x45)
     put(1, 0)
     put(2, (ln >> 8).to(torch.uint8))
@@ -528,11 +557,18 @@ def cpu_baseline(cfg, w, seconds: float) -> dict:
         cmask = np.zeros(m // 64, np.uint64)
         bounds = [int(np.searchsorted(offs, hi_b * t // T)) // 64 * 64 for t in range(T)] + [m]  # byte-balanced
 
+        v6 = cfg.get("ipver") == 6
+
         def go(lo, hi):
-            lib.oracle_go_rx_ipv4_tcp(_ptr(sample), _ptr(offs, lo), hi - lo, _ptr(cmask, lo // 64), None, None)
+            if v6:
+                lib.oracle_go_rx_ipv6_tcp(_ptr(sample), _ptr(offs, lo), hi - lo, _ptr(cmask, lo // 64), None)
+            else:
+                lib.oracle_go_rx_ipv4_tcp(_ptr(sample), _ptr(offs, lo), hi - lo, _ptr(cmask, lo // 64), None, None)
         nbytes = hi_b
-        desc = (f"first {m} frames of rank 0's batch: per frame the reference's checksum loop over the IPv4 header "
-                "and over pseudo-header ‖ TCP segment (allocate + concatenate + serial loop) + bit packing")
+        desc = (f"first {m} frames of rank 0's batch: per frame the reference's checksum loop over "
+                + ("pseudo-header ‖ TCP segment (IPv6)" if v6 else
+                   "the IPv4 header and over pseudo-header ‖ TCP segment")
+                + " (allocate + concatenate + serial loop) + bit packing")
         check["mask"] = lambda: np.array_equal(cmask, gpu)
     else:
         offs_all = w["offsets"]

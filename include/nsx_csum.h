@@ -198,6 +198,22 @@ int nsx_ipv4_hdr_verify_mask_dev(const void* d_base, uint64_t stride, uint32_t h
 int nsx_rx_ipv4_tcp_verify_dev(const void* d_base, const uint64_t* d_offsets, uint64_t n, uint64_t* d_mask,
                                uint16_t* d_ip_raw, uint16_t* d_tcp_raw, nsx_stream_t stream);
 
+/* The same receive pass for IPv6 (the IPv6 pseudo-header of
+ * ip.Addr.Raw(), network/ip/v6/ipv6.go:16): frame i is an IPv6 packet whose
+ * fixed 40-byte header (RFC 8200 §3) is followed directly by a TCP segment.
+ * Bit (i % 64) of d_mask[i / 64] is set iff frame i
+ *   - is well-formed: at least 40 bytes, version 6, 40 + payload length (bytes
+ *     4-5) == frame length, Next Header (byte 6) == 6 (ip.NextProtoTCP; a
+ *     packet with extension headers is not walked and does not verify), and a
+ *     payload of at least 20 bytes (tcp.go:131);
+ *   - has a valid TCP checksum: the raw sum over the RFC 8200 §8.1 pseudo-header
+ *     src(16) dst(16) payload length(4) 0 0 0 6 from the header's own addresses
+ *     ‖ the segment is 0xFFFF (tcp.go:70 over computeChecksum, tcp.go:72-95).
+ * IPv6 has no header checksum. d_tcp_raw (nullable): that raw sum, 0 unless the
+ * frame is well-formed. Layout rules as nsx_rx_ipv4_tcp_verify_dev. */
+int nsx_rx_ipv6_tcp_verify_dev(const void* d_base, const uint64_t* d_offsets, uint64_t n, uint64_t* d_mask,
+                               uint16_t* d_tcp_raw, nsx_stream_t stream);
+
 /* ----------------------------------------------------------------------------
  * Host-resident batches: pinned staging, H2D → kernel → D2H double-buffered
  * over two streams per GPU, segments sharded contiguously across num_gpus
@@ -215,6 +231,8 @@ int nsx_csum_ragged_host(const uint8_t* h_base, const uint64_t* h_offsets, uint6
  * datagrams: h_mask receives ceil(n/64) words. Shards and chunks start on
  * 64-frame mask words. */
 int nsx_rx_ipv4_tcp_verify_host(const uint8_t* h_base, const uint64_t* h_offsets, uint64_t n, uint64_t* h_mask,
+                                int num_gpus);
+int nsx_rx_ipv6_tcp_verify_host(const uint8_t* h_base, const uint64_t* h_offsets, uint64_t n, uint64_t* h_mask,
                                 int num_gpus);
 
 /* The host batch calls keep per-device streams and grow-only device/pinned

@@ -62,6 +62,8 @@ int nsx_ipv4_hdr_verify_mask_dev_tuned(const void* d_base, uint64_t stride, uint
 int nsx_rx_ipv4_tcp_verify_dev_tuned(const void* d_base, const uint64_t* d_offsets, uint64_t n, uint64_t* d_mask,
                                      uint16_t* d_ip_raw, uint16_t* d_tcp_raw, nsx_stream_t stream,
                                      const nsx_tune* tune);
+int nsx_rx_ipv6_tcp_verify_dev_tuned(const void* d_base, const uint64_t* d_offsets, uint64_t n, uint64_t* d_mask,
+                                     uint16_t* d_tcp_raw, nsx_stream_t stream, const nsx_tune* tune);
 int nsx_csum_fixed_host_tuned(const uint8_t* h_base, uint64_t stride, uint32_t seg_len, uint64_t n,
                               const uint32_t* h_prefix_partial, uint16_t* h_out, int num_gpus,
                               const nsx_tune* tune);
@@ -69,6 +71,8 @@ int nsx_csum_ragged_host_tuned(const uint8_t* h_base, const uint64_t* h_offsets,
                                const uint32_t* h_prefix_partial, uint16_t* h_out, int num_gpus,
                                const nsx_tune* tune);
 int nsx_rx_ipv4_tcp_verify_host_tuned(const uint8_t* h_base, const uint64_t* h_offsets, uint64_t n, uint64_t* h_mask,
+                                      int num_gpus, const nsx_tune* tune);
+int nsx_rx_ipv6_tcp_verify_host_tuned(const uint8_t* h_base, const uint64_t* h_offsets, uint64_t n, uint64_t* h_mask,
                                       int num_gpus, const nsx_tune* tune);
 
 /* Kernel launches one nsx_csum_fixed_dev(_tuned) call makes for this batch on the current device (its

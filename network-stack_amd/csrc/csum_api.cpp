@@ -207,8 +207,24 @@ int nsx_rx_ipv4_tcp_verify_dev_tuned(const void* d_base, const uint64_t* d_offse
     if (n > ((uint64_t)1 << 40)) return NSX_EINVAL;
     const int dev = current_device();
     if (dev < 0) return NSX_ENODEV;
-    return map_err(nsx::launch_rx_ipv4_tcp(make_cfg(dev, tune), d_base, d_offsets, n, d_mask, d_ip_raw, d_tcp_raw,
-                                           static_cast<hipStream_t>(stream)));
+    return map_err(nsx::launch_rx_tcp(make_cfg(dev, tune), 4, d_base, d_offsets, n, d_mask, d_ip_raw, d_tcp_raw,
+                                      static_cast<hipStream_t>(stream)));
+}
+
+int nsx_rx_ipv6_tcp_verify_dev(const void* d_base, const uint64_t* d_offsets, uint64_t n, uint64_t* d_mask,
+                               uint16_t* d_tcp_raw, nsx_stream_t stream) {
+    return nsx_rx_ipv6_tcp_verify_dev_tuned(d_base, d_offsets, n, d_mask, d_tcp_raw, stream, nullptr);
+}
+
+int nsx_rx_ipv6_tcp_verify_dev_tuned(const void* d_base, const uint64_t* d_offsets, uint64_t n, uint64_t* d_mask,
+                                     uint16_t* d_tcp_raw, nsx_stream_t stream, const nsx_tune* tune) {
+    if (n == 0) return NSX_OK;
+    if (!d_base || !d_offsets || !d_mask) return NSX_EINVAL;
+    if (n > ((uint64_t)1 << 40)) return NSX_EINVAL;
+    const int dev = current_device();
+    if (dev < 0) return NSX_ENODEV;
+    return map_err(nsx::launch_rx_tcp(make_cfg(dev, tune), 6, d_base, d_offsets, n, d_mask, nullptr, d_tcp_raw,
+                                      static_cast<hipStream_t>(stream)));
 }
 
 int nsx_pseudo_ipv4_partial_dev(const uint8_t* d_src, const uint8_t* d_dst, const uint32_t* d_len,

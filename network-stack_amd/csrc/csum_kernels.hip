@@ -760,8 +760,13 @@ __device__ __forceinline__ uint32_t bswap16u(uint32_t v) { return ((v & 0xFFu) <
 
 constexpr uint32_t kRxRun = 64;
 
-template <int R>
-__global__ __launch_bounds__(kBlock) void rx_ipv4_tcp_kernel(const uint8_t* __restrict__ base,
+// V6: IPv6 packets (RFC 8200 §3: fixed 40-byte header, Next Header 6 = TCP directly). There is no header
+// checksum, and the pseudo-header's addresses (RFC 8200 §8.1) are the header's own bytes 8-39, which the frame
+// sum F already holds in the same word pairing as the pseudo-header ‖ segment sum; so TCP sum =
+// fold(F − bytes 0-7) + payload length + 6 (the pseudo-header's length and next-header words), and the header
+// window is only the first 8 bytes (one 16 B load per lane).
+template <int R, bool V6>
+__global__ __launch_bounds__(kBlock) void rx_tcp_kernel(const uint8_t* __restrict__ base,
                                                              const uint64_t* __restrict__ offsets, uint32_t n,
                                                              uint64_t* __restrict__ mask,
                                                              uint16_t* __restrict__ ip_raw,
@@ -816,25 +821,50 @@ __global__ __launch_bounds__(kBlock) void rx_ipv4_tcp_kernel(const uint8_t* __re
         const bool narrow = span < (1ull << 31);
         const __amdgpu_buffer_rsrc_t hrs = make_rsrc(rbase, narrow ? ((span + 3) & ~3ull) : 0);
         const uint32_t hwo = live && narrow ? (uint32_t)brel & ~3u : kOOB;
+        constexpr int kWin = V6 ? 3 : 6;  // window dwords: bytes 0-7 (IPv6) / 0-19 (IPv4) at any hd
         {
             typedef uint32_t v2x __attribute__((ext_vector_type(2)));
             const u32x4 q = bld16<false>(hrs, hwo);
-            const v2x r = __builtin_amdgcn_raw_buffer_load_b64(hrs, hwo == kOOB ? kOOB : hwo + 16u, 0, 0);
-            d[0] = q.x, d[1] = q.y, d[2] = q.z, d[3] = q.w, d[4] = r.x, d[5] = r.y;
+            d[0] = q.x, d[1] = q.y, d[2] = q.z, d[3] = q.w;
+            if constexpr (!V6) {
+                const v2x r = __builtin_amdgcn_raw_buffer_load_b64(hrs, hwo == kOOB ? kOOB : hwo + 16u, 0, 0);
+                d[4] = r.x, d[5] = r.y;
+            }
         }
         const uint32_t* hw = reinterpret_cast<const uint32_t*>(fp - hd);
         const uint32_t* last_dw = reinterpret_cast<const uint32_t*>((uintptr_t)(base + (hi > lo ? hi - 1 : lo)) & ~(uintptr_t)3);
         if (!narrow && hi > lo) {  // clamped to the run's last readable dword: every lane loads unconditionally
 #pragma unroll
-            for (int k = 0; k < 6; ++k) d[k] = hw + k < last_dw ? hw[k] : *last_dw;
+            for (int k = 0; k < kWin; ++k) d[k] = hw + k < last_dw ? hw[k] : *last_dw;
         }
         // The run's bytes, S sampled at every frame start.
         uint64_t bval = 0, carry = 0;
         scan_span<R, true>(rbase, span, head, brel, lane, bval, carry);
         const uint64_t nbv = (uint64_t)__shfl_down((unsigned long long)bval, 1);
         const uint64_t F = (lane == cnt - 1 ? carry : nbv) - bval;  // the frame's weighted sum (exact)
-        // IPv4 header fields (RFC 791 §3.1): header dword m = bytes 4m..4m+3, little-endian view.
         const uint64_t flen = my_end - my_off;
+        const bool even = ((uintptr_t)fp & 1u) == 0;  // frame start parity = TCP segment start parity
+        typedef uint32_t v2w __attribute__((ext_vector_type(2)));
+        if constexpr (V6) {
+            const uint32_t H0 = __builtin_amdgcn_alignbyte(d[1], d[0], hd);  // version, class, flow label
+            const uint32_t H1 = __builtin_amdgcn_alignbyte(d[2], d[1], hd);  // payload length, next header, hops
+            const uint32_t plen = bswap16u(H1 & 0xFFFFu);
+            const bool well = live && flen >= 40u && (H0 & 0xF0u) == 0x60u && plen + 40u == flen &&
+                              ((H1 >> 16) & 0xFFu) == 6u && plen >= 20u;  // tcp.go:131
+            uint32_t h8 = 0;
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                h8 = __builtin_amdgcn_sad_u16(d[k] & keep_mask((int32_t)hd, (int32_t)(hd + 8u), 4 * k), 0u, h8);
+            const uint64_t T = F - h8;  // addresses ‖ segment
+            const uint32_t tle = fold32((uint32_t)T) + fold32((uint32_t)(T >> 32));
+            const uint32_t tcpr = well ? finish(tle, even, plen + 6u) : 0u;
+            const uint64_t bits = __builtin_amdgcn_ballot_w64(well && tcpr == 0xFFFFu);
+            __builtin_amdgcn_raw_buffer_store_b64(v2w{(uint32_t)bits, (uint32_t)(bits >> 32)}, mrs,
+                                                  lane == 0 ? (a / 64u) * 8u : kOOB, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)tcpr, trs, live ? (a + lane) * 2u : kOOB, 0, 0);
+            continue;
+        }
+        // IPv4 header fields (RFC 791 §3.1): header dword m = bytes 4m..4m+3, little-endian view.
         const uint32_t H0 = __builtin_amdgcn_alignbyte(d[1], d[0], hd);
         const uint32_t H1 = __builtin_amdgcn_alignbyte(d[2], d[1], hd);
         const uint32_t H2 = __builtin_amdgcn_alignbyte(d[3], d[2], hd);
@@ -868,7 +898,6 @@ __global__ __launch_bounds__(kBlock) void rx_ipv4_tcp_kernel(const uint8_t* __re
             for (int k = 6; k < 16; ++k)
                 hs = __builtin_amdgcn_sad_u16(d[k] & keep_mask((int32_t)hd, (int32_t)(hd + hlen), 4 * k), 0u, hs);
         }
-        const bool even = ((uintptr_t)fp & 1u) == 0;  // frame start parity = TCP segment start parity (IHL·4 even)
         const uint32_t ipr = hdr_ok ? finish(hs, even, 0u) : 0u;
         const uint64_t T = F - (hdr_ok ? hs : 0u);     // the TCP segment's weighted sum
         const uint32_t tle = fold32((uint32_t)T) + fold32((uint32_t)(T >> 32));
@@ -876,7 +905,6 @@ __global__ __launch_bounds__(kBlock) void rx_ipv4_tcp_kernel(const uint8_t* __re
                                 bswap16u(H4 >> 16) + 6u + ((total - hlen) & 0xFFFFu);
         const uint32_t tcpr = well ? finish(tle, even, pseudo) : 0u;
         const uint64_t bits = __builtin_amdgcn_ballot_w64(well && ipr == 0xFFFFu && tcpr == 0xFFFFu);
-        typedef uint32_t v2w __attribute__((ext_vector_type(2)));
         __builtin_amdgcn_raw_buffer_store_b64(v2w{(uint32_t)bits, (uint32_t)(bits >> 32)}, mrs,
                                               lane == 0 ? (a / 64u) * 8u : kOOB, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ipr, irs, live ? (a + lane) * 2u : kOOB, 0, 0);
@@ -1970,8 +1998,8 @@ hipError_t launch_ragged(const LaunchCfg& c, const void* d_base, const uint64_t*
     return launch_ragged_scan<false>(c, base, d_offsets, n, partial, out, nullptr, st);
 }
 
-hipError_t launch_rx_ipv4_tcp(const LaunchCfg& c, const void* d_base, const uint64_t* d_offsets, uint64_t n,
-                              uint64_t* mask, uint16_t* ip_raw, uint16_t* tcp_raw, hipStream_t st) {
+hipError_t launch_rx_tcp(const LaunchCfg& c, int ipver, const void* d_base, const uint64_t* d_offsets, uint64_t n,
+                         uint64_t* mask, uint16_t* ip_raw, uint16_t* tcp_raw, hipStream_t st) {
     // Double-buffered batches of 2 rows, 3 blocks/CU (tools/ab.py --config 10, same process: 0.1294 ms against
     // 0.1305 for batches of 4 rows, 0.1348 for single batches of 8 rows, 0.145 for 2 rows at 2 blocks/CU, 0.136
     // at 4); launches of ≤ 2^27 frames (a multiple of 64, so every launch starts on a mask word)
@@ -1984,8 +2012,11 @@ hipError_t launch_rx_ipv4_tcp(const LaunchCfg& c, const void* d_base, const uint
         uint16_t* ic = ip_raw ? ip_raw + c0 : nullptr;
         uint16_t* tc = tcp_raw ? tcp_raw + c0 : nullptr;
 #define NSX_RX(R_)                                                                                                \
-        if (rows == R_)                                                                                            \
-            hipLaunchKernelGGL((rx_ipv4_tcp_kernel<R_>), dim3(grid), dim3(kBlock), 0, st, base, d_offsets + c0, cn,  \
+        if (rows == R_ && ipver == 6)                                                                              \
+            hipLaunchKernelGGL((rx_tcp_kernel<R_, true>), dim3(grid), dim3(kBlock), 0, st, base, d_offsets + c0, cn,  \
+                               mask + c0 / 64, nullptr, tc);                                                       \
+        if (rows == R_ && ipver != 6)                                                                              \
+            hipLaunchKernelGGL((rx_tcp_kernel<R_, false>), dim3(grid), dim3(kBlock), 0, st, base, d_offsets + c0, cn, \
                                mask + c0 / 64, ic, tc);
         NSX_RX(2) NSX_RX(4) NSX_RX(8) NSX_RX(16)
 #undef NSX_RX

@@ -109,7 +109,8 @@ struct Job {
     uint64_t lo, hi;            // segment index range of the shard
     const uint32_t* h_partial;
     uint16_t* h_out;            // checksum mode: one raw sum per segment
-    uint64_t* h_mask;           // receive mode (nsx_rx_ipv4_tcp_verify_host): one validity bit per frame
+    uint64_t* h_mask;           // receive mode (nsx_rx_ipv*_tcp_verify_host): one validity bit per frame
+    int ipver;                  // receive mode: 4 or 6
     int dev;
     int slot;  // shard slot on the device (its own DevCtx: streams + staging)
     const nsx_tune* tune;
@@ -282,8 +283,8 @@ void run_job(Job* j) {
             uint64_t* d_off = ctx->d_off[s].as<uint64_t>();
             for (uint64_t i = 0; i <= cn; ++i) h_offstage[i] = j->h_offsets[c.c0 + i] - c.byte_lo;
             NSX_TRY(hipMemcpyAsync(d_off, h_offstage, (cn + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st[s]));
-            e = rx ? nsx::launch_rx_ipv4_tcp(cfg, d_data, d_off, cn, reinterpret_cast<uint64_t*>(d_out), nullptr,
-                                             nullptr, st[s])
+            e = rx ? nsx::launch_rx_tcp(cfg, j->ipver, d_data, d_off, cn, reinterpret_cast<uint64_t*>(d_out),
+                                        nullptr, nullptr, st[s])
                    : nsx::launch_ragged(cfg, d_data, d_off, cn, d_part, d_out, nullptr, st[s]);
         } else {
             e = nsx::launch_fixed(cfg, d_data, j->stride, j->seg_len, cn, d_part, d_out, st[s]);
@@ -309,7 +310,8 @@ done:
 // Shards: num_gpus × shards_per_device contiguous ranges (byte-balanced for ragged batches); shard g runs on
 // device g / shards_per_device in slot g % shards_per_device, one host thread per shard.
 int run_sharded(const uint8_t* h_base, uint64_t stride, uint32_t seg_len, const uint64_t* h_offsets, uint64_t n,
-                const uint32_t* h_partial, uint16_t* h_out, uint64_t* h_mask, int num_gpus, const nsx_tune* tune) {
+                const uint32_t* h_partial, uint16_t* h_out, uint64_t* h_mask, int ipver, int num_gpus,
+                const nsx_tune* tune) {
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess) {
         (void)hipGetLastError();
@@ -332,8 +334,8 @@ int run_sharded(const uint8_t* h_base, uint64_t stride, uint32_t seg_len, const 
         for (int g = 1; g < parts; ++g) bounds[g] = std::min<uint64_t>(n, (bounds[g] + 63) / 64 * 64);
     std::vector<Job> jobs(parts);
     for (int g = 0; g < parts; ++g)
-        jobs[g] = Job{h_base, stride, seg_len, h_offsets, bounds[g], bounds[g + 1], h_partial, h_out, h_mask, g / spd,
-                      g % spd, tune, NSX_OK};
+        jobs[g] = Job{h_base,  stride, seg_len, h_offsets, bounds[g], bounds[g + 1], h_partial, h_out, h_mask, ipver,
+                      g / spd, g % spd, tune,    NSX_OK};
     std::vector<std::thread> th;
     for (int g = 1; g < parts; ++g)
         if (jobs[g].hi > jobs[g].lo) th.emplace_back(run_job, &jobs[g]);
@@ -359,7 +361,7 @@ int nsx_csum_fixed_host_tuned(const uint8_t* h_base, uint64_t stride, uint32_t s
                               const nsx_tune* tune) {
     if (n == 0) return NSX_OK;
     if (!h_out || (seg_len && !h_base)) return NSX_EINVAL;
-    return run_sharded(h_base, stride, seg_len, nullptr, n, h_prefix_partial, h_out, nullptr, num_gpus, tune);
+    return run_sharded(h_base, stride, seg_len, nullptr, n, h_prefix_partial, h_out, nullptr, 0, num_gpus, tune);
 }
 
 int nsx_csum_ragged_host(const uint8_t* h_base, const uint64_t* h_offsets, uint64_t n,
@@ -374,7 +376,7 @@ int nsx_csum_ragged_host_tuned(const uint8_t* h_base, const uint64_t* h_offsets,
     if (!h_out || !h_offsets || !h_base) return NSX_EINVAL;
     for (uint64_t i = 0; i < n; ++i)
         if (h_offsets[i + 1] < h_offsets[i]) return NSX_EINVAL;
-    return run_sharded(h_base, 0, 0, h_offsets, n, h_prefix_partial, h_out, nullptr, num_gpus, tune);
+    return run_sharded(h_base, 0, 0, h_offsets, n, h_prefix_partial, h_out, nullptr, 0, num_gpus, tune);
 }
 
 int nsx_rx_ipv4_tcp_verify_host(const uint8_t* h_base, const uint64_t* h_offsets, uint64_t n, uint64_t* h_mask,
@@ -382,13 +384,28 @@ int nsx_rx_ipv4_tcp_verify_host(const uint8_t* h_base, const uint64_t* h_offsets
     return nsx_rx_ipv4_tcp_verify_host_tuned(h_base, h_offsets, n, h_mask, num_gpus, nullptr);
 }
 
-int nsx_rx_ipv4_tcp_verify_host_tuned(const uint8_t* h_base, const uint64_t* h_offsets, uint64_t n, uint64_t* h_mask,
-                                      int num_gpus, const nsx_tune* tune) {
+static int rx_host(int ipver, const uint8_t* h_base, const uint64_t* h_offsets, uint64_t n, uint64_t* h_mask,
+                   int num_gpus, const nsx_tune* tune) {
     if (n == 0) return NSX_OK;
     if (!h_mask || !h_offsets || !h_base) return NSX_EINVAL;
     for (uint64_t i = 0; i < n; ++i)
         if (h_offsets[i + 1] < h_offsets[i]) return NSX_EINVAL;
-    return run_sharded(h_base, 0, 0, h_offsets, n, nullptr, nullptr, h_mask, num_gpus, tune);
+    return run_sharded(h_base, 0, 0, h_offsets, n, nullptr, nullptr, h_mask, ipver, num_gpus, tune);
+}
+
+int nsx_rx_ipv4_tcp_verify_host_tuned(const uint8_t* h_base, const uint64_t* h_offsets, uint64_t n, uint64_t* h_mask,
+                                      int num_gpus, const nsx_tune* tune) {
+    return rx_host(4, h_base, h_offsets, n, h_mask, num_gpus, tune);
+}
+
+int nsx_rx_ipv6_tcp_verify_host(const uint8_t* h_base, const uint64_t* h_offsets, uint64_t n, uint64_t* h_mask,
+                                int num_gpus) {
+    return rx_host(6, h_base, h_offsets, n, h_mask, num_gpus, nullptr);
+}
+
+int nsx_rx_ipv6_tcp_verify_host_tuned(const uint8_t* h_base, const uint64_t* h_offsets, uint64_t n, uint64_t* h_mask,
+                                      int num_gpus, const nsx_tune* tune) {
+    return rx_host(6, h_base, h_offsets, n, h_mask, num_gpus, tune);
 }
 
 int nsx_host_cache_release(void) {

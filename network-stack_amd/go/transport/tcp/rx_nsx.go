@@ -1,10 +1,11 @@
 //go:build nsx
 
 // Receive-side batch verification over the MI355X library: received IPv4
-// datagrams carrying TCP are packed into pinned staging and checked in one
-// GPU pass (nsx_rx_ipv4_tcp_verify_host): the IPv4 header checksum, the
-// pseudo-header built from the header's own addresses (ip.Addr.Raw(),
-// network/ip/v4/ipv4.go:15; ip.NextProtoTCP, network/ip/protocols.go:8), and
+// datagrams (or IPv6 packets) carrying TCP are packed into pinned staging and
+// checked in one GPU pass (nsx_rx_ipv4_tcp_verify_host /
+// nsx_rx_ipv6_tcp_verify_host): the IPv4 header checksum, the pseudo-header
+// built from the header's own addresses (ip.Addr.Raw(), network/ip/v4/ipv4.go:15,
+// network/ip/v6/ipv6.go:16; ip.NextProtoTCP, network/ip/protocols.go:8), and
 // computeChecksum(pseudo) == 0xFFFF over the segment (tcp.go:70, :72-95).
 package tcp
 
@@ -23,6 +24,17 @@ import (
 // minSegmentLength bytes (tcp.go:131) whose header and TCP checksums both
 // verify. numGPUs 0 = all visible GPUs.
 func VerifyDatagrams(frames [][]byte, numGPUs int) ([]bool, error) {
+	return verifyFrames(frames, numGPUs, 4)
+}
+
+// VerifyPackets6 is VerifyDatagrams for IPv6 packets whose fixed header is
+// followed directly by TCP (Next Header 6): the TCP checksum over the RFC 8200
+// pseudo-header must verify (IPv6 has no header checksum).
+func VerifyPackets6(frames [][]byte, numGPUs int) ([]bool, error) {
+	return verifyFrames(frames, numGPUs, 6)
+}
+
+func verifyFrames(frames [][]byte, numGPUs int, ipver int) ([]bool, error) {
 	total := 0
 	for _, f := range frames {
 		total += len(f)
@@ -43,10 +55,16 @@ func VerifyDatagrams(frames [][]byte, numGPUs int) ([]bool, error) {
 		return ok, nil
 	}
 	mask := make([]uint64, (n+63)/64)
-	rc := C.nsx_rx_ipv4_tcp_verify_host((*C.uint8_t)(b.base), (*C.uint64_t)(unsafe.Pointer(&b.offsets[0])),
-		C.uint64_t(n), (*C.uint64_t)(unsafe.Pointer(&mask[0])), C.int(numGPUs))
+	base, offs := (*C.uint8_t)(b.base), (*C.uint64_t)(unsafe.Pointer(&b.offsets[0]))
+	words := (*C.uint64_t)(unsafe.Pointer(&mask[0]))
+	var rc C.int
+	if ipver == 6 {
+		rc = C.nsx_rx_ipv6_tcp_verify_host(base, offs, C.uint64_t(n), words, C.int(numGPUs))
+	} else {
+		rc = C.nsx_rx_ipv4_tcp_verify_host(base, offs, C.uint64_t(n), words, C.int(numGPUs))
+	}
 	if rc != C.NSX_OK {
-		return nil, fmt.Errorf("nsx_rx_ipv4_tcp_verify_host: %s", C.GoString(C.nsx_strerror(rc)))
+		return nil, fmt.Errorf("nsx_rx_ipv%d_tcp_verify_host: %s", ipver, C.GoString(C.nsx_strerror(rc)))
 	}
 	for i := range ok {
 		ok[i] = mask[i/64]>>(uint(i)%64)&1 == 1

@@ -85,6 +85,10 @@ def lib() -> ctypes.CDLL:
             "nsx_rx_ipv4_tcp_verify_dev_tuned": [vp, vp, u64, vp, vp, vp, vp, vp],
             "nsx_rx_ipv4_tcp_verify_host": [vp, vp, u64, vp, i32],
             "nsx_rx_ipv4_tcp_verify_host_tuned": [vp, vp, u64, vp, i32, vp],
+            "nsx_rx_ipv6_tcp_verify_dev": [vp, vp, u64, vp, vp, vp],
+            "nsx_rx_ipv6_tcp_verify_dev_tuned": [vp, vp, u64, vp, vp, vp, vp],
+            "nsx_rx_ipv6_tcp_verify_host": [vp, vp, u64, vp, i32],
+            "nsx_rx_ipv6_tcp_verify_host_tuned": [vp, vp, u64, vp, i32, vp],
             "nsx_tcp_build_dev": [vp, vp, vp, vp, vp, u64, vp, u64, vp, vp, vp, vp],
             "nsx_tcp_layout_host": [vp, vp, u64, vp],
             "nsx_abi_version": [],
@@ -197,15 +201,22 @@ def ragged_host(buf: np.ndarray, offsets: np.ndarray, partial: np.ndarray | None
     return out
 
 
-def rx_ipv4_tcp_verify_host(buf: np.ndarray, offsets: np.ndarray, num_gpus: int = 0, tune=None) -> np.ndarray:
-    """Fused receive pass over host-resident datagrams: the validity bitmask (uint64[ceil(n/64)])."""
+def rx_ipv4_tcp_verify_host(buf: np.ndarray, offsets: np.ndarray, num_gpus: int = 0, tune=None,
+                            ipver: int = 4) -> np.ndarray:
+    """Fused receive pass over host-resident datagrams (IPv4, or IPv6 with ipver=6): the validity bitmask
+    (uint64[ceil(n/64)])."""
     buf = np.ascontiguousarray(buf, np.uint8)
     offsets = np.ascontiguousarray(offsets, np.uint64)
     n = offsets.size - 1
     mask = np.zeros((max(n, 0) + 63) // 64, np.uint64)
-    _check(lib().nsx_rx_ipv4_tcp_verify_host_tuned(_np_ptr(buf), _np_ptr(offsets), n, _np_ptr(mask), num_gpus,
-                                                   _tune(tune)), "nsx_rx_ipv4_tcp_verify_host")
+    name = "nsx_rx_ipv6_tcp_verify_host" if ipver == 6 else "nsx_rx_ipv4_tcp_verify_host"
+    _check(getattr(lib(), name + "_tuned")(_np_ptr(buf), _np_ptr(offsets), n, _np_ptr(mask), num_gpus, _tune(tune)),
+           name)
     return mask
+
+
+def rx_ipv6_tcp_verify_host(buf: np.ndarray, offsets: np.ndarray, num_gpus: int = 0, tune=None) -> np.ndarray:
+    return rx_ipv4_tcp_verify_host(buf, offsets, num_gpus, tune, ipver=6)
 
 
 class PinnedBuffer:
@@ -321,6 +332,18 @@ def rx_ipv4_tcp_verify_dev(buf, offsets, mask=None, ip_raw=None, tcp_raw=None, s
     _check(lib().nsx_rx_ipv4_tcp_verify_dev_tuned(_dev_ptr(buf), _dev_ptr(offsets), n, _dev_ptr(mask),
                                                   _dev_ptr(ip_raw), _dev_ptr(tcp_raw), _stream(stream), _tune(tune)),
            "nsx_rx_ipv4_tcp_verify_dev")
+    return mask
+
+
+def rx_ipv6_tcp_verify_dev(buf, offsets, mask=None, tcp_raw=None, stream=None, tune=None):
+    """Fused receive pass over packed IPv6/TCP packets: validity bitmask (+ optional raw TCP sums)."""
+    import torch
+    n = offsets.numel() - 1
+    if mask is None:
+        mask = torch.empty((max(n, 0) + 63) // 64, dtype=torch.int64, device=offsets.device)  # u64 bits
+    _check(lib().nsx_rx_ipv6_tcp_verify_dev_tuned(_dev_ptr(buf), _dev_ptr(offsets), n, _dev_ptr(mask),
+                                                  _dev_ptr(tcp_raw), _stream(stream), _tune(tune)),
+           "nsx_rx_ipv6_tcp_verify_dev")
     return mask
 
 

@@ -370,6 +370,45 @@ ORACLE_EXPORT void oracle_go_rx_ipv4_tcp(const uint8_t* base, const uint64_t* of
     }
 }
 
+/* Frame i: an IPv6 packet (RFC 8200 §3, fixed 40-byte header) carrying TCP
+ * directly. The checks of nsx_rx_ipv6_tcp_verify_dev:
+ *   tcp_raw = computeChecksum(pseudo) over the payload (tcp.go:72-95), pseudo =
+ *             src(16) dst(16) len(4) 0 0 0 6 (RFC 8200 §8.1) from the header's own
+ *             addresses (ip.Addr.Raw(), network/ip/v6/ipv6.go:16; ip.NextProtoTCP,
+ *             protocols.go:8), when the frame holds >= 40 bytes, version 6,
+ *             40 + payload length == frame length, Next Header 6 and a payload of
+ *             >= 20 bytes (tcp.go:131); else 0;
+ *   bit i   = those checks apply and tcp_raw == 0xFFFF (tcp.go:70).
+ * mask holds ceil(n/64) words; tcp_raw nullable. */
+ORACLE_EXPORT void oracle_go_rx_ipv6_tcp(const uint8_t* base, const uint64_t* offsets, uint64_t n, uint64_t* mask,
+                                         uint16_t* tcp_raw) {
+    memset(mask, 0, (size_t)((n + 63) / 64) * 8);
+    for (uint64_t i = 0; i < n; i++) {
+        const uint8_t* p = base + offsets[i];
+        const uint64_t len = offsets[i + 1] - offsets[i];
+        uint32_t tcpr = 0;
+        int valid = 0;
+        if (len >= 40) {
+            const uint32_t plen = ((uint32_t)p[4] << 8) | p[5];
+            if ((p[0] >> 4) == 6 && 40u + plen == len && p[6] == 6 && plen >= 20) {
+                uint8_t pseudo[40];
+                memcpy(pseudo, p + 8, 16);       /* src: ip.Addr.Raw() */
+                memcpy(pseudo + 16, p + 24, 16); /* dst */
+                pseudo[32] = 0;
+                pseudo[33] = 0;
+                pseudo[34] = (uint8_t)(plen >> 8);
+                pseudo[35] = (uint8_t)plen;
+                pseudo[36] = pseudo[37] = pseudo[38] = 0;
+                pseudo[39] = 6;                  /* ip.NextProtoTCP */
+                tcpr = oracle_go_checksum(pseudo, 40, p + 40, plen);
+                valid = tcpr == 0xFFFFu;
+            }
+        }
+        if (tcp_raw) tcp_raw[i] = (uint16_t)tcpr;
+        if (valid) mask[i / 64] |= 1ull << (i % 64);
+    }
+}
+
 /* ---- synthetic data: splitmix64 stream, counter-based ---- */
 static inline uint64_t splitmix64_at(uint64_t seed, uint64_t i) {
     uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;

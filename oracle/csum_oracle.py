@@ -254,6 +254,37 @@ def ipv4_tcp_frame(seg: bytes, src: bytes, dst: bytes, ident: int = 0, ttl: int 
     return bytes(h) + bytes(seg)
 
 
+def rx_ipv6_tcp(frame: bytes) -> tuple:
+    """One received IPv6 packet through nsx_rx_ipv6_tcp_verify_dev's checks, pure Python: (tcp_raw, valid).
+    RFC 8200 §3 fixed header, Next Header 6 directly (no extension headers walked); the pseudo-header (RFC 8200
+    §8.1) from the packet's own addresses (ipv6.go:16 Raw) and ip.NextProtoTCP = 6 (protocols.go:8); a segment
+    is at least 20 bytes (tcp.go:131); the receiver accepts iff the sum is 0xFFFF (tcp.go:70)."""
+    f = bytes(frame)
+    if len(f) < 40:
+        return 0, False
+    plen = int.from_bytes(f[4:6], "big")
+    if f[0] >> 4 != 6 or 40 + plen != len(f) or f[6] != 6 or plen < 20:
+        return 0, False
+    tcpr = go_checksum(ipv6_pseudo_header(f[8:24], f[24:40], 6, plen), f[40:])
+    return tcpr, tcpr == 0xFFFF
+
+
+def ipv6_tcp_frame(seg: bytes, src: bytes, dst: bytes, hop: int = 64, flow: int = 0, tclass: int = 0,
+                   fix_tcp: bool = True) -> bytes:
+    """An IPv6 packet carrying the TCP segment `seg` (RFC 8200 §3 header, Next Header 6), with — when fix_tcp —
+    the segment's checksum field (bytes 16-17) set to ^computeChecksum(pseudo) over the segment with the field
+    zeroed (tcp.go:68-71, :110)."""
+    assert len(src) == 16 and len(dst) == 16 and len(seg) < 1 << 16
+    seg = bytearray(seg)
+    if fix_tcp and len(seg) >= 18:
+        seg[16:18] = b"\0\0"
+        raw = go_checksum(ipv6_pseudo_header(src, dst, 6, len(seg)), bytes(seg))
+        seg[16:18] = field_value(raw).to_bytes(2, "big")
+    h = ((6 << 28) | ((tclass & 0xFF) << 20) | (flow & 0xFFFFF)).to_bytes(4, "big") + len(seg).to_bytes(2, "big") + \
+        bytes([6, hop & 0xFF]) + bytes(src) + bytes(dst)
+    return h + bytes(seg)
+
+
 # ---------------------------------------------------------------------------
 # C restatement (oracle/csum_oracle.c) via ctypes
 # ---------------------------------------------------------------------------
@@ -286,6 +317,7 @@ def c_oracle():
                                               u8p, ctypes.c_size_t, u8p]
         lib.oracle_go_batch_ragged.argtypes = [u8p, u8p, ctypes.c_uint64, u8p, ctypes.c_size_t, u8p]
         lib.oracle_go_rx_ipv4_tcp.argtypes = [u8p, u8p, ctypes.c_uint64, u8p, u8p, u8p]
+        lib.oracle_go_rx_ipv6_tcp.argtypes = [u8p, u8p, ctypes.c_uint64, u8p, u8p]
         lib.oracle_splitmix64_fill.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]
         lib.oracle_go_tcp_build_batch.argtypes = [u8p] * 10 + [u8p, ctypes.c_size_t, ctypes.c_uint64, u8p, u8p, u8p]
         lib.oracle_go_tcp_build_batch.restype = ctypes.c_int
@@ -402,6 +434,18 @@ def c_rx_ipv4_tcp(buf: np.ndarray, offsets: np.ndarray):
     c_oracle().oracle_go_rx_ipv4_tcp(_ptr(buf if buf.size else np.zeros(1, np.uint8)), _ptr(offsets), n, _ptr(mask),
                                      _ptr(ipr), _ptr(tcpr))
     return mask, ipr, tcpr
+
+
+def c_rx_ipv6_tcp(buf: np.ndarray, offsets: np.ndarray):
+    """oracle_go_rx_ipv6_tcp over a packed packet batch: (mask u64[ceil(n/64)], tcp_raw u16[n])."""
+    buf = np.ascontiguousarray(buf, np.uint8)
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    n = offsets.size - 1
+    mask = np.zeros((n + 63) // 64, np.uint64)
+    tcpr = np.empty(n, np.uint16)
+    c_oracle().oracle_go_rx_ipv6_tcp(_ptr(buf if buf.size else np.zeros(1, np.uint8)), _ptr(offsets), n, _ptr(mask),
+                                     _ptr(tcpr))
+    return mask, tcpr
 
 
 def c_splitmix64(seed: int, nbytes: int, byte_off: int = 0) -> np.ndarray:

@@ -72,10 +72,54 @@ def frame(rng, kind: str, max_payload: int = 1460) -> bytes:
     return bytes(f)
 
 
-def batch(rng, n: int, kinds=KINDS, weights=None, lead: int = 0, max_payload: int = 1460):
-    """(buf uint8, offsets uint64[n+1], kinds list): n frames packed back to back behind `lead` bytes."""
+KINDS6 = ("valid", "bad_tcp_sum", "bad_addr", "udp", "ext_header", "len_short", "len_long", "version4", "short",
+          "tcp_lt20", "empty", "header_only", "odd_payload", "jumbo")
+VALID6 = ("valid", "header_only", "odd_payload")
+
+
+def frame6(rng, kind: str, max_payload: int = 1440) -> bytes:
+    """An IPv6 packet (RFC 8200 §3) carrying a TCP segment serialised by Segment.bytes(), valid or broken in
+    every way nsx_rx_ipv6_tcp_verify_dev distinguishes."""
+    src, dst = rng.integers(0, 256, 16, dtype=np.uint8).tobytes(), rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+    payload = int(rng.integers(0, max_payload + 1))
+    if kind == "odd_payload":
+        payload |= 1
+    if kind == "header_only":
+        payload = 0
+    if kind == "short":
+        return rng.integers(0, 256, int(rng.integers(1, 40)), dtype=np.uint8).tobytes()
+    if kind == "empty":
+        return b""
+    if kind == "tcp_lt20":
+        seg = rng.integers(0, 256, int(rng.integers(0, 20)), dtype=np.uint8).tobytes()
+        return O.ipv6_tcp_frame(seg, src, dst)
+    f = bytearray(O.ipv6_tcp_frame(_segment(rng, payload), src, dst, hop=int(rng.integers(256)),
+                                   flow=int(rng.integers(1 << 20)), tclass=int(rng.integers(256))))
+    if kind == "bad_tcp_sum":
+        f[40 + int(rng.integers(0, len(f) - 40))] ^= 1 << int(rng.integers(8))
+    elif kind == "bad_addr":  # a flipped address bit breaks the pseudo-header sum
+        f[8 + int(rng.integers(0, 32))] ^= 1 << int(rng.integers(8))
+    elif kind == "udp":
+        f[6] = 17
+    elif kind == "ext_header":  # hop-by-hop options header: not walked, so not accepted
+        f[6] = 0
+    elif kind == "len_short":  # the frame holds more than 40 + payload length
+        f += bytes([int(rng.integers(256))])
+    elif kind == "len_long":
+        f = f[:-1] if len(f) > 40 else f + b"\0"
+    elif kind == "version4":
+        f[0] = 0x40 | (f[0] & 15)
+    elif kind == "jumbo":  # payload length 0 (RFC 2675 jumbogram form) with a real payload behind it
+        f[4:6] = b"\0\0"
+    return bytes(f)
+
+
+def batch(rng, n: int, kinds=KINDS, weights=None, lead: int = 0, max_payload: int = 1460, ip: int = 4):
+    """(buf uint8, offsets uint64[n+1], kinds list): n frames (IPv4, or IPv6 with ip=6 and kinds=KINDS6) packed
+    back to back behind `lead` bytes."""
     ks = list(rng.choice(kinds, n, p=weights)) if n else []
-    frames = [frame(rng, k, max_payload) for k in ks]
+    make = frame6 if ip == 6 else frame
+    frames = [make(rng, k, max_payload) for k in ks]
     offs = np.zeros(n + 1, np.uint64)
     offs[1:] = np.cumsum([len(f) for f in frames]) if n else []
     offs += np.uint64(lead)

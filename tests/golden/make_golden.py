@@ -189,6 +189,31 @@ def rx(rng):
                   "valid": [bool(v) for v in valid], "mask": [int(x) for x in mask]}
 
 
+def rx6(rng):
+    """Received IPv6/TCP packets of every kind tests/_rx.py builds (KINDS6), packed behind an odd lead.
+    Expected per-packet (tcp_raw, valid) from O.rx_ipv6_tcp, checked against the C restatement."""
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE)))
+    import _rx
+    frames = []
+    for k in _rx.KINDS6:
+        frames += [_rx.frame6(rng, k, max_payload=300) for _ in range(12)]
+    frames = [frames[i] for i in rng.permutation(len(frames))]
+    lead = 5
+    offs = np.zeros(len(frames) + 1, np.uint64)
+    offs[1:] = np.cumsum([len(f) for f in frames])
+    offs += np.uint64(lead)
+    blob = bytes(range(lead)) + b"".join(frames)
+    res = [O.rx_ipv6_tcp(f) for f in frames]
+    mask, tcpr = O.c_rx_ipv6_tcp(np.frombuffer(blob, np.uint8), offs)
+    valid = np.array([v for _, v in res])
+    pad = np.zeros((len(frames) + 63) // 64 * 64, np.uint8)
+    pad[:len(frames)] = valid
+    assert np.array_equal(mask, np.packbits(pad, bitorder="little").view(np.uint64))
+    assert tcpr.tolist() == [a for a, _ in res]
+    return blob, {"offsets": [int(x) for x in offs], "tcp_raw": tcpr.tolist(), "valid": [bool(v) for v in valid],
+                  "mask": [int(x) for x in mask]}
+
+
 def main():
     rng = np.random.default_rng(0x1071)
     with open(os.path.join(HERE, "kat.json"), "w") as f:
@@ -210,6 +235,12 @@ def main():
         f.write(xblob)
     with open(os.path.join(HERE, "rx.json"), "w") as f:
         json.dump(xmeta, f)
+    x6blob, x6meta = rx6(np.random.default_rng(0x1079))
+    with open(os.path.join(HERE, "rx6.bin"), "wb") as f:
+        f.write(x6blob)
+    with open(os.path.join(HERE, "rx6.json"), "w") as f:
+        json.dump(x6meta, f)
+    print(f"rx6: {len(x6meta['valid'])} packets ({sum(x6meta['valid'])} valid), {len(x6blob)} B")
     print(f"vectors: {len(idx)} cases, {len(blob)} B; ragged: {len(rmeta['raw'])} segments, {len(rblob)} B; "
           f"rx: {len(xmeta['valid'])} frames ({sum(xmeta['valid'])} valid), {len(xblob)} B")
 

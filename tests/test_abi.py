@@ -38,7 +38,7 @@ def test_header_declares_the_boundary():
 def test_library_exports_every_declared_symbol():
     L = nsx.lib()
     declared = declared_functions() + declared_functions(TUNE_HEADER)
-    assert len(declared_functions(TUNE_HEADER)) == 11
+    assert len(declared_functions(TUNE_HEADER)) == 13
     missing = [n for n in declared if not hasattr(L, n)]
     assert not missing, missing
     out = subprocess.run(["nm", "-D", "--defined-only", nsx.LIB_PATH], capture_output=True, text=True).stdout
@@ -202,9 +202,12 @@ def test_device_calls_fail_loudly_without_gpu():
         nsx.fixed_host(buf, 1500, 1500, 2, tune=dict(shards_per_device=3))
     assert e.value.code == nsx.NSX_ENODEV
     assert L.nsx_rx_ipv4_tcp_verify_dev(fake, fake, 4, fake, None, None, None) == nsx.NSX_ENODEV
-    with pytest.raises(nsx.NsxError) as e:
-        nsx.rx_ipv4_tcp_verify_host(buf, np.array([0, 100, 3000], np.uint64))
-    assert e.value.code == nsx.NSX_ENODEV
+    assert L.nsx_rx_ipv6_tcp_verify_dev(fake, fake, 4, fake, None, None) == nsx.NSX_ENODEV
+    assert L.nsx_rx_ipv6_tcp_verify_dev_tuned(fake, fake, 4, fake, None, None, tune) == nsx.NSX_ENODEV
+    for v in (4, 6):
+        with pytest.raises(nsx.NsxError) as e:
+            nsx.rx_ipv4_tcp_verify_host(buf, np.array([0, 100, 3000], np.uint64), ipver=v)
+        assert e.value.code == nsx.NSX_ENODEV
     p = ctypes.c_void_p()
     assert L.nsx_alloc_pinned(64, ctypes.byref(p)) == nsx.NSX_ENODEV
     assert L.nsx_host_cache_release() == 0  # nothing cached, nothing to do

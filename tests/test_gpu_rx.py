@@ -126,3 +126,98 @@ def test_rx_host_batches_sharded(shards):
     assert np.array_equal(got, want), shards
     small = nsx.rx_ipv4_tcp_verify_host(buf0, offs0, tune=dict(shards_per_device=shards))
     assert np.array_equal(small, O.c_rx_ipv4_tcp(buf0, offs0)[0])
+
+
+# ------------------------------------------------------------------ IPv6 (nsx_rx_ipv6_tcp_verify_dev)
+
+def run_rx6(buf, offs, tune=None):
+    n = offs.size - 1
+    mask = torch.full(((n + 63) // 64,), 0x5A5A5A5A5A5A5A5A, dtype=torch.int64, device="cuda")
+    tcpr = torch.empty(n, dtype=torch.int16, device="cuda")
+    nsx.rx_ipv6_tcp_verify_dev(dev(buf), dev(offs.view(np.int64)), mask=mask, tcp_raw=tcpr, tune=tune)
+    return host(mask).view(np.uint64), u16(tcpr)
+
+
+def test_rx6_golden_packets():
+    meta = json.load(open(os.path.join(GOLDEN, "rx6.json")))
+    blob = np.fromfile(os.path.join(GOLDEN, "rx6.bin"), np.uint8)
+    mask, tcpr = run_rx6(blob, np.array(meta["offsets"], np.uint64))
+    assert mask.tolist() == meta["mask"]
+    assert tcpr.tolist() == meta["tcp_raw"]
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 129, 1000, 4099])
+@pytest.mark.parametrize("lead", [0, 1, 2, 3])
+def test_rx6_mixed_batches(n, lead):
+    rng = np.random.default_rng(n * 8 + lead + 1)
+    buf, offs, kinds = _rx.batch(rng, n, kinds=_rx.KINDS6, lead=lead, max_payload=1440, ip=6)
+    want = O.c_rx_ipv6_tcp(buf, offs)
+    got = run_rx6(buf, offs)
+    for w, g, what in zip(want, got, ("mask", "tcp_raw")):
+        assert np.array_equal(w, g), (what, n, lead)
+
+
+@pytest.mark.parametrize("tune", TUNES, ids=lambda t: ",".join(f"{k}={v}" for k, v in t.items()))
+def test_rx6_launch_shapes(tune):
+    rng = np.random.default_rng(0x7E6)
+    buf, offs, _ = _rx.batch(rng, 20_000, kinds=_rx.KINDS6, lead=3, max_payload=1440, ip=6)
+    want = O.c_rx_ipv6_tcp(buf, offs)
+    got = run_rx6(buf, offs, tune)
+    for w, g in zip(want, got):
+        assert np.array_equal(w, g), tune
+
+
+def test_rx6_maximum_packets_and_junk():
+    """Packets at the 16-bit payload length limit (65535 B of TCP), runs of empty frames, and a 4 MB junk
+    frame in the middle: its neighbours still verify."""
+    rng = np.random.default_rng(0x7F6)
+    frames = []
+    for i in range(500):
+        r = i % 5
+        if r == 0:
+            frames.append(O.ipv6_tcp_frame(_rx._segment(rng, 65535 - 20 - (i % 3)), rng.bytes(16), rng.bytes(16)))
+        elif r == 1:
+            frames.append(b"")
+        else:
+            frames.append(_rx.frame6(rng, "valid", max_payload=9000))
+    frames.insert(250, rng.integers(0, 256, 4 << 20, dtype=np.uint8).tobytes())
+    offs = np.zeros(len(frames) + 1, np.uint64)
+    offs[1:] = np.cumsum([len(f) for f in frames])
+    buf = np.frombuffer(b"".join(frames) + bytes(3), np.uint8)
+    want = O.c_rx_ipv6_tcp(buf, offs)
+    got = run_rx6(buf, offs)
+    for w, g in zip(want, got):
+        assert np.array_equal(w, g)
+    bits = np.unpackbits(want[0].view(np.uint8), bitorder="little")
+    assert bits[:len(frames)].sum() == sum(1 for i, f in enumerate(frames) if len(f) and i != 250)
+
+
+def test_rx6_bench_workload_full_size():
+    """The bench's workload 11 at full size: the device mask equals the oracle's, and exactly the corrupted
+    packets fail."""
+    import bench
+    cfg = bench.WORKLOADS[11]
+    w = bench.build_workload(cfg, 0, torch.device("cuda", 0))
+    w["step"]()
+    got = host(w["out"]).view(np.uint64)
+    want, _ = O.c_rx_ipv6_tcp(host(w["buf"]), w["offsets"])
+    assert np.array_equal(got, want)
+    n = cfg["n"]
+    valid = np.ones(n, bool)
+    valid[::1000] = False
+    pad = np.zeros((n + 63) // 64 * 64, np.uint8)
+    pad[:n] = valid
+    assert np.array_equal(got, np.packbits(pad, bitorder="little").view(np.uint64))
+
+
+@pytest.mark.parametrize("shards", [1, 3])
+def test_rx6_host_batches_sharded(shards):
+    rng = np.random.default_rng(0x90 + shards)
+    buf0, offs0, _ = _rx.batch(rng, 4999, kinds=_rx.KINDS6, lead=0, max_payload=1440, ip=6)
+    reps = 30
+    span = int(offs0[-1])
+    buf = np.concatenate([buf0[:span]] * reps + [np.zeros(3, np.uint8)])
+    offs = np.concatenate([offs0[:-1] + np.uint64(k * span) for k in range(reps)] + [np.array([reps * span], np.uint64)])
+    want, _ = O.c_rx_ipv6_tcp(buf, offs)
+    got = nsx.rx_ipv6_tcp_verify_host(buf, offs, tune=dict(shards_per_device=shards))
+    assert np.array_equal(got, want), shards

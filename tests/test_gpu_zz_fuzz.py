@@ -229,3 +229,26 @@ def test_fuzz_rx(case):
     if case % 4 == 0:
         assert np.array_equal(nsx.rx_ipv4_tcp_verify_host(buf, offs, tune=dict(shards_per_device=1 + case % 3)),
                               want_m), case
+
+
+@pytest.mark.parametrize("case", range(30 * SCALE))
+def test_fuzz_rx6(case):
+    """The IPv6 receive pass over random packet batches (every kind of tests/_rx.py's KINDS6 in random
+    proportions, random alignment, sizes and launch shapes), device and host entry points, against
+    oracle_go_rx_ipv6_tcp."""
+    import _rx
+    rng = np.random.default_rng(7000 + case)
+    n = int(rng.choice([int(rng.integers(1, 70)), int(rng.integers(60, 700)), int(rng.integers(500, 3000))]))
+    w = rng.random(len(_rx.KINDS6)) ** 3
+    buf, offs, _ = _rx.batch(rng, n, kinds=_rx.KINDS6, weights=w / w.sum(), lead=int(rng.integers(0, 8)),
+                             max_payload=int(rng.choice([64, 600, 1440, 9000])), ip=6)
+    want_m, want_t = O.c_rx_ipv6_tcp(buf, offs)
+    tune = dict(rows=int(rng.choice([0, 2, 4, 8, 16])), blocks_per_cu=int(rng.choice([0, 1, 2, 8])))
+    mask = torch.empty((n + 63) // 64, dtype=torch.int64, device="cuda")
+    tcpr = torch.empty(n, dtype=torch.int16, device="cuda")
+    nsx.rx_ipv6_tcp_verify_dev(_dev(buf), _dev(offs.view(np.int64)), mask=mask, tcp_raw=tcpr, tune=tune)
+    assert np.array_equal(mask.cpu().numpy().view(np.uint64), want_m), (case, n, tune)
+    assert np.array_equal(_u16(tcpr), want_t), (case, n, tune)
+    if case % 4 == 0:
+        assert np.array_equal(nsx.rx_ipv6_tcp_verify_host(buf, offs, tune=dict(shards_per_device=1 + case % 3)),
+                              want_m), case

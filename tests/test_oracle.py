@@ -283,6 +283,51 @@ def test_rx_rfc791_header_is_not_tcp():
     assert O.rx_ipv4_tcp(bytes(h) + bytes(0x73 - 20))[2] is False
 
 
+def test_rx6_golden_fixture_both_restatements():
+    meta = load("rx6.json")
+    blob = np.fromfile(os.path.join(GOLDEN, "rx6.bin"), np.uint8)
+    offs = np.array(meta["offsets"], np.uint64)
+    mask, tcpr = O.c_rx_ipv6_tcp(blob, offs)
+    assert mask.tolist() == meta["mask"] and tcpr.tolist() == meta["tcp_raw"]
+    for i in range(offs.size - 1):
+        f = blob[int(offs[i]):int(offs[i + 1])].tobytes()
+        assert O.rx_ipv6_tcp(f) == (meta["tcp_raw"][i], meta["valid"][i]), i
+    assert 0 < sum(meta["valid"]) < len(meta["valid"])
+
+
+def test_rx6_rules_per_kind():
+    """Every IPv6 kind lands on the side of the check it should; a valid packet's TCP sum re-verifies through
+    the wide-form sum over the RFC 8200 §8.1 pseudo-header built by hand (independent of rx_ipv6_tcp's slicing),
+    and malformed packets report tcp_raw 0."""
+    import _rx
+    rng = np.random.default_rng(0x7A)
+    for kind in _rx.KINDS6:
+        for _ in range(20):
+            f = _rx.frame6(rng, kind, max_payload=200)
+            tcpr, ok = O.rx_ipv6_tcp(f)
+            assert ok == (kind in _rx.VALID6), (kind, f.hex())
+            if kind in _rx.VALID6:
+                pseudo = f[8:40] + (len(f) - 40).to_bytes(4, "big") + b"\0\0\0\x06"
+                assert O.fold_checksum(pseudo, f[40:]) == 0xFFFF
+            if kind in ("short", "empty", "udp", "ext_header", "len_short", "len_long", "version4", "tcp_lt20",
+                        "jumbo"):
+                assert tcpr == 0, kind
+            if kind in ("bad_tcp_sum", "bad_addr"):
+                assert tcpr not in (0, 0xFFFF), kind
+
+
+def test_rx6_c_matches_python_random_batches():
+    import _rx
+    rng = np.random.default_rng(0x7B)
+    for lead in (0, 1, 2, 3):
+        buf, offs, kinds = _rx.batch(rng, 300, kinds=_rx.KINDS6, lead=lead, max_payload=400, ip=6)
+        mask, tcpr = O.c_rx_ipv6_tcp(buf, offs)
+        bits = np.unpackbits(mask.view(np.uint8), bitorder="little")[:300]
+        for i in range(300):
+            a, v = O.rx_ipv6_tcp(buf[int(offs[i]):int(offs[i + 1])].tobytes())
+            assert (tcpr[i], bool(bits[i])) == (a, v), (i, kinds[i])
+
+
 def test_rx_c_matches_python_random_batches():
     import _rx
     rng = np.random.default_rng(0x79)
