@@ -89,6 +89,21 @@ def main():
                      "frames": int(xoffs.size - 1)}
         print(name, json.dumps(res[name]), flush=True)
     xpin.free()
+    buf6, offs6, _ = _rx.batch(np.random.default_rng(0x107A), 4992, kinds=_rx.KINDS6, max_payload=1440, ip=6)
+    span6 = int(offs6[-1])
+    ybuf = np.concatenate([buf6[:span6]] * reps)
+    yoffs = np.concatenate([offs6[:-1] + np.uint64(k * span6) for k in range(reps)] +
+                           [np.array([reps * span6], np.uint64)])
+    want6 = O.c_rx_ipv6_tcp(buf6, offs6)[0]
+    ypin = nsx.PinnedBuffer(ybuf.nbytes)
+    ypin.array[:] = ybuf
+    for name, arr in (("rx6_pinned", ypin.array), ("rx6_pageable", ybuf)):
+        t, out = timed(lambda: nsx.rx_ipv6_tcp_verify_host(arr, yoffs, num_gpus=a.gpus), a.reps)
+        assert np.array_equal(out.reshape(reps, -1), np.tile(want6, (reps, 1))), name
+        res[name] = {"seconds": t, "GB_per_s": ybuf.nbytes / t / 1e9, "GiB_per_s": ybuf.nbytes / t / (1 << 30),
+                     "frames": int(yoffs.size - 1)}
+        print(name, json.dumps(res[name]), flush=True)
+    ypin.free()
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "e2e_host.json"), "w") as f:
         json.dump(res, f, indent=1)
