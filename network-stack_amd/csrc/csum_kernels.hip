@@ -1831,7 +1831,7 @@ __global__ __launch_bounds__(kBlock) void fill_bytes_kernel(uint8_t* __restrict_
 // 1..20 fixed, 0 auto, anything else off (contiguous eighths). Auto: chunks of at most 24 MiB of batch
 // (capped so that there are at least 64 chunks); off when that
 // leaves < 4 tasks a chunk. Contiguous eighths ran 8% slow on some allocations on some boxes; 2^10-2^14-task
-// chunks never did (tools/alloc_study.py).
+// chunks never did (round 1 allocation study).
 static uint32_t deal_clog(int param, uint64_t ntasks, uint64_t task_bytes) {
     if (param >= 1 && param <= 20) return (uint32_t)param;
     if (param != 0) return 0u;
@@ -1894,7 +1894,7 @@ static hipError_t launch_fixed_short(const LaunchCfg& c, const uint8_t* base, ui
                                      hipStream_t st) {
     // Aligned (config 2): the software-pipelined kernel, 8-segment tasks at one block per CU — two register
     // sets of 8 × 2 KiB per wave, a wave per SIMD (config 2 0.2222 → 0.2184 ms, config 5 3.712 → 3.626 ms
-    // against 4-segment tasks at 2 blocks/CU, tools/alloc_study.py). Unaligned: 4-segment tasks, 2 blocks/CU.
+    // against 4-segment tasks at 2 blocks/CU). Unaligned: 4-segment tasks, 2 blocks/CU.
     int u = (c.segs_per_wave == 1 || c.segs_per_wave == 2 || c.segs_per_wave == 4 || c.segs_per_wave == 8)
                 ? c.segs_per_wave : (aligned ? 8 : 4);
     if (nrows == 4 && u > 4) u = 4;
@@ -2094,7 +2094,7 @@ hipError_t launch_ipv4_hdr(const LaunchCfg& c, uint8_t* base, uint64_t stride, u
         }
     };
     if (stride == 20 && hdr_off == 0 && ((uintptr_t)base & 3u) == 0 && c.kernel == 0) {
-        // 1 block/CU with 2 tasks (10 KiB) in flight per wave = 40 KiB per CU (tools/sweep.py: 0.220 ms vs
+        // 1 block/CU with 2 tasks (10 KiB) in flight per wave = 40 KiB per CU (round 1 sweep: 0.220 ms vs
         // 0.232 at 2 blocks/CU, 0.284 at 1 task/wave); chunks keep each launch's results within one
         // descriptor (2^28 headers = 2^22 mask words)
         const uint32_t mb = max_blocks_of(c, 1);
