@@ -76,6 +76,11 @@ WORKLOADS = {
             metric="GiB/s fused TCP segment build (serialize + checksum + field write), wire bytes",
             name="f1+options: 1M TCP segments per GPU, 12B options (NOP NOP kind-2 len 10), 1468B payload -> 1500B wire images, "
                  "IPv4 pseudo-header partials, device-resident"),
+    # not a BASELINE config: f1 with jumbo-frame segments (9000 B MTU: 8960 B TCP segments), images of 9 rows
+    12: dict(kind="tcp_build", n=1 << 18, payload=8940, seed=0x107B,
+             metric="GiB/s fused TCP segment build (serialize + checksum + field write), wire bytes",
+             name="f1 jumbo: 256K option-less TCP segments per GPU, 8940B payload -> 8960B wire images (9000B MTU), "
+                  "IPv4 pseudo-header partials, device-resident"),
     # not a BASELINE config: f3's receive side fused with f2's bitmask (1 bit written per header)
     9: dict(kind="ipv4_hdr", mask=True, n=1 << 26, hdr=20, seed=0x1077,
             metric="GiB/s IPv4 header checksum verify into a bitmask, header bytes",
@@ -105,7 +110,7 @@ def parse_args(argv=None):
     ap.add_argument("--config", type=int, default=2, choices=sorted(WORKLOADS),
                     help="2-5: BASELINE configs (2 = headline); 6: f1 fused TCP build; 7: f3 IPv4 header verify; "
                          "8: f1 with 12 B options; 9: f3 verify into a bitmask; 10: fused receive pass (f2+f3); "
-                         "11: the receive pass over IPv6")
+                         "11: the receive pass over IPv6; 12: f1 with 9000 B MTU segments")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--settle-s", type=float, default=0.5, help="device clock settle time before warmup (setup)")
     ap.add_argument("--event-every", type=int, default=10,

@@ -1303,14 +1303,17 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
                 // image dword k to source dword k, so every row is one plain 16 B load per lane with no shift
                 // and no byte mask; bytes [0, hdr_end) of row 0 are replaced by the built header and options,
                 // dwords past the image read 0 (range check).
+                // Double-buffered batches of R rows: batch b + 1 loads while batch b is built (rows past the
+                // image are out of the descriptor's range: 0, no traffic).
                 constexpr uint32_t R = kBuildRows;
                 const __amdgpu_buffer_rsrc_t frs = make_rsrc(data + S.db - S.hdr_end, S.nb4);
                 OptRaw o{};
                 if (S.optlen && !staged) o = opt_load(opts, S.ob, S.optlen, lane * 16u);
-                for (uint32_t r0 = 0; r0 < S.rows; r0 += R) {
-                    u32x4 v[R];
+                auto fl = [&](uint32_t r0, u32x4 (&v)[R]) {
 #pragma unroll
                     for (uint32_t rr = 0; rr < R; ++rr) v[rr] = bld16<LP != 0>(frs, (r0 + rr) * kRow + lane * 16u);
+                };
+                auto fb = [&](uint32_t r0, u32x4 (&v)[R]) {
 #pragma unroll
                     for (uint32_t rr = 0; rr < R; ++rr) asm volatile("" : "+v"(v[rr]));
 #pragma unroll
@@ -1339,6 +1342,15 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
                             __builtin_amdgcn_raw_buffer_store_b96(v3u{x.y, x.z, x.w}, ors, d4 ? 20u : kOOB, 0, SP);
                     }
                     acc = fold32(acc);
+                };
+                u32x4 VA[R], VB[R];
+                fl(0, VA);
+                for (uint32_t r0 = 0; r0 < S.rows; r0 += 2u * R) {
+                    if (r0 + R < S.rows) fl(r0 + R, VB);
+                    fb(r0, VA);
+                    if (r0 + R >= S.rows) break;
+                    if (r0 + 2u * R < S.rows) fl(r0 + 2u * R, VA);
+                    fb(r0 + R, VB);
                 }
             } else if (S.hdr_end <= kRow - 16u) {
                 constexpr uint32_t R = kBuildRows;

@@ -7,7 +7,7 @@
 set -u
 tag=${1:-r02}
 mkdir -p gpurun_out/profiles
-for c in ${PROFILE_CONFIGS:-2 3 4 5 6 7 8 9 10 11}; do
+for c in ${PROFILE_CONFIGS:-2 3 4 5 6 7 8 9 10 11 12}; do
   bash tools/profile.sh $c $tag || exit 1
   python3 tools/prof_summary.py $tag $c > /dev/null || exit 1
   cp profiles/${tag}_config${c}.md profiles/${tag}_config${c}_kernel_stats.csv profiles/traffic_config${c}.json gpurun_out/profiles/ || exit 1

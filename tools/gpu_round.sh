@@ -32,6 +32,7 @@ step bench_c8 300 python bench.py --config 8 --steps 100 --cpu-seconds 5
 step bench_c9 300 python bench.py --config 9 --steps 100 --cpu-seconds 5
 step bench_c10 300 python bench.py --config 10 --steps 100 --cpu-seconds 5
 step bench_c11 300 python bench.py --config 11 --steps 100 --cpu-seconds 5
+step bench_c12 300 python bench.py --config 12 --steps 50 --cpu-seconds 5
 step e2e_host 600 python tools/e2e_host.py
 rm -f gpurun_out/loopback.jsonl
 for m in host batch ring-host ring-gpu; do

@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def main(tag):
     src, dst = os.path.join(ROOT, "gpurun_out"), os.path.join(ROOT, "profiles")
-    for c in range(2, 12):
+    for c in range(2, 13):
         p = os.path.join(src, f"bench_c{c}.log")
         if not os.path.exists(p):
             continue
