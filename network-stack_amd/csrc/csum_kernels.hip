@@ -589,12 +589,16 @@ __device__ __forceinline__ void seg_lower_bound2(__amdgpu_buffer_rsrc_t ofs, uin
 
 // Stream the bytes [rbase + head, rbase + span) as 1 KiB rows of one wave (rbase 128-byte aligned, so a row
 // touches exactly 8 lines), R rows per load batch, and sample S (the weighted byte sum of the ragged scan
-// kernel, relative to rbase) at every lane's boundary brel (−1: none): bval = S(brel). A boundary at or past
-// the last row gets the total; carry = S(span) on return. Bytes before head and past span count as 0.
+// kernel, relative to rbase) at every lane's boundaries brel[k] (−1: none), k < NS: bval[k] = S(brel[k]). A
+// boundary at or past the last row gets the total; carry = S(span) on return. Bytes before head and past span
+// count as 0. NS boundary slots per lane let one pass cover NS sets of 64 boundaries: the per-span costs (the
+// pipeline filling at its start and draining at its end, the caller's setup and results) are paid once per NS
+// sets — with frames of a few hundred bytes a span of 64 is ~50 KB and those costs were ~7% of the time.
 // PIPE: two register sets — batch r0 + R loads while batch r0 is scanned.
-template <int R, bool PIPE = false>
-__device__ __forceinline__ void scan_span(const uint8_t* rbase, uint64_t span, uint32_t head, int64_t brel,
-                                          uint32_t lane, uint64_t& bval, uint64_t& carry) {
+template <int R, bool PIPE = false, int NS = 1>
+__device__ __forceinline__ void scan_span(const uint8_t* rbase, uint64_t span, uint32_t head,
+                                          const int64_t (&brel)[NS], uint32_t lane, uint64_t (&bval)[NS],
+                                          uint64_t& carry) {
     const uint64_t nrows = (span + kRow - 1) / kRow;
     // Batch r0 = rows [r0, r0 + R), one descriptor based at its first row (rows past the run read 0).
     auto issue = [&](uint64_t r0, u32x4 (&v)[R]) {
@@ -626,31 +630,38 @@ __device__ __forceinline__ void scan_span(const uint8_t* rbase, uint64_t span, u
         }
 #pragma unroll
         for (int j = 0; j < R; ++j) incl[j] = wave_incl_scan(sl[j]);
-        // Phase 2: boundaries that fall in this batch (rows past nrows hold zeros).
-        const int64_t qb = brel - (int64_t)(r0 * kRow);
-        const bool in_batch = qb >= 0 && qb < (int64_t)R * kRow;
-        if (__builtin_amdgcn_ballot_w64(in_batch)) {
-            uint64_t c = carry;
+        uint64_t crow[R];  // S at the start of row j
+        uint64_t c = carry;
 #pragma unroll
-            for (int j = 0; j < R; ++j) {
-                const int64_t q = qb - (int64_t)j * kRow;  // boundary position inside row j
-                const bool here = q >= 0 && q < (int64_t)kRow;
-                if (__builtin_amdgcn_ballot_w64(here)) {
-                    const uint32_t src = here ? (uint32_t)(q >> 4) : lane;
-                    const uint32_t pre = bperm(incl[j] - sl[j], src);
-                    u32x4 y;
-                    y.x = bperm(v[j].x, src);
-                    y.y = bperm(v[j].y, src);
-                    y.z = bperm(v[j].z, src);
-                    y.w = bperm(v[j].w, src);
-                    const uint32_t part = sad4(keep_bytes(y, 0, (int32_t)(q & 15)), 0u);
-                    if (here) bval = c + pre + part;
+        for (int j = 0; j < R; ++j) {
+            crow[j] = c;
+            c += __builtin_amdgcn_readlane(incl[j], 63);
+        }
+        // Phase 2: boundaries that fall in this batch (rows past nrows hold zeros).
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+            const int64_t qb = brel[k] - (int64_t)(r0 * kRow);
+            const bool in_batch = qb >= 0 && qb < (int64_t)R * kRow;
+            if (__builtin_amdgcn_ballot_w64(in_batch)) {
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    const int64_t q = qb - (int64_t)j * kRow;  // boundary position inside row j
+                    const bool here = q >= 0 && q < (int64_t)kRow;
+                    if (__builtin_amdgcn_ballot_w64(here)) {
+                        const uint32_t src = here ? (uint32_t)(q >> 4) : lane;
+                        const uint32_t pre = bperm(incl[j] - sl[j], src);
+                        u32x4 y;
+                        y.x = bperm(v[j].x, src);
+                        y.y = bperm(v[j].y, src);
+                        y.z = bperm(v[j].z, src);
+                        y.w = bperm(v[j].w, src);
+                        const uint32_t part = sad4(keep_bytes(y, 0, (int32_t)(q & 15)), 0u);
+                        if (here) bval[k] = crow[j] + pre + part;
+                    }
                 }
-                c += __builtin_amdgcn_readlane(incl[j], 63);
             }
         }
-#pragma unroll
-        for (int j = 0; j < R; ++j) carry += __builtin_amdgcn_readlane(incl[j], 63);
+        carry = c;
     };
     if constexpr (PIPE) {
         u32x4 A[R], B[R];
@@ -669,10 +680,12 @@ __device__ __forceinline__ void scan_span(const uint8_t* rbase, uint64_t span, u
             process(r0, v);
         }
     }
-    if (brel >= (int64_t)(nrows * kRow)) bval = carry;  // boundary at the very end of the rows
+#pragma unroll
+    for (int k = 0; k < NS; ++k)
+        if (brel[k] >= (int64_t)(nrows * kRow)) bval[k] = carry;  // boundary at the very end of the rows
 }
 
-template <int R, bool VERIFY, bool PIPE>
+template <int R, bool VERIFY, bool PIPE, int NS>
 __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, uint32_t n,
     const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t run) {
@@ -683,10 +696,10 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
     const __amdgpu_buffer_rsrc_t prs = make_rsrc(partial, partial ? (uint64_t)n * 4 : 0);
     const __amdgpu_buffer_rsrc_t ors = make_rsrc(out, out ? (uint64_t)n * 2 : 0);
     const __amdgpu_buffer_rsrc_t oks = make_rsrc(ok, VERIFY ? (uint64_t)n : 0);
-    // The wave's tasks are runs [a, a + cnt) of ≤ run segments, a = a0, a0 + run, ... < a_end; a run never
-    // crosses a_end. Byte-balanced: wave g (XCD-contiguous numbering) owns the segments that start in the g-th
-    // of W equal byte slices of the batch, so every wave streams the same bytes (± one segment) and none is
-    // left running alone at the end of the launch.
+    // The wave's tasks are runs of NS sets [a_k, a_k + cnt_k) of ≤ run segments each (a_k = a + k·run), a = a0,
+    // a0 + NS·run, ... < a_end; a run never crosses a_end. Byte-balanced: wave g (XCD-contiguous numbering) owns
+    // the segments that start in the g-th of W equal byte slices of the batch, so every wave streams the same
+    // bytes (± one segment) and none is left running alone at the end of the launch.
     uint32_t a0, a_end;
     {
         const uint32_t nb = gridDim.x, b = blockIdx.x, W = nb * kWavesPerBlock;
@@ -699,37 +712,62 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
         a0 = g == 0 ? 0u : s[0];
         a_end = g + 1 == W ? n : s[1];
     }
-    const uint32_t a_step = run;
+    const uint32_t a_step = run * NS;
     auto load_offs = [&](uint32_t a) -> uint64_t {  // lane l ≤ run length: offsets[a + l]
         const uint32_t voff = (a < a_end && lane <= run && a + lane <= n) ? (a + lane) * 8 : kOOB;
         const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, voff, 0, 0);
         return ((uint64_t)x.y << 32) | x.x;
     };
-    uint64_t nxt_off = load_offs(a0);
+    uint64_t nxt_off[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) nxt_off[k] = load_offs(a0 + k * run);
     for (uint32_t a = a0; a < a_end; a += a_step) {
-        const uint32_t cnt = min(run, a_end - a);
-        const uint64_t my_off = nxt_off;  // boundary `lane` of the run (lanes 0..cnt)
-        nxt_off = load_offs(a + a_step);
-        const uint32_t my_part = __builtin_amdgcn_raw_buffer_load_b32(prs, lane < cnt ? (a + lane) * 4 : kOOB, 0, 0);
-        const uint64_t lo = readlane64(my_off, 0), hi = readlane64(my_off, cnt);
+        uint64_t my_off[NS];  // set k: boundary `lane` (lanes 0..cnt_k)
+        uint32_t cnt[NS], my_part[NS];
+        int64_t brel[NS];
+        uint64_t bval[NS];
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+            const uint32_t ak = a + k * run;
+            cnt[k] = ak < a_end ? min(run, a_end - ak) : 0u;
+            my_off[k] = nxt_off[k];
+            nxt_off[k] = load_offs(a + a_step + k * run);
+            my_part[k] = __builtin_amdgcn_raw_buffer_load_b32(prs, lane < cnt[k] ? (ak + lane) * 4 : kOOB, 0, 0);
+            bval[k] = 0;
+        }
+        // the run's last boundary: set kl = the last set with segments, its lane cnt
+        uint32_t kl = 0;
+#pragma unroll
+        for (int k = 1; k < NS; ++k) kl = cnt[k] ? (uint32_t)k : kl;
+        uint64_t hi = 0;
+#pragma unroll
+        for (int k = 0; k < NS; ++k)
+            if ((uint32_t)k == kl) hi = readlane64(my_off[k], cnt[k]);
+        const uint64_t lo = readlane64(my_off[0], 0);
         // Rows start on a 128-byte line so a 1 KiB row touches exactly 8 lines.
         const uint8_t* rbase = reinterpret_cast<const uint8_t*>(((uintptr_t)(base + lo)) & ~(uintptr_t)127);
         const uint64_t span = (uint64_t)((base + hi) - rbase);           // bytes from rbase to the run's end
         const uint32_t head = (uint32_t)((uintptr_t)(base + lo) & 127u);  // bytes before the run in row 0
         // Boundary lane state: its position relative to rbase, and S there.
-        const int64_t brel = lane <= cnt ? (int64_t)((base + my_off) - rbase) : -1;
-        uint64_t bval = 0, carry = 0;
-        scan_span<R, PIPE>(rbase, span, head, brel, lane, bval, carry);
-        // Segment `lane` = [boundary lane, boundary lane+1).
-        const uint64_t nb = ((uint64_t)__shfl_down((unsigned long long)bval, 1));
-        const uint64_t d = nb - bval;
-        const uint32_t le = fold32((uint32_t)(d & 0xFFFFFFFFu)) + fold32((uint32_t)(d >> 32));
-        const bool even = (((uintptr_t)base + my_off) & 1u) == 0;
-        const uint32_t res = finish(le, even, my_part);
-        const bool mine = lane < cnt;
-        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, mine ? (a + lane) * 2 : kOOB, 0, 0);
-        if constexpr (VERIFY)
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(res == 0xFFFFu), oks, mine ? a + lane : kOOB, 0, 0);
+#pragma unroll
+        for (int k = 0; k < NS; ++k)
+            brel[k] = cnt[k] && lane <= cnt[k] ? (int64_t)((base + my_off[k]) - rbase) : -1;
+        uint64_t carry = 0;
+        scan_span<R, PIPE, NS>(rbase, span, head, brel, lane, bval, carry);
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+            // Segment `lane` of set k = [boundary lane, boundary lane+1).
+            const uint64_t nb = ((uint64_t)__shfl_down((unsigned long long)bval[k], 1));
+            const uint64_t d = nb - bval[k];
+            const uint32_t le = fold32((uint32_t)(d & 0xFFFFFFFFu)) + fold32((uint32_t)(d >> 32));
+            const bool even = (((uintptr_t)base + my_off[k]) & 1u) == 0;
+            const uint32_t res = finish(le, even, my_part[k]);
+            const bool mine = lane < cnt[k];
+            const uint32_t ak = a + k * run;
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, mine ? (ak + lane) * 2 : kOOB, 0, 0);
+            if constexpr (VERIFY)
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(res == 0xFFFFu), oks, mine ? ak + lane : kOOB, 0, 0);
+        }
     }
 }
 
@@ -838,8 +876,10 @@ __global__ __launch_bounds__(kBlock) void rx_tcp_kernel(const uint8_t* __restric
             for (int k = 0; k < kWin; ++k) d[k] = hw + k < last_dw ? hw[k] : *last_dw;
         }
         // The run's bytes, S sampled at every frame start.
-        uint64_t bval = 0, carry = 0;
-        scan_span<R, true>(rbase, span, head, brel, lane, bval, carry);
+        uint64_t bvals[1] = {0}, carry = 0;
+        const int64_t brels[1] = {brel};
+        scan_span<R, true, 1>(rbase, span, head, brels, lane, bvals, carry);
+        const uint64_t bval = bvals[0];
         const uint64_t nbv = (uint64_t)__shfl_down((unsigned long long)bval, 1);
         const uint64_t F = (lane == cnt - 1 ? carry : nbv) - bval;  // the frame's weighted sum (exact)
         const uint64_t flen = my_end - my_off;
@@ -1973,19 +2013,24 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
     const int rows = pipe ? (c.rows == 2 || c.rows == 4 || c.rows == 8 ? c.rows : 2)
                           : (c.rows == 4 || c.rows == 8 || c.rows == 16 ? c.rows : 8);
     const uint32_t run = (c.run_segs >= 1 && c.run_segs <= (int)kScanRun) ? (uint32_t)c.run_segs : kScanRun;
+    // 2 boundary sets per lane (runs of 126 segments) on the default shape: the per-run pipeline fill and drain
+    // are paid half as often (config 3 0.684 → 0.682 ms, 40-1500 B frames 0.1320 → 0.1293; 4 sets: 0.683 /
+    // 0.1308, more registers and phase-2 checks); segs_per_wave = 1 keeps one set.
+    const int ns = (pipe && rows == 2 && c.segs_per_wave != 1) ? 2 : 1;
     const uint32_t mb = max_blocks_of(c, 2);
     for (uint64_t c0 = 0; c0 < n; c0 += kRaggedChunk) {
         const uint32_t cn = (uint32_t)(n - c0 < kRaggedChunk ? n - c0 : kRaggedChunk);
-        const uint32_t grid = grid_for((cn + run - 1) / run, mb);
+        const uint32_t grid = grid_for((cn + run * ns - 1) / (run * ns), mb);
         const uint32_t* pc = partial ? partial + c0 : nullptr;
         uint16_t* oc = out ? out + c0 : nullptr;
         uint8_t* kc = ok ? ok + c0 : nullptr;
-#define NSX_RSCAN(R_, P_)                                                                                      \
-        if (rows == R_ && pipe == P_)                                                                           \
-            hipLaunchKernelGGL((csum_ragged_scan_kernel<R_, VERIFY, P_>), dim3(grid), dim3(kBlock), 0, st, base, \
-                               offsets + c0, cn, pc, oc, kc, run);
-        NSX_RSCAN(2, true) NSX_RSCAN(4, true) NSX_RSCAN(8, true)
-        NSX_RSCAN(4, false) NSX_RSCAN(8, false) NSX_RSCAN(16, false)
+#define NSX_RSCAN(R_, P_, NS_)                                                                                 \
+        if (rows == R_ && pipe == P_ && ns == NS_)                                                              \
+            hipLaunchKernelGGL((csum_ragged_scan_kernel<R_, VERIFY, P_, NS_>), dim3(grid), dim3(kBlock), 0, st,  \
+                               base, offsets + c0, cn, pc, oc, kc, run);
+        NSX_RSCAN(2, true, 1) NSX_RSCAN(4, true, 1) NSX_RSCAN(8, true, 1)
+        NSX_RSCAN(4, false, 1) NSX_RSCAN(8, false, 1) NSX_RSCAN(16, false, 1)
+        NSX_RSCAN(2, true, 2)
 #undef NSX_RSCAN
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;

@@ -118,6 +118,8 @@ def test_all_launch_shapes_bit_exact():
 
 RAGGED_TUNES = [dict(kernel=k, rows=r, run_segs=rs, blocks_per_cu=b)  # pipelined (rows 2/4/8) and plain (4/8/16)
                 for k, rows in ((0, (0, 4, 8)), (nsx.KERNEL_SCAN_PLAIN, (0, 4, 16))) for r in rows
+                for rs in (0, 1, 16, 63) for b in (0, 1, 8)] + \
+               [dict(segs_per_wave=1, run_segs=rs, blocks_per_cu=b)  # one boundary set per lane (default: two)
                 for rs in (0, 1, 16, 63) for b in (0, 1, 8)]
 
 

@@ -24,7 +24,8 @@ FIXED_KNOBS = [dict(), dict(segs_per_wave=4, blocks_per_cu=2), dict(segs_per_wav
                dict(block_mode=2), dict(block_mode=1), dict(window_bytes=1_000_000), dict(window_bytes=7_777)]
 RAGGED_KNOBS = [dict(), dict(rows=4), dict(rows=8), dict(run_segs=1), dict(run_segs=17, blocks_per_cu=1),
                 dict(blocks_per_cu=8), dict(block_mode=2), dict(block_mode=1), dict(kernel=nsx.KERNEL_SCAN_PLAIN),
-                dict(kernel=nsx.KERNEL_SCAN_PLAIN, rows=16, run_segs=5)]
+                dict(kernel=nsx.KERNEL_SCAN_PLAIN, rows=16, run_segs=5), dict(segs_per_wave=1),
+                dict(segs_per_wave=1, run_segs=7)]
 
 
 def _dev(a):
