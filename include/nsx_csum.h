@@ -144,6 +144,47 @@ int nsx_tcp_build_dev(const nsx_tcp_hdr_soa* hdr, const uint8_t* d_opts, const u
                       const uint32_t* d_prefix_partial, uint64_t n, uint8_t* d_out, const uint64_t* d_out_off,
                       uint16_t* d_raw, nsx_stream_t stream);
 
+/* Receive-side parse (parseSegment, transport/tcp/tcp.go:130-185) of n TCP
+ * segments d_base[d_offsets[i], d_offsets[i+1]) (any alignment, d_offsets as
+ * for nsx_csum_ragged_dev) into device arrays of n entries; every member of
+ * *out is nullable. Fields as the reference reads them (offset = the whole byte
+ * 12, control = ctl.byte(), checksum = bytes 16-17); data_off[i] = d_offsets[i]
+ * + offset*4 (the payload, s.data = raw[dataAt:]); n_options = the options the
+ * reference appends (NOP and MSS; EOL ends the walk). status[i]:
+ *   NSX_TCP_PARSE_OK            parsed;
+ *   NSX_TCP_PARSE_SHORT         fewer than 20 bytes ("segment too short", :131);
+ *   NSX_TCP_PARSE_OFFSET        offset*4 > length ("advertised data offset too
+ *                               long", :152);
+ *   NSX_TCP_PARSE_OPTION_RANGE  an MSS option whose length runs past the segment
+ *                               (the reference's slice panics or reads past the
+ *                               segment, :173-174);
+ *   NSX_TCP_PARSE_OPTION_KIND   an option kind other than 0-2 before dataAt (the
+ *                               reference's loop never advances, :160-179).
+ * On any status but OK the fields, data_off and n_options are 0 (the reference
+ * returns segment{}). */
+#define NSX_TCP_PARSE_OK 0
+#define NSX_TCP_PARSE_SHORT 1
+#define NSX_TCP_PARSE_OFFSET 2
+#define NSX_TCP_PARSE_OPTION_RANGE 3
+#define NSX_TCP_PARSE_OPTION_KIND 4
+typedef struct {
+    uint16_t* src_port;
+    uint16_t* dst_port;
+    uint32_t* seq_num;
+    uint32_t* ack_num;
+    uint8_t* offset;
+    uint8_t* control;
+    uint16_t* window;
+    uint16_t* checksum;
+    uint16_t* urgent_ptr;
+    uint64_t* data_off;
+    uint8_t* n_options;
+    uint8_t* status;
+} nsx_tcp_parsed_soa;
+
+int nsx_tcp_parse_dev(const void* d_base, const uint64_t* d_offsets, uint64_t n, const nsx_tcp_parsed_soa* out,
+                      nsx_stream_t stream);
+
 /* Wire length of segment.bytes() with opt_len option bytes (tcp.go:98-128). */
 uint64_t nsx_tcp_wire_len(uint64_t opt_len, uint64_t data_len);
 

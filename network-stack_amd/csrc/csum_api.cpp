@@ -300,6 +300,19 @@ int nsx_tcp_build_dev_tuned(const nsx_tcp_hdr_soa* hdr, const uint8_t* d_opts, c
                                          static_cast<hipStream_t>(stream)));
 }
 
+int nsx_tcp_parse_dev(const void* d_base, const uint64_t* d_offsets, uint64_t n, const nsx_tcp_parsed_soa* out,
+                      nsx_stream_t stream) {
+    if (n == 0) return NSX_OK;
+    if (!d_base || !d_offsets || !out) return NSX_EINVAL;
+    const int dev = current_device();
+    if (dev < 0) return NSX_ENODEV;
+    const nsx::TcpParsedSoA o{out->src_port, out->dst_port, out->seq_num,    out->ack_num,
+                              out->offset,   out->control,  out->window,     out->checksum,
+                              out->urgent_ptr, out->data_off, out->n_options, out->status};
+    return map_err(nsx::launch_tcp_parse(make_cfg(dev, nullptr), d_base, d_offsets, n, o,
+                                         static_cast<hipStream_t>(stream)));
+}
+
 static int ipv4_args_ok(const void* d_base, uint64_t stride, uint32_t hdr_off, uint64_t n) {
     if (!d_base) return NSX_EINVAL;
     if (n > 1 && stride == 0) return NSX_EINVAL;

@@ -58,6 +58,23 @@ hipError_t launch_tcp_build(const LaunchCfg& c, const TcpHdrSoA& h, const uint8_
                             const uint8_t* data, const uint64_t* data_off, uint64_t data_bytes,
                             const uint32_t* partial, uint64_t n, uint8_t* out, const uint64_t* out_off,
                             uint16_t* raw, hipStream_t st);
+struct TcpParsedSoA {  // device arrays, one entry per segment; every member nullable
+    uint16_t* src_port;
+    uint16_t* dst_port;
+    uint32_t* seq;
+    uint32_t* ack;
+    uint8_t* offset;
+    uint8_t* ctl;
+    uint16_t* window;
+    uint16_t* checksum;
+    uint16_t* urgent;
+    uint64_t* data_off;
+    uint8_t* n_options;
+    uint8_t* status;
+};
+// parseSegment (tcp.go:130-185) over segments d_base[d_offsets[i], d_offsets[i+1]).
+hipError_t launch_tcp_parse(const LaunchCfg& c, const void* d_base, const uint64_t* d_offsets, uint64_t n,
+                            const TcpParsedSoA& o, hipStream_t st);
 // mode 0 verify (out), 1 fill (out nullable), 2 verify into the bitmask `mask` (ceil(n/64) words)
 hipError_t launch_ipv4_hdr(const LaunchCfg& c, uint8_t* base, uint64_t stride, uint32_t hdr_off, uint64_t n,
                            int mode, uint16_t* out, uint64_t* mask, hipStream_t st);

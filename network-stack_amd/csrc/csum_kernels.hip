@@ -1831,6 +1831,89 @@ __global__ __launch_bounds__(kBlock) void pseudo_ipv6_kernel(const uint8_t* __re
 }
 
 // ---------------------------------------------------------------------------
+// Receive-side parse (parseSegment, transport/tcp/tcp.go:130-185) of a batch of
+// TCP segments, d_base[offsets[i], offsets[i+1]), any alignment, into SoA
+// fields. One thread per segment (the work is the 20-byte header, not the
+// payload): the header's dwords are loaded from the 4-aligned address below its
+// start — only those holding segment bytes, so nothing past the segment's last
+// dword is read — and realigned with v_alignbyte. Fields are the reference's:
+// offset is the whole byte 12 (tcp.go:142), dataAt = offset·4 (:150). Options
+// (offset > 5) are walked byte by byte exactly as the reference does — EOL ends
+// the walk, NOP advances 1, MSS reads its length and advances 6 whatever the
+// length (:160-179) — and counted. Where the reference fails the segment comes
+// back zero with a status: too short (:131), data offset past the end (:152);
+// where it would panic on the MSS slice (:173-174, bytes past the segment) or
+// loop forever on another option kind (:162-178, optIdx never advances), the
+// status says so and the walk stops.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void tcp_parse_kernel(const uint8_t* __restrict__ base,
+                                                           const uint64_t* __restrict__ offsets, uint64_t n,
+                                                           TcpParsedSoA o) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t s0 = offsets[i], s1 = offsets[i + 1];
+        const uint64_t len = s1 > s0 ? s1 - s0 : 0;
+        const uint8_t* p = base + s0;
+        uint32_t status = 0, nopt = 0;
+        uint32_t H[5] = {0u, 0u, 0u, 0u, 0u};
+        if (len < 20) {
+            status = 1;  // "segment too short"
+        } else {
+            const uint32_t sh = (uint32_t)((uintptr_t)p & 3u);
+            const uint32_t* pa = reinterpret_cast<const uint32_t*>((uintptr_t)p - sh);
+            uint32_t w[6];
+#pragma unroll
+            for (int k = 0; k < 6; ++k)  // dword k holds segment bytes iff it starts before the segment's end
+                w[k] = (uint64_t)(4 * k) < len + sh ? pa[k] : 0u;
+#pragma unroll
+            for (int k = 0; k < 5; ++k) H[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+            const uint32_t off = H[3] & 0xFFu;
+            const uint64_t data_at = (uint64_t)off * 4u;
+            if (data_at > len) {
+                status = 2;  // "advertised data offset too long"
+            } else if (off > 5u) {
+                uint64_t idx = 20;
+                while (idx < data_at) {
+                    const uint32_t kind = p[idx];
+                    if (kind == 0u) break;  // EOL: the rest is padding
+                    if (kind == 1u) {
+                        ++idx;
+                    } else if (kind == 2u) {
+                        if (idx + 2 > len || idx + 2 + p[idx + 1] > len) {
+                            status = 3;  // the MSS slice would run past the segment
+                            break;
+                        }
+                        idx += 6;  // 1(kind) + 1(length) + 4(data), as tcp.go:175
+                    } else {
+                        status = 4;  // unknown kind: the reference's loop never advances
+                        break;
+                    }
+                    ++nopt;
+                }
+            }
+            if (o.data_off) o.data_off[i] = status ? 0u : s0 + data_at;
+        }
+        if (status) {
+            nopt = 0;
+#pragma unroll
+            for (int k = 0; k < 5; ++k) H[k] = 0u;  // the reference returns segment{}
+            if (len < 20 && o.data_off) o.data_off[i] = 0u;
+        }
+        if (o.src_port) o.src_port[i] = (uint16_t)bswap16u(H[0] & 0xFFFFu);
+        if (o.dst_port) o.dst_port[i] = (uint16_t)bswap16u(H[0] >> 16);
+        if (o.seq) o.seq[i] = bswap32u(H[1]);
+        if (o.ack) o.ack[i] = bswap32u(H[2]);
+        if (o.offset) o.offset[i] = (uint8_t)H[3];
+        if (o.ctl) o.ctl[i] = (uint8_t)(H[3] >> 8);
+        if (o.window) o.window[i] = (uint16_t)bswap16u(H[3] >> 16);
+        if (o.checksum) o.checksum[i] = (uint16_t)bswap16u(H[4] & 0xFFFFu);
+        if (o.urgent) o.urgent[i] = (uint16_t)bswap16u(H[4] >> 16);
+        if (o.n_options) o.n_options[i] = (uint8_t)min(nopt, 255u);
+        if (o.status) o.status[i] = (uint8_t)status;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Receive-side verify as a bitmask (tcp.go:70): bit i of the mask is
 // (raw[i] == 0xFFFF). One wave covers 64 sums and its ballot is one u64 word.
 // ---------------------------------------------------------------------------
@@ -2099,6 +2182,15 @@ hipError_t launch_pseudo_ipv6(const uint8_t* src, const uint8_t* dst, const uint
     const bool aligned = (((uintptr_t)src | (uintptr_t)dst) & 3u) == 0;
     hipLaunchKernelGGL(pseudo_ipv6_kernel, dim3(grid), dim3(kBlock), 0, st, src, dst, len, (uint32_t)nh, n,
                        aligned, partial);
+    return hipGetLastError();
+}
+
+hipError_t launch_tcp_parse(const LaunchCfg& c, const void* d_base, const uint64_t* d_offsets, uint64_t n,
+                            const TcpParsedSoA& o, hipStream_t st) {
+    const uint32_t grid = (uint32_t)std::max<uint64_t>(
+        1, std::min<uint64_t>((n + kBlock - 1) / kBlock, max_blocks_of(c, 4)));
+    hipLaunchKernelGGL(tcp_parse_kernel, dim3(grid), dim3(kBlock), 0, st, static_cast<const uint8_t*>(d_base),
+                       d_offsets, n, o);
     return hipGetLastError();
 }
 

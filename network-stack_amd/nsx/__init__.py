@@ -85,6 +85,7 @@ def lib() -> ctypes.CDLL:
             "nsx_rx_ipv4_tcp_verify_dev_tuned": [vp, vp, u64, vp, vp, vp, vp, vp],
             "nsx_rx_ipv4_tcp_verify_host": [vp, vp, u64, vp, i32],
             "nsx_rx_ipv4_tcp_verify_host_tuned": [vp, vp, u64, vp, i32, vp],
+            "nsx_tcp_parse_dev": [vp, vp, u64, vp, vp],
             "nsx_rx_ipv6_tcp_verify_dev": [vp, vp, u64, vp, vp, vp],
             "nsx_rx_ipv6_tcp_verify_dev_tuned": [vp, vp, u64, vp, vp, vp, vp],
             "nsx_rx_ipv6_tcp_verify_host": [vp, vp, u64, vp, i32],
@@ -350,6 +351,32 @@ def rx_ipv6_tcp_verify_dev(buf, offsets, mask=None, tcp_raw=None, stream=None, t
 class TcpHdrSoA(ctypes.Structure):
     _fields_ = [(name, ctypes.c_void_p) for name in
                 ("src_port", "dst_port", "seq_num", "ack_num", "offset", "control", "window", "urgent_ptr")]
+
+
+PARSE_FIELDS = (("src_port", "int16"), ("dst_port", "int16"), ("seq_num", "int32"), ("ack_num", "int32"),
+                ("offset", "uint8"), ("control", "uint8"), ("window", "int16"), ("checksum", "int16"),
+                ("urgent_ptr", "int16"), ("data_off", "int64"), ("n_options", "uint8"), ("status", "uint8"))
+PARSE_OK, PARSE_SHORT, PARSE_OFFSET, PARSE_OPTION_RANGE, PARSE_OPTION_KIND = 0, 1, 2, 3, 4
+
+
+class TcpParsedSoA(ctypes.Structure):
+    _fields_ = [(name, ctypes.c_void_p) for name, _ in PARSE_FIELDS]
+
+
+def tcp_parse_dev(buf, offsets, fields=None, want=None, stream=None) -> dict:
+    """parseSegment (tcp.go:130-185) over the segments buf[offsets[i], offsets[i+1]) into device tensors (dict
+    by field; `want` = the field names to produce, default all; `fields` = caller tensors to fill)."""
+    import torch
+    n = offsets.numel() - 1
+    names = [k for k, _ in PARSE_FIELDS] if want is None else list(want)
+    out = dict(fields or {})
+    for k, dt in PARSE_FIELDS:
+        if k in names and k not in out:
+            out[k] = torch.empty(max(n, 0), dtype=getattr(torch, dt), device=offsets.device)
+    soa = TcpParsedSoA(*[_dev_ptr(out.get(k)) for k, _ in PARSE_FIELDS])
+    _check(lib().nsx_tcp_parse_dev(_dev_ptr(buf), _dev_ptr(offsets), n, ctypes.byref(soa), _stream(stream)),
+           "nsx_tcp_parse_dev")
+    return out
 
 
 def tcp_wire_len(opt_len: int, data_len: int) -> int:

@@ -204,6 +204,46 @@ class Segment:
         return go_checksum(pseudo, self.bytes())
 
 
+PARSE_OK, PARSE_SHORT, PARSE_OFFSET, PARSE_OPTION_RANGE, PARSE_OPTION_KIND = 0, 1, 2, 3, 4
+
+
+def parse_segment(raw: bytes):
+    """parseSegment (tcp.go:130-185), statement by statement: (Segment, status). On a reference error the
+    segment is Segment() (Go's segment{}) with status SHORT (:131-133) or OFFSET (:152-154). Where the reference
+    would panic on the MSS data slice (:173-174, a slice past the segment) or loop forever on another option kind
+    (:160-179, optIdx never advances) the status is OPTION_RANGE / OPTION_KIND and the segment is Segment()."""
+    raw = bytes(raw)
+    if len(raw) < 20:
+        return Segment(), PARSE_SHORT
+    s = Segment(src_port=int.from_bytes(raw[0:2], "big"), dst_port=int.from_bytes(raw[2:4], "big"),
+                seq_num=int.from_bytes(raw[4:8], "big"), ack_num=int.from_bytes(raw[8:12], "big"),
+                offset=raw[12], control=Ctl.from_byte(raw[13]), window=int.from_bytes(raw[14:16], "big"),
+                checksum=int.from_bytes(raw[16:18], "big"), urgent_ptr=int.from_bytes(raw[18:20], "big"))
+    data_at = s.offset * 4
+    if data_at > len(raw):
+        return Segment(), PARSE_OFFSET
+    if s.offset > 20 // 4:
+        idx = 20
+        while idx < data_at:
+            kind = raw[idx]
+            if kind == 0:  # EOL: the rest is padding
+                break
+            opt = Option(kind=kind)
+            if kind == 1:
+                idx += 1
+            elif kind == 2:
+                if idx + 2 > len(raw) or idx + 2 + raw[idx + 1] > len(raw):
+                    return Segment(), PARSE_OPTION_RANGE
+                opt.length = raw[idx + 1]
+                opt.data = raw[idx + 2:idx + 2 + opt.length]
+                idx += 6  # 1(kind) + 1(length) + 4(data)
+            else:
+                return Segment(), PARSE_OPTION_KIND
+            s.options.append(opt)
+    s.data = raw[data_at:]
+    return s, PARSE_OK
+
+
 def ipv4_pseudo_header(src: bytes, dst: bytes, proto: int, length: int) -> bytes:
     """RFC 9293 §3.1 IPv4 pseudo-header: src(4) dst(4) zero(1) proto(1) len(2).
     Inputs as ip.Addr.Raw() (ipv4.go:15) and ip.NextProtoTCP = 6 (protocols.go:8)."""

@@ -214,6 +214,27 @@ def rx6(rng):
                   "mask": [int(x) for x in mask]}
 
 
+def parse(rng):
+    """TCP segments of every kind tests/_parse.py builds (valid with and without options, and every case
+    parseSegment rejects or cannot handle), packed behind an odd lead; expected per-segment fields, data
+    offset, option count and status from O.parse_segment (tcp.go:130-185)."""
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE)))
+    import _parse
+    segs = []
+    for k in _parse.KINDS:
+        segs += [_parse.segment(rng, k, max_payload=200) for _ in range(8)]
+    segs = [segs[i] for i in rng.permutation(len(segs))]
+    lead = 7
+    offs = np.zeros(len(segs) + 1, np.uint64)
+    offs[1:] = np.cumsum([len(s) for s in segs])
+    offs += np.uint64(lead)
+    blob = bytes(range(lead)) + b"".join(segs)
+    exp = _parse.expected(np.frombuffer(blob, np.uint8), offs)
+    meta = {"offsets": [int(x) for x in offs]}
+    meta.update({k: [int(x) for x in v] for k, v in exp.items()})
+    return blob, meta
+
+
 def main():
     rng = np.random.default_rng(0x1071)
     with open(os.path.join(HERE, "kat.json"), "w") as f:
@@ -240,6 +261,12 @@ def main():
         f.write(x6blob)
     with open(os.path.join(HERE, "rx6.json"), "w") as f:
         json.dump(x6meta, f)
+    pblob, pmeta = parse(np.random.default_rng(0x107C))
+    with open(os.path.join(HERE, "parse.bin"), "wb") as f:
+        f.write(pblob)
+    with open(os.path.join(HERE, "parse.json"), "w") as f:
+        json.dump(pmeta, f)
+    print(f"parse: {len(pmeta['status'])} segments, statuses {sorted(set(pmeta['status']))}")
     print(f"rx6: {len(x6meta['valid'])} packets ({sum(x6meta['valid'])} valid), {len(x6blob)} B")
     print(f"vectors: {len(idx)} cases, {len(blob)} B; ragged: {len(rmeta['raw'])} segments, {len(rblob)} B; "
           f"rx: {len(xmeta['valid'])} frames ({sum(xmeta['valid'])} valid), {len(xblob)} B")

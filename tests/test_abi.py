@@ -203,6 +203,9 @@ def test_device_calls_fail_loudly_without_gpu():
     assert e.value.code == nsx.NSX_ENODEV
     assert L.nsx_rx_ipv4_tcp_verify_dev(fake, fake, 4, fake, None, None, None) == nsx.NSX_ENODEV
     assert L.nsx_rx_ipv6_tcp_verify_dev(fake, fake, 4, fake, None, None) == nsx.NSX_ENODEV
+    parsed = nsx.TcpParsedSoA()
+    assert L.nsx_tcp_parse_dev(fake, fake, 4, ctypes.byref(parsed), None) == nsx.NSX_ENODEV
+    assert L.nsx_tcp_parse_dev(fake, fake, 4, None, None) == nsx.NSX_EINVAL
     assert L.nsx_rx_ipv6_tcp_verify_dev_tuned(fake, fake, 4, fake, None, None, tune) == nsx.NSX_ENODEV
     for v in (4, 6):
         with pytest.raises(nsx.NsxError) as e:

@@ -328,6 +328,46 @@ def test_rx6_c_matches_python_random_batches():
             assert (tcpr[i], bool(bits[i])) == (a, v), (i, kinds[i])
 
 
+def test_parse_segment_restates_reference_cases():
+    """parseSegment (tcp.go:130-185) on the reference's own case (tcp_test.go:26-32: segment{data:"hello"},
+    offset 0, so dataAt 0 and the data is the whole segment), round trips of bytes() with the options the
+    reference serialises faithfully (NOP, MSS of length 4), and every error and would-panic/loop case."""
+    s, st = O.parse_segment(bytes(20) + b"hello")
+    assert st == O.PARSE_OK and s.offset == 0 and s.data == bytes(20) + b"hello" and s.options == []
+    t = O.Segment(src_port=1, dst_port=2, seq_num=3, ack_num=4, control=O.Ctl.from_byte(0x12), window=5,
+                  checksum=6, urgent_ptr=7, options=[O.Option(kind=1), O.Option(kind=2, length=4, data=b"abcd")],
+                  data=b"payload")
+    t.offset = t.compute_offset()
+    # 7 option bytes: bytes() pads 27 → 30 with `remainder` = 3 zeros (tcp.go:118-121) while offset = 7 puts
+    # dataAt at 28, so the parsed data starts with the last 2 padding bytes
+    s, st = O.parse_segment(t.bytes())
+    assert st == O.PARSE_OK and s.options == t.options and s.data == b"\0\0payload"
+    t.options.insert(0, O.Option(kind=1))  # 8 option bytes: no padding, an exact round trip
+    t.offset = t.compute_offset()
+    s, st = O.parse_segment(t.bytes())
+    assert st == O.PARSE_OK and s == t
+    assert O.parse_segment(bytes(19))[1] == O.PARSE_SHORT
+    b = bytearray(t.bytes())
+    b[12] = 200
+    assert O.parse_segment(bytes(b)) == (O.Segment(), O.PARSE_OFFSET)
+    b = bytearray(t.bytes())
+    b[23] = 60  # MSS length past the end (options NOP NOP MSS: the length byte is 23)
+    assert O.parse_segment(bytes(b))[1] == O.PARSE_OPTION_RANGE
+    b = bytearray(t.bytes())
+    b[20] = 9  # unknown kind
+    assert O.parse_segment(bytes(b))[1] == O.PARSE_OPTION_KIND
+
+
+def test_parse_golden_fixture_is_the_oracle():
+    import _parse
+    meta = load("parse.json")
+    blob = np.fromfile(os.path.join(GOLDEN, "parse.bin"), np.uint8)
+    exp = _parse.expected(blob, np.array(meta["offsets"], np.uint64))
+    for k, v in exp.items():
+        assert v.tolist() == meta[k], k
+    assert set(meta["status"]) == {0, 1, 2, 3, 4}
+
+
 def test_rx_c_matches_python_random_batches():
     import _rx
     rng = np.random.default_rng(0x79)

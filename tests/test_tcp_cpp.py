@@ -30,3 +30,27 @@ def test_cpp_tcp_mirror(tmp_path):
     assert set(got) == set(want)
     for name, c in want.items():
         assert got[name] == (c["offset"], c["bytes"], c["raw"], c["raw_with_pseudo"]), name
+
+
+def test_cpp_parse_segment_matches_python_oracle_on_golden_segments(tmp_path):
+    """The two restatements of parseSegment (tcp.go:130-185) — the C++ mirror's parse_segment and the Python
+    oracle's parse_segment, which made tests/golden/parse.json — agree on every golden segment: fields, data
+    offset, option count and status (errors, and the cases where the reference would panic or loop)."""
+    exe = tmp_path / "parse_dump"
+    libdir = os.path.dirname(nsx.LIB_PATH)
+    subprocess.check_call(["g++", "-std=c++17", "-O2", "-Wall", "-Wextra", "-Werror",
+                           os.path.join(ROOT, "tests", "cpp", "parse_dump.cpp"),
+                           "-I", os.path.join(ROOT, "network-stack_amd", "include"),
+                           "-L", libdir, "-lnsx_csum", f"-Wl,-rpath,{libdir}", "-o", str(exe)])
+    meta = json.load(open(os.path.join(GOLDEN, "parse.json")))
+    offs = tmp_path / "offs.txt"
+    offs.write_text("\n".join(str(x) for x in meta["offsets"]))
+    out = subprocess.run([str(exe), os.path.join(GOLDEN, "parse.bin"), str(offs)], capture_output=True, text=True)
+    assert out.returncode == 0, out.stderr
+    cols = ("status", "src_port", "dst_port", "seq_num", "ack_num", "offset", "control", "window", "checksum",
+            "urgent_ptr", "data_off", "n_options")
+    lines = out.stdout.strip().splitlines()
+    assert len(lines) == len(meta["status"])
+    for i, ln in enumerate(lines):
+        got = [int(x) for x in ln.split()]
+        assert got == [meta[c][i] for c in cols], (i, got)
