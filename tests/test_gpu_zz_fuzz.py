@@ -253,3 +253,19 @@ def test_fuzz_rx6(case):
     if case % 4 == 0:
         assert np.array_equal(nsx.rx_ipv6_tcp_verify_host(buf, offs, tune=dict(shards_per_device=1 + case % 3)),
                               want_m), case
+
+
+@pytest.mark.parametrize("case", range(30 * SCALE))
+def test_fuzz_parse(case):
+    """Random segment batches for the receive-side parse (every kind of tests/_parse.py in random proportions,
+    random alignment and sizes) against the oracle's parseSegment (tcp.go:130-185)."""
+    import _parse
+    rng = np.random.default_rng(8000 + case)
+    n = int(rng.choice([int(rng.integers(1, 70)), int(rng.integers(60, 700)), int(rng.integers(500, 4000))]))
+    w = rng.random(len(_parse.KINDS)) ** 3
+    buf, offs, _ = _parse.batch(rng, n, weights=w / w.sum(), lead=int(rng.integers(0, 8)),
+                                max_payload=int(rng.choice([0, 40, 600, 1460])))
+    exp = _parse.expected(buf, offs)
+    got = nsx.tcp_parse_dev(_dev(buf), _dev(offs.view(np.int64)))
+    for k, v in got.items():
+        assert np.array_equal(v.cpu().numpy().view(exp[k].dtype), exp[k]), (case, k)
