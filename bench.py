@@ -113,8 +113,6 @@ def parse_args(argv=None):
                          "11: the receive pass over IPv6; 12: f1 with 9000 B MTU segments")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--settle-s", type=float, default=0.5, help="device clock settle time before warmup (setup)")
-    ap.add_argument("--event-every", type=int, default=10,
-                    help="record the per-launch HIP event pair around every N-th timed launch")
     ap.add_argument("--tune", action="append", default=[], metavar="FIELD=V",
                     help="per-call launch override (include/nsx_tune.h nsx_tune field), e.g. blocks_per_cu=2")
     ap.add_argument("--dry-run", action="store_true",
@@ -190,40 +188,41 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def timed_loop(step, sync, barrier, steps: int, warmup: int, ev_pair=None, every: int = 1):
+def timed_loop(step, sync, barrier, steps: int, warmup: int, ev_pair=None):
     """W untimed steps; then EXACTLY K steps bracketed by barrier + sync on both
-    sides. ev_pair() → (start, end) events recorded around every `every`-th
-    launch on the launch stream (per-launch kernel duration).
-    Returns (wall_s, [launch_ms])."""
+    sides. ev_pair() → (start, end) events recorded on the launch stream around
+    the K timed steps (the timed region): the mean step duration on the device,
+    inter-launch gaps included, no host synchronisation or barrier inside.
+    (Round 1 bracketed single launches; an event between two launches makes the
+    next kernel wait for the event's completion and exposes its dispatch
+    latency, which read 5-7% above the traced duration for 0.13 ms kernels.)
+    Returns (wall_s, [mean_step_ms]) ([] without ev_pair)."""
     for _ in range(warmup):
         step()
     sync()
     barrier()
     sync()
-    every = max(1, every)
-    evs = {i: ev_pair() for i in range(0, steps, every)} if ev_pair else {}
+    ev = ev_pair() if ev_pair else None
     t0 = time.perf_counter()
-    for i in range(steps):
-        e = evs.get(i)
-        if e:
-            e[0].record()
+    if ev:
+        ev[0].record()
+    for _ in range(steps):
         step()
-        if e:
-            e[1].record()
+    if ev:
+        ev[1].record()
     sync()
     barrier()
     sync()
     wall = time.perf_counter() - t0
-    launch_ms = [a.elapsed_time(b) for a, b in evs.values()]
-    return wall, launch_ms
+    return wall, ([ev[0].elapsed_time(ev[1]) / steps] if ev else [])
 
 
 def result_line(*, world, steps, warmup, wall_max, bytes_per_rank_step, units_total, workload, cfg, launch_ms,
                 alg_bytes_per_launch, cpu_baseline, traffic, dtype="u16", metric=METRIC, launches=1) -> dict:
     total_bytes = bytes_per_rank_step * world * steps
-    # launch_ms brackets one step; a step of `launches` back-to-back launches is reported per launch
-    # (alg bytes and duration divided evenly, the gaps between launches included) so that it compares
-    # with the rocprofv3 per-launch average and the PMC traffic per launch.
+    # launch_ms: mean device time of one step over the timed region; a step of `launches` back-to-back
+    # launches is reported per launch (alg bytes and duration divided evenly, the gaps between launches
+    # included) so that it compares with the rocprofv3 per-launch average and the PMC traffic per launch.
     mean_launch_ms = sum(launch_ms) / len(launch_ms) / launches if launch_ms else None
     alg_bytes_per_launch = alg_bytes_per_launch // launches
     achieved = alg_bytes_per_launch / (mean_launch_ms * 1e-3) / 1e9 if mean_launch_ms else None
@@ -707,7 +706,7 @@ def main(argv=None) -> int:
         return torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
     wall, launch_ms = timed_loop(w["step"], torch.cuda.synchronize, lambda: dist.barrier(dev_id),
-                                 args.steps, args.warmup, ev_pair, args.event_every)
+                                 args.steps, args.warmup, ev_pair)
     wall_max = dist.max(wall, device)
     cpu = None
     if dist.world == 1 and args.cpu_seconds > 0:
