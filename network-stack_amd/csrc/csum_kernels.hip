@@ -1842,9 +1842,11 @@ __global__ __launch_bounds__(kBlock) void pseudo_ipv6_kernel(const uint8_t* __re
 // the walk, NOP advances 1, MSS reads its length and advances 6 whatever the
 // length (:160-179) — and counted. Where the reference fails the segment comes
 // back zero with a status: too short (:131), data offset past the end (:152);
-// where it would panic on the MSS slice (:173-174, bytes past the segment) or
-// loop forever on another option kind (:162-178, optIdx never advances), the
-// status says so and the walk stops.
+// where its MSS slice runs past the segment (:173-174: raw[optIdx+1] past the
+// end panics; a data slice past len(raw) panics, or reads the caller's bytes
+// beyond the segment when the slice has spare capacity — not a property of the
+// bytes) or it would loop forever on another option kind (:162-178, optIdx
+// never advances), the status says so and the walk stops.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void tcp_parse_kernel(const uint8_t* __restrict__ base,
                                                            const uint64_t* __restrict__ offsets, uint64_t n,

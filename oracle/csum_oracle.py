@@ -209,9 +209,11 @@ PARSE_OK, PARSE_SHORT, PARSE_OFFSET, PARSE_OPTION_RANGE, PARSE_OPTION_KIND = 0, 
 
 def parse_segment(raw: bytes):
     """parseSegment (tcp.go:130-185), statement by statement: (Segment, status). On a reference error the
-    segment is Segment() (Go's segment{}) with status SHORT (:131-133) or OFFSET (:152-154). Where the reference
-    would panic on the MSS data slice (:173-174, a slice past the segment) or loop forever on another option kind
-    (:160-179, optIdx never advances) the status is OPTION_RANGE / OPTION_KIND and the segment is Segment()."""
+    segment is Segment() (Go's segment{}) with status SHORT (:131-133) or OFFSET (:152-154). Where the reference's
+    MSS slice runs past the segment (:173-174: the length byte past the end panics; a data slice past len(raw)
+    panics, or reads the caller's bytes beyond the segment when the slice has spare capacity, which the bytes
+    alone cannot tell) or it would loop forever on another option kind (:160-179, optIdx never advances) the
+    status is OPTION_RANGE / OPTION_KIND and the segment is Segment()."""
     raw = bytes(raw)
     if len(raw) < 20:
         return Segment(), PARSE_SHORT
