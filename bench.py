@@ -350,7 +350,7 @@ def build_workload(cfg, rank, device, tune=None):
         nsx.fill_splitmix64_dev(buf, seed)
         d_offs = torch.from_numpy(offs.view(np.int64)).to(device)
         out = torch.empty(n, dtype=torch.int16, device=device)
-        w.update(buf=buf, out=out, offsets=offs, bytes=total, alg=total + 2 * n + 8 * (n + 1),
+        w.update(buf=buf, out=out, offsets=offs, d_offs=d_offs, bytes=total, alg=total + 2 * n + 8 * (n + 1),
                  step_for=lambda t: lambda: nsx.ragged_dev(buf, d_offs, out=out, tune=t))
     w["step"] = w["step_for"](tune)  # one pass of the hot path; step_for(t) = the same with other overrides
     return w

@@ -64,6 +64,7 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             res[name].append(e0.elapsed_time(e1) / a.launches / launches)
+        print(f"round {r}: " + " ".join(f"{k} {v[-1]:.5f}" for k, v in res.items()), flush=True)
     base = None
     for name, _, launches in variants:
         med = statistics.median(res[name])
