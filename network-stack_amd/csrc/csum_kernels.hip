@@ -186,6 +186,8 @@ __device__ __forceinline__ uint32_t keep_mask(int32_t lo_r, int32_t hi_r, int32_
 }
 
 constexpr uint32_t kOOB = 0x80000000u;  // voffset that is always out of range (num_records < 2^31)
+// Cache-policy operand of a buffer store on gfx950: sc1 (bit 4) = write-through, the line leaves the XCD's L2.
+constexpr int kStoreSc1 = 16;
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint64_t bytes) {
     // Wave-uniform inputs only, so no waterfall loop (guide T20); clamp without a
@@ -1748,13 +1750,15 @@ __global__ __launch_bounds__(kBlock) void ipv4_hdr20_kernel(uint8_t* __restrict_
                 const uint32_t wi = S.tk[u] * (kHdr20Task / kWave) + (lane >> 4);  // < 2^22 (n < 2^28 per launch)
                 if (j == 15u && wi * kWave < n) mask[wi] = ((uint64_t)hi << 32) | lo;
             } else if (S.cnt[u] == kHdr20Task) {
+                // sc1 (write-through): a task's 512 B of sums are whole lines; sent on at once instead of sitting
+                // dirty in L2 until evicted among the reads, they cost 4.7% less time
                 __builtin_amdgcn_raw_buffer_store_b64(v2u{res[0] | (res[1] << 16), res[2] | (res[3] << 16)}, ors,
-                                                      i0 * 2u, 0, 0);
+                                                      i0 * 2u, 0, kStoreSc1);
             } else {
 #pragma unroll
                 for (int h = 0; h < 4; ++h)
                     __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res[h], ors, i0 + h < n ? (i0 + h) * 2u : kOOB, 0,
-                                                          0);
+                                                          kStoreSc1);
             }
             if constexpr (MODE == 1) {
 #pragma unroll
