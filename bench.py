@@ -9,7 +9,7 @@ GPU (torchrun), each checksumming its own batch: the path shards with no
 exchange, so there is no data-path collective and scaling is
 weak. value = Σ bytes over all ranks ÷ max over ranks of the timed region.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2-9]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2-12]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 `--gpus N` with N > 1 and no WORLD_SIZE in the environment launches the N rank
@@ -25,11 +25,15 @@ the same bar, each with its own metric string: 6 = the fused sender pass
 tcp.go:98-128/:68-71) over 1M 1500 B wire images; 7 = IPv4 header checksum
 verify (nsx_ipv4_hdr_csum_dev) over 64M packed 20 B headers; 8 = config 6 with a
 12 B option block per segment (the build kernel's option path); 9 =
-workload 7 verified straight into a validity bitmask (nsx_ipv4_hdr_verify_mask_dev).
+workload 7 verified straight into a validity bitmask (nsx_ipv4_hdr_verify_mask_dev);
+10 / 11 = the fused receive pass over 1M IPv4 datagrams / IPv6 packets
+(nsx_rx_ipv4_tcp_verify_dev / nsx_rx_ipv6_tcp_verify_dev); 12 = config 6 with
+9000 B MTU segments.
 
 Printed by rank 0: one JSON line with the contract fields plus
   roofline     — dominant kernel: algorithmic bytes per launch ÷ its mean
-                 duration (HIP events on the launch stream) vs 8 TB/s HBM;
+                 duration (one HIP event pair on the launch stream around
+                 the K timed steps, per launch) vs 8 TB/s HBM;
                  traffic = PMC-measured HBM bytes per launch from the committed
                  rocprofv3 summary (profiles/), or null;
   cpu_baseline — the Go-faithful CPU restatement (oracle) timed on a bounded
