@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <algorithm>
 #include <vector>
 
@@ -46,16 +47,22 @@ float run(const u32x4* p, uint64_t n16, uint32_t* out, int blocks) {
     return t[2];
 }
 
-int main() {
-    const uint64_t sizes[2] = {1572864000ull, 17179869184ull};
+// Usage: read_ceiling [bytes ...]  (default: config 2's and config 4's byte counts)
+int main(int argc, char** argv) {
+    std::vector<uint64_t> sizes = {1572864000ull, 17179869184ull};
+    if (argc > 1) {
+        sizes.clear();
+        for (int i = 1; i < argc; ++i) sizes.push_back(strtoull(argv[i], nullptr, 10) & ~15ull);
+    }
+    const uint64_t maxb = *std::max_element(sizes.begin(), sizes.end());
     int cus = 0;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
     void* buf = nullptr;
     uint32_t* out = nullptr;
-    if (hipMalloc(&buf, sizes[1]) != hipSuccess || hipMalloc(&out, 64) != hipSuccess) return 1;
-    (void)hipMemset(buf, 0x5A, sizes[1]);
+    if (hipMalloc(&buf, maxb) != hipSuccess || hipMalloc(&out, 64) != hipSuccess) return 1;
+    (void)hipMemset(buf, 0x5A, maxb);
     const u32x4* p = (const u32x4*)buf;
-    for (int k = 0; k < 200; ++k) hipLaunchKernelGGL((read_sum<4, true>), dim3(cus * 4), dim3(256), 0, 0, p, sizes[0] / 16, out);
+    for (int k = 0; k < 200; ++k) hipLaunchKernelGGL((read_sum<4, true>), dim3(cus * 4), dim3(256), 0, 0, p, std::min(maxb, sizes[0]) / 16, out);
     (void)hipDeviceSynchronize();
     for (uint64_t bytes : sizes) {
         const uint64_t n16 = bytes / 16;
