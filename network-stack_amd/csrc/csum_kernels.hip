@@ -793,12 +793,23 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
 // frame's first 20 header bytes (plus the option dwords when some lane has
 // IHL > 5): H = the header's weighted sum, computed in registers — those lines
 // are the run's own first bytes, read again from cache — and the TCP segment's
-// sum is F − H, exact. Runs are 64 frames aligned to 64, so each run's ballot is
-// one whole mask word.
+// sum is F − H, exact. Runs are 64 frames starting at a multiple of 8, so each
+// run's ballot is whole mask bytes (rx_store_mask).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t bswap16u(uint32_t v) { return ((v & 0xFFu) << 8) | ((v >> 8) & 0xFFu); }
 
 constexpr uint32_t kRxRun = 64;
+
+// A run's validity ballot (frames [a, a + cnt), a a multiple of 8) as mask bytes a/8 ..: one byte per lane
+// (lanes 0-7), so wave ranges need only be cut at multiples of 8 frames, not at whole 64-bit words; the
+// batch's last run also zero-fills the rest of the mask's last word.
+__device__ __forceinline__ void rx_store_mask(__amdgpu_buffer_rsrc_t mrs, uint64_t bits, uint32_t a, uint32_t cnt,
+                                              uint32_t n, uint32_t lane) {
+    const uint32_t nbytes = (uint64_t)a + cnt >= n ? (uint32_t)((((uint64_t)n + 63u) / 64u) * 8u - a / 8u)
+                                                   : (cnt + 7u) / 8u;
+    const uint32_t v = lane < 8u ? (uint32_t)(bits >> (8u * lane)) & 0xFFu : 0u;
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, mrs, lane < nbytes ? a / 8u + lane : kOOB, 0, 0);
+}
 
 // V6: IPv6 packets (RFC 8200 §3: fixed 40-byte header, Next Header 6 = TCP directly). There is no header
 // checksum, and the pseudo-header's addresses (RFC 8200 §8.1) are the header's own bytes 8-39, which the frame
@@ -818,7 +829,9 @@ __global__ __launch_bounds__(kBlock) void rx_tcp_kernel(const uint8_t* __restric
     const __amdgpu_buffer_rsrc_t mrs = make_rsrc(mask, (((uint64_t)n + 63) / 64) * 8);
     const __amdgpu_buffer_rsrc_t irs = make_rsrc(ip_raw, ip_raw ? (uint64_t)n * 2 : 0);
     const __amdgpu_buffer_rsrc_t trs = make_rsrc(tcp_raw, tcp_raw ? (uint64_t)n * 2 : 0);
-    // Byte-balanced wave ranges (as csum_ragged_scan_kernel), cut at multiples of 64 frames.
+    // Byte-balanced wave ranges (as csum_ragged_scan_kernel), cut at multiples of 8 frames. Cut at whole mask
+    // words (64 frames, ~50 KB) instead, a wave streamed up to one run more than the mean, and the launch
+    // waited ~20 µs for those waves at any batch size.
     uint32_t a0, a_end;
     {
         const uint32_t nb = gridDim.x, b = blockIdx.x, W = nb * kWavesPerBlock;
@@ -828,8 +841,8 @@ __global__ __launch_bounds__(kBlock) void rx_tcp_kernel(const uint8_t* __restric
         const uint64_t tot = o_hi - o_lo;
         uint32_t s[2];
         seg_lower_bound2(ofs, n, o_lo + tot * g / W, o_lo + tot * (g + 1) / W, lane, s);
-        a0 = g == 0 ? 0u : min((s[0] + 63u) & ~63u, n);
-        a_end = g + 1 == W ? n : min((s[1] + 63u) & ~63u, n);
+        a0 = g == 0 ? 0u : min((s[0] + 7u) & ~7u, n);
+        a_end = g + 1 == W ? n : min((s[1] + 7u) & ~7u, n);
     }
     auto load_off = [&](uint32_t i, bool live) -> uint64_t {
         const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, live ? i * 8 : kOOB, 0, 0);
@@ -901,8 +914,7 @@ __global__ __launch_bounds__(kBlock) void rx_tcp_kernel(const uint8_t* __restric
             const uint32_t tle = fold32((uint32_t)T) + fold32((uint32_t)(T >> 32));
             const uint32_t tcpr = well ? finish(tle, even, plen + 6u) : 0u;
             const uint64_t bits = __builtin_amdgcn_ballot_w64(well && tcpr == 0xFFFFu);
-            __builtin_amdgcn_raw_buffer_store_b64(v2w{(uint32_t)bits, (uint32_t)(bits >> 32)}, mrs,
-                                                  lane == 0 ? (a / 64u) * 8u : kOOB, 0, 0);
+            rx_store_mask(mrs, bits, a, cnt, n, lane);
             __builtin_amdgcn_raw_buffer_store_b16((uint16_t)tcpr, trs, live ? (a + lane) * 2u : kOOB, 0, 0);
             continue;
         }
@@ -947,8 +959,7 @@ __global__ __launch_bounds__(kBlock) void rx_tcp_kernel(const uint8_t* __restric
                                 bswap16u(H4 >> 16) + 6u + ((total - hlen) & 0xFFFFu);
         const uint32_t tcpr = well ? finish(tle, even, pseudo) : 0u;
         const uint64_t bits = __builtin_amdgcn_ballot_w64(well && ipr == 0xFFFFu && tcpr == 0xFFFFu);
-        __builtin_amdgcn_raw_buffer_store_b64(v2w{(uint32_t)bits, (uint32_t)(bits >> 32)}, mrs,
-                                              lane == 0 ? (a / 64u) * 8u : kOOB, 0, 0);
+        rx_store_mask(mrs, bits, a, cnt, n, lane);
         __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ipr, irs, live ? (a + lane) * 2u : kOOB, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b16((uint16_t)tcpr, trs, live ? (a + lane) * 2u : kOOB, 0, 0);
     }
