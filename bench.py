@@ -336,6 +336,8 @@ def build_workload(cfg, rank, device, tune=None):
             out = torch.empty(n, dtype=torch.int16, device=device)
             w.update(buf=buf, out=out, bytes=n * H, alg=n * (H + 2),
                      step_for=lambda t: lambda: nsx.ipv4_hdr_csum_dev(buf, H, n, mode=0, out=out, tune=t))
+        # launches per step: the library's count of its back-to-back header windows (64M headers: 2)
+        w.update(launches=nsx.ipv4_hdr_launch_count(buf, H, n, tune=tune))
     elif cfg["kind"] == "rx":
         w.update(build_rx_frames(cfg, seed, device))
         n, buf, d_offs, total = cfg["n"], w["buf"], w["d_offs"], w["bytes"]

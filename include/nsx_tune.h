@@ -79,6 +79,10 @@ int nsx_rx_ipv6_tcp_verify_host_tuned(const uint8_t* h_base, const uint64_t* h_o
 /* Kernel launches one nsx_csum_fixed_dev(_tuned) call makes for this batch on the current device (its
  * back-to-back windows; 1 for most batches), for per-launch timing in benchmarks. */
 int nsx_fixed_launch_count(uint64_t stride, uint32_t seg_len, uint64_t n, const nsx_tune* tune, uint64_t* out_count);
+/* The same for nsx_ipv4_hdr_csum_dev / nsx_ipv4_hdr_verify_mask_dev(_tuned) (d_base only for its alignment):
+ * packed 20 B headers of at least 2^26 go out as back-to-back windows of about 2^25. */
+int nsx_ipv4_hdr_launch_count(const void* d_base, uint64_t stride, uint32_t hdr_off, uint64_t n, const nsx_tune* tune,
+                              uint64_t* out_count);
 
 #ifdef __cplusplus
 }

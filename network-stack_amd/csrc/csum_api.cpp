@@ -159,6 +159,15 @@ int nsx_fixed_launch_count(uint64_t stride, uint32_t seg_len, uint64_t n, const 
     return NSX_OK;
 }
 
+int nsx_ipv4_hdr_launch_count(const void* d_base, uint64_t stride, uint32_t hdr_off, uint64_t n, const nsx_tune* tune,
+                              uint64_t* out_count) {
+    if (!out_count) return NSX_EINVAL;
+    const int dev = current_device();
+    if (dev < 0) return NSX_ENODEV;
+    *out_count = nsx::ipv4_hdr_launch_count(make_cfg(dev, tune), (uintptr_t)d_base, stride, hdr_off, n);
+    return NSX_OK;
+}
+
 int nsx_csum_ragged_dev(const void* d_base, const uint64_t* d_offsets, uint64_t n,
                         const uint32_t* d_prefix_partial, uint16_t* d_out, nsx_stream_t stream) {
     return nsx_csum_ragged_dev_tuned(d_base, d_offsets, n, d_prefix_partial, d_out, stream, nullptr);

@@ -29,6 +29,8 @@ LaunchCfg launch_cfg(int cus, const nsx_tune* t);
 
 // Kernel launches nsx_csum_fixed_dev makes for this batch (its back-to-back windows).
 uint64_t fixed_launch_count(const LaunchCfg& c, uintptr_t base, uint64_t stride, uint32_t seg_len, uint64_t n);
+// Launches one IPv4 header call makes (the packed 20 B kernel's windows).
+uint64_t ipv4_hdr_launch_count(const LaunchCfg& c, uintptr_t base, uint64_t stride, uint32_t hdr_off, uint64_t n);
 
 hipError_t launch_fixed(const LaunchCfg& c, const void* d_base, uint64_t stride, uint32_t seg_len,
                         uint64_t n, const uint32_t* partial, uint16_t* out, hipStream_t st);

@@ -104,6 +104,7 @@ def lib() -> ctypes.CDLL:
             "nsx_csum_fixed_host_tuned": [vp, u64, u32, u64, vp, vp, i32, vp],
             "nsx_csum_ragged_host_tuned": [vp, vp, u64, vp, vp, i32, vp],
             "nsx_fixed_launch_count": [u64, u32, u64, vp, ctypes.POINTER(u64)],
+            "nsx_ipv4_hdr_launch_count": [vp, u64, u32, u64, vp, ctypes.POINTER(u64)],
         }
         for name, args in sig.items():
             f = getattr(L, name)
@@ -171,6 +172,14 @@ def shard_plan(n: int, parts: int, offsets: np.ndarray | None = None) -> np.ndar
     off = None if offsets is None else np.ascontiguousarray(offsets, np.uint64)
     _check(lib().nsx_shard_plan(_np_ptr(off), n, parts, _np_ptr(b)), "nsx_shard_plan")
     return b
+
+
+def ipv4_hdr_launch_count(buf, stride: int, n: int, hdr_off: int = 0, tune=None) -> int:
+    """Kernel launches one IPv4 header call makes for this batch on the current device."""
+    c = ctypes.c_uint64(0)
+    _check(lib().nsx_ipv4_hdr_launch_count(ctypes.c_void_p(buf.data_ptr()), stride, hdr_off, n, _tune(tune),
+                                           ctypes.byref(c)), "nsx_ipv4_hdr_launch_count")
+    return c.value
 
 
 def fixed_launch_count(stride: int, seg_len: int, n: int, tune=None) -> int:

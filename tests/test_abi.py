@@ -38,7 +38,7 @@ def test_header_declares_the_boundary():
 def test_library_exports_every_declared_symbol():
     L = nsx.lib()
     declared = declared_functions() + declared_functions(TUNE_HEADER)
-    assert len(declared_functions(TUNE_HEADER)) == 13
+    assert len(declared_functions(TUNE_HEADER)) == 14
     missing = [n for n in declared if not hasattr(L, n)]
     assert not missing, missing
     out = subprocess.run(["nm", "-D", "--defined-only", nsx.LIB_PATH], capture_output=True, text=True).stdout
@@ -192,6 +192,7 @@ def test_device_calls_fail_loudly_without_gpu():
                                      None, tune) == nsx.NSX_ENODEV
     cnt = ctypes.c_uint64(7)
     assert L.nsx_fixed_launch_count(1500, 1500, 4, None, ctypes.byref(cnt)) == nsx.NSX_ENODEV
+    assert L.nsx_ipv4_hdr_launch_count(fake, 20, 0, 4, None, ctypes.byref(cnt)) == nsx.NSX_ENODEV
     buf = np.zeros(3000, np.uint8)
     with pytest.raises(nsx.NsxError) as e:
         nsx.fixed_host(buf, 1500, 1500, 2)

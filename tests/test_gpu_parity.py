@@ -429,6 +429,34 @@ def test_ipv4_packed_headers_past_the_launch_chunk():
     assert (mask[:-1] == np.uint64(0xFFFFFFFFFFFFFFFF)).all() and mask[-1] == np.uint64((1 << (n % 64)) - 1)
 
 
+def test_ipv4_packed_headers_auto_windows():
+    """2^26 + 300 packed headers (1.34 GB) go out as three back-to-back windows of whole 256-header tasks
+    (kHdrAutoWindow): raw sums and the validity bitmask equal one launch over the whole batch, and headers either
+    side of every window edge match the oracle."""
+    n, H, seed = (1 << 26) + 300, 20, 0x2A
+    t = torch.empty(n * H, dtype=torch.uint8, device="cuda")
+    nsx.fill_splitmix64_dev(t, seed)
+    t.view(n, H)[:, 0] = 0x45
+    t.view(n, H)[::7, 10] ^= 0x5A  # some headers invalid
+    one = dict(window_bytes=-1)
+    assert nsx.ipv4_hdr_launch_count(t, H, n) == 3 and nsx.ipv4_hdr_launch_count(t, H, n, tune=one) == 1
+    assert nsx.ipv4_hdr_launch_count(t, H, (1 << 26) - 1) == 1
+    win = -(-(-(-n // 3)) // 256) * 256
+    raw = u16(nsx.ipv4_hdr_csum_dev(t, H, n, mode=0))
+    assert np.array_equal(raw, u16(nsx.ipv4_hdr_csum_dev(t, H, n, mode=0, tune=one)))
+    mask = host(nsx.ipv4_hdr_verify_mask_dev(t, H, n)).view(np.uint64)
+    assert np.array_equal(mask, host(nsx.ipv4_hdr_verify_mask_dev(t, H, n, tune=one)).view(np.uint64))
+    for e in (win, 2 * win, n):
+        lo = e - 70
+        hb = host(t[lo * H:min(e + 70, n) * H])
+        m = hb.size // H
+        want = O.c_batch(hb, m, stride=20, seg_len=20)
+        assert np.array_equal(raw[lo:lo + m], want), e
+        bits = np.array([(int(mask[i // 64]) >> (i % 64)) & 1 for i in range(lo, lo + m)])
+        assert np.array_equal(bits, (want == 0xFFFF).astype(int)), e
+    assert mask[-1] >> np.uint64(n % 64) == 0
+
+
 def test_f1_build_1M_segments_full_size_roundtrip():
     """The bench's f1 workload at full size (1M x 1500 B images): the raw sums the
     build kernel reports equal an independent checksum of the images it wrote
