@@ -29,14 +29,17 @@ def main(tag, cfg, kernel_substr="csum"):
     trace = [r for r in csv.DictReader(open(os.path.join(src, "kt", "run_kernel_trace.csv")))
              if kernel_substr in r["Kernel_Name"]]
     dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in trace]
-    kname = trace[0]["Kernel_Name"]
+    # the workload kernel = the most-launched match (setup launches of the same template, e.g. the header
+    # kernel's fill mode before a verify bench, are left out of the durations and the counters)
+    kname = collections.Counter(r["Kernel_Name"] for r in trace).most_common(1)[0][0]
+    trace = [r for r in trace if r["Kernel_Name"] == kname]
     counters = collections.defaultdict(list)
     for grp in ("fetch", "write", "sq", "sq2", "tcc", "ta"):
         p = os.path.join(src, grp, "run_counter_collection.csv")
         if not os.path.exists(p):
             continue
         for r in csv.DictReader(open(p)):
-            if kernel_substr in r["Kernel_Name"]:
+            if r["Kernel_Name"] == kname:
                 counters[r["Counter_Name"]].append(float(r["Counter_Value"]))
     mean = {k: statistics.mean(v) for k, v in counters.items()}
     fetch_b = mean.get("FETCH_SIZE", 0) * 1024 * 2
