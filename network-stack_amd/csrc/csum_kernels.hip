@@ -2226,6 +2226,8 @@ hipError_t launch_verify_mask(const uint16_t* raw, uint64_t n, uint64_t* mask, u
     return hipGetLastError();
 }
 
+constexpr uint64_t kBuildGroupBytes = 24576;  // images per TCP build wave task, about
+
 hipError_t launch_tcp_build(const LaunchCfg& c, const TcpHdrSoA& h, const uint8_t* opts, const uint64_t* opt_off,
                             const uint8_t* data, const uint64_t* data_off, uint64_t data_bytes,
                             const uint32_t* partial, uint64_t n, uint8_t* out, const uint64_t* out_off,
@@ -2237,13 +2239,18 @@ hipError_t launch_tcp_build(const LaunchCfg& c, const TcpHdrSoA& h, const uint8_
     // chip's waves then hold a compact window of the batch (2048 × 16 segments in flight instead of 4096 × 64):
     // same process, three boxes, workloads 6 / 8: 0.602 / 0.609 ms against 0.633 / 0.640 for 64-segment groups
     // at 4 blocks/CU (tools/ab.py).
+    // Longer images take fewer segments per task, so that a task stays near 24 KiB of images: 256K jumbo builds
+    // (8960 B images, workload 12) in groups of 3 ran 0.888 ms against 0.934 for 16 (2: 0.891, 1: 0.901, 32:
+    // 0.946). The image size comes from the payload bytes per segment the caller passes.
     const uint32_t max_blocks = max_blocks_of(c, 2);
     const uint64_t waves = (uint64_t)max_blocks * kWavesPerBlock;
-    uint32_t group = (uint32_t)std::min<uint64_t>(16, std::max<uint64_t>(1, (n + waves - 1) / waves));
+    const uint64_t wire = data_bytes / n + 20;  // mean image bytes (options aside)
+    const uint64_t by_size = std::max<uint64_t>(1, (kBuildGroupBytes + wire / 2) / wire);
+    uint32_t group = (uint32_t)std::min<uint64_t>(std::min<uint64_t>(16, by_size), std::max<uint64_t>(1, (n + waves - 1) / waves));
     if (c.run_segs >= 1 && c.run_segs <= 64) group = (uint32_t)c.run_segs;
     const uint64_t tasks = (n + group - 1) / group;
     const uint32_t grid = grid_for(tasks, max_blocks);
-    const uint32_t clog = deal_clog(c.xcd_chunk, tasks, (uint64_t)group * 3000u);  // ~payload + image per segment
+    const uint32_t clog = deal_clog(c.xcd_chunk, tasks, (uint64_t)group * 2u * wire);  // payload + image per segment
     const int pipe = c.kernel == 2 ? 0 : c.kernel == 3 ? 2 : 1;
     if (opt_off)
         hipLaunchKernelGGL((tcp_build_kernel<0, 0, 2, true>), dim3(grid), dim3(kBlock), 0, st, h, opts, opt_off, data,
