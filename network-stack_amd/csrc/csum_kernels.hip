@@ -816,13 +816,186 @@ __device__ __forceinline__ void rx_store_mask(__amdgpu_buffer_rsrc_t mrs, uint64
 // sum F already holds in the same word pairing as the pseudo-header ‖ segment sum; so TCP sum =
 // fold(F − bytes 0-7) + payload length + 6 (the pseudo-header's length and next-header words), and the header
 // window is only the first 8 bytes (one 16 B load per lane).
+//
+// NS: 64-frame sets per run (one stream, one boundary slot per set and lane). Runs of one set suit the bench's
+// 40-1500 B frames (~50 KB per run; two sets ran 7.6% slower); a wave whose frames average
+// under kRxSmallFrame bytes takes runs of four sets, so that small frames do not pay a pipeline fill and drain
+// per few KB (§7 step 41).
+constexpr uint32_t kRxSmallFrame = 128;
+
+template <int R, bool V6, int NS>
+__device__ __forceinline__ void rx_runs(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
+                                        uint32_t a0, uint32_t a_end, uint32_t lane, __amdgpu_buffer_rsrc_t mrs,
+                                        __amdgpu_buffer_rsrc_t irs, __amdgpu_buffer_rsrc_t trs) {
+    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+    auto load_off = [&](uint32_t i, bool live) -> uint64_t {
+        const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, live ? i * 8 : kOOB, 0, 0);
+        return ((uint64_t)x.y << 32) | x.x;
+    };
+    constexpr uint32_t kStep = kRxRun * NS;
+    // lane l of set k: offsets[a + 64k + l] and offsets[a + 64k + l + 1] of the next run, prefetched one run ahead
+    uint64_t nxt_off[NS], nxt_end[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+        const uint32_t an = a0 + k * kRxRun;
+        nxt_off[k] = load_off(an + lane, an < a_end && an + lane <= n);
+        nxt_end[k] = load_off(an + lane + 1, an < a_end && an + lane + 1 <= n);
+    }
+    for (uint32_t a = a0; a < a_end; a += kStep) {
+        uint32_t cnt[NS];
+        uint64_t my_off[NS], my_end[NS];  // frame a + 64k + lane = [my_off[k], my_end[k]) for lane < cnt[k]
+        uint32_t kl = 0;                  // the last set with frames (only a wave's last run has fewer sets)
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+            const uint32_t ak = a + k * kRxRun;
+            cnt[k] = ak < a_end ? min(kRxRun, a_end - ak) : 0u;
+            kl = cnt[k] ? (uint32_t)k : kl;
+            my_off[k] = nxt_off[k], my_end[k] = nxt_end[k];
+            const uint32_t an = ak + kStep;
+            nxt_off[k] = load_off(an + lane, an < a_end && an + lane <= n);
+            nxt_end[k] = load_off(an + lane + 1, an < a_end && an + lane + 1 <= n);
+        }
+        const uint64_t lo = readlane64(my_off[0], 0);
+        uint64_t hi = 0;
+#pragma unroll
+        for (int k = 0; k < NS; ++k)
+            if ((uint32_t)k == kl) hi = readlane64(my_end[k], cnt[k] - 1);
+        const uint8_t* rbase = reinterpret_cast<const uint8_t*>(((uintptr_t)(base + lo)) & ~(uintptr_t)127);
+        const uint64_t span = (uint64_t)((base + hi) - rbase);
+        const uint32_t head = (uint32_t)((uintptr_t)(base + lo) & 127u);
+        // Header window: the 4-aligned dwords from the frame start, 24 bytes (a 16 B and an 8 B load per lane)
+        // through one descriptor over the run (rbase is 128-aligned, so window offset = brel & ~3); dwords past
+        // the run read 0, bytes past the frame or the header are masked below. Issued ahead of the stream:
+        // nothing waits for them until the run's last header step. A run wider than a descriptor (2 GiB of
+        // frames — only possible behind frames longer than any IPv4 datagram) loads per lane instead.
+        constexpr int kWin = V6 ? 3 : 6;  // window dwords: bytes 0-7 (IPv6) / 0-19 (IPv4) at any hd
+        const bool narrow = span < (1ull << 31);
+        const __amdgpu_buffer_rsrc_t hrs = make_rsrc(rbase, narrow ? ((span + 3) & ~3ull) : 0);
+        const uint32_t* last_dw =
+            reinterpret_cast<const uint32_t*>((uintptr_t)(base + (hi > lo ? hi - 1 : lo)) & ~(uintptr_t)3);
+        int64_t brel[NS];
+        uint32_t hwo[NS], d[NS][6];
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+            const bool live = lane < cnt[k];
+            brel[k] = live ? (int64_t)((base + my_off[k]) - rbase) : -1;
+            hwo[k] = live && narrow ? (uint32_t)brel[k] & ~3u : kOOB;
+            typedef uint32_t v2x __attribute__((ext_vector_type(2)));
+            const u32x4 q = bld16<false>(hrs, hwo[k]);
+            d[k][0] = q.x, d[k][1] = q.y, d[k][2] = q.z, d[k][3] = q.w;
+            d[k][4] = d[k][5] = 0u;
+            if constexpr (!V6) {
+                const v2x r = __builtin_amdgcn_raw_buffer_load_b64(hrs, hwo[k] == kOOB ? kOOB : hwo[k] + 16u, 0, 0);
+                d[k][4] = r.x, d[k][5] = r.y;
+            }
+            if (!narrow && hi > lo) {  // clamped to the run's last readable dword: every lane loads unconditionally
+                const uint8_t* fp = base + (live ? my_off[k] : lo);
+                const uint32_t* hw = reinterpret_cast<const uint32_t*>(fp - ((uintptr_t)fp & 3u));
+#pragma unroll
+                for (int j = 0; j < kWin; ++j) d[k][j] = hw + j < last_dw ? hw[j] : *last_dw;
+            }
+        }
+        // The run's bytes, S sampled at every frame start.
+        uint64_t bval[NS], carry = 0;
+#pragma unroll
+        for (int k = 0; k < NS; ++k) bval[k] = 0;
+        scan_span<R, true, NS>(rbase, span, head, brel, lane, bval, carry);
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+            if (cnt[k] == 0) break;  // wave-uniform
+            const uint32_t ak = a + k * kRxRun;
+            const bool live = lane < cnt[k];
+            const uint8_t* fp = base + (live ? my_off[k] : lo);
+            const uint32_t hd = (uint32_t)((uintptr_t)fp & 3u);
+            // a frame ends where the next one starts: the next lane's boundary, the next set's first, or the run's
+            // end (the carry)
+            uint64_t nxt = (uint64_t)__shfl_down((unsigned long long)bval[k], 1);
+            if (lane == cnt[k] - 1) {
+                uint64_t e = carry;
+#pragma unroll
+                for (int j = 0; j < NS; ++j)
+                    if (j == k + 1 && (uint32_t)k < kl) e = readlane64(bval[j], 0);
+                nxt = e;
+            }
+            const uint64_t F = nxt - bval[k];  // the frame's weighted sum (exact)
+            const uint64_t flen = my_end[k] - my_off[k];
+            const bool even = ((uintptr_t)fp & 1u) == 0;  // frame start parity = TCP segment start parity
+            if constexpr (V6) {
+                const uint32_t H0 = __builtin_amdgcn_alignbyte(d[k][1], d[k][0], hd);  // version, class, flow label
+                const uint32_t H1 = __builtin_amdgcn_alignbyte(d[k][2], d[k][1], hd);  // payload length, next header
+                const uint32_t plen = bswap16u(H1 & 0xFFFFu);
+                const bool well = live && flen >= 40u && (H0 & 0xF0u) == 0x60u && plen + 40u == flen &&
+                                  ((H1 >> 16) & 0xFFu) == 6u && plen >= 20u;  // tcp.go:131
+                uint32_t h8 = 0;
+#pragma unroll
+                for (int j = 0; j < 3; ++j)
+                    h8 = __builtin_amdgcn_sad_u16(d[k][j] & keep_mask((int32_t)hd, (int32_t)(hd + 8u), 4 * j), 0u, h8);
+                const uint64_t T = F - h8;  // addresses ‖ segment
+                const uint32_t tle = fold32((uint32_t)T) + fold32((uint32_t)(T >> 32));
+                const uint32_t tcpr = well ? finish(tle, even, plen + 6u) : 0u;
+                const uint64_t bits = __builtin_amdgcn_ballot_w64(well && tcpr == 0xFFFFu);
+                rx_store_mask(mrs, bits, ak, cnt[k], n, lane);
+                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)tcpr, trs, live ? (ak + lane) * 2u : kOOB, 0, 0);
+            } else {
+                // IPv4 header fields (RFC 791 §3.1): header dword m = bytes 4m..4m+3, little-endian view.
+                const uint32_t H0 = __builtin_amdgcn_alignbyte(d[k][1], d[k][0], hd);
+                const uint32_t H1 = __builtin_amdgcn_alignbyte(d[k][2], d[k][1], hd);
+                const uint32_t H2 = __builtin_amdgcn_alignbyte(d[k][3], d[k][2], hd);
+                const uint32_t H3 = __builtin_amdgcn_alignbyte(d[k][4], d[k][3], hd);
+                const uint32_t H4 = __builtin_amdgcn_alignbyte(d[k][5], d[k][4], hd);
+                const uint32_t ihl = H0 & 15u, hlen = ihl * 4u;
+                const uint32_t total = bswap16u(H0 >> 16);
+                const uint32_t frag = bswap16u(H1 >> 16);  // flags + fragment offset
+                const uint32_t proto = (H2 >> 8) & 0xFFu;
+                const bool hdr_ok = live && flen >= 20u && ihl >= 5u && hlen <= flen;
+                const bool well = hdr_ok && (H0 & 0xF0u) == 0x40u && total == flen && (frag & 0x3FFFu) == 0u &&
+                                  proto == 6u && total - hlen >= 20u;  // tcp.go:131: a segment is at least 20 bytes
+                // Header sum over window bytes [hd, hd + hlen): dwords 0..5 always, 6..15 when some lane has options.
+                uint32_t hs = 0;
+#pragma unroll
+                for (int j = 0; j < 6; ++j)
+                    hs = __builtin_amdgcn_sad_u16(d[k][j] & keep_mask((int32_t)hd, (int32_t)(hd + hlen), 4 * j), 0u, hs);
+                if (__builtin_amdgcn_ballot_w64(hdr_ok && ihl > 5u)) {  // option dwords 6..15
+                    uint32_t o[10];
+                    if (narrow) {
+                        typedef uint32_t v2x __attribute__((ext_vector_type(2)));
+                        const uint32_t w = hwo[k] == kOOB ? kOOB : hwo[k] + 24u;
+                        const u32x4 q0 = bld16<false>(hrs, w), q1 = bld16<false>(hrs, w == kOOB ? kOOB : w + 16u);
+                        const v2x r = __builtin_amdgcn_raw_buffer_load_b64(hrs, w == kOOB ? kOOB : w + 32u, 0, 0);
+                        o[0] = q0.x, o[1] = q0.y, o[2] = q0.z, o[3] = q0.w, o[4] = q1.x, o[5] = q1.y, o[6] = q1.z;
+                        o[7] = q1.w, o[8] = r.x, o[9] = r.y;
+                    } else {
+                        const uint32_t* hw = reinterpret_cast<const uint32_t*>(fp - hd);
+#pragma unroll
+                        for (int j = 6; j < 16; ++j) o[j - 6] = hw + j < last_dw ? hw[j] : *last_dw;
+                    }
+#pragma unroll
+                    for (int j = 6; j < 16; ++j)
+                        hs = __builtin_amdgcn_sad_u16(o[j - 6] & keep_mask((int32_t)hd, (int32_t)(hd + hlen), 4 * j), 0u,
+                                                      hs);
+                }
+                const uint32_t ipr = hdr_ok ? finish(hs, even, 0u) : 0u;
+                const uint64_t T = F - (hdr_ok ? hs : 0u);  // the TCP segment's weighted sum
+                const uint32_t tle = fold32((uint32_t)T) + fold32((uint32_t)(T >> 32));
+                const uint32_t pseudo = bswap16u(H3 & 0xFFFFu) + bswap16u(H3 >> 16) + bswap16u(H4 & 0xFFFFu) +
+                                        bswap16u(H4 >> 16) + 6u + ((total - hlen) & 0xFFFFu);
+                const uint32_t tcpr = well ? finish(tle, even, pseudo) : 0u;
+                const uint64_t bits = __builtin_amdgcn_ballot_w64(well && ipr == 0xFFFFu && tcpr == 0xFFFFu);
+                rx_store_mask(mrs, bits, ak, cnt[k], n, lane);
+                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ipr, irs, live ? (ak + lane) * 2u : kOOB, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)tcpr, trs, live ? (ak + lane) * 2u : kOOB, 0, 0);
+            }
+        }
+    }
+}
+
+// sets: 0 = by the wave's mean frame size (kRxSmallFrame), 1 / 4 = force runs of that many 64-frame sets.
 template <int R, bool V6>
 __global__ __launch_bounds__(kBlock) void rx_tcp_kernel(const uint8_t* __restrict__ base,
                                                              const uint64_t* __restrict__ offsets, uint32_t n,
                                                              uint64_t* __restrict__ mask,
                                                              uint16_t* __restrict__ ip_raw,
-                                                             uint16_t* __restrict__ tcp_raw) {
-    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+                                                             uint16_t* __restrict__ tcp_raw, int sets) {
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const __amdgpu_buffer_rsrc_t ofs = make_rsrc(offsets, ((uint64_t)n + 1) * 8);
@@ -833,6 +1006,7 @@ __global__ __launch_bounds__(kBlock) void rx_tcp_kernel(const uint8_t* __restric
     // words (64 frames, ~50 KB) instead, a wave streamed up to one run more than the mean, and the launch
     // waited ~20 µs for those waves at any batch size.
     uint32_t a0, a_end;
+    uint64_t wave_bytes;
     {
         const uint32_t nb = gridDim.x, b = blockIdx.x, W = nb * kWavesPerBlock;
         const uint32_t g = (nb >= 16 && (nb & 7) == 0) ? ((b & 7) * (nb >> 3) + (b >> 3)) * kWavesPerBlock + wave
@@ -843,125 +1017,13 @@ __global__ __launch_bounds__(kBlock) void rx_tcp_kernel(const uint8_t* __restric
         seg_lower_bound2(ofs, n, o_lo + tot * g / W, o_lo + tot * (g + 1) / W, lane, s);
         a0 = g == 0 ? 0u : min((s[0] + 7u) & ~7u, n);
         a_end = g + 1 == W ? n : min((s[1] + 7u) & ~7u, n);
+        wave_bytes = tot * (g + 1) / W - tot * g / W;
     }
-    auto load_off = [&](uint32_t i, bool live) -> uint64_t {
-        const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, live ? i * 8 : kOOB, 0, 0);
-        return ((uint64_t)x.y << 32) | x.x;
-    };
-    // lane l: offsets[a + l] and offsets[a + l + 1] of the next run, prefetched one run ahead
-    uint64_t nxt_off = load_off(a0 + lane, a0 < a_end && a0 + lane <= n);
-    uint64_t nxt_end = load_off(a0 + lane + 1, a0 < a_end && a0 + lane + 1 <= n);
-    for (uint32_t a = a0; a < a_end; a += kRxRun) {
-        const uint32_t cnt = min(kRxRun, a_end - a);
-        const uint64_t my_off = nxt_off, my_end = nxt_end;  // frame a + lane = [my_off, my_end) for lane < cnt
-        const uint32_t an = a + kRxRun;
-        nxt_off = load_off(an + lane, an < a_end && an + lane <= n);
-        nxt_end = load_off(an + lane + 1, an < a_end && an + lane + 1 <= n);
-        const bool live = lane < cnt;
-        const uint64_t lo = readlane64(my_off, 0), hi = readlane64(my_end, cnt - 1);
-        const uint8_t* fp = base + (live ? my_off : lo);
-        const uint32_t hd = (uint32_t)((uintptr_t)fp & 3u);
-        const uint8_t* rbase = reinterpret_cast<const uint8_t*>(((uintptr_t)(base + lo)) & ~(uintptr_t)127);
-        const uint64_t span = (uint64_t)((base + hi) - rbase);
-        const uint32_t head = (uint32_t)((uintptr_t)(base + lo) & 127u);
-        const int64_t brel = live ? (int64_t)((base + my_off) - rbase) : -1;
-        // Header window: the 4-aligned dwords from the frame start, 24 bytes (a 16 B and an 8 B load per lane)
-        // through one descriptor over the run (rbase is 128-aligned, so window offset = brel & ~3); dwords past
-        // the run read 0, bytes past the frame or the header are masked below. Issued ahead of the stream:
-        // nothing waits for them until the run's last header step. A run wider than a descriptor (2 GiB of
-        // frames — only possible behind frames longer than any IPv4 datagram) loads per lane instead.
-        uint32_t d[16];
-        const bool narrow = span < (1ull << 31);
-        const __amdgpu_buffer_rsrc_t hrs = make_rsrc(rbase, narrow ? ((span + 3) & ~3ull) : 0);
-        const uint32_t hwo = live && narrow ? (uint32_t)brel & ~3u : kOOB;
-        constexpr int kWin = V6 ? 3 : 6;  // window dwords: bytes 0-7 (IPv6) / 0-19 (IPv4) at any hd
-        {
-            typedef uint32_t v2x __attribute__((ext_vector_type(2)));
-            const u32x4 q = bld16<false>(hrs, hwo);
-            d[0] = q.x, d[1] = q.y, d[2] = q.z, d[3] = q.w;
-            if constexpr (!V6) {
-                const v2x r = __builtin_amdgcn_raw_buffer_load_b64(hrs, hwo == kOOB ? kOOB : hwo + 16u, 0, 0);
-                d[4] = r.x, d[5] = r.y;
-            }
-        }
-        const uint32_t* hw = reinterpret_cast<const uint32_t*>(fp - hd);
-        const uint32_t* last_dw = reinterpret_cast<const uint32_t*>((uintptr_t)(base + (hi > lo ? hi - 1 : lo)) & ~(uintptr_t)3);
-        if (!narrow && hi > lo) {  // clamped to the run's last readable dword: every lane loads unconditionally
-#pragma unroll
-            for (int k = 0; k < kWin; ++k) d[k] = hw + k < last_dw ? hw[k] : *last_dw;
-        }
-        // The run's bytes, S sampled at every frame start.
-        uint64_t bvals[1] = {0}, carry = 0;
-        const int64_t brels[1] = {brel};
-        scan_span<R, true, 1>(rbase, span, head, brels, lane, bvals, carry);
-        const uint64_t bval = bvals[0];
-        const uint64_t nbv = (uint64_t)__shfl_down((unsigned long long)bval, 1);
-        const uint64_t F = (lane == cnt - 1 ? carry : nbv) - bval;  // the frame's weighted sum (exact)
-        const uint64_t flen = my_end - my_off;
-        const bool even = ((uintptr_t)fp & 1u) == 0;  // frame start parity = TCP segment start parity
-        if constexpr (V6) {
-            const uint32_t H0 = __builtin_amdgcn_alignbyte(d[1], d[0], hd);  // version, class, flow label
-            const uint32_t H1 = __builtin_amdgcn_alignbyte(d[2], d[1], hd);  // payload length, next header, hops
-            const uint32_t plen = bswap16u(H1 & 0xFFFFu);
-            const bool well = live && flen >= 40u && (H0 & 0xF0u) == 0x60u && plen + 40u == flen &&
-                              ((H1 >> 16) & 0xFFu) == 6u && plen >= 20u;  // tcp.go:131
-            uint32_t h8 = 0;
-#pragma unroll
-            for (int k = 0; k < 3; ++k)
-                h8 = __builtin_amdgcn_sad_u16(d[k] & keep_mask((int32_t)hd, (int32_t)(hd + 8u), 4 * k), 0u, h8);
-            const uint64_t T = F - h8;  // addresses ‖ segment
-            const uint32_t tle = fold32((uint32_t)T) + fold32((uint32_t)(T >> 32));
-            const uint32_t tcpr = well ? finish(tle, even, plen + 6u) : 0u;
-            const uint64_t bits = __builtin_amdgcn_ballot_w64(well && tcpr == 0xFFFFu);
-            rx_store_mask(mrs, bits, a, cnt, n, lane);
-            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)tcpr, trs, live ? (a + lane) * 2u : kOOB, 0, 0);
-            continue;
-        }
-        // IPv4 header fields (RFC 791 §3.1): header dword m = bytes 4m..4m+3, little-endian view.
-        const uint32_t H0 = __builtin_amdgcn_alignbyte(d[1], d[0], hd);
-        const uint32_t H1 = __builtin_amdgcn_alignbyte(d[2], d[1], hd);
-        const uint32_t H2 = __builtin_amdgcn_alignbyte(d[3], d[2], hd);
-        const uint32_t H3 = __builtin_amdgcn_alignbyte(d[4], d[3], hd);
-        const uint32_t H4 = __builtin_amdgcn_alignbyte(d[5], d[4], hd);
-        const uint32_t ihl = H0 & 15u, hlen = ihl * 4u;
-        const uint32_t total = bswap16u(H0 >> 16);
-        const uint32_t frag = bswap16u(H1 >> 16);        // flags + fragment offset
-        const uint32_t proto = (H2 >> 8) & 0xFFu;
-        const bool hdr_ok = live && flen >= 20u && ihl >= 5u && hlen <= flen;
-        const bool well = hdr_ok && (H0 & 0xF0u) == 0x40u && total == flen && (frag & 0x3FFFu) == 0u &&
-                          proto == 6u && total - hlen >= 20u;  // tcp.go:131: a segment is at least 20 bytes
-        // Header sum over window bytes [hd, hd + hlen): dwords 0..5 always, 6..15 when some lane has options.
-        uint32_t hs = 0;
-#pragma unroll
-        for (int k = 0; k < 6; ++k)
-            hs = __builtin_amdgcn_sad_u16(d[k] & keep_mask((int32_t)hd, (int32_t)(hd + hlen), 4 * k), 0u, hs);
-        if (__builtin_amdgcn_ballot_w64(hdr_ok && ihl > 5u)) {  // option dwords 6..15
-            if (narrow) {
-                typedef uint32_t v2x __attribute__((ext_vector_type(2)));
-                const uint32_t o = hwo == kOOB ? kOOB : hwo + 24u;
-                const u32x4 q0 = bld16<false>(hrs, o), q1 = bld16<false>(hrs, o == kOOB ? kOOB : o + 16u);
-                const v2x r = __builtin_amdgcn_raw_buffer_load_b64(hrs, o == kOOB ? kOOB : o + 32u, 0, 0);
-                d[6] = q0.x, d[7] = q0.y, d[8] = q0.z, d[9] = q0.w, d[10] = q1.x, d[11] = q1.y, d[12] = q1.z;
-                d[13] = q1.w, d[14] = r.x, d[15] = r.y;
-            } else {
-#pragma unroll
-                for (int k = 6; k < 16; ++k) d[k] = hw + k < last_dw ? hw[k] : *last_dw;
-            }
-#pragma unroll
-            for (int k = 6; k < 16; ++k)
-                hs = __builtin_amdgcn_sad_u16(d[k] & keep_mask((int32_t)hd, (int32_t)(hd + hlen), 4 * k), 0u, hs);
-        }
-        const uint32_t ipr = hdr_ok ? finish(hs, even, 0u) : 0u;
-        const uint64_t T = F - (hdr_ok ? hs : 0u);     // the TCP segment's weighted sum
-        const uint32_t tle = fold32((uint32_t)T) + fold32((uint32_t)(T >> 32));
-        const uint32_t pseudo = bswap16u(H3 & 0xFFFFu) + bswap16u(H3 >> 16) + bswap16u(H4 & 0xFFFFu) +
-                                bswap16u(H4 >> 16) + 6u + ((total - hlen) & 0xFFFFu);
-        const uint32_t tcpr = well ? finish(tle, even, pseudo) : 0u;
-        const uint64_t bits = __builtin_amdgcn_ballot_w64(well && ipr == 0xFFFFu && tcpr == 0xFFFFu);
-        rx_store_mask(mrs, bits, a, cnt, n, lane);
-        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ipr, irs, live ? (a + lane) * 2u : kOOB, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)tcpr, trs, live ? (a + lane) * 2u : kOOB, 0, 0);
-    }
+    const bool small = sets == 4 || (sets == 0 && wave_bytes < (uint64_t)kRxSmallFrame * (a_end - a0));
+    if (small)
+        rx_runs<R, V6, 4>(base, ofs, n, a0, a_end, lane, mrs, irs, trs);
+    else
+        rx_runs<R, V6, 1>(base, ofs, n, a0, a_end, lane, mrs, irs, trs);
 }
 
 // ---------------------------------------------------------------------------
@@ -2168,6 +2230,8 @@ hipError_t launch_rx_tcp(const LaunchCfg& c, int ipver, const void* d_base, cons
     // 0.1305 for batches of 4 rows, 0.1348 for single batches of 8 rows, 0.145 for 2 rows at 2 blocks/CU, 0.136
     // at 4); launches of ≤ 2^27 frames (a multiple of 64, so every launch starts on a mask word)
     const int rows = (c.rows == 2 || c.rows == 4 || c.rows == 8 || c.rows == 16) ? c.rows : 2;
+    // 64-frame sets per run: by each wave's mean frame size, or forced by segs_per_wave 1 / 4 (tests)
+    const int sets = c.segs_per_wave == 1 || c.segs_per_wave == 4 ? c.segs_per_wave : 0;
     const uint32_t mb = max_blocks_of(c, 3);
     const uint8_t* base = static_cast<const uint8_t*>(d_base);
     for (uint64_t c0 = 0; c0 < n; c0 += kRaggedChunk) {
@@ -2178,10 +2242,10 @@ hipError_t launch_rx_tcp(const LaunchCfg& c, int ipver, const void* d_base, cons
 #define NSX_RX(R_)                                                                                                \
         if (rows == R_ && ipver == 6)                                                                              \
             hipLaunchKernelGGL((rx_tcp_kernel<R_, true>), dim3(grid), dim3(kBlock), 0, st, base, d_offsets + c0, cn,  \
-                               mask + c0 / 64, nullptr, tc);                                                       \
+                               mask + c0 / 64, nullptr, tc, sets);                                                       \
         if (rows == R_ && ipver != 6)                                                                              \
             hipLaunchKernelGGL((rx_tcp_kernel<R_, false>), dim3(grid), dim3(kBlock), 0, st, base, d_offsets + c0, cn, \
-                               mask + c0 / 64, ic, tc);
+                               mask + c0 / 64, ic, tc, sets);
         NSX_RX(2) NSX_RX(4) NSX_RX(8) NSX_RX(16)
 #undef NSX_RX
         const hipError_t e = hipGetLastError();

@@ -53,7 +53,22 @@ def test_rx_mixed_batches(n, lead):
         assert np.array_equal(w, g), (what, n, lead)
 
 
-TUNES = [dict(rows=2), dict(rows=4), dict(rows=16), dict(blocks_per_cu=1), dict(blocks_per_cu=8), dict(rows=16, blocks_per_cu=1)]
+TUNES = [dict(rows=2), dict(rows=4), dict(rows=16), dict(blocks_per_cu=1), dict(blocks_per_cu=8), dict(rows=16, blocks_per_cu=1),
+         dict(segs_per_wave=4), dict(segs_per_wave=4, rows=4), dict(segs_per_wave=1)]  # runs of 4 / 1 frame sets
+
+
+@pytest.mark.parametrize("n", [1, 255, 256, 257, 1000, 30_001])
+@pytest.mark.parametrize("lead", [0, 3])
+def test_rx_small_frames_runs_of_four_sets(n, lead):
+    """Frames of at most 40 B of payload: waves whose frames average under 128 B stream runs of four 64-frame sets
+    (DESIGN.md §7 step 41); every set boundary, partial last sets and both run forms equal the oracle."""
+    rng = np.random.default_rng(n * 2 + lead)
+    buf, offs, _ = _rx.batch(rng, n, lead=lead, max_payload=40)
+    want = O.c_rx_ipv4_tcp(buf, offs)
+    for tune in (None, dict(segs_per_wave=1), dict(segs_per_wave=4)):
+        got = run_rx(buf, offs, tune)
+        for w, g, what in zip(want, got, ("mask", "ip_raw", "tcp_raw")):
+            assert np.array_equal(w, g), (what, n, lead, tune)
 
 
 @pytest.mark.parametrize("tune", TUNES, ids=lambda t: ",".join(f"{k}={v}" for k, v in t.items()))

@@ -33,11 +33,15 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--launches", type=int, default=50)
     ap.add_argument("--n", type=int, default=0, help="override the workload's unit count")
+    ap.add_argument("--set", action="append", default=[], help="override a workload field, key=int")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     cfg = dict(bench.WORKLOADS[a.config])
     if a.n:
         cfg["n"] = a.n
+    for kv in a.set:
+        k, _, v = kv.partition("=")
+        cfg[k] = int(v)
     w = bench.build_workload(cfg, 0, torch.device("cuda", 0))
     variants = []
     for item in a.variants.split(";"):
@@ -73,7 +77,7 @@ def main():
         med = statistics.median(res[name])
         frac = w["alg"] / launches / (med * 1e-3) / 1e9 / bench.HBM_PEAK_GBPS
         base = base or med
-        print(f"AB config{a.config}{f' n={a.n}' if a.n else ''} {name:16s} median {med:.5f} ms/launch  frac {frac:.4f}  vs first {med / base:.4f}  "
+        print(f"AB config{a.config}{f' n={a.n}' if a.n else ''}{''.join(' ' + x for x in a.set)} {name:16s} median {med:.5f} ms/launch  frac {frac:.4f}  vs first {med / base:.4f}  "
               f"min {min(res[name]):.5f} max {max(res[name]):.5f}", flush=True)
 
 
