@@ -687,33 +687,15 @@ __device__ __forceinline__ void scan_span(const uint8_t* rbase, uint64_t span, u
         if (brel[k] >= (int64_t)(nrows * kRow)) bval[k] = carry;  // boundary at the very end of the rows
 }
 
+constexpr uint32_t kScanSmallSeg = 256;
+
+// The wave's runs [a0, a_end) of NS sets of ≤ run segments (see csum_ragged_scan_kernel).
 template <int R, bool VERIFY, bool PIPE, int NS>
-__global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
-    const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, uint32_t n,
-    const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t run) {
+__device__ __forceinline__ void ragged_runs(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
+                                            __amdgpu_buffer_rsrc_t prs, __amdgpu_buffer_rsrc_t ors,
+                                            __amdgpu_buffer_rsrc_t oks, uint32_t run, uint32_t a0, uint32_t a_end,
+                                            uint32_t lane) {
     typedef uint32_t v2u __attribute__((ext_vector_type(2)));
-    const uint32_t lane = threadIdx.x & (kWave - 1);
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const __amdgpu_buffer_rsrc_t ofs = make_rsrc(offsets, ((uint64_t)n + 1) * 8);
-    const __amdgpu_buffer_rsrc_t prs = make_rsrc(partial, partial ? (uint64_t)n * 4 : 0);
-    const __amdgpu_buffer_rsrc_t ors = make_rsrc(out, out ? (uint64_t)n * 2 : 0);
-    const __amdgpu_buffer_rsrc_t oks = make_rsrc(ok, VERIFY ? (uint64_t)n : 0);
-    // The wave's tasks are runs of NS sets [a_k, a_k + cnt_k) of ≤ run segments each (a_k = a + k·run), a = a0,
-    // a0 + NS·run, ... < a_end; a run never crosses a_end. Byte-balanced: wave g (XCD-contiguous numbering) owns
-    // the segments that start in the g-th of W equal byte slices of the batch, so every wave streams the same
-    // bytes (± one segment) and none is left running alone at the end of the launch.
-    uint32_t a0, a_end;
-    {
-        const uint32_t nb = gridDim.x, b = blockIdx.x, W = nb * kWavesPerBlock;
-        const uint32_t g = (nb >= 16 && (nb & 7) == 0) ? ((b & 7) * (nb >> 3) + (b >> 3)) * kWavesPerBlock + wave
-                                                        : b * kWavesPerBlock + wave;
-        const uint64_t o_lo = ld_off(ofs, 0), o_hi = ld_off(ofs, n);
-        const uint64_t tot = o_hi - o_lo;
-        uint32_t s[2];
-        seg_lower_bound2(ofs, n, o_lo + tot * g / W, o_lo + tot * (g + 1) / W, lane, s);
-        a0 = g == 0 ? 0u : s[0];
-        a_end = g + 1 == W ? n : s[1];
-    }
     const uint32_t a_step = run * NS;
     auto load_offs = [&](uint32_t a) -> uint64_t {  // lane l ≤ run length: offsets[a + l]
         const uint32_t voff = (a < a_end && lane <= run && a + lane <= n) ? (a + lane) * 8 : kOOB;
@@ -771,6 +753,43 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
                 __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(res == 0xFFFFu), oks, mine ? ak + lane : kOOB, 0, 0);
         }
     }
+}
+
+
+template <int R, bool VERIFY, bool PIPE, int NS>
+__global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
+    const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, uint32_t n,
+    const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t run, int sets) {
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const __amdgpu_buffer_rsrc_t ofs = make_rsrc(offsets, ((uint64_t)n + 1) * 8);
+    const __amdgpu_buffer_rsrc_t prs = make_rsrc(partial, partial ? (uint64_t)n * 4 : 0);
+    const __amdgpu_buffer_rsrc_t ors = make_rsrc(out, out ? (uint64_t)n * 2 : 0);
+    const __amdgpu_buffer_rsrc_t oks = make_rsrc(ok, VERIFY ? (uint64_t)n : 0);
+    // The wave's tasks are runs of NS sets [a_k, a_k + cnt_k) of ≤ run segments each (a_k = a + k·run), a = a0,
+    // a0 + NS·run, ... < a_end; a run never crosses a_end. Byte-balanced: wave g (XCD-contiguous numbering) owns
+    // the segments that start in the g-th of W equal byte slices of the batch, so every wave streams the same
+    // bytes (± one segment) and none is left running alone at the end of the launch.
+    uint32_t a0, a_end;
+    uint64_t wave_bytes;
+    {
+        const uint32_t nb = gridDim.x, b = blockIdx.x, W = nb * kWavesPerBlock;
+        const uint32_t g = (nb >= 16 && (nb & 7) == 0) ? ((b & 7) * (nb >> 3) + (b >> 3)) * kWavesPerBlock + wave
+                                                        : b * kWavesPerBlock + wave;
+        const uint64_t o_lo = ld_off(ofs, 0), o_hi = ld_off(ofs, n);
+        const uint64_t tot = o_hi - o_lo;
+        uint32_t s[2];
+        seg_lower_bound2(ofs, n, o_lo + tot * g / W, o_lo + tot * (g + 1) / W, lane, s);
+        a0 = g == 0 ? 0u : s[0];
+        a_end = g + 1 == W ? n : s[1];
+        wave_bytes = tot * (g + 1) / W - tot * g / W;
+    }
+    // Two sets per run suit segments of a few hundred bytes and up (config 3); a wave whose segments average under
+    // kScanSmallSeg bytes takes runs of four sets, so that each run still streams tens of KB (§7 step 42).
+    if (NS == 2 && (sets == 4 || (sets == 0 && wave_bytes < (uint64_t)kScanSmallSeg * (a_end - a0))))
+        ragged_runs<R, VERIFY, PIPE, 4>(base, ofs, n, prs, ors, oks, run, a0, a_end, lane);
+    else
+        ragged_runs<R, VERIFY, PIPE, NS>(base, ofs, n, prs, ors, oks, run, a0, a_end, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -2186,6 +2205,7 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
     // are paid half as often (config 3 0.684 → 0.682 ms, 40-1500 B frames 0.1320 → 0.1293; 4 sets: 0.683 /
     // 0.1308, more registers and phase-2 checks); segs_per_wave = 1 keeps one set.
     const int ns = (pipe && rows == 2 && c.segs_per_wave != 1) ? 2 : 1;
+    const int sets = c.segs_per_wave == 4 ? 4 : 0;  // force runs of four sets (tests); 0: by mean segment size
     const uint32_t mb = max_blocks_of(c, 2);
     for (uint64_t c0 = 0; c0 < n; c0 += kRaggedChunk) {
         const uint32_t cn = (uint32_t)(n - c0 < kRaggedChunk ? n - c0 : kRaggedChunk);
@@ -2196,7 +2216,7 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
 #define NSX_RSCAN(R_, P_, NS_)                                                                                 \
         if (rows == R_ && pipe == P_ && ns == NS_)                                                              \
             hipLaunchKernelGGL((csum_ragged_scan_kernel<R_, VERIFY, P_, NS_>), dim3(grid), dim3(kBlock), 0, st,  \
-                               base, offsets + c0, cn, pc, oc, kc, run);
+                               base, offsets + c0, cn, pc, oc, kc, run, sets);
         NSX_RSCAN(2, true, 1) NSX_RSCAN(4, true, 1) NSX_RSCAN(8, true, 1)
         NSX_RSCAN(4, false, 1) NSX_RSCAN(8, false, 1) NSX_RSCAN(16, false, 1)
         NSX_RSCAN(2, true, 2)

@@ -120,7 +120,31 @@ RAGGED_TUNES = [dict(kernel=k, rows=r, run_segs=rs, blocks_per_cu=b)  # pipeline
                 for k, rows in ((0, (0, 4, 8)), (nsx.KERNEL_SCAN_PLAIN, (0, 4, 16))) for r in rows
                 for rs in (0, 1, 16, 63) for b in (0, 1, 8)] + \
                [dict(segs_per_wave=1, run_segs=rs, blocks_per_cu=b)  # one boundary set per lane (default: two)
+                for rs in (0, 1, 16, 63) for b in (0, 1, 8)] + \
+               [dict(segs_per_wave=4, run_segs=rs, blocks_per_cu=b)  # runs of four sets (small segments' form)
                 for rs in (0, 1, 16, 63) for b in (0, 1, 8)]
+
+
+@pytest.mark.parametrize("n", [1, 126, 252, 253, 30_001])
+def test_ragged_small_segments_runs_of_four_sets(n):
+    """Segments of 0-200 B (mean ~100): waves whose segments average under 256 B take runs of four 63-segment sets
+    (DESIGN.md §7 step 42); the automatic choice and both forced forms equal the oracle, with and without partials."""
+    rng = np.random.default_rng(n + 42)
+    lens = rng.integers(0, 201, n).astype(np.uint64)
+    offs = np.zeros(n + 1, np.uint64)
+    offs[1:] = np.cumsum(lens)
+    offs += np.uint64(3)
+    buf = O.c_splitmix64(0x42, int(offs[-1]) + 3)
+    part = rng.integers(0, 1 << 31, n, dtype=np.uint32)
+    want = O.c_batch(buf, n, offsets=offs)
+    want_p = O.c_batch(buf, n, offsets=offs, partial=part)
+    d, o, p = dev(buf), dev(offs.view(np.int64)), dev(part.view(np.int32))
+    for tune in (None, dict(segs_per_wave=1), dict(segs_per_wave=4)):
+        out = torch.empty(n, dtype=torch.int16, device="cuda")
+        nsx.ragged_dev(d, o, out=out, tune=tune)
+        assert np.array_equal(u16(out), want), tune
+        nsx.ragged_dev(d, o, partial=p, out=out, tune=tune)
+        assert np.array_equal(u16(out), want_p), tune
 
 
 def test_ragged_launch_shapes_bit_exact():
