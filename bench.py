@@ -9,14 +9,18 @@ GPU (torchrun), each checksumming its own batch: the path shards with no
 exchange, so there is no data-path collective and scaling is
 weak. value = Σ bytes over all ranks ÷ max over ranks of the timed region.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2-12]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2-16]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 `--gpus N` with N > 1 and no WORLD_SIZE in the environment launches the N rank
 processes itself (a torch.distributed.run child, rendezvous at 127.0.0.1) before
 anything touches a GPU, and relays rank 0's line; under a launcher that already
 set WORLD_SIZE, a WORLD_SIZE that differs from --gpus is an error (exit 2), as is
-more RCCL ranks than visible GPUs.
+more RCCL ranks than visible GPUs. Each rank makes its GPU (LOCAL_RANK) current
+before the process group is created; the ranks then exchange their devices' PCI
+address and UUID, every line carries `ranks`, `distinct_devices` and the device
+list with n_gpus = distinct devices, and RCCL ranks that landed on fewer distinct
+GPUs than ranks exit 3 instead of printing a line.
 
 Configs 2-5 are BASELINE.json's device-resident configurations (2 is the
 headline and the default). Configs 6 and 7 measure SURVEY.md §8's next rows to
@@ -28,7 +32,9 @@ verify (nsx_ipv4_hdr_csum_dev) over 64M packed 20 B headers; 8 = config 6 with a
 workload 7 verified straight into a validity bitmask (nsx_ipv4_hdr_verify_mask_dev);
 10 / 11 = the fused receive pass over 1M IPv4 datagrams / IPv6 packets
 (nsx_rx_ipv4_tcp_verify_dev / nsx_rx_ipv6_tcp_verify_dev); 12 = config 6 with
-9000 B MTU segments.
+9000 B MTU segments; 13 / 16 = the receive pass over 8M ACK-sized (40-100 B IPv4 /
+60-120 B IPv6) frames; 14 = over a bimodal mix of ACKs and 1500 B data frames;
+15 = config 3's small-segment twin (8M ragged 64-128 B segments).
 
 Printed by rank 0: one JSON line with the contract fields plus
   roofline     — dominant kernel: algorithmic bytes per launch ÷ its mean
@@ -103,7 +109,37 @@ WORKLOADS = {
              metric="GiB/s fused receive verify (IPv6 pseudo-header + TCP checksum into a bitmask), packet bytes",
              name="f2 rx6: 1M IPv6/TCP packets per GPU, 60-1500B (uniform), densely packed (odd starts), "
                   "1 in 1000 corrupted, verified into a validity bitmask, device-resident"),
+    # not BASELINE configs: the receiver's common case, ACK-sized frames (a TCP receiver's 40-66 B ACKs;
+    # tcp.go:70 receiver rule, tcp.go:56,131 minSegmentLength 20 B): small-frame twins of workloads 10, 11 and 3
+    13: dict(kind="rx", n=1 << 23, lo=40, hi=100, seed=0x107C,
+             metric="GiB/s fused receive verify (IPv4 header + pseudo-header + TCP checksum into a bitmask), frame bytes",
+             name="f2+f3 rx small: 8M IPv4/TCP datagrams per GPU, 40-100B (uniform, ACK-sized), densely packed "
+                  "(odd starts), 1 in 1000 corrupted, verified into a validity bitmask, device-resident"),
+    14: dict(kind="rx", n=1 << 21, mix="ack_data", seed=0x107D,
+             metric="GiB/s fused receive verify (IPv4 header + pseudo-header + TCP checksum into a bitmask), frame bytes",
+             name="f2+f3 rx bimodal: 2M IPv4/TCP datagrams per GPU, half 40-66B ACKs and half 1500B data frames "
+                  "(random order), densely packed (odd starts), 1 in 1000 corrupted, verified into a validity "
+                  "bitmask, device-resident"),
+    15: dict(kind="ragged", n=1 << 23, lo=64, hi=128, seed=0x107E,
+             metric="GiB/s device-resident Internet checksum, ragged segments",
+             name="config3 small-segment twin: 8M ragged 64-128B segments per GPU, densely packed (odd starts), "
+                  "device-resident"),
+    16: dict(kind="rx", ipver=6, n=1 << 23, lo=60, hi=120, seed=0x107F,
+             metric="GiB/s fused receive verify (IPv6 pseudo-header + TCP checksum into a bitmask), packet bytes",
+             name="f2 rx6 small: 8M IPv6/TCP packets per GPU, 60-120B (uniform, ACK-sized), densely packed "
+                  "(odd starts), 1 in 1000 corrupted, verified into a validity bitmask, device-resident"),
 }
+
+
+def frame_lengths(cfg):
+    """Per-unit byte lengths of a ragged / receive workload (the same on every rank; bytes differ by seed):
+    uniform on [lo, hi], or the bimodal ACK/data mix (half uniform on [40, 66], half 1500)."""
+    import numpy as np
+    rng = np.random.default_rng(cfg["seed"])
+    n = cfg["n"]
+    if cfg.get("mix") == "ack_data":
+        return np.where(rng.random(n) < 0.5, rng.integers(40, 67, n), 1500).astype(np.uint64)
+    return rng.integers(cfg["lo"], cfg["hi"] + 1, n).astype(np.uint64)
 
 
 def parse_args(argv=None):
@@ -114,7 +150,9 @@ def parse_args(argv=None):
     ap.add_argument("--config", type=int, default=2, choices=sorted(WORKLOADS),
                     help="2-5: BASELINE configs (2 = headline); 6: f1 fused TCP build; 7: f3 IPv4 header verify; "
                          "8: f1 with 12 B options; 9: f3 verify into a bitmask; 10: fused receive pass (f2+f3); "
-                         "11: the receive pass over IPv6; 12: f1 with 9000 B MTU segments")
+                         "11: the receive pass over IPv6; 12: f1 with 9000 B MTU segments; 13 / 16: the receive "
+                         "pass over 8M ACK-sized IPv4 / IPv6 frames; 14: over a bimodal ACK/1500 B mix; 15: config 3's "
+                         "small-segment twin (8M x 64-128 B)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--settle-s", type=float, default=0.5, help="device clock settle time before warmup (setup)")
     ap.add_argument("--tune", action="append", default=[], metavar="FIELD=V",
@@ -151,7 +189,10 @@ def launch_ranks(nranks: int, argv: list) -> int:
 # distributed plumbing (shared with the gloo CPU tests)
 # ---------------------------------------------------------------------------
 class Dist:
-    def __init__(self, backend: str | None):
+    def __init__(self, backend: str | None, device_id=None):
+        """device_id: this rank's GPU, already made current by the caller (torch.cuda.set_device BEFORE
+        init_process_group, so no rank's communicator is created on GPU 0); passed on for nccl so RCCL
+        binds the rank to it eagerly."""
         import torch.distributed as dist
         self.dist = dist
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -160,7 +201,16 @@ class Dist:
         self.on = self.world > 1
         if self.on and not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            dist.init_process_group(backend=backend)
+            kw = {"device_id": device_id} if backend == "nccl" and device_id is not None else {}
+            dist.init_process_group(backend=backend, **kw)
+
+    def gather(self, obj) -> list:
+        """Every rank's `obj`, in rank order (one rank: [obj])."""
+        if not self.on:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
 
     def barrier(self, device=None):
         if self.on:
@@ -221,8 +271,30 @@ def timed_loop(step, sync, barrier, steps: int, warmup: int, ev_pair=None):
     return wall, ([ev[0].elapsed_time(ev[1]) / steps] if ev else [])
 
 
+def device_identity(dev_id: int) -> dict:
+    """This rank's GPU as the driver sees it: hostname + PCI domain:bus:device and UUID. Two ranks on one
+    physical GPU give the same key, so the line can prove how many distinct GPUs produced it."""
+    import torch
+    p = torch.cuda.get_device_properties(dev_id)
+    pci = "%04x:%02x:%02x" % (getattr(p, "pci_domain_id", 0), getattr(p, "pci_bus_id", 0),
+                              getattr(p, "pci_device_id", 0))
+    uuid = str(getattr(p, "uuid", "") or "")
+    return {"host": socket.gethostname(), "local_device": dev_id, "pci": pci, "uuid": uuid,
+            "key": f"{socket.gethostname()}/{pci}/{uuid}"}
+
+
+def device_fields(idents: list) -> dict:
+    """Line fields from every rank's device_identity (rank order): n_gpus = distinct physical devices."""
+    distinct = len({d["key"] for d in idents})
+    return {"n_gpus": distinct, "ranks": len(idents), "distinct_devices": distinct,
+            "devices": [{k: d[k] for k in ("host", "local_device", "pci", "uuid")} for d in idents]}
+
+
 def result_line(*, world, steps, warmup, wall_max, bytes_per_rank_step, units_total, workload, cfg, launch_ms,
-                alg_bytes_per_launch, cpu_baseline, traffic, dtype="u16", metric=METRIC, launches=1) -> dict:
+                alg_bytes_per_launch, cpu_baseline, traffic, dtype="u16", metric=METRIC, launches=1,
+                n_gpus=None) -> dict:
+    """world = ranks (each processed bytes_per_rank_step per step); n_gpus = distinct physical GPUs behind
+    them (default: one per rank)."""
     total_bytes = bytes_per_rank_step * world * steps
     # launch_ms: mean device time of one step over the timed region; a step of `launches` back-to-back
     # launches is reported per launch (alg bytes and duration divided evenly, the gaps between launches
@@ -235,7 +307,8 @@ def result_line(*, world, steps, warmup, wall_max, bytes_per_rank_step, units_to
         "value": round(total_bytes / wall_max / GIB, 3),
         "unit": "GiB/s",
         "value_per_gpu": round(total_bytes / wall_max / GIB / world, 3),
-        "n_gpus": world,
+        "n_gpus": world if n_gpus is None else n_gpus,
+        "ranks": world,
         "steps": steps,
         "warmup": warmup,
         "ms_per_step": round(wall_max / steps * 1e3, 5),
@@ -346,9 +419,8 @@ def build_workload(cfg, rank, device, tune=None):
         w.update(out=out, alg=total + 8 * (n + 1) + (n + 63) // 64 * 8,
                  step_for=lambda t: lambda: rx(buf, d_offs, mask=out, tune=t))
     else:
-        rng = np.random.default_rng(cfg["seed"])  # same lengths on every rank, bytes differ by seed
         n = cfg["n"]
-        lens = rng.integers(cfg["lo"], cfg["hi"] + 1, n).astype(np.uint64)
+        lens = frame_lengths(cfg)  # same lengths on every rank, bytes differ by seed
         offs = np.zeros(n + 1, np.uint64)
         offs[1:] = np.cumsum(lens)
         total = int(offs[-1])
@@ -409,8 +481,7 @@ def build_rx_frames(cfg, seed, device) -> dict:
     import torch
     import nsx
     n = cfg["n"]
-    rng = np.random.default_rng(cfg["seed"])
-    lens = rng.integers(cfg["lo"], cfg["hi"] + 1, n).astype(np.uint64)
+    lens = frame_lengths(cfg)
     offs = np.zeros(n + 1, np.uint64)
     offs[1:] = np.cumsum(lens)
     total = int(offs[-1])
@@ -653,11 +724,16 @@ def dry_run(args) -> int:
     wall, launch_ms = timed_loop(lambda: O.c_batch(buf, n, stride=L, seg_len=L, threads=1), lambda: None,
                                  dist.barrier, args.steps, args.warmup)
     wall_max = dist.max(wall)
+    idents = dist.gather({"host": socket.gethostname(), "local_device": None, "pci": None, "uuid": None,
+                          "key": None})
     line = result_line(world=dist.world, steps=args.steps, warmup=args.warmup, wall_max=wall_max,
                        bytes_per_rank_step=n * L, units_total=n * dist.world, workload="dry run", cfg={"n": n, "seed": 0x1071},
-                       launch_ms=launch_ms, alg_bytes_per_launch=n * L + 2 * n, cpu_baseline=None, traffic=None)
+                       launch_ms=launch_ms, alg_bytes_per_launch=n * L + 2 * n, cpu_baseline=None, traffic=None,
+                       n_gpus=0)
+    # no GPU behind any rank: n_gpus 0, the rank count separate
     line.update(dry_run=True, data="dry run: the CPU oracle stands in for the GPU kernel; not a measurement",
-                ranks=dist.world, backend="gloo")
+                backend="gloo", rehearsal=True, distinct_devices=0,
+                devices=[{k: d[k] for k in ("host", "local_device", "pci", "uuid")} for d in idents])
     if dist.rank == 0:
         print(json.dumps(line), flush=True)
     dist.close()
@@ -688,10 +764,19 @@ def main(argv=None) -> int:
         print(f"bench.py: {world} ranks but {ndev} visible GPU(s): one rank per GPU is required "
               "(NSX_BENCH_BACKEND=gloo runs a labelled rehearsal)", file=sys.stderr)
         return 2
-    dist = Dist(backend)
-    dev_id = dist.local_rank % ndev if dist.on else 0
+    # this rank's GPU is made current BEFORE the process group exists (and handed to it), so RCCL never
+    # creates a rank's communicator on GPU 0
+    dev_id = int(os.environ.get("LOCAL_RANK", "0")) % ndev if world > 1 else 0
     torch.cuda.set_device(dev_id)
     device = torch.device("cuda", dev_id)
+    dist = Dist(backend, device_id=device)
+    devf = device_fields(dist.gather(device_identity(dev_id)))
+    if dist.on and backend == "nccl" and devf["distinct_devices"] < dist.world:
+        if dist.rank == 0:
+            print(f"bench.py: {dist.world} RCCL ranks ran on {devf['distinct_devices']} distinct GPU(s) "
+                  f"({devf['devices']}): refusing to report them as {dist.world} GPUs", file=sys.stderr)
+        dist.close()
+        return 3
     tune = parse_tune(args.tune) or None
 
     cfg = WORKLOADS[args.config]
@@ -722,10 +807,11 @@ def main(argv=None) -> int:
                        cfg=cfg, launch_ms=launch_ms, alg_bytes_per_launch=w["alg"], cpu_baseline=cpu,
                        # the committed PMC traffic was profiled at the default launch shape
                        traffic=None if tune else load_traffic(args.config), metric=cfg.get("metric", METRIC),
-                       launches=w.get("launches", 1))
+                       launches=w.get("launches", 1), n_gpus=devf["n_gpus"])
     line["backend"] = backend if dist.on else None
-    if dist.on and world > ndev:
-        line.update(rehearsal=True, distinct_devices=ndev)
+    line.update({k: v for k, v in devf.items() if k != "n_gpus"})
+    if devf["distinct_devices"] < dist.world:  # gloo rehearsal: ranks share a GPU; n_gpus counts GPUs
+        line["rehearsal"] = True
     if tune:
         line["config"]["tune"] = tune
     if dist.rank == 0:

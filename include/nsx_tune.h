@@ -29,8 +29,13 @@ extern "C" {
 
 typedef struct nsx_tune {
     int32_t blocks_per_cu;     /* persistent grid: 1..8 blocks of 256 threads per CU */
-    int32_t segs_per_wave;     /* fixed batches of <= 4 KiB segments: segments per wave task (1, 2, 4, 8);
-                                  ragged scan: 1 = one boundary set per lane (default two) */
+    int32_t segs_per_wave;     /* fixed batches of <= 4 KiB segments: segments per wave task (1, 2, 4, 8).
+                                  Ragged scan, 63-segment boundary sets per run: 0 auto (four sets in waves
+                                  whose segments average < 256 B, else two), 1 = one set, 4 = four sets in
+                                  every wave. Only the default pipelined 2-row shape has more than one
+                                  set: with kernel = SCAN_PLAIN or rows != 2 every run is one set.
+                                  Receive kernels, 64-frame sets per run: 0 auto (four sets in waves whose
+                                  frames average < 128 B, else one), 1 = one set, 4 = four sets in every wave. */
     int32_t block_mode;        /* 0 auto (a block per segment when n < 4 * CUs), 1 never, 2 always */
     int32_t rows;              /* ragged scan / receive kernels: 1 KiB rows per load batch (4, 8, 16) */
     int32_t run_segs;          /* segments per wave task: ragged scan kernel 1..63, TCP build 1..64 */

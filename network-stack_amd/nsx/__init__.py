@@ -128,7 +128,35 @@ def _np_ptr(a):
 
 
 def _dev_ptr(t):
-    return None if t is None else ctypes.c_void_p(t.data_ptr())
+    """A device tensor's address for the C call (a host tensor is refused: the device entry points take HBM
+    pointers). Called after every _span check of the wrapper, so extent errors are reported first."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ValueError(f"must be a device (HIP) tensor, got one on {t.device}")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _span(t, nbytes: int, what: str, elem: int | None = None):
+    """The C ABI takes bare device pointers and cannot see extents, so every device wrapper checks its tensors
+    here, before the C call: contiguous, `elem`-byte elements (when given), at least `nbytes` bytes (_dev_ptr then
+    refuses host tensors). An undersized tensor would otherwise be an out-of-bounds device access. (Data-dependent extents — a ragged
+    batch's last offset — live in device memory and are not read here: that would synchronise the stream.)"""
+    if t is None:
+        return
+    if not t.is_contiguous():
+        raise ValueError(f"{what}: tensor must be contiguous")
+    if elem is not None and t.element_size() != elem:
+        raise ValueError(f"{what}: needs {elem}-byte elements, got {t.dtype}")
+    have = t.numel() * t.element_size()
+    if have < nbytes:
+        raise ValueError(f"{what}: {have} B given, {nbytes} B needed")
+
+
+def _count(offsets, what: str) -> int:
+    """n from an (n+1)-entry offsets tensor of 8-byte elements."""
+    _span(offsets, 8, what, elem=8)
+    return offsets.numel() - 1
 
 
 def _stream(stream):
@@ -194,6 +222,10 @@ def fixed_host(buf: np.ndarray, stride: int, seg_len: int, n: int, partial: np.n
     buf = np.ascontiguousarray(buf, np.uint8)
     out = np.empty(n, np.uint16)
     part = None if partial is None else np.ascontiguousarray(partial, np.uint32)
+    if n > 0 and buf.size < (n - 1) * stride + seg_len:
+        raise ValueError(f"fixed_host buf: {buf.size} B given, {(n - 1) * stride + seg_len} B needed")
+    if part is not None and part.size < n:
+        raise ValueError(f"fixed_host partial: {part.size} entries for {n} segments")
     _check(lib().nsx_csum_fixed_host_tuned(_np_ptr(buf), stride, seg_len, n, _np_ptr(part), _np_ptr(out), num_gpus,
                                            _tune(tune)), "nsx_csum_fixed_host")
     return out
@@ -206,6 +238,10 @@ def ragged_host(buf: np.ndarray, offsets: np.ndarray, partial: np.ndarray | None
     n = offsets.size - 1
     out = np.empty(max(n, 0), np.uint16)
     part = None if partial is None else np.ascontiguousarray(partial, np.uint32)
+    if n > 0 and buf.size < int(offsets[-1]):
+        raise ValueError(f"ragged_host buf: {buf.size} B given, offsets end at {int(offsets[-1])}")
+    if part is not None and part.size < n:
+        raise ValueError(f"ragged_host partial: {part.size} entries for {n} segments")
     _check(lib().nsx_csum_ragged_host_tuned(_np_ptr(buf), _np_ptr(offsets), n, _np_ptr(part), _np_ptr(out), num_gpus,
                                             _tune(tune)), "nsx_csum_ragged_host")
     return out
@@ -219,6 +255,8 @@ def rx_ipv4_tcp_verify_host(buf: np.ndarray, offsets: np.ndarray, num_gpus: int 
     offsets = np.ascontiguousarray(offsets, np.uint64)
     n = offsets.size - 1
     mask = np.zeros((max(n, 0) + 63) // 64, np.uint64)
+    if n > 0 and buf.size < int(offsets[-1]):
+        raise ValueError(f"rx host buf: {buf.size} B given, offsets end at {int(offsets[-1])}")
     name = "nsx_rx_ipv6_tcp_verify_host" if ipver == 6 else "nsx_rx_ipv4_tcp_verify_host"
     _check(getattr(lib(), name + "_tuned")(_np_ptr(buf), _np_ptr(offsets), n, _np_ptr(mask), num_gpus, _tune(tune)),
            name)
@@ -259,6 +297,9 @@ def fixed_dev(buf, stride: int, seg_len: int, n: int, partial=None, out=None, st
     import torch
     if out is None:
         out = torch.empty(n, dtype=torch.int16, device=buf.device)  # u16 bits
+    _span(buf, (n - 1) * stride + seg_len if n > 0 else 0, "fixed_dev buf")
+    _span(partial, 4 * n, "fixed_dev partial", elem=4)
+    _span(out, 2 * n, "fixed_dev out", elem=2)
     _check(lib().nsx_csum_fixed_dev_tuned(_dev_ptr(buf), stride, seg_len, n, _dev_ptr(partial), _dev_ptr(out),
                                           _stream(stream), _tune(tune)), "nsx_csum_fixed_dev")
     return out
@@ -266,9 +307,12 @@ def fixed_dev(buf, stride: int, seg_len: int, n: int, partial=None, out=None, st
 
 def ragged_dev(buf, offsets, partial=None, out=None, stream=None, tune=None):
     import torch
-    n = offsets.numel() - 1
+    n = _count(offsets, "ragged_dev offsets")
     if out is None:
         out = torch.empty(max(n, 0), dtype=torch.int16, device=offsets.device)  # u16 bits
+    _span(buf, 0, "ragged_dev buf")
+    _span(partial, 4 * n, "ragged_dev partial", elem=4)
+    _span(out, 2 * n, "ragged_dev out", elem=2)
     _check(lib().nsx_csum_ragged_dev_tuned(_dev_ptr(buf), _dev_ptr(offsets), n, _dev_ptr(partial), _dev_ptr(out),
                                            _stream(stream), _tune(tune)), "nsx_csum_ragged_dev")
     return out
@@ -276,8 +320,11 @@ def ragged_dev(buf, offsets, partial=None, out=None, stream=None, tune=None):
 
 def verify_ragged_dev(buf, offsets, partial=None, raw=None, stream=None, tune=None):
     import torch
-    n = offsets.numel() - 1
+    n = _count(offsets, "verify_ragged_dev offsets")
     ok = torch.empty(max(n, 0), dtype=torch.uint8, device=offsets.device)
+    _span(buf, 0, "verify_ragged_dev buf")
+    _span(partial, 4 * n, "verify_ragged_dev partial", elem=4)
+    _span(raw, 2 * n, "verify_ragged_dev raw", elem=2)
     _check(lib().nsx_verify_ragged_dev_tuned(_dev_ptr(buf), _dev_ptr(offsets), n, _dev_ptr(partial), _dev_ptr(ok),
                                              _dev_ptr(raw), _stream(stream), _tune(tune)), "nsx_verify_ragged_dev")
     return ok
@@ -288,6 +335,10 @@ def pseudo_ipv4_partial_dev(src, dst, length, proto: int = 6, out=None, stream=N
     n = length.numel()
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=length.device)  # u32 bits
+    _span(length, 4 * n, "pseudo_ipv4_partial_dev length", elem=4)
+    _span(src, 4 * n, "pseudo_ipv4_partial_dev src")
+    _span(dst, 4 * n, "pseudo_ipv4_partial_dev dst")
+    _span(out, 4 * n, "pseudo_ipv4_partial_dev out", elem=4)
     _check(lib().nsx_pseudo_ipv4_partial_dev(_dev_ptr(src), _dev_ptr(dst), _dev_ptr(length), proto, n,
                                              _dev_ptr(out), _stream(stream)), "nsx_pseudo_ipv4_partial_dev")
     return out
@@ -298,6 +349,10 @@ def pseudo_ipv6_partial_dev(src, dst, length, next_header: int = 6, out=None, st
     n = length.numel()
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=length.device)  # u32 bits
+    _span(length, 4 * n, "pseudo_ipv6_partial_dev length", elem=4)
+    _span(src, 16 * n, "pseudo_ipv6_partial_dev src")
+    _span(dst, 16 * n, "pseudo_ipv6_partial_dev dst")
+    _span(out, 4 * n, "pseudo_ipv6_partial_dev out", elem=4)
     _check(lib().nsx_pseudo_ipv6_partial_dev(_dev_ptr(src), _dev_ptr(dst), _dev_ptr(length), next_header, n,
                                              _dev_ptr(out), _stream(stream)), "nsx_pseudo_ipv6_partial_dev")
     return out
@@ -309,6 +364,8 @@ def verify_mask_dev(raw, out=None, stream=None):
     n = raw.numel()
     if out is None:
         out = torch.empty((n + 63) // 64, dtype=torch.int64, device=raw.device)  # u64 bits
+    _span(raw, 2 * n, "verify_mask_dev raw", elem=2)
+    _span(out, 8 * ((n + 63) // 64), "verify_mask_dev out", elem=8)
     _check(lib().nsx_verify_mask_dev(_dev_ptr(raw), n, _dev_ptr(out), _stream(stream)), "nsx_verify_mask_dev")
     return out
 
@@ -318,6 +375,8 @@ def ipv4_hdr_csum_dev(buf, stride: int, n: int, hdr_off: int = 0, mode: int = 0,
     import torch
     if out is None and mode == 0:
         out = torch.empty(n, dtype=torch.int16, device=buf.device)  # u16 bits
+    _span(buf, (n - 1) * stride + hdr_off + 20 if n > 0 else 0, "ipv4_hdr_csum_dev buf")
+    _span(out, 2 * n, "ipv4_hdr_csum_dev out", elem=2)
     _check(lib().nsx_ipv4_hdr_csum_dev_tuned(_dev_ptr(buf), stride, hdr_off, n, mode, _dev_ptr(out), _stream(stream),
                                              _tune(tune)), "nsx_ipv4_hdr_csum_dev")
     return out
@@ -328,6 +387,8 @@ def ipv4_hdr_verify_mask_dev(buf, stride: int, n: int, hdr_off: int = 0, mask=No
     import torch
     if mask is None:
         mask = torch.empty((n + 63) // 64, dtype=torch.int64, device=buf.device)  # u64 bits
+    _span(buf, (n - 1) * stride + hdr_off + 20 if n > 0 else 0, "ipv4_hdr_verify_mask_dev buf")
+    _span(mask, 8 * ((n + 63) // 64), "ipv4_hdr_verify_mask_dev mask", elem=8)
     _check(lib().nsx_ipv4_hdr_verify_mask_dev_tuned(_dev_ptr(buf), stride, hdr_off, n, _dev_ptr(mask),
                                                     _stream(stream), _tune(tune)), "nsx_ipv4_hdr_verify_mask_dev")
     return mask
@@ -336,9 +397,13 @@ def ipv4_hdr_verify_mask_dev(buf, stride: int, n: int, hdr_off: int = 0, mask=No
 def rx_ipv4_tcp_verify_dev(buf, offsets, mask=None, ip_raw=None, tcp_raw=None, stream=None, tune=None):
     """Fused receive pass over packed IPv4/TCP frames: validity bitmask (+ optional raw sums)."""
     import torch
-    n = offsets.numel() - 1
+    n = _count(offsets, "rx_ipv4_tcp_verify_dev offsets")
     if mask is None:
         mask = torch.empty((max(n, 0) + 63) // 64, dtype=torch.int64, device=offsets.device)  # u64 bits
+    _span(buf, 0, "rx_ipv4_tcp_verify_dev buf")
+    _span(mask, 8 * ((n + 63) // 64), "rx_ipv4_tcp_verify_dev mask", elem=8)
+    _span(ip_raw, 2 * n, "rx_ipv4_tcp_verify_dev ip_raw", elem=2)
+    _span(tcp_raw, 2 * n, "rx_ipv4_tcp_verify_dev tcp_raw", elem=2)
     _check(lib().nsx_rx_ipv4_tcp_verify_dev_tuned(_dev_ptr(buf), _dev_ptr(offsets), n, _dev_ptr(mask),
                                                   _dev_ptr(ip_raw), _dev_ptr(tcp_raw), _stream(stream), _tune(tune)),
            "nsx_rx_ipv4_tcp_verify_dev")
@@ -348,18 +413,24 @@ def rx_ipv4_tcp_verify_dev(buf, offsets, mask=None, ip_raw=None, tcp_raw=None, s
 def rx_ipv6_tcp_verify_dev(buf, offsets, mask=None, tcp_raw=None, stream=None, tune=None):
     """Fused receive pass over packed IPv6/TCP packets: validity bitmask (+ optional raw TCP sums)."""
     import torch
-    n = offsets.numel() - 1
+    n = _count(offsets, "rx_ipv6_tcp_verify_dev offsets")
     if mask is None:
         mask = torch.empty((max(n, 0) + 63) // 64, dtype=torch.int64, device=offsets.device)  # u64 bits
+    _span(buf, 0, "rx_ipv6_tcp_verify_dev buf")
+    _span(mask, 8 * ((n + 63) // 64), "rx_ipv6_tcp_verify_dev mask", elem=8)
+    _span(tcp_raw, 2 * n, "rx_ipv6_tcp_verify_dev tcp_raw", elem=2)
     _check(lib().nsx_rx_ipv6_tcp_verify_dev_tuned(_dev_ptr(buf), _dev_ptr(offsets), n, _dev_ptr(mask),
                                                   _dev_ptr(tcp_raw), _stream(stream), _tune(tune)),
            "nsx_rx_ipv6_tcp_verify_dev")
     return mask
 
 
+BUILD_FIELDS = (("src_port", 2), ("dst_port", 2), ("seq_num", 4), ("ack_num", 4), ("offset", 1), ("control", 1),
+                ("window", 2), ("urgent_ptr", 2))  # nsx_tcp_hdr_soa members and their element sizes
+
+
 class TcpHdrSoA(ctypes.Structure):
-    _fields_ = [(name, ctypes.c_void_p) for name in
-                ("src_port", "dst_port", "seq_num", "ack_num", "offset", "control", "window", "urgent_ptr")]
+    _fields_ = [(name, ctypes.c_void_p) for name, _ in BUILD_FIELDS]
 
 
 PARSE_FIELDS = (("src_port", "int16"), ("dst_port", "int16"), ("seq_num", "int32"), ("ack_num", "int32"),
@@ -376,13 +447,17 @@ def tcp_parse_dev(buf, offsets, fields=None, want=None, stream=None) -> dict:
     """parseSegment (tcp.go:130-185) over the segments buf[offsets[i], offsets[i+1]) into device tensors (dict
     by field; `want` = the field names to produce, default all; `fields` = caller tensors to fill)."""
     import torch
-    n = offsets.numel() - 1
+    n = _count(offsets, "tcp_parse_dev offsets")
     names = [k for k, _ in PARSE_FIELDS] if want is None else list(want)
     out = dict(fields or {})
     for k, dt in PARSE_FIELDS:
         if k in names and k not in out:
             out[k] = torch.empty(max(n, 0), dtype=getattr(torch, dt), device=offsets.device)
-    soa = TcpParsedSoA(*[_dev_ptr(out.get(k)) for k, _ in PARSE_FIELDS])
+    _span(buf, 0, "tcp_parse_dev buf")
+    for k, dt in PARSE_FIELDS:
+        size = np.dtype(dt).itemsize
+        _span(out.get(k), size * n, f"tcp_parse_dev {k}", elem=size)
+    soa =TcpParsedSoA(*[_dev_ptr(out.get(k)) for k, _ in PARSE_FIELDS])
     _check(lib().nsx_tcp_parse_dev(_dev_ptr(buf), _dev_ptr(offsets), n, ctypes.byref(soa), _stream(stream)),
            "nsx_tcp_parse_dev")
     return out
@@ -405,9 +480,21 @@ def tcp_build_dev(fields: dict, data, data_off, out, out_off, opts=None, opt_off
                   stream=None, tune=None):
     """Fused segment.bytes() + checksum + field write (fields: dict of device tensors; a missing or None
     "offset" computes byte 12 on the device as computeOffset() does, tcp.go:59-66)."""
-    soa = TcpHdrSoA(*[_dev_ptr(fields.get(k)) for k in
-                      ("src_port", "dst_port", "seq_num", "ack_num", "offset", "control", "window", "urgent_ptr")])
-    n = data_off.numel() - 1
+    n = _count(data_off, "tcp_build_dev data_off")
+    for k, size in BUILD_FIELDS:
+        if fields.get(k) is None and k != "offset":  # only byte 12 may be computed on the device
+            raise ValueError(f"tcp_build_dev: header field {k!r} missing")
+        _span(fields.get(k), size * n, f"tcp_build_dev {k}", elem=size)
+    _span(data, 0, "tcp_build_dev data")
+    _span(out_off, 8 * (n + 1), "tcp_build_dev out_off", elem=8)
+    _span(out, 0, "tcp_build_dev out")
+    _span(opt_off, 8 * (n + 1), "tcp_build_dev opt_off", elem=8)
+    if opt_off is not None and opts is None:
+        raise ValueError("tcp_build_dev: opt_off given without opts")
+    _span(opts, 0, "tcp_build_dev opts")
+    _span(partial, 4 * n, "tcp_build_dev partial", elem=4)
+    _span(raw, 2 * n, "tcp_build_dev raw", elem=2)
+    soa = TcpHdrSoA(*[_dev_ptr(fields.get(k)) for k, _ in BUILD_FIELDS])
     _check(lib().nsx_tcp_build_dev_tuned(ctypes.byref(soa), _dev_ptr(opts), _dev_ptr(opt_off), _dev_ptr(data),
                                          _dev_ptr(data_off), data.numel(), _dev_ptr(partial), n, _dev_ptr(out),
                                          _dev_ptr(out_off), _dev_ptr(raw), _stream(stream), _tune(tune)),
@@ -416,6 +503,7 @@ def tcp_build_dev(fields: dict, data, data_off, out, out_off, opts=None, opt_off
 
 
 def fill_splitmix64_dev(buf, seed: int, byte_off: int = 0, stream=None):
+    _span(buf, 0, "fill_splitmix64_dev buf")
     _check(lib().nsx_fill_splitmix64_dev(_dev_ptr(buf), byte_off, buf.numel() * buf.element_size(), seed,
                                          _stream(stream)), "nsx_fill_splitmix64_dev")
     return buf

@@ -12,7 +12,9 @@
 //                 buffer is the batch (pinned for ring-gpu); the receiver
 //                 verifies the frames in place — per segment on the host, or
 //                 one GPU batch straight from the pipe's buffer (no copy).
-// Prints one JSON line.
+// Prints one JSON line. --dump FILE also writes, per segment, the 12-byte pseudo-header, the seg_len bytes
+// sent and the raw sum the receiver computed on the last repetition (u16 LE), so a test can compare every raw
+// sum with the oracle's computeChecksum over the same bytes (tests/test_pipe_cpp.py).
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -27,7 +29,7 @@
 
 int main(int argc, char** argv) {
     int nseg = 64, seg_len = 1500, reps = 200, corrupt = -1;
-    std::string mode = "host";
+    std::string mode = "host", dump;
     for (int i = 1; i + 1 < argc; i += 2) {
         const std::string k = argv[i];
         if (k == "--segments") nseg = std::atoi(argv[i + 1]);
@@ -35,9 +37,10 @@ int main(int argc, char** argv) {
         else if (k == "--reps") reps = std::atoi(argv[i + 1]);
         else if (k == "--mode") mode = argv[i + 1];
         else if (k == "--corrupt") corrupt = std::atoi(argv[i + 1]);  // flip a bit of segment K
+        else if (k == "--dump") dump = argv[i + 1];
     }
     if (seg_len < 20 || corrupt >= nseg || nseg < 1 || reps < 1 || (mode != "host" && mode != "batch" && mode != "ring-host" && mode != "ring-gpu")) {
-        std::fprintf(stderr, "usage: nsx_loopback [--segments N] [--seg-len L>=20] [--reps R] [--mode host|batch|ring-host|ring-gpu] [--corrupt K]\n");
+        std::fprintf(stderr, "usage: nsx_loopback [--segments N] [--seg-len L>=20] [--reps R] [--mode host|batch|ring-host|ring-gpu] [--corrupt K] [--dump FILE]\n");
         return 2;
     }
     // Build the segments once (sender side of tcp.go: field zero, sum, store ~sum).
@@ -81,6 +84,7 @@ int main(int argc, char** argv) {
     auto host_verify = [&](int i, const uint8_t* seg) {
         uint16_t sum = 0;
         nsx_csum16(pseudo[i].data(), pseudo[i].size(), seg, seg_len, &sum);
+        raw[i] = sum;
         bad += !nsx_verify(sum);
     };
     auto gpu_verify = [&](const uint8_t* frames) {  // one batch call; raw sums come back per segment
@@ -136,6 +140,17 @@ int main(int argc, char** argv) {
         return 1;
     }
     if (pinned) nsx_free_pinned(pinned);
+    if (!dump.empty()) {
+        FILE* f = std::fopen(dump.c_str(), "wb");
+        if (!f) return 1;
+        for (int i = 0; i < nseg; ++i) {
+            const uint8_t r[2] = {(uint8_t)(raw[i] & 0xFF), (uint8_t)(raw[i] >> 8)};
+            std::fwrite(pseudo[i].data(), 1, pseudo[i].size(), f);
+            std::fwrite(wire[i].data(), 1, wire[i].size(), f);
+            std::fwrite(r, 1, 2, f);
+        }
+        std::fclose(f);
+    }
     const double bytes = (double)nseg * seg_len;
     std::printf("{\"config\": \"config1: %d x %dB TCP segments over nsx::pipe loopback\", \"mode\": \"%s\", "
                 "\"reps\": %d, \"bad\": %ld, \"corrupt\": %d, \"best_us_per_batch\": %.2f, \"mean_us_per_batch\": %.2f, "

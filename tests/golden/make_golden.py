@@ -126,9 +126,10 @@ def ragged(rng: np.random.Generator):
                             "raw": raw, "raw_with_partial": raw_p}
 
 
-def segments() -> list:
-    """Struct-level cases: the exact segments of transport/tcp/tcp_test.go plus
-    option-bearing ones exercising the reference's padding (tcp.go:118-121)."""
+def segment_cases() -> list:
+    """(name, O.Segment) for the struct-level cases: the exact segments of transport/tcp/tcp_test.go plus
+    option-bearing ones exercising the reference's padding (tcp.go:118-121), offset set as each test sets it
+    (also used by tests/test_gpu_00_baseline.py to drive the device build + parse)."""
     cases = [
         ("TestSegmentComputeChecksum", O.Segment(data=b"hello")),
         ("TestSegmentCodec", O.Segment(src_port=1, dst_port=2, seq_num=3, ack_num=4, offset=5, window=6,
@@ -143,12 +144,17 @@ def segments() -> list:
                                                                 O.Option(kind=1), O.Option(kind=0)],
                                            data=bytes(range(37)))),
     ]
-    out = []
     for name, s in cases:
         # tcp_test.go:27 never sets offset (it stays 0, so byte 12 is 0x00); tcp_test.go:47 and every other
         # case set it with computeOffset (tcp.go:59-66)
         if name != "TestSegmentComputeChecksum":
             s.offset = s.compute_offset()
+    return cases
+
+
+def segments() -> list:
+    out = []
+    for name, s in segment_cases():
         b = s.bytes()
         pseudo = O.ipv4_pseudo_header(bytes([192, 168, 0, 1]), bytes([192, 168, 0, 2]), 6, len(b))
         raw = agreed(b"", b)

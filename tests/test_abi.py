@@ -236,6 +236,54 @@ def test_device_calls_validate_before_device():
                                   np.zeros(2, np.uint16).ctypes.data_as(ctypes.c_void_p), 0) == nsx.NSX_EINVAL
 
 
+def test_binding_checks_extents_before_the_c_call():
+    """the C ABI cannot see a tensor's extent, so the Python wrappers refuse undersized,
+    wrongly typed, non-contiguous or host tensors with ValueError before any C call (CPU tensors here: every
+    check runs before the device check, and a well-formed CPU tensor is refused as not on a device)."""
+    import torch
+    u8 = lambda k: torch.zeros(k, dtype=torch.uint8)  # noqa: E731
+    i16 = lambda k: torch.zeros(k, dtype=torch.int16)  # noqa: E731
+    offs = torch.tensor([0, 10, 20, 30], dtype=torch.int64)
+    cases = [
+        (lambda: nsx.fixed_dev(u8(2999), 1500, 1500, 2, out=i16(2)), "3000 B needed"),
+        (lambda: nsx.fixed_dev(u8(3000), 1500, 1500, 2, out=i16(1)), "fixed_dev out"),
+        (lambda: nsx.fixed_dev(u8(3000), 1500, 1500, 2, out=torch.zeros(2, dtype=torch.int32)), "2-byte elements"),
+        (lambda: nsx.fixed_dev(u8(3000), 1500, 1500, 2, out=i16(4)[::2]), "contiguous"),
+        (lambda: nsx.fixed_dev(u8(3000), 1500, 1500, 2, partial=torch.zeros(1, dtype=torch.int32), out=i16(2)),
+         "fixed_dev partial"),
+        (lambda: nsx.fixed_dev(u8(3000), 1500, 1500, 2, out=i16(2)), "device"),
+        (lambda: nsx.ragged_dev(u8(30), offs.to(torch.int32)), "8-byte elements"),
+        (lambda: nsx.ragged_dev(u8(30), offs, out=i16(2)), "ragged_dev out"),
+        (lambda: nsx.ragged_dev(u8(30), offs, partial=torch.zeros(2, dtype=torch.int32), out=i16(3)),
+         "ragged_dev partial"),
+        (lambda: nsx.verify_mask_dev(i16(65), out=torch.zeros(1, dtype=torch.int64)), "verify_mask_dev out"),
+        (lambda: nsx.ipv4_hdr_csum_dev(u8(20 * 9 + 19), 20, 10, out=i16(10)), "200 B needed"),
+        (lambda: nsx.ipv4_hdr_verify_mask_dev(u8(20 * 65), 20, 65, mask=torch.zeros(1, dtype=torch.int64)), "mask"),
+        (lambda: nsx.rx_ipv4_tcp_verify_dev(u8(30), offs, mask=torch.zeros(1, dtype=torch.int64), ip_raw=i16(2)),
+         "ip_raw"),
+        (lambda: nsx.rx_ipv6_tcp_verify_dev(u8(30), offs, mask=torch.zeros(0, dtype=torch.int64)), "mask"),
+        (lambda: nsx.tcp_parse_dev(u8(30), offs, fields={"seq_num": torch.zeros(3, dtype=torch.int16)}),
+         "seq_num"),
+        (lambda: nsx.pseudo_ipv4_partial_dev(u8(7), u8(8), torch.zeros(2, dtype=torch.int32)), "src"),
+        (lambda: nsx.fixed_host(np.zeros(2999, np.uint8), 1500, 1500, 2), "3000 B needed"),
+        (lambda: nsx.ragged_host(np.zeros(29, np.uint8), np.array([0, 10, 30], np.uint64)), "end at 30"),
+    ]
+    n = 3
+    fields = {k: torch.zeros(n, dtype={1: torch.uint8, 2: torch.int16, 4: torch.int32}[s]) for k, s in nsx.BUILD_FIELDS}
+    build = dict(data=u8(30), data_off=offs, out=u8(200), out_off=offs)
+    cases += [
+        (lambda: nsx.tcp_build_dev(dict(fields, window=torch.zeros(2, dtype=torch.int16)), **build), "window"),
+        (lambda: nsx.tcp_build_dev(dict(fields, seq_num=None), **build), "'seq_num' missing"),
+        (lambda: nsx.tcp_build_dev(fields, **dict(build, out_off=offs[:3])), "out_off"),
+        (lambda: nsx.tcp_build_dev(fields, **build, raw=i16(2)), "raw"),
+        (lambda: nsx.tcp_build_dev(fields, **build, opt_off=offs), "opt_off given without opts"),
+    ]
+    for fn, msg in cases:
+        with pytest.raises(ValueError) as e:
+            fn()
+        assert msg in str(e.value), (msg, str(e.value))
+
+
 def test_c_caller_compiles_and_links(tmp_path):
     """A plain C program (what cgo compiles) includes the header and links the library."""
     src = tmp_path / "caller.c"

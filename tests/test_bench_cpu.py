@@ -32,8 +32,24 @@ def test_gpus_2_launches_two_ranks_itself():
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout  # rank 0 only
     line = lines[0]
-    assert line["n_gpus"] == 2 and line["ranks"] == 2 and line["dry_run"]
+    # two ranks, no GPU behind them: n_gpus counts distinct devices (0), the rank count is separate
+    assert line["ranks"] == 2 and line["dry_run"] and line["rehearsal"]
+    assert line["n_gpus"] == 0 and line["distinct_devices"] == 0 and len(line["devices"]) == 2
     assert line["config"]["units_per_step_all_gpus"] == 2 * line["config"]["units_per_gpu"]
+
+
+def test_device_fields_count_distinct_gpus():
+    """a SCALE reader must see from the line alone how many physical GPUs the ranks ran on."""
+    a = {"host": "h", "local_device": 0, "pci": "0000:05:00", "uuid": "u0", "key": "h/0000:05:00/u0"}
+    b = dict(a, local_device=1, pci="0000:15:00", uuid="u1", key="h/0000:15:00/u1")
+    two = bench.device_fields([a, b])
+    assert two["n_gpus"] == 2 and two["ranks"] == 2 and [d["pci"] for d in two["devices"]] == [a["pci"], b["pci"]]
+    shared = bench.device_fields([a, dict(a)])  # two ranks on one GPU (a rehearsal)
+    assert shared["n_gpus"] == 1 and shared["ranks"] == 2 and shared["distinct_devices"] == 1
+    line = bench.result_line(world=2, steps=1, warmup=0, wall_max=1.0, bytes_per_rank_step=10, units_total=2,
+                             workload="w", cfg={"n": 1, "seed": 1}, launch_ms=[], alg_bytes_per_launch=10,
+                             cpu_baseline=None, traffic=None, n_gpus=shared["n_gpus"])
+    assert line["n_gpus"] == 1 and line["ranks"] == 2
 
 
 def test_world_size_disagreeing_with_gpus_is_an_error():

@@ -125,10 +125,13 @@ RAGGED_TUNES = [dict(kernel=k, rows=r, run_segs=rs, blocks_per_cu=b)  # pipeline
                 for rs in (0, 1, 16, 63) for b in (0, 1, 8)]
 
 
-@pytest.mark.parametrize("n", [1, 126, 252, 253, 30_001])
+@pytest.mark.parametrize("n", [1, 126, 252, 253, 30_001, 400_003])
 def test_ragged_small_segments_runs_of_four_sets(n):
     """Segments of 0-200 B (mean ~100): waves whose segments average under 256 B take runs of four 63-segment sets
-    (DESIGN.md §7 step 42); the automatic choice and both forced forms equal the oracle, with and without partials."""
+    (DESIGN.md §7 step 42); the automatic choice and both forced forms equal the oracle, with and without partials.
+    block_mode=1 keeps even the smallest batches on the scan kernel, and short runs (run_segs 1, 16) at one block
+    per CU make every wave stream many runs, so all four sets, partial last sets and set-to-set frame ends run
+    (ADVICE r2); n = 400K reaches the four sets with the default run length too."""
     rng = np.random.default_rng(n + 42)
     lens = rng.integers(0, 201, n).astype(np.uint64)
     offs = np.zeros(n + 1, np.uint64)
@@ -136,10 +139,13 @@ def test_ragged_small_segments_runs_of_four_sets(n):
     offs += np.uint64(3)
     buf = O.c_splitmix64(0x42, int(offs[-1]) + 3)
     part = rng.integers(0, 1 << 31, n, dtype=np.uint32)
-    want = O.c_batch(buf, n, offsets=offs)
-    want_p = O.c_batch(buf, n, offsets=offs, partial=part)
+    want = O.c_batch(buf, n, offsets=offs, threads=16)
+    want_p = O.c_batch(buf, n, offsets=offs, partial=part, threads=16)
     d, o, p = dev(buf), dev(offs.view(np.int64)), dev(part.view(np.int32))
-    for tune in (None, dict(segs_per_wave=1), dict(segs_per_wave=4)):
+    tunes = [None, dict(segs_per_wave=1), dict(segs_per_wave=4)]
+    tunes += [dict(block_mode=1, blocks_per_cu=1, run_segs=rs, **sp)
+              for rs in (0, 1, 16) for sp in ({}, dict(segs_per_wave=1), dict(segs_per_wave=4))]
+    for tune in tunes:
         out = torch.empty(n, dtype=torch.int16, device="cuda")
         nsx.ragged_dev(d, o, out=out, tune=tune)
         assert np.array_equal(u16(out), want), tune

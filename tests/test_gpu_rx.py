@@ -71,6 +71,74 @@ def test_rx_small_frames_runs_of_four_sets(n, lead):
             assert np.array_equal(w, g), (what, n, lead, tune)
 
 
+def _device_frames(cfg, seed):
+    """Frames built on the device (bench.build_rx_frames: valid IPv4 / IPv6 datagrams, every 1000th corrupted),
+    then broken further so the large small-frame batches hold every outcome: bit flips in the TCP bytes of ~3% of
+    the frames, and in the IPv4 case the protocol set to UDP in ~1% and the total length off by one in ~1%."""
+    import bench
+    w = bench.build_rx_frames(cfg, seed, torch.device("cuda", 0))
+    buf, d_offs = w["buf"], w["d_offs"]
+    st = d_offs[:-1]
+    ln = d_offs[1:] - st
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    n = cfg["n"]
+    pick = torch.randint(0, n, (n // 33,), generator=g, device="cuda")
+    hl = 40 if cfg.get("ipver") == 6 else 20
+    pos = st[pick] + hl + torch.remainder(torch.randint(0, 1 << 30, pick.shape, generator=g, device="cuda"), ln[pick] - hl)
+    buf[pos] ^= (1 << torch.randint(0, 8, pick.shape, generator=g, device="cuda")).to(torch.uint8)
+    if cfg.get("ipver") != 6:
+        udp = torch.randint(0, n, (n // 100,), generator=g, device="cuda")
+        buf[st[udp] + 9] = 17
+        bad_len = torch.randint(0, n, (n // 100,), generator=g, device="cuda")
+        buf[st[bad_len] + 3] ^= 1
+    torch.cuda.synchronize()
+    return w
+
+
+@pytest.mark.parametrize("ipver", [4, 6])
+def test_rx_small_frames_300K_every_set_form_vs_oracle(ipver):
+    """~300K ACK-sized frames (40-100 B IPv4 / 60-120 B IPv6), enough that waves stream many
+    runs, so the four-set run form's sets 2 and 3, the cross-set frame ends and partial last sets all run. The
+    automatic choice and the forced one- and four-set forms, at the default grid and at one block per CU, against
+    the oracle's mask and raw sums on every frame."""
+    cfg = dict(n=300_007, lo=40, hi=100, seed=0x5A11) if ipver == 4 else \
+        dict(ipver=6, n=300_007, lo=60, hi=120, seed=0x5A16)
+    w = _device_frames(cfg, cfg["seed"])
+    buf_h = host(w["buf"])
+    offs = w["offsets"]
+    n = cfg["n"]
+    want = O.c_rx_ipv4_tcp(buf_h, offs) if ipver == 4 else O.c_rx_ipv6_tcp(buf_h, offs)
+    bits = np.unpackbits(want[0].view(np.uint8), bitorder="little")[:n]
+    assert 0.85 * n < bits.sum() < 0.985 * n  # mostly valid, every kind of failure present
+    for tune in (None, dict(segs_per_wave=1), dict(segs_per_wave=4), dict(blocks_per_cu=1),
+                 dict(blocks_per_cu=1, segs_per_wave=1), dict(blocks_per_cu=1, segs_per_wave=4)):
+        got = run_rx(buf_h, offs, tune) if ipver == 4 else run_rx6(buf_h, offs, tune)
+        for wv, g, what in zip(want, got, ("mask", "ip_raw", "tcp_raw") if ipver == 4 else ("mask", "tcp_raw")):
+            bad = np.nonzero(wv != g)[0]
+            assert bad.size == 0, (what, tune, bad[:5])
+
+
+@pytest.mark.parametrize("config", [13, 14, 16])
+def test_rx_small_frame_bench_workloads_full_size(config):
+    """The bench's small-frame receive workloads at full size (13: 8M IPv4 frames of 40-100 B; 14: 2M frames, half
+    40-66 B ACKs and half 1500 B; 16: 8M IPv6 packets of 60-120 B): the device mask equals the oracle's on every
+    frame, and exactly the corrupted frames fail."""
+    import bench
+    cfg = bench.WORKLOADS[config]
+    w = bench.build_workload(cfg, 0, torch.device("cuda", 0))
+    w["step"]()
+    got = host(w["out"]).view(np.uint64)
+    rx = O.c_rx_ipv6_tcp if cfg.get("ipver") == 6 else O.c_rx_ipv4_tcp
+    want = rx(host(w["buf"]), w["offsets"])[0]
+    assert np.array_equal(got, want)
+    n = cfg["n"]
+    valid = np.ones(n, bool)
+    valid[::1000] = False
+    pad = np.zeros((n + 63) // 64 * 64, np.uint8)
+    pad[:n] = valid
+    assert np.array_equal(got, np.packbits(pad, bitorder="little").view(np.uint64))
+
+
 @pytest.mark.parametrize("tune", TUNES, ids=lambda t: ",".join(f"{k}={v}" for k, v in t.items()))
 def test_rx_launch_shapes(tune):
     rng = np.random.default_rng(0x7E)

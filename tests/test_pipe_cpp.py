@@ -74,14 +74,46 @@ def test_loopback_gpu_modes_refuse_without_gpu(mode):
     assert rc == 1 and "error" in r
 
 
+def _raw_sums_vs_oracle(tmp_path, mode, seg_len=1500, segments=64, corrupt=None):
+    """Every raw sum the receiver computed (nsx_loopback --dump) equals the oracle's computeChecksum
+    (tcp.go:72-95, Go-faithful C loop) over the same pseudo-header and the bytes that were sent."""
+    import numpy as np
+    from oracle import csum_oracle as O
+    path = tmp_path / f"dump_{mode}_{seg_len}.bin"
+    args = ["--mode", mode, "--reps", "3", "--seg-len", str(seg_len), "--segments", str(segments), "--dump", str(path)]
+    if corrupt is not None:
+        args += ["--corrupt", str(corrupt)]
+    rc, r = _loopback(*args)
+    assert rc == 0, r
+    blob = path.read_bytes()
+    rec = 12 + seg_len + 2
+    assert len(blob) == segments * rec
+    for i in range(segments):
+        b = blob[i * rec:(i + 1) * rec]
+        pseudo, wire, raw = b[:12], b[12:12 + seg_len], int.from_bytes(b[-2:], "little")
+        assert raw == O.c_go_checksum(pseudo, wire), (mode, seg_len, i)
+        assert O.verify(raw) == (i != corrupt), (mode, i)
+    return r
+
+
+@pytest.mark.parametrize("mode", ["host", "ring-host"])
+def test_loopback_host_raw_sums_vs_oracle(tmp_path, mode):
+    for L, corrupt in ((1500, None), (1500, 17), (21, None), (9001, None)):
+        _raw_sums_vs_oracle(tmp_path, mode, L, 64 if L == 1500 else 9, corrupt)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["batch", "ring-gpu"])
-def test_loopback_config1_gpu_batch(mode):
+def test_loopback_config1_gpu_batch(mode, tmp_path):
+    """Config 1's GPU modes: the raw sums of the GPU batch (what arrived through the pipe, one host batch call)
+    against the oracle on every segment, intact and with a segment damaged in transit; odd lengths."""
     rc, r = _loopback("--mode", mode, "--reps", "50")
     assert rc == 0 and r["bad"] == 0
-    rc, r = _loopback("--mode", mode, "--reps", "3", "--corrupt", "63")
-    assert rc == 0 and r["bad"] == 3
-    for L in ("21", "1501", "9001"):
-        rc, r = _loopback("--mode", mode, "--reps", "2", "--seg-len", L, "--segments", "9")
-        assert rc == 0 and r["bad"] == 0, L
+    r = _raw_sums_vs_oracle(tmp_path, mode)
+    assert r["bad"] == 0
+    r = _raw_sums_vs_oracle(tmp_path, mode, corrupt=63)
+    assert r["bad"] == 3
+    for L in (21, 1501, 9001):
+        r = _raw_sums_vs_oracle(tmp_path, mode, seg_len=L, segments=9)
+        assert r["bad"] == 0, L
 
