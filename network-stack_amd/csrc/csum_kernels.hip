@@ -49,6 +49,15 @@ __device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
     else return *reinterpret_cast<const u32x4*>(p);
 }
 
+// 16-byte LDS chunks with their natural alignment (u32x4 is only 4-aligned, which splits LDS accesses into
+// ds_read2_b32 / ds_write2_b32; a slot chunk is always 16-aligned, so ds_read_b128 / ds_write_b128)
+typedef uint32_t lds16 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ u32x4 lds_get(const lds16* slot, uint32_t c) {
+    const lds16 v = slot[c];
+    return u32x4{v.x, v.y, v.z, v.w};
+}
+
 // Only at the very end of the readable span: load the whole dwords below
 // safe_end (a 4-aligned dword holding a readable byte never crosses a page).
 __device__ __forceinline__ u32x4 ld16_guarded(const uint8_t* p, const uint8_t* safe_end) {
@@ -103,6 +112,16 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     v += __builtin_amdgcn_update_dpp(0u, v, 0x121, 0xF, 0xF, false);  // row_ror:1
     return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) +
            __builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48);
+}
+
+// Wave-wide maximum (DPP row_ror inside each row, then the 4 row maxima via v_readlane): a scalar.
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x128, 0xF, 0xF, false));  // row_ror:8
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x124, 0xF, 0xF, false));  // row_ror:4
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x122, 0xF, 0xF, false));  // row_ror:2
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x121, 0xF, 0xF, false));  // row_ror:1
+    return max(max(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+               max(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
 }
 
 // Wave total of LE half-sums → raw BE one's-complement sum, plus the prefix partial.
@@ -689,6 +708,52 @@ __device__ __forceinline__ void scan_span(const uint8_t* rbase, uint64_t span, u
 
 constexpr uint32_t kScanSmallSeg = 256;
 
+// One run of NS sets of ≤ run segments in the streaming form: set k = segments [a + k·run, + cnt[k]), lane l ≤
+// cnt[k] holds boundary my_off[k] = offsets[a + k·run + l] and (l < cnt[k]) the partial my_part[k].
+template <int R, bool VERIFY, bool PIPE, int NS>
+__device__ __forceinline__ void ragged_run_stream(const uint8_t* __restrict__ base, uint32_t a, uint32_t run,
+                                                  const uint32_t (&cnt)[NS], const uint64_t (&my_off)[NS],
+                                                  const uint32_t (&my_part)[NS], __amdgpu_buffer_rsrc_t ors,
+                                                  __amdgpu_buffer_rsrc_t oks, uint32_t lane) {
+    int64_t brel[NS];
+    uint64_t bval[NS];
+    // the run's last boundary: set kl = the last set with segments, its lane cnt
+    uint32_t kl = 0;
+#pragma unroll
+    for (int k = 1; k < NS; ++k) kl = cnt[k] ? (uint32_t)k : kl;
+    uint64_t hi = 0;
+#pragma unroll
+    for (int k = 0; k < NS; ++k)
+        if ((uint32_t)k == kl) hi = readlane64(my_off[k], cnt[k]);
+    const uint64_t lo = readlane64(my_off[0], 0);
+    // Rows start on a 128-byte line so a 1 KiB row touches exactly 8 lines.
+    const uint8_t* rbase = reinterpret_cast<const uint8_t*>(((uintptr_t)(base + lo)) & ~(uintptr_t)127);
+    const uint64_t span = (uint64_t)((base + hi) - rbase);           // bytes from rbase to the run's end
+    const uint32_t head = (uint32_t)((uintptr_t)(base + lo) & 127u);  // bytes before the run in row 0
+    // Boundary lane state: its position relative to rbase, and S there.
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+        brel[k] = cnt[k] && lane <= cnt[k] ? (int64_t)((base + my_off[k]) - rbase) : -1;
+        bval[k] = 0;
+    }
+    uint64_t carry = 0;
+    scan_span<R, PIPE, NS>(rbase, span, head, brel, lane, bval, carry);
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+        // Segment `lane` of set k = [boundary lane, boundary lane+1).
+        const uint64_t nb = ((uint64_t)__shfl_down((unsigned long long)bval[k], 1));
+        const uint64_t d = nb - bval[k];
+        const uint32_t le = fold32((uint32_t)(d & 0xFFFFFFFFu)) + fold32((uint32_t)(d >> 32));
+        const bool even = (((uintptr_t)base + my_off[k]) & 1u) == 0;
+        const uint32_t res = finish(le, even, my_part[k]);
+        const bool mine = lane < cnt[k];
+        const uint32_t ak = a + k * run;
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, mine ? (ak + lane) * 2 : kOOB, 0, 0);
+        if constexpr (VERIFY)
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(res == 0xFFFFu), oks, mine ? ak + lane : kOOB, 0, 0);
+    }
+}
+
 // The wave's runs [a0, a_end) of NS sets of ≤ run segments (see csum_ragged_scan_kernel).
 template <int R, bool VERIFY, bool PIPE, int NS>
 __device__ __forceinline__ void ragged_runs(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
@@ -708,8 +773,6 @@ __device__ __forceinline__ void ragged_runs(const uint8_t* __restrict__ base, __
     for (uint32_t a = a0; a < a_end; a += a_step) {
         uint64_t my_off[NS];  // set k: boundary `lane` (lanes 0..cnt_k)
         uint32_t cnt[NS], my_part[NS];
-        int64_t brel[NS];
-        uint64_t bval[NS];
 #pragma unroll
         for (int k = 0; k < NS; ++k) {
             const uint32_t ak = a + k * run;
@@ -717,44 +780,132 @@ __device__ __forceinline__ void ragged_runs(const uint8_t* __restrict__ base, __
             my_off[k] = nxt_off[k];
             nxt_off[k] = load_offs(a + a_step + k * run);
             my_part[k] = __builtin_amdgcn_raw_buffer_load_b32(prs, lane < cnt[k] ? (ak + lane) * 4 : kOOB, 0, 0);
-            bval[k] = 0;
         }
-        // the run's last boundary: set kl = the last set with segments, its lane cnt
-        uint32_t kl = 0;
-#pragma unroll
-        for (int k = 1; k < NS; ++k) kl = cnt[k] ? (uint32_t)k : kl;
-        uint64_t hi = 0;
-#pragma unroll
-        for (int k = 0; k < NS; ++k)
-            if ((uint32_t)k == kl) hi = readlane64(my_off[k], cnt[k]);
-        const uint64_t lo = readlane64(my_off[0], 0);
-        // Rows start on a 128-byte line so a 1 KiB row touches exactly 8 lines.
-        const uint8_t* rbase = reinterpret_cast<const uint8_t*>(((uintptr_t)(base + lo)) & ~(uintptr_t)127);
-        const uint64_t span = (uint64_t)((base + hi) - rbase);           // bytes from rbase to the run's end
-        const uint32_t head = (uint32_t)((uintptr_t)(base + lo) & 127u);  // bytes before the run in row 0
-        // Boundary lane state: its position relative to rbase, and S there.
-#pragma unroll
-        for (int k = 0; k < NS; ++k)
-            brel[k] = cnt[k] && lane <= cnt[k] ? (int64_t)((base + my_off[k]) - rbase) : -1;
-        uint64_t carry = 0;
-        scan_span<R, PIPE, NS>(rbase, span, head, brel, lane, bval, carry);
-#pragma unroll
-        for (int k = 0; k < NS; ++k) {
-            // Segment `lane` of set k = [boundary lane, boundary lane+1).
-            const uint64_t nb = ((uint64_t)__shfl_down((unsigned long long)bval[k], 1));
-            const uint64_t d = nb - bval[k];
-            const uint32_t le = fold32((uint32_t)(d & 0xFFFFFFFFu)) + fold32((uint32_t)(d >> 32));
-            const bool even = (((uintptr_t)base + my_off[k]) & 1u) == 0;
-            const uint32_t res = finish(le, even, my_part[k]);
-            const bool mine = lane < cnt[k];
-            const uint32_t ak = a + k * run;
-            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, mine ? (ak + lane) * 2 : kOOB, 0, 0);
-            if constexpr (VERIFY)
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(res == 0xFFFFu), oks, mine ? ak + lane : kOOB, 0, 0);
-        }
+        ragged_run_stream<R, VERIFY, PIPE, NS>(base, a, run, cnt, my_off, my_part, ors, oks, lane);
     }
 }
 
+// Sum of the bytes [p, e) of a wave's LDS slot (p, e slot positions; e - p < 2^15): the 16 B chunks [p/16,
+// ceil(e/16)) whole, eight reads in flight per lane, minus the bytes before p in the first chunk and from e on in
+// the last. The weighted byte sum of the range (LE half-sums of its 4-aligned dwords, as in scan_span): the slot
+// keeps every byte's address mod 128.
+__device__ __forceinline__ uint32_t lds_range_sum(const lds16* slot, uint32_t p, uint32_t e) {
+    const uint32_t c0 = p >> 4, c1 = (e + 15u) >> 4, nch = c1 - c0;
+    const uint32_t clast = nch ? nch - 1u : 0u;
+    // Blocks of 8 chunks, a wave-uniform trip count from the wave's longest range (an SGPR loop counter: a loop
+    // ending on a ballot left hipcc an undefined exit value that it read with v_readfirstlane from a register
+    // still being loaded — a vmcnt wait that drained the next run's rows before this run's sums began).
+    const uint32_t nblk = wave_max((nch + 7u) >> 3);
+    uint32_t acc = 0, head_x = 0;
+    for (uint32_t j0 = 0; j0 < nblk * 8u; j0 += 8u) {
+        u32x4 x[8];
+#pragma unroll
+        for (uint32_t j = 0; j < 8u; ++j) x[j] = lds_get(slot, c0 + min(j0 + j, clast));
+        if (j0 == 0) head_x = sad4(keep_bytes(x[0], 0, (int32_t)(p & 15u)), 0u);
+#pragma unroll
+        for (uint32_t j = 0; j < 8u; ++j) {
+            const uint32_t s4 = sad4(x[j], 0u);
+            acc += j0 + j < nch ? s4 : 0u;
+        }
+    }
+    const uint32_t t = e - (c1 - 1u) * 16u;  // bytes of the last chunk inside the range, 1..16 (nch > 0)
+    const uint32_t tail_x = nch ? sad4(keep_bytes(lds_get(slot, c0 + clast), (int32_t)t, 16), 0u) : 0u;
+    return acc - (nch ? head_x : 0u) - tail_x;
+}
+
+// Stage the rows [0, span) of a run into the wave's slot (rows already loaded into V, all in flight; only the
+// rows the run covers are written). The previous run's LDS reads come first: a wave's DS operations stay in
+// order, and the wave barriers keep the compiler from moving reads or writes across.
+template <uint32_t ROWS>
+__device__ __forceinline__ void lds_stage(lds16* slot, u32x4 (&V)[ROWS], uint64_t span, uint32_t lane) {
+#pragma unroll
+    for (uint32_t r = 0; r < ROWS; ++r) asm volatile("" : "+v"(V[r]));
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (uint32_t r = 0; r < ROWS; ++r)
+        if ((uint64_t)r * kRow < span) slot[r * (kRow / 16u) + lane] = lds16{V[r].x, V[r].y, V[r].z, V[r].w};
+    __builtin_amdgcn_wave_barrier();
+}
+
+// The LDS form of the ragged checksum for waves of small segments, the receive pass's
+// (rx_runs_lds) applied to runs of ≤ run segments: lane l sums segment a + l out of the wave's slot. A run too
+// wide for the slot takes the streaming form (one set).
+constexpr uint32_t kScanSlotRows = 8;
+constexpr uint32_t kScanSlot = kScanSlotRows * kRow;
+
+template <int R, bool VERIFY, bool PIPE>
+__device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
+                                                __amdgpu_buffer_rsrc_t prs, __amdgpu_buffer_rsrc_t ors,
+                                                __amdgpu_buffer_rsrc_t oks, uint32_t run, uint32_t a0, uint32_t a_end,
+                                                uint32_t lane, lds16* slot) {
+    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+    auto load_offs = [&](uint32_t a) -> uint64_t {  // lane l ≤ run length: offsets[a + l]
+        const uint32_t voff = (a < a_end && lane <= run && a + lane <= n) ? (a + lane) * 8 : kOOB;
+        const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, voff, 0, 0);
+        return ((uint64_t)x.y << 32) | x.x;
+    };
+    struct Run {
+        const uint8_t* rbase;
+        uint64_t span;
+        uint32_t cnt;
+        bool lds;
+    };
+    auto geo = [&](uint32_t a, uint64_t off) {  // wave-uniform geometry of run a (boundaries in lanes 0..cnt)
+        Run g{base, 0, a < a_end ? min(run, a_end - a) : 0u, false};
+        if (g.cnt) {
+            const uint64_t lo = readlane64(off, 0), hi = readlane64(off, g.cnt);
+            g.rbase = reinterpret_cast<const uint8_t*>(((uintptr_t)(base + lo)) & ~(uintptr_t)127);
+            g.span = (uint64_t)((base + hi) - g.rbase);
+            g.lds = g.span <= (uint64_t)kScanSlot;
+        }
+        return g;
+    };
+    u32x4 V[kScanSlotRows];
+    auto issue = [&](const Run& g) {  // rows past the run: out of the descriptor's range, 0, no traffic
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(g.rbase, (g.span + 3) & ~3ull);
+#pragma unroll
+        for (uint32_t r = 0; r < kScanSlotRows; ++r) V[r] = bld16<true>(rs, r * kRow + lane * 16u);
+    };
+    // As rx_runs_lds: the LDS loop runs while consecutive runs fit the slot; a run that does not is streamed on
+    // its own in the outer loop, so the streaming form's loads in flight at its end never merge into the LDS
+    // loop's wait counts.
+    uint32_t a = a0;
+    while (a < a_end) {
+        uint64_t c_off = load_offs(a);
+        Run cur = geo(a, c_off);
+        if (!cur.lds) {  // too wide for the slot: the streaming form
+            const uint32_t part = __builtin_amdgcn_raw_buffer_load_b32(prs, lane < cur.cnt ? (a + lane) * 4 : kOOB, 0, 0);
+            const uint32_t cnt1[1] = {cur.cnt}, part1[1] = {part};
+            const uint64_t o1[1] = {c_off};
+            ragged_run_stream<R, VERIFY, PIPE, 1>(base, a, run, cnt1, o1, part1, ors, oks, lane);
+            a += run;
+            continue;
+        }
+        issue(cur);
+        uint64_t n_off = load_offs(a + run);
+        for (;;) {
+            const uint32_t part = __builtin_amdgcn_raw_buffer_load_b32(prs, lane < cur.cnt ? (a + lane) * 4 : kOOB, 0, 0);
+            lds_stage<kScanSlotRows>(slot, V, cur.span, lane);
+            Run nxt = geo(a + run, n_off);
+            if (!nxt.lds) nxt.span = 0;  // a run that will be streamed is not staged: empty loads
+            issue(nxt);
+            const uint64_t p_off = load_offs(a + 2u * run);
+            // segment a + lane = [boundary lane, boundary lane + 1)
+            const uint64_t e_off = (uint64_t)__shfl_down((unsigned long long)c_off, 1);
+            const bool mine = lane < cur.cnt;
+            const uint32_t p = mine ? (uint32_t)((base + c_off) - cur.rbase) : 0u;
+            const uint32_t e = mine ? (uint32_t)((base + e_off) - cur.rbase) : 0u;
+            const uint32_t res = finish(fold32(lds_range_sum(slot, p, e)), (p & 1u) == 0, part);
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, mine ? (a + lane) * 2 : kOOB, 0, 0);
+            if constexpr (VERIFY)
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(res == 0xFFFFu), oks, mine ? a + lane : kOOB, 0, 0);
+            a += run;
+            if (!nxt.lds) break;  // the end of the wave's range, or a run for the outer loop
+            cur = nxt;
+            c_off = n_off, n_off = p_off;
+        }
+    }
+}
 
 template <int R, bool VERIFY, bool PIPE, int NS>
 __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
@@ -786,10 +937,15 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
     }
     // Two sets per run suit segments of a few hundred bytes and up (config 3); a wave whose segments average under
     // kScanSmallSeg bytes takes runs of four sets, so that each run still streams tens of KB (§7 step 42).
-    if (NS == 2 && (sets == 4 || (sets == 0 && wave_bytes < (uint64_t)kScanSmallSeg * (a_end - a0))))
+    if (sets == 2 || (NS == 2 && sets == 0 && wave_bytes < (uint64_t)kScanSmallSeg * (a_end - a0))) {
+        extern __shared__ lds16 lds_scan[];
+        ragged_runs_lds<R, VERIFY, PIPE>(base, ofs, n, prs, ors, oks, run, a0, a_end, lane,
+                                         lds_scan + wave * (kScanSlot / 16u));
+    } else if (NS == 2 && sets == 4) {
         ragged_runs<R, VERIFY, PIPE, 4>(base, ofs, n, prs, ors, oks, run, a0, a_end, lane);
-    else
+    } else {
         ragged_runs<R, VERIFY, PIPE, NS>(base, ofs, n, prs, ors, oks, run, a0, a_end, lane);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -842,38 +998,78 @@ __device__ __forceinline__ void rx_store_mask(__amdgpu_buffer_rsrc_t mrs, uint64
 // per few KB (§7 step 41).
 constexpr uint32_t kRxSmallFrame = 128;
 
-template <int R, bool V6, int NS>
-__device__ __forceinline__ void rx_runs(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
-                                        uint32_t a0, uint32_t a_end, uint32_t lane, __amdgpu_buffer_rsrc_t mrs,
-                                        __amdgpu_buffer_rsrc_t irs, __amdgpu_buffer_rsrc_t trs) {
-    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
-    auto load_off = [&](uint32_t i, bool live) -> uint64_t {
-        const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, live ? i * 8 : kOOB, 0, 0);
-        return ((uint64_t)x.y << 32) | x.x;
-    };
-    constexpr uint32_t kStep = kRxRun * NS;
-    // lane l of set k: offsets[a + 64k + l] and offsets[a + 64k + l + 1] of the next run, prefetched one run ahead
-    uint64_t nxt_off[NS], nxt_end[NS];
+// Per-frame verdict of the receive pass, shared by the streaming and the LDS forms. F = the frame's weighted byte
+// sum (exact; weights 1 / 256 at even / odd addresses, the LE half-sum rule); d[0..5] = the dwords from the
+// frame's start rounded down to 4 B (hd = start & 3; IPv6 reads d[0..2]); opt(o) fills the IPv4 option dwords
+// 6..15, called only when some lane has IHL > 5. Writes the run's mask bytes and the raw sums.
+template <bool V6, typename OptFn>
+__device__ __forceinline__ void rx_frame_out(uint64_t F, const uint32_t (&d)[6], uint32_t hd, uint64_t flen, bool even,
+                                             bool live, uint32_t ak, uint32_t cnt, uint32_t n, uint32_t lane,
+                                             __amdgpu_buffer_rsrc_t mrs, __amdgpu_buffer_rsrc_t irs,
+                                             __amdgpu_buffer_rsrc_t trs, OptFn&& opt) {
+    if constexpr (V6) {
+        const uint32_t H0 = __builtin_amdgcn_alignbyte(d[1], d[0], hd);  // version, class, flow label
+        const uint32_t H1 = __builtin_amdgcn_alignbyte(d[2], d[1], hd);  // payload length, next header
+        const uint32_t plen = bswap16u(H1 & 0xFFFFu);
+        const bool well = live && flen >= 40u && (H0 & 0xF0u) == 0x60u && plen + 40u == flen &&
+                          ((H1 >> 16) & 0xFFu) == 6u && plen >= 20u;  // tcp.go:131
+        uint32_t h8 = 0;
 #pragma unroll
-    for (int k = 0; k < NS; ++k) {
-        const uint32_t an = a0 + k * kRxRun;
-        nxt_off[k] = load_off(an + lane, an < a_end && an + lane <= n);
-        nxt_end[k] = load_off(an + lane + 1, an < a_end && an + lane + 1 <= n);
-    }
-    for (uint32_t a = a0; a < a_end; a += kStep) {
-        uint32_t cnt[NS];
-        uint64_t my_off[NS], my_end[NS];  // frame a + 64k + lane = [my_off[k], my_end[k]) for lane < cnt[k]
-        uint32_t kl = 0;                  // the last set with frames (only a wave's last run has fewer sets)
+        for (int j = 0; j < 3; ++j)
+            h8 = __builtin_amdgcn_sad_u16(d[j] & keep_mask((int32_t)hd, (int32_t)(hd + 8u), 4 * j), 0u, h8);
+        const uint64_t T = F - h8;  // addresses ‖ segment
+        const uint32_t tle = fold32((uint32_t)T) + fold32((uint32_t)(T >> 32));
+        const uint32_t tcpr = well ? finish(tle, even, plen + 6u) : 0u;
+        const uint64_t bits = __builtin_amdgcn_ballot_w64(well && tcpr == 0xFFFFu);
+        rx_store_mask(mrs, bits, ak, cnt, n, lane);
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)tcpr, trs, live ? (ak + lane) * 2u : kOOB, 0, 0);
+    } else {
+        // IPv4 header fields (RFC 791 §3.1): header dword m = bytes 4m..4m+3, little-endian view.
+        const uint32_t H0 = __builtin_amdgcn_alignbyte(d[1], d[0], hd);
+        const uint32_t H1 = __builtin_amdgcn_alignbyte(d[2], d[1], hd);
+        const uint32_t H2 = __builtin_amdgcn_alignbyte(d[3], d[2], hd);
+        const uint32_t H3 = __builtin_amdgcn_alignbyte(d[4], d[3], hd);
+        const uint32_t H4 = __builtin_amdgcn_alignbyte(d[5], d[4], hd);
+        const uint32_t ihl = H0 & 15u, hlen = ihl * 4u;
+        const uint32_t total = bswap16u(H0 >> 16);
+        const uint32_t frag = bswap16u(H1 >> 16);  // flags + fragment offset
+        const uint32_t proto = (H2 >> 8) & 0xFFu;
+        const bool hdr_ok = live && flen >= 20u && ihl >= 5u && hlen <= flen;
+        const bool well = hdr_ok && (H0 & 0xF0u) == 0x40u && total == flen && (frag & 0x3FFFu) == 0u &&
+                          proto == 6u && total - hlen >= 20u;  // tcp.go:131: a segment is at least 20 bytes
+        // Header sum over window bytes [hd, hd + hlen): dwords 0..5 always, 6..15 when some lane has options.
+        uint32_t hs = 0;
 #pragma unroll
-        for (int k = 0; k < NS; ++k) {
-            const uint32_t ak = a + k * kRxRun;
-            cnt[k] = ak < a_end ? min(kRxRun, a_end - ak) : 0u;
-            kl = cnt[k] ? (uint32_t)k : kl;
-            my_off[k] = nxt_off[k], my_end[k] = nxt_end[k];
-            const uint32_t an = ak + kStep;
-            nxt_off[k] = load_off(an + lane, an < a_end && an + lane <= n);
-            nxt_end[k] = load_off(an + lane + 1, an < a_end && an + lane + 1 <= n);
+        for (int j = 0; j < 6; ++j)
+            hs = __builtin_amdgcn_sad_u16(d[j] & keep_mask((int32_t)hd, (int32_t)(hd + hlen), 4 * j), 0u, hs);
+        if (__builtin_amdgcn_ballot_w64(hdr_ok && ihl > 5u)) {  // option dwords 6..15
+            uint32_t o[10];
+            opt(o);
+#pragma unroll
+            for (int j = 6; j < 16; ++j)
+                hs = __builtin_amdgcn_sad_u16(o[j - 6] & keep_mask((int32_t)hd, (int32_t)(hd + hlen), 4 * j), 0u, hs);
         }
+        const uint32_t ipr = hdr_ok ? finish(hs, even, 0u) : 0u;
+        const uint64_t T = F - (hdr_ok ? hs : 0u);  // the TCP segment's weighted sum
+        const uint32_t tle = fold32((uint32_t)T) + fold32((uint32_t)(T >> 32));
+        const uint32_t pseudo = bswap16u(H3 & 0xFFFFu) + bswap16u(H3 >> 16) + bswap16u(H4 & 0xFFFFu) +
+                                bswap16u(H4 >> 16) + 6u + ((total - hlen) & 0xFFFFu);
+        const uint32_t tcpr = well ? finish(tle, even, pseudo) : 0u;
+        const uint64_t bits = __builtin_amdgcn_ballot_w64(well && ipr == 0xFFFFu && tcpr == 0xFFFFu);
+        rx_store_mask(mrs, bits, ak, cnt, n, lane);
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ipr, irs, live ? (ak + lane) * 2u : kOOB, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)tcpr, trs, live ? (ak + lane) * 2u : kOOB, 0, 0);
+    }
+}
+
+// One run of NS sets of ≤ 64 frames in the streaming form: frame a + 64k + lane = [my_off[k], my_end[k]) for
+// lane < cnt[k]; kl = the last set with frames.
+template <int R, bool V6, int NS>
+__device__ __forceinline__ void rx_run_stream(const uint8_t* __restrict__ base, uint32_t a, const uint32_t (&cnt)[NS],
+                                              const uint64_t (&my_off)[NS], const uint64_t (&my_end)[NS], uint32_t kl,
+                                              uint32_t n, uint32_t lane, __amdgpu_buffer_rsrc_t mrs,
+                                              __amdgpu_buffer_rsrc_t irs, __amdgpu_buffer_rsrc_t trs) {
+    {
         const uint64_t lo = readlane64(my_off[0], 0);
         uint64_t hi = 0;
 #pragma unroll
@@ -937,78 +1133,169 @@ __device__ __forceinline__ void rx_runs(const uint8_t* __restrict__ base, __amdg
                 nxt = e;
             }
             const uint64_t F = nxt - bval[k];  // the frame's weighted sum (exact)
-            const uint64_t flen = my_end[k] - my_off[k];
-            const bool even = ((uintptr_t)fp & 1u) == 0;  // frame start parity = TCP segment start parity
-            if constexpr (V6) {
-                const uint32_t H0 = __builtin_amdgcn_alignbyte(d[k][1], d[k][0], hd);  // version, class, flow label
-                const uint32_t H1 = __builtin_amdgcn_alignbyte(d[k][2], d[k][1], hd);  // payload length, next header
-                const uint32_t plen = bswap16u(H1 & 0xFFFFu);
-                const bool well = live && flen >= 40u && (H0 & 0xF0u) == 0x60u && plen + 40u == flen &&
-                                  ((H1 >> 16) & 0xFFu) == 6u && plen >= 20u;  // tcp.go:131
-                uint32_t h8 = 0;
+            // IPv4 option dwords 6..15 (only when some lane has IHL > 5)
+            auto opt = [&](uint32_t (&o)[10]) {
+                if (narrow) {
+                    typedef uint32_t v2x __attribute__((ext_vector_type(2)));
+                    const uint32_t w = hwo[k] == kOOB ? kOOB : hwo[k] + 24u;
+                    const u32x4 q0 = bld16<false>(hrs, w), q1 = bld16<false>(hrs, w == kOOB ? kOOB : w + 16u);
+                    const v2x r = __builtin_amdgcn_raw_buffer_load_b64(hrs, w == kOOB ? kOOB : w + 32u, 0, 0);
+                    o[0] = q0.x, o[1] = q0.y, o[2] = q0.z, o[3] = q0.w, o[4] = q1.x, o[5] = q1.y, o[6] = q1.z;
+                    o[7] = q1.w, o[8] = r.x, o[9] = r.y;
+                } else {
+                    const uint32_t* hw = reinterpret_cast<const uint32_t*>(fp - hd);
 #pragma unroll
-                for (int j = 0; j < 3; ++j)
-                    h8 = __builtin_amdgcn_sad_u16(d[k][j] & keep_mask((int32_t)hd, (int32_t)(hd + 8u), 4 * j), 0u, h8);
-                const uint64_t T = F - h8;  // addresses ‖ segment
-                const uint32_t tle = fold32((uint32_t)T) + fold32((uint32_t)(T >> 32));
-                const uint32_t tcpr = well ? finish(tle, even, plen + 6u) : 0u;
-                const uint64_t bits = __builtin_amdgcn_ballot_w64(well && tcpr == 0xFFFFu);
-                rx_store_mask(mrs, bits, ak, cnt[k], n, lane);
-                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)tcpr, trs, live ? (ak + lane) * 2u : kOOB, 0, 0);
-            } else {
-                // IPv4 header fields (RFC 791 §3.1): header dword m = bytes 4m..4m+3, little-endian view.
-                const uint32_t H0 = __builtin_amdgcn_alignbyte(d[k][1], d[k][0], hd);
-                const uint32_t H1 = __builtin_amdgcn_alignbyte(d[k][2], d[k][1], hd);
-                const uint32_t H2 = __builtin_amdgcn_alignbyte(d[k][3], d[k][2], hd);
-                const uint32_t H3 = __builtin_amdgcn_alignbyte(d[k][4], d[k][3], hd);
-                const uint32_t H4 = __builtin_amdgcn_alignbyte(d[k][5], d[k][4], hd);
-                const uint32_t ihl = H0 & 15u, hlen = ihl * 4u;
-                const uint32_t total = bswap16u(H0 >> 16);
-                const uint32_t frag = bswap16u(H1 >> 16);  // flags + fragment offset
-                const uint32_t proto = (H2 >> 8) & 0xFFu;
-                const bool hdr_ok = live && flen >= 20u && ihl >= 5u && hlen <= flen;
-                const bool well = hdr_ok && (H0 & 0xF0u) == 0x40u && total == flen && (frag & 0x3FFFu) == 0u &&
-                                  proto == 6u && total - hlen >= 20u;  // tcp.go:131: a segment is at least 20 bytes
-                // Header sum over window bytes [hd, hd + hlen): dwords 0..5 always, 6..15 when some lane has options.
-                uint32_t hs = 0;
-#pragma unroll
-                for (int j = 0; j < 6; ++j)
-                    hs = __builtin_amdgcn_sad_u16(d[k][j] & keep_mask((int32_t)hd, (int32_t)(hd + hlen), 4 * j), 0u, hs);
-                if (__builtin_amdgcn_ballot_w64(hdr_ok && ihl > 5u)) {  // option dwords 6..15
-                    uint32_t o[10];
-                    if (narrow) {
-                        typedef uint32_t v2x __attribute__((ext_vector_type(2)));
-                        const uint32_t w = hwo[k] == kOOB ? kOOB : hwo[k] + 24u;
-                        const u32x4 q0 = bld16<false>(hrs, w), q1 = bld16<false>(hrs, w == kOOB ? kOOB : w + 16u);
-                        const v2x r = __builtin_amdgcn_raw_buffer_load_b64(hrs, w == kOOB ? kOOB : w + 32u, 0, 0);
-                        o[0] = q0.x, o[1] = q0.y, o[2] = q0.z, o[3] = q0.w, o[4] = q1.x, o[5] = q1.y, o[6] = q1.z;
-                        o[7] = q1.w, o[8] = r.x, o[9] = r.y;
-                    } else {
-                        const uint32_t* hw = reinterpret_cast<const uint32_t*>(fp - hd);
-#pragma unroll
-                        for (int j = 6; j < 16; ++j) o[j - 6] = hw + j < last_dw ? hw[j] : *last_dw;
-                    }
-#pragma unroll
-                    for (int j = 6; j < 16; ++j)
-                        hs = __builtin_amdgcn_sad_u16(o[j - 6] & keep_mask((int32_t)hd, (int32_t)(hd + hlen), 4 * j), 0u,
-                                                      hs);
+                    for (int j = 6; j < 16; ++j) o[j - 6] = hw + j < last_dw ? hw[j] : *last_dw;
                 }
-                const uint32_t ipr = hdr_ok ? finish(hs, even, 0u) : 0u;
-                const uint64_t T = F - (hdr_ok ? hs : 0u);  // the TCP segment's weighted sum
-                const uint32_t tle = fold32((uint32_t)T) + fold32((uint32_t)(T >> 32));
-                const uint32_t pseudo = bswap16u(H3 & 0xFFFFu) + bswap16u(H3 >> 16) + bswap16u(H4 & 0xFFFFu) +
-                                        bswap16u(H4 >> 16) + 6u + ((total - hlen) & 0xFFFFu);
-                const uint32_t tcpr = well ? finish(tle, even, pseudo) : 0u;
-                const uint64_t bits = __builtin_amdgcn_ballot_w64(well && ipr == 0xFFFFu && tcpr == 0xFFFFu);
-                rx_store_mask(mrs, bits, ak, cnt[k], n, lane);
-                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ipr, irs, live ? (ak + lane) * 2u : kOOB, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)tcpr, trs, live ? (ak + lane) * 2u : kOOB, 0, 0);
-            }
+            };
+            rx_frame_out<V6>(F, d[k], hd, my_end[k] - my_off[k], ((uintptr_t)fp & 1u) == 0, live, ak, cnt[k], n, lane,
+                             mrs, irs, trs, opt);
         }
     }
 }
 
-// sets: 0 = by the wave's mean frame size (kRxSmallFrame), 1 / 4 = force runs of that many 64-frame sets.
+template <int R, bool V6, int NS>
+__device__ __forceinline__ void rx_runs(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
+                                        uint32_t a0, uint32_t a_end, uint32_t lane, __amdgpu_buffer_rsrc_t mrs,
+                                        __amdgpu_buffer_rsrc_t irs, __amdgpu_buffer_rsrc_t trs) {
+    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+    auto load_off = [&](uint32_t i, bool live) -> uint64_t {
+        const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, live ? i * 8 : kOOB, 0, 0);
+        return ((uint64_t)x.y << 32) | x.x;
+    };
+    constexpr uint32_t kStep = kRxRun * NS;
+    // lane l of set k: offsets[a + 64k + l] and offsets[a + 64k + l + 1] of the next run, prefetched one run ahead
+    uint64_t nxt_off[NS], nxt_end[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+        const uint32_t an = a0 + k * kRxRun;
+        nxt_off[k] = load_off(an + lane, an < a_end && an + lane <= n);
+        nxt_end[k] = load_off(an + lane + 1, an < a_end && an + lane + 1 <= n);
+    }
+    for (uint32_t a = a0; a < a_end; a += kStep) {
+        uint32_t cnt[NS];
+        uint64_t my_off[NS], my_end[NS];  // frame a + 64k + lane = [my_off[k], my_end[k]) for lane < cnt[k]
+        uint32_t kl = 0;                  // the last set with frames (only a wave's last run has fewer sets)
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+            const uint32_t ak = a + k * kRxRun;
+            cnt[k] = ak < a_end ? min(kRxRun, a_end - ak) : 0u;
+            kl = cnt[k] ? (uint32_t)k : kl;
+            my_off[k] = nxt_off[k], my_end[k] = nxt_end[k];
+            const uint32_t an = ak + kStep;
+            nxt_off[k] = load_off(an + lane, an < a_end && an + lane <= n);
+            nxt_end[k] = load_off(an + lane + 1, an < a_end && an + lane + 1 <= n);
+        }
+        rx_run_stream<R, V6, NS>(base, a, cnt, my_off, my_end, kl, n, lane, mrs, irs, trs);
+    }
+}
+
+// The LDS form of the receive pass, for waves of small frames. A run of 64 frames whose
+// bytes fit kRxSlotRows rows is staged whole into the wave's LDS slot — coalesced 16 B-per-lane row loads, issued
+// one run ahead (the next run's rows are in flight while this one is summed), then ds_write_b128 — and each lane
+// sums ITS OWN frame out of LDS: the frame's 16 B chunks (ds_read_b128, eight in flight per lane), minus the bytes
+// of the first chunk before the frame and of the last chunk past it; its header window comes from the slot too
+// (no second fetch of the header bytes). No boundary scan, no ds_bpermute, no per-row ballots: per frame the work
+// is its own length. A run whose bytes do not fit (a large frame among small ones) takes the streaming form.
+constexpr uint32_t kRxSlotRows = 8;
+constexpr uint32_t kRxSlot = kRxSlotRows * kRow + 128;  // + pad: a header window read past the slot's last frame
+
+template <bool V6>
+__device__ __forceinline__ void rx_run_lds(const uint8_t* __restrict__ base, const uint8_t* rbase, uint32_t a,
+                                           uint32_t cnt, uint64_t my_off, uint64_t my_end, uint32_t n, uint32_t lane,
+                                           const lds16* slot, __amdgpu_buffer_rsrc_t mrs, __amdgpu_buffer_rsrc_t irs,
+                                           __amdgpu_buffer_rsrc_t trs) {
+    const uint32_t* sdw = reinterpret_cast<const uint32_t*>(slot);
+    const bool live = lane < cnt;
+    // frame position in the slot (rbase is 128-aligned, so the slot keeps every byte's address mod 128)
+    const uint32_t p = live ? (uint32_t)((base + my_off) - rbase) : 0u;
+    const uint32_t e = live ? (uint32_t)((base + my_end) - rbase) : 0u;
+    const uint32_t hd = p & 3u, w0 = p >> 2;
+    uint32_t d[6];
+#pragma unroll
+    for (int j = 0; j < (V6 ? 3 : 6); ++j) d[j] = sdw[w0 + j];
+    if constexpr (V6) d[3] = d[4] = d[5] = 0u;
+    const uint64_t F = lds_range_sum(slot, p, e);  // the frame's weighted sum
+    auto opt = [&](uint32_t (&o)[10]) {
+#pragma unroll
+        for (int j = 6; j < 16; ++j) o[j - 6] = sdw[w0 + j];
+    };
+    rx_frame_out<V6>(F, d, hd, my_end - my_off, (p & 1u) == 0, live, a, cnt, n, lane, mrs, irs, trs, opt);
+}
+
+// A wave's runs [a0, a_end) in the LDS form (runs of 64 frames from a multiple of 8, as rx_runs).
+template <int R, bool V6>
+__device__ __forceinline__ void rx_runs_lds(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
+                                            uint32_t a0, uint32_t a_end, uint32_t lane, lds16* slot,
+                                            __amdgpu_buffer_rsrc_t mrs, __amdgpu_buffer_rsrc_t irs,
+                                            __amdgpu_buffer_rsrc_t trs) {
+    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+    auto load_off = [&](uint32_t i, bool live) -> uint64_t {
+        const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, live ? i * 8 : kOOB, 0, 0);
+        return ((uint64_t)x.y << 32) | x.x;
+    };
+    struct Run {
+        const uint8_t* rbase;
+        uint64_t span;
+        uint32_t cnt;
+        bool lds;
+    };
+    auto geo = [&](uint32_t a, uint64_t off, uint64_t end) {  // wave-uniform geometry of run a
+        Run g{base, 0, a < a_end ? min(kRxRun, a_end - a) : 0u, false};
+        if (g.cnt) {
+            const uint64_t lo = readlane64(off, 0), hi = readlane64(end, g.cnt - 1u);
+            g.rbase = reinterpret_cast<const uint8_t*>(((uintptr_t)(base + lo)) & ~(uintptr_t)127);
+            g.span = (uint64_t)((base + hi) - g.rbase);
+            g.lds = g.span <= (uint64_t)kRxSlotRows * kRow;
+        }
+        return g;
+    };
+    u32x4 V[kRxSlotRows];
+    auto issue = [&](const Run& g) {  // rows past the run: out of the descriptor's range, 0, no traffic
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(g.rbase, (g.span + 3) & ~3ull);
+#pragma unroll
+        for (uint32_t r = 0; r < kRxSlotRows; ++r) V[r] = bld16<true>(rs, r * kRow + lane * 16u);
+    };
+    // The LDS loop runs while consecutive runs fit the slot; a run that does not is streamed on its own in the
+    // outer loop. (Kept apart so that the streaming form's loads still in flight at its end — its pipeline issues
+    // one empty batch past the run — never merge into the LDS loop's wait counts: at a merge hipcc waits
+    // vmcnt(0) before reusing such a register, which drained the next run's rows right after their issue.)
+    uint32_t a = a0;
+    while (a < a_end) {
+        uint64_t c_off = load_off(a + lane, a + lane <= n);
+        uint64_t c_end = load_off(a + lane + 1u, a + lane + 1u <= n);
+        Run cur = geo(a, c_off, c_end);
+        if (!cur.lds) {  // a run too wide for the slot: the streaming form
+            uint32_t cnt1[1] = {cur.cnt};
+            uint64_t o1[1] = {c_off}, e1[1] = {c_end};
+            rx_run_stream<R, V6, 1>(base, a, cnt1, o1, e1, 0u, n, lane, mrs, irs, trs);
+            a += kRxRun;
+            continue;
+        }
+        issue(cur);
+        uint32_t an = a + kRxRun;
+        uint64_t n_off = load_off(an + lane, an < a_end && an + lane <= n);
+        uint64_t n_end = load_off(an + lane + 1u, an < a_end && an + lane + 1u <= n);
+        for (;;) {
+            lds_stage<kRxSlotRows>(slot, V, cur.span, lane);
+            Run nxt = geo(an, n_off, n_end);
+            if (!nxt.lds) nxt.span = 0;  // the rows of a run that will be streamed are not staged: empty loads
+            issue(nxt);
+            const uint32_t an2 = an + kRxRun;
+            const uint64_t p_off = load_off(an2 + lane, an2 < a_end && an2 + lane <= n);
+            const uint64_t p_end = load_off(an2 + lane + 1u, an2 < a_end && an2 + lane + 1u <= n);
+            rx_run_lds<V6>(base, cur.rbase, a, cur.cnt, c_off, c_end, n, lane, slot, mrs, irs, trs);
+            a = an;
+            if (!nxt.lds) break;  // the end of the wave's range, or a run for the outer loop
+            cur = nxt;
+            c_off = n_off, c_end = n_end, n_off = p_off, n_end = p_end;
+            an = an2;
+        }
+    }
+}
+
+// sets: 0 = by the wave's mean frame size (the LDS form below kRxSmallFrame, else streamed runs of one 64-frame
+// set); 1 / 4 = force streamed runs of that many sets; 2 = force the LDS form.
 template <int R, bool V6>
 __global__ __launch_bounds__(kBlock) void rx_tcp_kernel(const uint8_t* __restrict__ base,
                                                              const uint64_t* __restrict__ offsets, uint32_t n,
@@ -1038,11 +1325,15 @@ __global__ __launch_bounds__(kBlock) void rx_tcp_kernel(const uint8_t* __restric
         a_end = g + 1 == W ? n : min((s[1] + 7u) & ~7u, n);
         wave_bytes = tot * (g + 1) / W - tot * g / W;
     }
-    const bool small = sets == 4 || (sets == 0 && wave_bytes < (uint64_t)kRxSmallFrame * (a_end - a0));
-    if (small)
+    const bool small = sets == 2 || (sets == 0 && wave_bytes < (uint64_t)kRxSmallFrame * (a_end - a0));
+    if (small) {
+        extern __shared__ lds16 lds_rx[];
+        rx_runs_lds<R, V6>(base, ofs, n, a0, a_end, lane, lds_rx + wave * (kRxSlot / 16u), mrs, irs, trs);
+    } else if (sets == 4) {
         rx_runs<R, V6, 4>(base, ofs, n, a0, a_end, lane, mrs, irs, trs);
-    else
+    } else {
         rx_runs<R, V6, 1>(base, ofs, n, a0, a_end, lane, mrs, irs, trs);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -2205,7 +2496,9 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
     // are paid half as often (config 3 0.684 → 0.682 ms, 40-1500 B frames 0.1320 → 0.1293; 4 sets: 0.683 /
     // 0.1308, more registers and phase-2 checks); segs_per_wave = 1 keeps one set.
     const int ns = (pipe && rows == 2 && c.segs_per_wave != 1) ? 2 : 1;
-    const int sets = c.segs_per_wave == 4 ? 4 : 0;  // force runs of four sets (tests); 0: by mean segment size
+    // force runs of four sets (4) or the LDS form (2; tests and A/B); 0: by mean segment size
+    const int sets = c.segs_per_wave == 4 || c.segs_per_wave == 2 ? c.segs_per_wave : 0;
+    const size_t lds = (size_t)kScanSlot * kWavesPerBlock;  // the LDS form's per-wave slots
     const uint32_t mb = max_blocks_of(c, 2);
     for (uint64_t c0 = 0; c0 < n; c0 += kRaggedChunk) {
         const uint32_t cn = (uint32_t)(n - c0 < kRaggedChunk ? n - c0 : kRaggedChunk);
@@ -2215,7 +2508,7 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
         uint8_t* kc = ok ? ok + c0 : nullptr;
 #define NSX_RSCAN(R_, P_, NS_)                                                                                 \
         if (rows == R_ && pipe == P_ && ns == NS_)                                                              \
-            hipLaunchKernelGGL((csum_ragged_scan_kernel<R_, VERIFY, P_, NS_>), dim3(grid), dim3(kBlock), 0, st,  \
+            hipLaunchKernelGGL((csum_ragged_scan_kernel<R_, VERIFY, P_, NS_>), dim3(grid), dim3(kBlock), lds, st,\
                                base, offsets + c0, cn, pc, oc, kc, run, sets);
         NSX_RSCAN(2, true, 1) NSX_RSCAN(4, true, 1) NSX_RSCAN(8, true, 1)
         NSX_RSCAN(4, false, 1) NSX_RSCAN(8, false, 1) NSX_RSCAN(16, false, 1)
@@ -2251,7 +2544,8 @@ hipError_t launch_rx_tcp(const LaunchCfg& c, int ipver, const void* d_base, cons
     // at 4); launches of ≤ 2^27 frames (a multiple of 64, so every launch starts on a mask word)
     const int rows = (c.rows == 2 || c.rows == 4 || c.rows == 8 || c.rows == 16) ? c.rows : 2;
     // 64-frame sets per run: by each wave's mean frame size, or forced by segs_per_wave 1 / 4 (tests)
-    const int sets = c.segs_per_wave == 1 || c.segs_per_wave == 4 ? c.segs_per_wave : 0;
+    const int sets = c.segs_per_wave == 1 || c.segs_per_wave == 2 || c.segs_per_wave == 4 ? c.segs_per_wave : 0;
+    const size_t lds = (size_t)kRxSlot * kWavesPerBlock;  // the LDS form's per-wave slots (3 blocks/CU: 100 KB)
     const uint32_t mb = max_blocks_of(c, 3);
     const uint8_t* base = static_cast<const uint8_t*>(d_base);
     for (uint64_t c0 = 0; c0 < n; c0 += kRaggedChunk) {
@@ -2261,10 +2555,10 @@ hipError_t launch_rx_tcp(const LaunchCfg& c, int ipver, const void* d_base, cons
         uint16_t* tc = tcp_raw ? tcp_raw + c0 : nullptr;
 #define NSX_RX(R_)                                                                                                \
         if (rows == R_ && ipver == 6)                                                                              \
-            hipLaunchKernelGGL((rx_tcp_kernel<R_, true>), dim3(grid), dim3(kBlock), 0, st, base, d_offsets + c0, cn,  \
+            hipLaunchKernelGGL((rx_tcp_kernel<R_, true>), dim3(grid), dim3(kBlock), lds, st, base, d_offsets + c0, cn,\
                                mask + c0 / 64, nullptr, tc, sets);                                                       \
         if (rows == R_ && ipver != 6)                                                                              \
-            hipLaunchKernelGGL((rx_tcp_kernel<R_, false>), dim3(grid), dim3(kBlock), 0, st, base, d_offsets + c0, cn, \
+            hipLaunchKernelGGL((rx_tcp_kernel<R_, false>), dim3(grid), dim3(kBlock), lds, st, base, d_offsets + c0, cn,\
                                mask + c0 / 64, ic, tc, sets);
         NSX_RX(2) NSX_RX(4) NSX_RX(8) NSX_RX(16)
 #undef NSX_RX

@@ -121,14 +121,17 @@ RAGGED_TUNES = [dict(kernel=k, rows=r, run_segs=rs, blocks_per_cu=b)  # pipeline
                 for rs in (0, 1, 16, 63) for b in (0, 1, 8)] + \
                [dict(segs_per_wave=1, run_segs=rs, blocks_per_cu=b)  # one boundary set per lane (default: two)
                 for rs in (0, 1, 16, 63) for b in (0, 1, 8)] + \
-               [dict(segs_per_wave=4, run_segs=rs, blocks_per_cu=b)  # runs of four sets (small segments' form)
-                for rs in (0, 1, 16, 63) for b in (0, 1, 8)]
+               [dict(segs_per_wave=4, run_segs=rs, blocks_per_cu=b)  # runs of four sets
+                for rs in (0, 1, 16, 63) for b in (0, 1, 8)] + \
+               [dict(segs_per_wave=2, run_segs=rs, blocks_per_cu=b, kernel=k)  # the LDS form (small segments' form)
+                for rs in (0, 1, 16, 63) for b in (0, 1, 8) for k in (0, nsx.KERNEL_SCAN_PLAIN)]
 
 
 @pytest.mark.parametrize("n", [1, 126, 252, 253, 30_001, 400_003])
 def test_ragged_small_segments_runs_of_four_sets(n):
-    """Segments of 0-200 B (mean ~100): waves whose segments average under 256 B take runs of four 63-segment sets
-    (DESIGN.md §7 step 42); the automatic choice and both forced forms equal the oracle, with and without partials.
+    """Segments of 0-200 B (mean ~100): waves whose segments average under 256 B take the LDS form (DESIGN.md §7
+    step 44); it, the streamed runs of one and of four 63-segment sets (§7 step 42) and the automatic choice equal
+    the oracle, with and without partials.
     block_mode=1 keeps even the smallest batches on the scan kernel, and short runs (run_segs 1, 16) at one block
     per CU make every wave stream many runs, so all four sets, partial last sets and set-to-set frame ends run
     (ADVICE r2); n = 400K reaches the four sets with the default run length too."""
@@ -142,9 +145,9 @@ def test_ragged_small_segments_runs_of_four_sets(n):
     want = O.c_batch(buf, n, offsets=offs, threads=16)
     want_p = O.c_batch(buf, n, offsets=offs, partial=part, threads=16)
     d, o, p = dev(buf), dev(offs.view(np.int64)), dev(part.view(np.int32))
-    tunes = [None, dict(segs_per_wave=1), dict(segs_per_wave=4)]
+    tunes = [None, dict(segs_per_wave=1), dict(segs_per_wave=4), dict(segs_per_wave=2)]
     tunes += [dict(block_mode=1, blocks_per_cu=1, run_segs=rs, **sp)
-              for rs in (0, 1, 16) for sp in ({}, dict(segs_per_wave=1), dict(segs_per_wave=4))]
+              for rs in (0, 1, 16) for sp in ({}, dict(segs_per_wave=1), dict(segs_per_wave=4), dict(segs_per_wave=2))]
     for tune in tunes:
         out = torch.empty(n, dtype=torch.int16, device="cuda")
         nsx.ragged_dev(d, o, out=out, tune=tune)

@@ -54,18 +54,20 @@ def test_rx_mixed_batches(n, lead):
 
 
 TUNES = [dict(rows=2), dict(rows=4), dict(rows=16), dict(blocks_per_cu=1), dict(blocks_per_cu=8), dict(rows=16, blocks_per_cu=1),
-         dict(segs_per_wave=4), dict(segs_per_wave=4, rows=4), dict(segs_per_wave=1)]  # runs of 4 / 1 frame sets
+         dict(segs_per_wave=4), dict(segs_per_wave=4, rows=4), dict(segs_per_wave=1),  # streamed runs of 4 / 1 frame sets
+         dict(segs_per_wave=2), dict(segs_per_wave=2, blocks_per_cu=1), dict(segs_per_wave=2, blocks_per_cu=8)]  # LDS form
 
 
 @pytest.mark.parametrize("n", [1, 255, 256, 257, 1000, 30_001])
 @pytest.mark.parametrize("lead", [0, 3])
 def test_rx_small_frames_runs_of_four_sets(n, lead):
-    """Frames of at most 40 B of payload: waves whose frames average under 128 B stream runs of four 64-frame sets
-    (DESIGN.md §7 step 41); every set boundary, partial last sets and both run forms equal the oracle."""
+    """Frames of at most 40 B of payload: waves whose frames average under 128 B take the LDS form (DESIGN.md §7
+    step 43); it, and the streamed runs of one and of four 64-frame sets (§7 step 41), equal the oracle at every
+    run boundary and partial last run."""
     rng = np.random.default_rng(n * 2 + lead)
     buf, offs, _ = _rx.batch(rng, n, lead=lead, max_payload=40)
     want = O.c_rx_ipv4_tcp(buf, offs)
-    for tune in (None, dict(segs_per_wave=1), dict(segs_per_wave=4)):
+    for tune in (None, dict(segs_per_wave=1), dict(segs_per_wave=4), dict(segs_per_wave=2)):
         got = run_rx(buf, offs, tune)
         for w, g, what in zip(want, got, ("mask", "ip_raw", "tcp_raw")):
             assert np.array_equal(w, g), (what, n, lead, tune)
@@ -110,8 +112,9 @@ def test_rx_small_frames_300K_every_set_form_vs_oracle(ipver):
     want = O.c_rx_ipv4_tcp(buf_h, offs) if ipver == 4 else O.c_rx_ipv6_tcp(buf_h, offs)
     bits = np.unpackbits(want[0].view(np.uint8), bitorder="little")[:n]
     assert 0.85 * n < bits.sum() < 0.985 * n  # mostly valid, every kind of failure present
-    for tune in (None, dict(segs_per_wave=1), dict(segs_per_wave=4), dict(blocks_per_cu=1),
-                 dict(blocks_per_cu=1, segs_per_wave=1), dict(blocks_per_cu=1, segs_per_wave=4)):
+    for tune in (None, dict(segs_per_wave=1), dict(segs_per_wave=4), dict(segs_per_wave=2), dict(blocks_per_cu=1),
+                 dict(blocks_per_cu=1, segs_per_wave=1), dict(blocks_per_cu=1, segs_per_wave=4),
+                 dict(blocks_per_cu=1, segs_per_wave=2)):
         got = run_rx(buf_h, offs, tune) if ipver == 4 else run_rx6(buf_h, offs, tune)
         for wv, g, what in zip(want, got, ("mask", "ip_raw", "tcp_raw") if ipver == 4 else ("mask", "tcp_raw")):
             bad = np.nonzero(wv != g)[0]
