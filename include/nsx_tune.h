@@ -28,14 +28,20 @@ extern "C" {
 #define NSX_TUNE_KERNEL_SCAN_PLAIN    2  /* ragged scan: single row batches (rows 4, 8 or 16) */
 
 typedef struct nsx_tune {
-    int32_t blocks_per_cu;     /* persistent grid: 1..8 blocks of 256 threads per CU */
+    int32_t blocks_per_cu;     /* persistent grid: 1..8 blocks of 256 threads per CU. Default of the ragged
+                                  scan and receive kernels: 4 per CU, of which a batch whose mean segment /
+                                  frame is >= 256 B / 128 B uses 2 / 3 (the rest return at once); a value
+                                  here runs exactly that grid */
     int32_t segs_per_wave;     /* fixed batches of <= 4 KiB segments: segments per wave task (1, 2, 4, 8).
-                                  Ragged scan, 63-segment boundary sets per run: 0 auto (four sets in waves
-                                  whose segments average < 256 B, else two), 1 = one set, 4 = four sets in
-                                  every wave. Only the default pipelined 2-row shape has more than one
-                                  set: with kernel = SCAN_PLAIN or rows != 2 every run is one set.
-                                  Receive kernels, 64-frame sets per run: 0 auto (four sets in waves whose
-                                  frames average < 128 B, else one), 1 = one set, 4 = four sets in every wave. */
+                                  Ragged scan, per wave: 0 auto (the LDS form in waves whose segments
+                                  average < 128 B, streamed runs of four 63-segment sets < 256 B, else runs
+                                  of two sets), 1 = runs of one set, 2 = the LDS form, 4 = runs of four sets
+                                  in every wave. Only the default pipelined 2-row shape has more than one
+                                  set: with kernel = SCAN_PLAIN or rows != 2 a 4 gives runs of one set.
+                                  Receive kernels, per wave: 0 auto (the LDS form in waves whose frames
+                                  average < 128 B, else streamed runs of 64 frames), 1 = streamed runs,
+                                  2 = the LDS form. (A run that does not fit the LDS form's 8 KiB slot is
+                                  streamed in any case.) */
     int32_t block_mode;        /* 0 auto (a block per segment when n < 4 * CUs), 1 never, 2 always */
     int32_t rows;              /* ragged scan / receive kernels: 1 KiB rows per load batch (4, 8, 16) */
     int32_t run_segs;          /* segments per wave task: ragged scan kernel 1..63, TCP build 1..64 */

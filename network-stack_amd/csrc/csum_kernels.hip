@@ -707,6 +707,22 @@ __device__ __forceinline__ void scan_span(const uint8_t* rbase, uint64_t span, u
 }
 
 constexpr uint32_t kScanSmallSeg = 256;
+constexpr uint32_t kScanLdsSeg = 128;  // runs of 63 such segments fit the LDS form's 8 KiB slot
+
+// Blocks of this launch that take work. The persistent grids of the ragged scan and the receive pass are sized for
+// small units (4 blocks/CU: every wave's rows in flight count when each unit costs a header check or an LDS
+// sum); a batch whose mean unit is at least `big_mean` bytes streams best on fewer waves (config 3 at 2 blocks/CU
+// 2.7% faster than at 4, workload 10 at 3 blocks/CU 2.8% faster), so only its first ⌊gridDim·keep/4⌋ blocks
+// (rounded to the 8 XCDs) take byte ranges and the rest return at once. keep = 0: every block.
+__device__ __forceinline__ uint32_t active_blocks(__amdgpu_buffer_rsrc_t ofs, uint32_t n, uint32_t big_mean,
+                                                  uint32_t keep) {
+    const uint32_t nb = gridDim.x;
+    if (keep == 0 || nb < 64) return nb;
+    const uint64_t tot = ld_off(ofs, n) - ld_off(ofs, 0);
+    if (tot < (uint64_t)big_mean * n) return nb;
+    const uint32_t k = (nb / 4u * keep) & ~7u;
+    return k ? k : nb;
+}
 
 // One run of NS sets of ≤ run segments in the streaming form: set k = segments [a + k·run, + cnt[k]), lane l ≤
 // cnt[k] holds boundary my_off[k] = offsets[a + k·run + l] and (l < cnt[k]) the partial my_part[k].
@@ -794,13 +810,16 @@ __device__ __forceinline__ uint32_t lds_range_sum(const lds16* slot, uint32_t p,
     const uint32_t clast = nch ? nch - 1u : 0u;
     // Blocks of 8 chunks, a wave-uniform trip count from the wave's longest range (an SGPR loop counter: a loop
     // ending on a ballot left hipcc an undefined exit value that it read with v_readfirstlane from a register
-    // still being loaded — a vmcnt wait that drained the next run's rows before this run's sums began).
+    // still being loaded — a vmcnt wait that drained the next run's rows before this run's sums began). A block
+    // reads chunks c0 + j0 .. c0 + j0 + 7 unclamped (one address, immediate offsets; the slot's pad keeps the
+    // reads past its last chunk inside it) and keeps those below nch.
     const uint32_t nblk = wave_max((nch + 7u) >> 3);
     uint32_t acc = 0, head_x = 0;
     for (uint32_t j0 = 0; j0 < nblk * 8u; j0 += 8u) {
         u32x4 x[8];
+        const lds16* blk = slot + c0 + j0;
 #pragma unroll
-        for (uint32_t j = 0; j < 8u; ++j) x[j] = lds_get(slot, c0 + min(j0 + j, clast));
+        for (uint32_t j = 0; j < 8u; ++j) x[j] = lds_get(blk, j);
         if (j0 == 0) head_x = sad4(keep_bytes(x[0], 0, (int32_t)(p & 15u)), 0u);
 #pragma unroll
         for (uint32_t j = 0; j < 8u; ++j) {
@@ -821,9 +840,10 @@ __device__ __forceinline__ void lds_stage(lds16* slot, u32x4 (&V)[ROWS], uint64_
 #pragma unroll
     for (uint32_t r = 0; r < ROWS; ++r) asm volatile("" : "+v"(V[r]));
     __builtin_amdgcn_wave_barrier();
+    const uint32_t rows = __builtin_amdgcn_readfirstlane((uint32_t)((span + kRow - 1) / kRow));  // ≤ ROWS (scalar)
 #pragma unroll
     for (uint32_t r = 0; r < ROWS; ++r)
-        if ((uint64_t)r * kRow < span) slot[r * (kRow / 16u) + lane] = lds16{V[r].x, V[r].y, V[r].z, V[r].w};
+        if (r < rows) slot[r * (kRow / 16u) + lane] = lds16{V[r].x, V[r].y, V[r].z, V[r].w};
     __builtin_amdgcn_wave_barrier();
 }
 
@@ -831,7 +851,7 @@ __device__ __forceinline__ void lds_stage(lds16* slot, u32x4 (&V)[ROWS], uint64_
 // (rx_runs_lds) applied to runs of ≤ run segments: lane l sums segment a + l out of the wave's slot. A run too
 // wide for the slot takes the streaming form (one set).
 constexpr uint32_t kScanSlotRows = 8;
-constexpr uint32_t kScanSlot = kScanSlotRows * kRow;
+constexpr uint32_t kScanSlot = kScanSlotRows * kRow + 256;  // + pad: lds_range_sum's chunk blocks read past the end
 
 template <int R, bool VERIFY, bool PIPE>
 __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
@@ -856,7 +876,7 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
             const uint64_t lo = readlane64(off, 0), hi = readlane64(off, g.cnt);
             g.rbase = reinterpret_cast<const uint8_t*>(((uintptr_t)(base + lo)) & ~(uintptr_t)127);
             g.span = (uint64_t)((base + hi) - g.rbase);
-            g.lds = g.span <= (uint64_t)kScanSlot;
+            g.lds = g.span <= (uint64_t)kScanSlotRows * kRow;
         }
         return g;
     };
@@ -910,13 +930,17 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
 template <int R, bool VERIFY, bool PIPE, int NS>
 __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, uint32_t n,
-    const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t run, int sets) {
+    const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t run, int sets,
+    uint32_t big_keep) {
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const __amdgpu_buffer_rsrc_t ofs = make_rsrc(offsets, ((uint64_t)n + 1) * 8);
     const __amdgpu_buffer_rsrc_t prs = make_rsrc(partial, partial ? (uint64_t)n * 4 : 0);
     const __amdgpu_buffer_rsrc_t ors = make_rsrc(out, out ? (uint64_t)n * 2 : 0);
     const __amdgpu_buffer_rsrc_t oks = make_rsrc(ok, VERIFY ? (uint64_t)n : 0);
+    // The grid is sized for small segments (4 blocks/CU); a batch of large ones streams on big_keep of them.
+    const uint32_t nb = active_blocks(ofs, n, kScanSmallSeg, big_keep);
+    if (blockIdx.x >= nb) return;
     // The wave's tasks are runs of NS sets [a_k, a_k + cnt_k) of ≤ run segments each (a_k = a + k·run), a = a0,
     // a0 + NS·run, ... < a_end; a run never crosses a_end. Byte-balanced: wave g (XCD-contiguous numbering) owns
     // the segments that start in the g-th of W equal byte slices of the batch, so every wave streams the same
@@ -924,7 +948,7 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
     uint32_t a0, a_end;
     uint64_t wave_bytes;
     {
-        const uint32_t nb = gridDim.x, b = blockIdx.x, W = nb * kWavesPerBlock;
+        const uint32_t b = blockIdx.x, W = nb * kWavesPerBlock;
         const uint32_t g = (nb >= 16 && (nb & 7) == 0) ? ((b & 7) * (nb >> 3) + (b >> 3)) * kWavesPerBlock + wave
                                                         : b * kWavesPerBlock + wave;
         const uint64_t o_lo = ld_off(ofs, 0), o_hi = ld_off(ofs, n);
@@ -935,13 +959,14 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
         a_end = g + 1 == W ? n : s[1];
         wave_bytes = tot * (g + 1) / W - tot * g / W;
     }
-    // Two sets per run suit segments of a few hundred bytes and up (config 3); a wave whose segments average under
-    // kScanSmallSeg bytes takes runs of four sets, so that each run still streams tens of KB (§7 step 42).
-    if (sets == 2 || (NS == 2 && sets == 0 && wave_bytes < (uint64_t)kScanSmallSeg * (a_end - a0))) {
+    // Two sets per run suit segments of a few hundred bytes and up (config 3). A wave whose segments average under
+    // kScanLdsSeg bytes sums them out of LDS (§7 step 44); under kScanSmallSeg it takes runs of four sets, so that
+    // each run still streams tens of KB (§7 step 42).
+    if (sets == 2 || (NS == 2 && sets == 0 && wave_bytes < (uint64_t)kScanLdsSeg * (a_end - a0))) {
         extern __shared__ lds16 lds_scan[];
         ragged_runs_lds<R, VERIFY, PIPE>(base, ofs, n, prs, ors, oks, run, a0, a_end, lane,
                                          lds_scan + wave * (kScanSlot / 16u));
-    } else if (NS == 2 && sets == 4) {
+    } else if (NS == 2 && (sets == 4 || (sets == 0 && wave_bytes < (uint64_t)kScanSmallSeg * (a_end - a0)))) {
         ragged_runs<R, VERIFY, PIPE, 4>(base, ofs, n, prs, ors, oks, run, a0, a_end, lane);
     } else {
         ragged_runs<R, VERIFY, PIPE, NS>(base, ofs, n, prs, ors, oks, run, a0, a_end, lane);
@@ -1198,7 +1223,7 @@ __device__ __forceinline__ void rx_runs(const uint8_t* __restrict__ base, __amdg
 // (no second fetch of the header bytes). No boundary scan, no ds_bpermute, no per-row ballots: per frame the work
 // is its own length. A run whose bytes do not fit (a large frame among small ones) takes the streaming form.
 constexpr uint32_t kRxSlotRows = 8;
-constexpr uint32_t kRxSlot = kRxSlotRows * kRow + 128;  // + pad: a header window read past the slot's last frame
+constexpr uint32_t kRxSlot = kRxSlotRows * kRow + 256;  // + pad: a header window or chunk block read past the end
 
 template <bool V6>
 __device__ __forceinline__ void rx_run_lds(const uint8_t* __restrict__ base, const uint8_t* rbase, uint32_t a,
@@ -1295,13 +1320,17 @@ __device__ __forceinline__ void rx_runs_lds(const uint8_t* __restrict__ base, __
 }
 
 // sets: 0 = by the wave's mean frame size (the LDS form below kRxSmallFrame, else streamed runs of one 64-frame
-// set); 1 / 4 = force streamed runs of that many sets; 2 = force the LDS form.
-template <int R, bool V6>
-__global__ __launch_bounds__(kBlock) void rx_tcp_kernel(const uint8_t* __restrict__ base,
+// set); 1 = force the streamed runs; 2 = force the LDS form. (Round 2's streamed runs of four sets for small
+// frames, §7 step 41, were removed: the LDS form beat them by 30-40% on every small-frame mix, §7 step 43.)
+// WPS: waves per SIMD the registers must allow (__launch_bounds__'s second argument): 1 = no constraint (158 VGPRs,
+// 3 waves per SIMD at the default 3 blocks/CU); 4 = the 4-blocks/CU instantiation (≤ 128 VGPRs).
+template <int R, bool V6, int WPS>
+__global__ __launch_bounds__(kBlock, WPS) void rx_tcp_kernel(const uint8_t* __restrict__ base,
                                                              const uint64_t* __restrict__ offsets, uint32_t n,
                                                              uint64_t* __restrict__ mask,
                                                              uint16_t* __restrict__ ip_raw,
-                                                             uint16_t* __restrict__ tcp_raw, int sets) {
+                                                             uint16_t* __restrict__ tcp_raw, int sets,
+                                                             uint32_t big_keep) {
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const __amdgpu_buffer_rsrc_t ofs = make_rsrc(offsets, ((uint64_t)n + 1) * 8);
@@ -1311,10 +1340,13 @@ __global__ __launch_bounds__(kBlock) void rx_tcp_kernel(const uint8_t* __restric
     // Byte-balanced wave ranges (as csum_ragged_scan_kernel), cut at multiples of 8 frames. Cut at whole mask
     // words (64 frames, ~50 KB) instead, a wave streamed up to one run more than the mean, and the launch
     // waited ~20 µs for those waves at any batch size.
+    // The grid is sized for small frames (4 blocks/CU); a batch of large ones streams on big_keep of them.
+    const uint32_t nb = active_blocks(ofs, n, kRxSmallFrame, big_keep);
+    if (blockIdx.x >= nb) return;
     uint32_t a0, a_end;
     uint64_t wave_bytes;
     {
-        const uint32_t nb = gridDim.x, b = blockIdx.x, W = nb * kWavesPerBlock;
+        const uint32_t b = blockIdx.x, W = nb * kWavesPerBlock;
         const uint32_t g = (nb >= 16 && (nb & 7) == 0) ? ((b & 7) * (nb >> 3) + (b >> 3)) * kWavesPerBlock + wave
                                                         : b * kWavesPerBlock + wave;
         const uint64_t o_lo = ld_off(ofs, 0), o_hi = ld_off(ofs, n);
@@ -1329,8 +1361,6 @@ __global__ __launch_bounds__(kBlock) void rx_tcp_kernel(const uint8_t* __restric
     if (small) {
         extern __shared__ lds16 lds_rx[];
         rx_runs_lds<R, V6>(base, ofs, n, a0, a_end, lane, lds_rx + wave * (kRxSlot / 16u), mrs, irs, trs);
-    } else if (sets == 4) {
-        rx_runs<R, V6, 4>(base, ofs, n, a0, a_end, lane, mrs, irs, trs);
     } else {
         rx_runs<R, V6, 1>(base, ofs, n, a0, a_end, lane, mrs, irs, trs);
     }
@@ -2499,7 +2529,11 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
     // force runs of four sets (4) or the LDS form (2; tests and A/B); 0: by mean segment size
     const int sets = c.segs_per_wave == 4 || c.segs_per_wave == 2 ? c.segs_per_wave : 0;
     const size_t lds = (size_t)kScanSlot * kWavesPerBlock;  // the LDS form's per-wave slots
-    const uint32_t mb = max_blocks_of(c, 2);
+    // Default grid: 4 blocks/CU, of which a batch of segments averaging ≥ 256 B uses 2 (active_blocks; config 3
+    // keeps its 2 blocks/CU). A blocks_per_cu override runs exactly that grid.
+    const bool pick = c.blocks_per_cu == 0 && pipe && rows == 2 && sets == 0;
+    const uint32_t mb = pick ? (uint32_t)c.cus * 4u : max_blocks_of(c, 2);
+    const uint32_t keep = pick ? 2u : 0u;
     for (uint64_t c0 = 0; c0 < n; c0 += kRaggedChunk) {
         const uint32_t cn = (uint32_t)(n - c0 < kRaggedChunk ? n - c0 : kRaggedChunk);
         const uint32_t grid = grid_for((cn + run * ns - 1) / (run * ns), mb);
@@ -2509,7 +2543,7 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
 #define NSX_RSCAN(R_, P_, NS_)                                                                                 \
         if (rows == R_ && pipe == P_ && ns == NS_)                                                              \
             hipLaunchKernelGGL((csum_ragged_scan_kernel<R_, VERIFY, P_, NS_>), dim3(grid), dim3(kBlock), lds, st,\
-                               base, offsets + c0, cn, pc, oc, kc, run, sets);
+                               base, offsets + c0, cn, pc, oc, kc, run, sets, keep);
         NSX_RSCAN(2, true, 1) NSX_RSCAN(4, true, 1) NSX_RSCAN(8, true, 1)
         NSX_RSCAN(4, false, 1) NSX_RSCAN(8, false, 1) NSX_RSCAN(16, false, 1)
         NSX_RSCAN(2, true, 2)
@@ -2544,23 +2578,29 @@ hipError_t launch_rx_tcp(const LaunchCfg& c, int ipver, const void* d_base, cons
     // at 4); launches of ≤ 2^27 frames (a multiple of 64, so every launch starts on a mask word)
     const int rows = (c.rows == 2 || c.rows == 4 || c.rows == 8 || c.rows == 16) ? c.rows : 2;
     // 64-frame sets per run: by each wave's mean frame size, or forced by segs_per_wave 1 / 4 (tests)
-    const int sets = c.segs_per_wave == 1 || c.segs_per_wave == 2 || c.segs_per_wave == 4 ? c.segs_per_wave : 0;
+    const int sets = c.segs_per_wave == 1 || c.segs_per_wave == 2 ? c.segs_per_wave : 0;
     const size_t lds = (size_t)kRxSlot * kWavesPerBlock;  // the LDS form's per-wave slots (3 blocks/CU: 100 KB)
-    const uint32_t mb = max_blocks_of(c, 3);
+    // Default grid: 4 blocks/CU with the register-capped instantiation (≤ 128 VGPRs, four waves per SIMD), of
+    // which a batch of frames averaging ≥ kRxSmallFrame uses 3 (active_blocks; workload 10 keeps its 3 blocks/CU).
+    // A blocks_per_cu override runs exactly that grid (the capped instantiation from 4 blocks/CU up).
+    const bool pick = c.blocks_per_cu == 0 && rows == 2 && sets == 0;
+    const uint32_t mb = pick ? (uint32_t)c.cus * 4u : max_blocks_of(c, 3);
+    const uint32_t keep = pick ? 3u : 0u;
+    const bool w4 = rows == 2 && mb >= (uint32_t)c.cus * 4u;
     const uint8_t* base = static_cast<const uint8_t*>(d_base);
     for (uint64_t c0 = 0; c0 < n; c0 += kRaggedChunk) {
         const uint32_t cn = (uint32_t)(n - c0 < kRaggedChunk ? n - c0 : kRaggedChunk);
         const uint32_t grid = grid_for((cn + kRxRun - 1) / kRxRun, mb);
         uint16_t* ic = ip_raw ? ip_raw + c0 : nullptr;
         uint16_t* tc = tcp_raw ? tcp_raw + c0 : nullptr;
-#define NSX_RX(R_)                                                                                                \
-        if (rows == R_ && ipver == 6)                                                                              \
-            hipLaunchKernelGGL((rx_tcp_kernel<R_, true>), dim3(grid), dim3(kBlock), lds, st, base, d_offsets + c0, cn,\
-                               mask + c0 / 64, nullptr, tc, sets);                                                       \
-        if (rows == R_ && ipver != 6)                                                                              \
-            hipLaunchKernelGGL((rx_tcp_kernel<R_, false>), dim3(grid), dim3(kBlock), lds, st, base, d_offsets + c0, cn,\
-                               mask + c0 / 64, ic, tc, sets);
-        NSX_RX(2) NSX_RX(4) NSX_RX(8) NSX_RX(16)
+#define NSX_RX(R_, W_)                                                                                            \
+        if (rows == R_ && w4 == (W_ == 4) && ipver == 6)                                                           \
+            hipLaunchKernelGGL((rx_tcp_kernel<R_, true, W_>), dim3(grid), dim3(kBlock), lds, st, base, d_offsets + c0, \
+                               cn, mask + c0 / 64, nullptr, tc, sets, keep);                                             \
+        if (rows == R_ && w4 == (W_ == 4) && ipver != 6)                                                           \
+            hipLaunchKernelGGL((rx_tcp_kernel<R_, false, W_>), dim3(grid), dim3(kBlock), lds, st, base,                \
+                               d_offsets + c0, cn, mask + c0 / 64, ic, tc, sets, keep);
+        NSX_RX(2, 1) NSX_RX(4, 1) NSX_RX(8, 1) NSX_RX(16, 1) NSX_RX(2, 4)
 #undef NSX_RX
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;

@@ -54,20 +54,21 @@ def test_rx_mixed_batches(n, lead):
 
 
 TUNES = [dict(rows=2), dict(rows=4), dict(rows=16), dict(blocks_per_cu=1), dict(blocks_per_cu=8), dict(rows=16, blocks_per_cu=1),
-         dict(segs_per_wave=4), dict(segs_per_wave=4, rows=4), dict(segs_per_wave=1),  # streamed runs of 4 / 1 frame sets
-         dict(segs_per_wave=2), dict(segs_per_wave=2, blocks_per_cu=1), dict(segs_per_wave=2, blocks_per_cu=8)]  # LDS form
+         dict(segs_per_wave=1), dict(segs_per_wave=1, rows=4), dict(segs_per_wave=1, blocks_per_cu=4),  # streamed runs
+         dict(segs_per_wave=2), dict(segs_per_wave=2, blocks_per_cu=1), dict(segs_per_wave=2, blocks_per_cu=4),
+         dict(segs_per_wave=2, blocks_per_cu=8), dict(blocks_per_cu=4)]  # LDS form; 4 blocks/CU = the capped kernel
 
 
 @pytest.mark.parametrize("n", [1, 255, 256, 257, 1000, 30_001])
 @pytest.mark.parametrize("lead", [0, 3])
 def test_rx_small_frames_runs_of_four_sets(n, lead):
     """Frames of at most 40 B of payload: waves whose frames average under 128 B take the LDS form (DESIGN.md §7
-    step 43); it, and the streamed runs of one and of four 64-frame sets (§7 step 41), equal the oracle at every
-    run boundary and partial last run."""
+    step 43); it, and the streamed runs of 64-frame sets, equal the oracle at every run boundary and partial last
+    run, at the default 4-blocks/CU grid and at 3."""
     rng = np.random.default_rng(n * 2 + lead)
     buf, offs, _ = _rx.batch(rng, n, lead=lead, max_payload=40)
     want = O.c_rx_ipv4_tcp(buf, offs)
-    for tune in (None, dict(segs_per_wave=1), dict(segs_per_wave=4), dict(segs_per_wave=2)):
+    for tune in (None, dict(segs_per_wave=1), dict(segs_per_wave=2), dict(blocks_per_cu=3)):
         got = run_rx(buf, offs, tune)
         for w, g, what in zip(want, got, ("mask", "ip_raw", "tcp_raw")):
             assert np.array_equal(w, g), (what, n, lead, tune)
@@ -99,10 +100,10 @@ def _device_frames(cfg, seed):
 
 @pytest.mark.parametrize("ipver", [4, 6])
 def test_rx_small_frames_300K_every_set_form_vs_oracle(ipver):
-    """~300K ACK-sized frames (40-100 B IPv4 / 60-120 B IPv6), enough that waves stream many
-    runs, so the four-set run form's sets 2 and 3, the cross-set frame ends and partial last sets all run. The
-    automatic choice and the forced one- and four-set forms, at the default grid and at one block per CU, against
-    the oracle's mask and raw sums on every frame."""
+    """~300K ACK-sized frames (40-100 B IPv4 / 60-120 B IPv6), enough that every wave walks
+    many runs of its form (the LDS form's run-to-run pipeline, its fallback-free loop, partial last runs). The
+    automatic choice and the forced streamed and LDS forms, at the default grid and at 1, 3 and 4 blocks per CU,
+    against the oracle's mask and raw sums on every frame."""
     cfg = dict(n=300_007, lo=40, hi=100, seed=0x5A11) if ipver == 4 else \
         dict(ipver=6, n=300_007, lo=60, hi=120, seed=0x5A16)
     w = _device_frames(cfg, cfg["seed"])
@@ -112,9 +113,9 @@ def test_rx_small_frames_300K_every_set_form_vs_oracle(ipver):
     want = O.c_rx_ipv4_tcp(buf_h, offs) if ipver == 4 else O.c_rx_ipv6_tcp(buf_h, offs)
     bits = np.unpackbits(want[0].view(np.uint8), bitorder="little")[:n]
     assert 0.85 * n < bits.sum() < 0.985 * n  # mostly valid, every kind of failure present
-    for tune in (None, dict(segs_per_wave=1), dict(segs_per_wave=4), dict(segs_per_wave=2), dict(blocks_per_cu=1),
-                 dict(blocks_per_cu=1, segs_per_wave=1), dict(blocks_per_cu=1, segs_per_wave=4),
-                 dict(blocks_per_cu=1, segs_per_wave=2)):
+    for tune in (None, dict(segs_per_wave=1), dict(segs_per_wave=2), dict(blocks_per_cu=1), dict(blocks_per_cu=3),
+                 dict(blocks_per_cu=1, segs_per_wave=1), dict(blocks_per_cu=1, segs_per_wave=2),
+                 dict(blocks_per_cu=4, segs_per_wave=1)):
         got = run_rx(buf_h, offs, tune) if ipver == 4 else run_rx6(buf_h, offs, tune)
         for wv, g, what in zip(want, got, ("mask", "ip_raw", "tcp_raw") if ipver == 4 else ("mask", "tcp_raw")):
             bad = np.nonzero(wv != g)[0]
