@@ -25,16 +25,17 @@ extern "C" {
 #define NSX_TUNE_KERNEL_HDR_DENSE     2  /* IPv4 headers: LDS-staged 64-header spans (stride <= 64) */
 #define NSX_TUNE_KERNEL_BUILD_PLAIN   2  /* TCP build: no software pipelining */
 #define NSX_TUNE_KERNEL_BUILD_GENERAL 3  /* TCP build: the general pipelined composition for every layout */
+#define NSX_TUNE_KERNEL_BUILD_BPERM   4  /* TCP build: fast path with header dwords pulled by ds_bpermute (A/B) */
 #define NSX_TUNE_KERNEL_SCAN_PLAIN    2  /* ragged scan: single row batches (rows 4, 8 or 16) */
 
 typedef struct nsx_tune {
     int32_t blocks_per_cu;     /* persistent grid: 1..8 blocks of 256 threads per CU. Default of the ragged
                                   scan and receive kernels: 4 per CU, of which a batch whose mean segment /
-                                  frame is >= 256 B / 128 B uses 2 / 3 (the rest return at once); a value
+                                  frame is >= 2048 B / 640 B uses 2 / 3 (the rest return at once); a value
                                   here runs exactly that grid */
     int32_t segs_per_wave;     /* fixed batches of <= 4 KiB segments: segments per wave task (1, 2, 4, 8).
                                   Ragged scan, per wave: 0 auto (the LDS form in waves whose segments
-                                  average < 128 B, streamed runs of four 63-segment sets < 256 B, else runs
+                                  average < 128 B, streamed runs of four 63-segment sets < 2048 B, else runs
                                   of two sets), 1 = runs of one set, 2 = the LDS form, 4 = runs of four sets
                                   in every wave. Only the default pipelined 2-row shape has more than one
                                   set: with kernel = SCAN_PLAIN or rows != 2 a 4 gives runs of one set.

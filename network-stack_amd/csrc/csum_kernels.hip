@@ -706,14 +706,20 @@ __device__ __forceinline__ void scan_span(const uint8_t* rbase, uint64_t span, u
         if (brel[k] >= (int64_t)(nrows * kRow)) bval[k] = carry;  // boundary at the very end of the rows
 }
 
-constexpr uint32_t kScanSmallSeg = 256;
-constexpr uint32_t kScanLdsSeg = 128;  // runs of 63 such segments fit the LDS form's 8 KiB slot
+// Ragged scan forms by mean segment size (tools/r03_sweep.sh, profiles/r03_grid_sweep.txt): per wave, the LDS form
+// under kScanLdsSeg (runs of 63 such segments fit its 8 KiB slot), runs of four 63-segment sets under
+// kScanSmallSeg, else runs of two sets; per batch, 4 blocks/CU under kScanBigMean, else 2.
+constexpr uint32_t kScanSmallSeg = 2048;
+constexpr uint32_t kScanLdsSeg = 128;
+constexpr uint32_t kScanBigMean = 2048;
 
 // Blocks of this launch that take work. The persistent grids of the ragged scan and the receive pass are sized for
 // small units (4 blocks/CU: every wave's rows in flight count when each unit costs a header check or an LDS
 // sum); a batch whose mean unit is at least `big_mean` bytes streams best on fewer waves (config 3 at 2 blocks/CU
-// 2.7% faster than at 4, workload 10 at 3 blocks/CU 2.8% faster), so only its first ⌊gridDim·keep/4⌋ blocks
-// (rounded to the 8 XCDs) take byte ranges and the rest return at once. keep = 0: every block.
+// 3% faster than at 4, workload 10 at 3 blocks/CU 2.9% faster), so only its first
+// ⌊gridDim·keep/4⌋ blocks (rounded to the 8 XCDs) take byte ranges and the rest return at once. keep = 0: every
+// block. (Blocks are dealt to CUs breadth-first, so the first 3/4 of a 4-per-CU grid is 3 per CU: workload 10 ran
+// within 0.4% of a 3-per-CU launch.)
 __device__ __forceinline__ uint32_t active_blocks(__amdgpu_buffer_rsrc_t ofs, uint32_t n, uint32_t big_mean,
                                                   uint32_t keep) {
     const uint32_t nb = gridDim.x;
@@ -939,7 +945,7 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
     const __amdgpu_buffer_rsrc_t ors = make_rsrc(out, out ? (uint64_t)n * 2 : 0);
     const __amdgpu_buffer_rsrc_t oks = make_rsrc(ok, VERIFY ? (uint64_t)n : 0);
     // The grid is sized for small segments (4 blocks/CU); a batch of large ones streams on big_keep of them.
-    const uint32_t nb = active_blocks(ofs, n, kScanSmallSeg, big_keep);
+    const uint32_t nb = active_blocks(ofs, n, kScanBigMean, big_keep);
     if (blockIdx.x >= nb) return;
     // The wave's tasks are runs of NS sets [a_k, a_k + cnt_k) of ≤ run segments each (a_k = a + k·run), a = a0,
     // a0 + NS·run, ... < a_end; a run never crosses a_end. Byte-balanced: wave g (XCD-contiguous numbering) owns
@@ -1018,10 +1024,13 @@ __device__ __forceinline__ void rx_store_mask(__amdgpu_buffer_rsrc_t mrs, uint64
 // window is only the first 8 bytes (one 16 B load per lane).
 //
 // NS: 64-frame sets per run (one stream, one boundary slot per set and lane). Runs of one set suit the bench's
-// 40-1500 B frames (~50 KB per run; two sets ran 7.6% slower); a wave whose frames average
-// under kRxSmallFrame bytes takes runs of four sets, so that small frames do not pay a pipeline fill and drain
-// per few KB (§7 step 41).
+// 40-1500 B frames (~50 KB per run; two sets ran 7.6% slower). A wave whose frames average
+// under kRxSmallFrame bytes takes the LDS form instead (rx_runs_lds, §7 step 43), which replaced round 2's runs of
+// four sets (§7 step 41).
 constexpr uint32_t kRxSmallFrame = 128;
+// 4 blocks/CU for batches whose mean frame is under kRxBigMean, else 3 (tools/r03_sweep.sh: 4 blocks 9% faster at a
+// 170 B mean, 3.4% at 320 B, 0.4% at 520 B; 3 blocks 2.9% faster at workload 10's 770 B)
+constexpr uint32_t kRxBigMean = 640;
 
 // Per-frame verdict of the receive pass, shared by the streaming and the LDS forms. F = the frame's weighted byte
 // sum (exact; weights 1 / 256 at even / odd addresses, the LE half-sum rule); d[0..5] = the dwords from the
@@ -1341,7 +1350,7 @@ __global__ __launch_bounds__(kBlock, WPS) void rx_tcp_kernel(const uint8_t* __re
     // words (64 frames, ~50 KB) instead, a wave streamed up to one run more than the mean, and the launch
     // waited ~20 µs for those waves at any batch size.
     // The grid is sized for small frames (4 blocks/CU); a batch of large ones streams on big_keep of them.
-    const uint32_t nb = active_blocks(ofs, n, kRxSmallFrame, big_keep);
+    const uint32_t nb = active_blocks(ofs, n, kRxBigMean, big_keep);
     if (blockIdx.x >= nb) return;
     uint32_t a0, a_end;
     uint64_t wave_bytes;
@@ -1626,7 +1635,7 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
         // in flight through its own header/sum/store phases (tools/probes/copy_layout.hip seg_swp vs seg).
         const bool mfast = (mhdr & 3u) == 0 && (mdb & 3u) == 0 && mdb >= mhdr && (mwire & 3u) == 0 &&
                            mwire <= 2u * kRow;
-        if (pipe == 1 && (!OPT || staged) && __builtin_amdgcn_ballot_w64(!(mfast || lane >= cnt)) == 0) {
+        if ((pipe == 1 || pipe == 3) && (!OPT || staged) && __builtin_amdgcn_ballot_w64(!(mfast || lane >= cnt)) == 0) {
             struct Rows {
                 u32x4 v[PS][2];
             };
@@ -1649,20 +1658,33 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
                     const uint32_t kk = k0 + e;
                     if (kk >= cnt) break;  // wave-uniform
                     BuildSeg S;
-                    S.D0 = __builtin_amdgcn_readlane(mD0, kk);
-                    S.D1 = __builtin_amdgcn_readlane(mD1, kk);
-                    S.D2 = __builtin_amdgcn_readlane(mD2, kk);
-                    S.D3 = __builtin_amdgcn_readlane(mD3, kk);
-                    S.D4 = __builtin_amdgcn_readlane(mD4, kk);
                     const uint32_t nb4 = __builtin_amdgcn_readlane(mwire, kk);
                     const __amdgpu_buffer_rsrc_t ors = make_rsrc(out + readlane64(moo, kk), nb4);
                     u32x4 x = F.v[e][0];
                     if (OPT)  // image dwords [5, hdr/4): options and padding, not the source bytes under them
                         x = staged_opts<true>(od, kk, (__builtin_amdgcn_readlane(mhdr, kk) - 20u) >> 2, lane, x);
-                    x.x = lane == 0 ? S.D0 : (lane == 1 ? S.D4 : x.x);
-                    x.y = lane == 0 ? S.D1 : x.y;
-                    x.z = lane == 0 ? S.D2 : x.z;
-                    x.w = lane == 0 ? S.D3 : x.w;
+                    if (pipe == 3) {
+                        // VERDICT r2 item 5, tried: the header dwords D0-D3 of segment kk pulled from lane kk by
+                        // ds_bpermute instead of four v_readlane broadcasts and their scalar copies (D4 stays a
+                        // readlane: the field's dword is needed as a scalar below)
+                        S.D4 = __builtin_amdgcn_readlane(mD4, kk);
+                        const uint32_t h0 = bperm(mD0, kk), h1 = bperm(mD1, kk);
+                        const uint32_t h2 = bperm(mD2, kk), h3 = bperm(mD3, kk);
+                        x.x = lane == 0 ? h0 : (lane == 1 ? S.D4 : x.x);
+                        x.y = lane == 0 ? h1 : x.y;
+                        x.z = lane == 0 ? h2 : x.z;
+                        x.w = lane == 0 ? h3 : x.w;
+                    } else {
+                        S.D0 = __builtin_amdgcn_readlane(mD0, kk);
+                        S.D1 = __builtin_amdgcn_readlane(mD1, kk);
+                        S.D2 = __builtin_amdgcn_readlane(mD2, kk);
+                        S.D3 = __builtin_amdgcn_readlane(mD3, kk);
+                        S.D4 = __builtin_amdgcn_readlane(mD4, kk);
+                        x.x = lane == 0 ? S.D0 : (lane == 1 ? S.D4 : x.x);
+                        x.y = lane == 0 ? S.D1 : x.y;
+                        x.z = lane == 0 ? S.D2 : x.z;
+                        x.w = lane == 0 ? S.D3 : x.w;
+                    }
                     const u32x4 y = F.v[e][1];  // row 1: zeros past the image (range check), stores clipped likewise
                     const uint32_t raw = seg_raw(kk, fold32(sad4(y, sad4(x, 0u))));
                     // both rows leave once the sum is known, one store each: dword 4 (lane 1's first) carries the
@@ -2529,8 +2551,8 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
     // force runs of four sets (4) or the LDS form (2; tests and A/B); 0: by mean segment size
     const int sets = c.segs_per_wave == 4 || c.segs_per_wave == 2 ? c.segs_per_wave : 0;
     const size_t lds = (size_t)kScanSlot * kWavesPerBlock;  // the LDS form's per-wave slots
-    // Default grid: 4 blocks/CU, of which a batch of segments averaging ≥ 256 B uses 2 (active_blocks; config 3
-    // keeps its 2 blocks/CU). A blocks_per_cu override runs exactly that grid.
+    // Default grid: 4 blocks/CU, of which a batch of segments averaging ≥ kScanBigMean uses 2 (active_blocks;
+    // config 3 keeps its 2 blocks/CU). A blocks_per_cu override runs exactly that grid.
     const bool pick = c.blocks_per_cu == 0 && pipe && rows == 2 && sets == 0;
     const uint32_t mb = pick ? (uint32_t)c.cus * 4u : max_blocks_of(c, 2);
     const uint32_t keep = pick ? 2u : 0u;
@@ -2581,7 +2603,7 @@ hipError_t launch_rx_tcp(const LaunchCfg& c, int ipver, const void* d_base, cons
     const int sets = c.segs_per_wave == 1 || c.segs_per_wave == 2 ? c.segs_per_wave : 0;
     const size_t lds = (size_t)kRxSlot * kWavesPerBlock;  // the LDS form's per-wave slots (3 blocks/CU: 100 KB)
     // Default grid: 4 blocks/CU with the register-capped instantiation (≤ 128 VGPRs, four waves per SIMD), of
-    // which a batch of frames averaging ≥ kRxSmallFrame uses 3 (active_blocks; workload 10 keeps its 3 blocks/CU).
+    // which a batch of frames averaging ≥ kRxBigMean uses 3 (active_blocks; workload 10 keeps its 3 blocks/CU).
     // A blocks_per_cu override runs exactly that grid (the capped instantiation from 4 blocks/CU up).
     const bool pick = c.blocks_per_cu == 0 && rows == 2 && sets == 0;
     const uint32_t mb = pick ? (uint32_t)c.cus * 4u : max_blocks_of(c, 3);
@@ -2669,7 +2691,7 @@ hipError_t launch_tcp_build(const LaunchCfg& c, const TcpHdrSoA& h, const uint8_
     const uint64_t tasks = (n + group - 1) / group;
     const uint32_t grid = grid_for(tasks, max_blocks);
     const uint32_t clog = deal_clog(c.xcd_chunk, tasks, (uint64_t)group * 2u * wire);  // payload + image per segment
-    const int pipe = c.kernel == 2 ? 0 : c.kernel == 3 ? 2 : 1;
+    const int pipe = c.kernel == 2 ? 0 : c.kernel == 3 ? 2 : c.kernel == 4 ? 3 : 1;
     if (opt_off)
         hipLaunchKernelGGL((tcp_build_kernel<0, 0, 2, true>), dim3(grid), dim3(kBlock), 0, st, h, opts, opt_off, data,
                            data_off, data_bytes, partial, n, out, out_off, raw, group, clog, pipe);

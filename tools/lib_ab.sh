@@ -2,7 +2,7 @@
 # Same-box A/B of two library builds, for changes a tune field cannot switch: the working tree's library
 # against one built from a git ref, in alternating processes (tools/ab.py per workload, default launch shape).
 #
-#   bash tools/lib_ab.sh build [ref]          # here (CPU): builds <ref> (default HEAD) into lib_ab/libnsx_csum.so
+#   bash tools/lib_ab.sh build [ref]          # here (CPU): builds <ref> (default HEAD) into network-stack_amd/lib_base/libnsx_csum.so
 #   bash tools/lib_ab.sh run "10 11" [pairs]  # on the GPU box: new, base, new, base, ... for each workload
 #
 # Both builds share include/ and the ABI of the working tree; only use it for kernel-internal changes.
@@ -14,10 +14,10 @@ case "${1:-}" in
     tmp=$(mktemp -d)
     git archive "$ref" include network-stack_amd | tar -x -C "$tmp"
     make -s -C "$tmp/network-stack_amd" -j8 lib/libnsx_csum.so
-    mkdir -p lib_ab
-    cp "$tmp/network-stack_amd/lib/libnsx_csum.so" lib_ab/libnsx_csum.so
+    mkdir -p network-stack_amd/lib_base
+    cp "$tmp/network-stack_amd/lib/libnsx_csum.so" network-stack_amd/lib_base/libnsx_csum.so
     rm -rf "$tmp"
-    echo "lib_ab/libnsx_csum.so built from $(git rev-parse --short "$ref")"
+    echo "network-stack_amd/lib_base/libnsx_csum.so built from $(git rev-parse --short "$ref")"
     ;;
   run)
     configs=${2:-2}
@@ -27,7 +27,7 @@ case "${1:-}" in
     trap 'cp /tmp/lib_ab_new.so "$lib"' EXIT
     for ((i = 0; i < pairs; i++)); do
       for k in new base; do
-        if [ "$k" = base ]; then cp lib_ab/libnsx_csum.so "$lib"; else cp /tmp/lib_ab_new.so "$lib"; fi
+        if [ "$k" = base ]; then cp network-stack_amd/lib_base/libnsx_csum.so "$lib"; else cp /tmp/lib_ab_new.so "$lib"; fi
         for c in $configs; do
           timeout -k 10 200 python tools/ab.py --config "$c" --variants "$k:" --rounds 5 2>/dev/null | grep AB
         done
