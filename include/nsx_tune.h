@@ -25,7 +25,6 @@ extern "C" {
 #define NSX_TUNE_KERNEL_HDR_DENSE     2  /* IPv4 headers: LDS-staged 64-header spans (stride <= 64) */
 #define NSX_TUNE_KERNEL_BUILD_PLAIN   2  /* TCP build: no software pipelining */
 #define NSX_TUNE_KERNEL_BUILD_GENERAL 3  /* TCP build: the general pipelined composition for every layout */
-#define NSX_TUNE_KERNEL_BUILD_BPERM   4  /* TCP build: fast path with header dwords pulled by ds_bpermute (A/B) */
 #define NSX_TUNE_KERNEL_SCAN_PLAIN    2  /* ragged scan: single row batches (rows 4, 8 or 16) */
 
 typedef struct nsx_tune {

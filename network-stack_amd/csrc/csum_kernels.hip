@@ -205,6 +205,8 @@ __device__ __forceinline__ uint32_t keep_mask(int32_t lo_r, int32_t hi_r, int32_
 }
 
 constexpr uint32_t kOOB = 0x80000000u;  // voffset that is always out of range (num_records < 2^31)
+// s_waitcnt operand (gfx9 encoding): vmcnt(0), expcnt and lgkmcnt left at their maxima (no wait)
+constexpr int kWaitVm0 = 0x0F70;
 // Cache-policy operand of a buffer store on gfx950: sc1 (bit 4) = write-through, the line leaves the XCD's L2.
 constexpr int kStoreSc1 = 16;
 
@@ -807,35 +809,72 @@ __device__ __forceinline__ void ragged_runs(const uint8_t* __restrict__ base, __
     }
 }
 
-// Sum of the bytes [p, e) of a wave's LDS slot (p, e slot positions; e - p < 2^15): the 16 B chunks [p/16,
-// ceil(e/16)) whole, eight reads in flight per lane, minus the bytes before p in the first chunk and from e on in
-// the last. The weighted byte sum of the range (LE half-sums of its 4-aligned dwords, as in scan_span): the slot
-// keeps every byte's address mod 128.
-__device__ __forceinline__ uint32_t lds_range_sum(const lds16* slot, uint32_t p, uint32_t e) {
+// Sum of the bytes [p, e) of a wave's LDS slot for the lanes' consecutive ranges of one run (p, e slot positions;
+// e - p < 2^15): lane l's range ends where lane l + 1's begins (e_l = p_{l+1}), lanes past the run have live =
+// false, and the slot's bytes from the run's end up to the next 16 B boundary are 0 (lds_zero_tail). dq = the slot
+// dword holding byte p. The weighted byte sum of the range (LE half-sums of its 4-aligned dwords, as in
+// scan_span): the slot keeps every byte's address mod 128.
+//
+// The 16 B chunks [p/16, ceil(e/16)) are summed whole, eight reads in flight per lane, minus
+//   head = the first chunk's bytes before p: the v_sad_u16 chain that sums that chunk yields its dword prefix
+//          sums, so head = prefix(p/4 mod 4) + the low p mod 4 bytes of dq — no byte masks;
+//   tail = the last chunk's bytes from e on = lane l + 1's first-chunk bytes from p_{l+1} = e on (one DPP shift
+//          across the wave), or 0 when e is a multiple of 16; the last lane of the run gets 0 from a lane past
+//          it (or past the wave), which is right because the bytes after the run's end are 0.
+// (Round-3 first form: both ends masked byte-wise with keep_bytes, ~56 VALU per run)
+__device__ __forceinline__ uint32_t lds_range_sum(const lds16* slot, uint32_t p, uint32_t e, uint32_t dq, bool live) {
     const uint32_t c0 = p >> 4, c1 = (e + 15u) >> 4, nch = c1 - c0;
-    const uint32_t clast = nch ? nch - 1u : 0u;
     // Blocks of 8 chunks, a wave-uniform trip count from the wave's longest range (an SGPR loop counter: a loop
     // ending on a ballot left hipcc an undefined exit value that it read with v_readfirstlane from a register
     // still being loaded — a vmcnt wait that drained the next run's rows before this run's sums began). A block
     // reads chunks c0 + j0 .. c0 + j0 + 7 unclamped (one address, immediate offsets; the slot's pad keeps the
-    // reads past its last chunk inside it) and keeps those below nch.
+    // reads past its last chunk inside it) and keeps those below nch. The first block is always read (its first
+    // chunk gives head and the neighbour's tail even for an empty range).
     const uint32_t nblk = wave_max((nch + 7u) >> 3);
-    uint32_t acc = 0, head_x = 0;
-    for (uint32_t j0 = 0; j0 < nblk * 8u; j0 += 8u) {
+    uint32_t acc;
+    {
+        u32x4 x[8];
+        const lds16* blk = slot + c0;
+#pragma unroll
+        for (uint32_t j = 0; j < 8u; ++j) x[j] = lds_get(blk, j);
+        const uint32_t pre1 = __builtin_amdgcn_sad_u16(x[0].x, 0u, 0u);
+        const uint32_t pre2 = __builtin_amdgcn_sad_u16(x[0].y, 0u, pre1);
+        const uint32_t pre3 = __builtin_amdgcn_sad_u16(x[0].z, 0u, pre2);
+        const uint32_t s0 = __builtin_amdgcn_sad_u16(x[0].w, 0u, pre3);
+        const uint32_t q = (p >> 2) & 3u;
+        const uint32_t pq = q == 0u ? 0u : q == 1u ? pre1 : q == 2u ? pre2 : pre3;
+        const uint32_t head = __builtin_amdgcn_sad_u16(dq & ((1u << (8u * (p & 3u))) - 1u), 0u, pq);
+        const uint32_t g = live ? s0 - head : 0u;  // this lane's first-chunk bytes from p on
+        const uint32_t gn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)g, 0x130, 0xF, 0xF, false);  // wave_shl:1
+        const uint32_t tail = (e & 15u) ? gn : 0u;
+        acc = (nch ? s0 : 0u) - tail - head;  // an empty range (nch = 0) starts 16-aligned: head = tail = 0
+#pragma unroll
+        for (uint32_t j = 1; j < 8u; ++j) {
+            const uint32_t s4 = sad4(x[j], 0u);
+            acc += j < nch ? s4 : 0u;
+        }
+    }
+    for (uint32_t j0 = 8; j0 < nblk * 8u; j0 += 8u) {
         u32x4 x[8];
         const lds16* blk = slot + c0 + j0;
 #pragma unroll
         for (uint32_t j = 0; j < 8u; ++j) x[j] = lds_get(blk, j);
-        if (j0 == 0) head_x = sad4(keep_bytes(x[0], 0, (int32_t)(p & 15u)), 0u);
 #pragma unroll
         for (uint32_t j = 0; j < 8u; ++j) {
             const uint32_t s4 = sad4(x[j], 0u);
             acc += j0 + j < nch ? s4 : 0u;
         }
     }
-    const uint32_t t = e - (c1 - 1u) * 16u;  // bytes of the last chunk inside the range, 1..16 (nch > 0)
-    const uint32_t tail_x = nch ? sad4(keep_bytes(lds_get(slot, c0 + clast), (int32_t)t, 16), 0u) : 0u;
-    return acc - (nch ? head_x : 0u) - tail_x;
+    return acc;
+}
+
+// Zero the slot's bytes [span, 4·ceil(span/4)) after lds_stage: the bytes of the run's last dword past its end (the
+// row loads read whole dwords; from there on to the 16 B boundary they already read 0), so lds_range_sum's last
+// range needs no tail.
+__device__ __forceinline__ void lds_zero_tail(lds16* slot, uint64_t span, uint32_t lane) {
+    const uint32_t z = (uint32_t)span, k = (4u - (z & 3u)) & 3u;
+    if (lane < k) reinterpret_cast<uint8_t*>(slot)[z + lane] = 0;
+    __builtin_amdgcn_wave_barrier();
 }
 
 // Stage the rows [0, span) of a run into the wave's slot (rows already loaded into V, all in flight; only the
@@ -909,9 +948,11 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
         }
         issue(cur);
         uint64_t n_off = load_offs(a + run);
+        __builtin_amdgcn_s_waitcnt(kWaitVm0);  // as in rx_runs_lds: nothing in flight at the loop's entry
         for (;;) {
             const uint32_t part = __builtin_amdgcn_raw_buffer_load_b32(prs, lane < cur.cnt ? (a + lane) * 4 : kOOB, 0, 0);
             lds_stage<kScanSlotRows>(slot, V, cur.span, lane);
+            lds_zero_tail(slot, cur.span, lane);
             Run nxt = geo(a + run, n_off);
             if (!nxt.lds) nxt.span = 0;  // a run that will be streamed is not staged: empty loads
             issue(nxt);
@@ -921,7 +962,8 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
             const bool mine = lane < cur.cnt;
             const uint32_t p = mine ? (uint32_t)((base + c_off) - cur.rbase) : 0u;
             const uint32_t e = mine ? (uint32_t)((base + e_off) - cur.rbase) : 0u;
-            const uint32_t res = finish(fold32(lds_range_sum(slot, p, e)), (p & 1u) == 0, part);
+            const uint32_t dq = reinterpret_cast<const uint32_t*>(slot)[p >> 2];
+            const uint32_t res = finish(fold32(lds_range_sum(slot, p, e, dq, mine)), (p & 1u) == 0, part);
             __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, mine ? (a + lane) * 2 : kOOB, 0, 0);
             if constexpr (VERIFY)
                 __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(res == 0xFFFFu), oks, mine ? a + lane : kOOB, 0, 0);
@@ -1047,10 +1089,9 @@ __device__ __forceinline__ void rx_frame_out(uint64_t F, const uint32_t (&d)[6],
         const uint32_t plen = bswap16u(H1 & 0xFFFFu);
         const bool well = live && flen >= 40u && (H0 & 0xF0u) == 0x60u && plen + 40u == flen &&
                           ((H1 >> 16) & 0xFFu) == 6u && plen >= 20u;  // tcp.go:131
-        uint32_t h8 = 0;
-#pragma unroll
-        for (int j = 0; j < 3; ++j)
-            h8 = __builtin_amdgcn_sad_u16(d[j] & keep_mask((int32_t)hd, (int32_t)(hd + 8u), 4 * j), 0u, h8);
+        const uint32_t rot = hd & 1u;  // see the IPv4 header sum below
+        const uint32_t h8 = __builtin_amdgcn_sad_u16(__builtin_amdgcn_alignbyte(H1, H1, rot), 0u,
+                                                     __builtin_amdgcn_sad_u16(__builtin_amdgcn_alignbyte(H0, H0, rot), 0u, 0u));
         const uint64_t T = F - h8;  // addresses ‖ segment
         const uint32_t tle = fold32((uint32_t)T) + fold32((uint32_t)(T >> 32));
         const uint32_t tcpr = well ? finish(tle, even, plen + 6u) : 0u;
@@ -1071,23 +1112,34 @@ __device__ __forceinline__ void rx_frame_out(uint64_t F, const uint32_t (&d)[6],
         const bool hdr_ok = live && flen >= 20u && ihl >= 5u && hlen <= flen;
         const bool well = hdr_ok && (H0 & 0xF0u) == 0x40u && total == flen && (frag & 0x3FFFu) == 0u &&
                           proto == 6u && total - hlen >= 20u;  // tcp.go:131: a segment is at least 20 bytes
-        // Header sum over window bytes [hd, hd + hlen): dwords 0..5 always, 6..15 when some lane has options.
-        uint32_t hs = 0;
-#pragma unroll
-        for (int j = 0; j < 6; ++j)
-            hs = __builtin_amdgcn_sad_u16(d[j] & keep_mask((int32_t)hd, (int32_t)(hd + hlen), 4 * j), 0u, hs);
+        // Header sum over bytes [start, start + hlen), hlen = 4·IHL: the frame-relative dwords H_j, j < IHL, whole.
+        // F weights bytes by address parity (the LE half-sum rule), so for an odd start each H_j is rotated one
+        // byte before its v_sad_u16 (the halves then pair byte 1 with 2 and 3 with 0): no byte masks (round 2's
+        // keep_mask per window dword cost ~45 VALU per frame set).
+        const uint32_t rot = hd & 1u;
+        auto hsum = [&](uint32_t h, uint32_t acc) {
+            return __builtin_amdgcn_sad_u16(__builtin_amdgcn_alignbyte(h, h, rot), 0u, acc);
+        };
+        uint32_t hs = hsum(H4, hsum(H3, hsum(H2, hsum(H1, hsum(H0, 0u)))));
         if (__builtin_amdgcn_ballot_w64(hdr_ok && ihl > 5u)) {  // option dwords 6..15
             uint32_t o[10];
             opt(o);
+            uint32_t lo = d[5];
 #pragma unroll
-            for (int j = 6; j < 16; ++j)
-                hs = __builtin_amdgcn_sad_u16(o[j - 6] & keep_mask((int32_t)hd, (int32_t)(hd + hlen), 4 * j), 0u, hs);
+            for (int j = 5; j < 15; ++j) {  // H_j = window bytes hd + 4j .. hd + 4j + 3
+                const uint32_t hj = __builtin_amdgcn_alignbyte(o[j - 5], lo, hd);
+                hs = (uint32_t)j < ihl ? hsum(hj, hs) : hs;
+                lo = o[j - 5];
+            }
         }
         const uint32_t ipr = hdr_ok ? finish(hs, even, 0u) : 0u;
         const uint64_t T = F - (hdr_ok ? hs : 0u);  // the TCP segment's weighted sum
         const uint32_t tle = fold32((uint32_t)T) + fold32((uint32_t)(T >> 32));
-        const uint32_t pseudo = bswap16u(H3 & 0xFFFFu) + bswap16u(H3 >> 16) + bswap16u(H4 & 0xFFFFu) +
-                                bswap16u(H4 >> 16) + 6u + ((total - hlen) & 0xFFFFu);
+        // Pseudo-header source and destination (header dwords 3-4) as BE words: Σ bswap16(half) = the v_sad_u16
+        // of the dword rotated one byte.
+        const uint32_t pseudo = __builtin_amdgcn_sad_u16(
+            __builtin_amdgcn_alignbyte(H4, H4, 1u), 0u,
+            __builtin_amdgcn_sad_u16(__builtin_amdgcn_alignbyte(H3, H3, 1u), 0u, 6u + ((total - hlen) & 0xFFFFu)));
         const uint32_t tcpr = well ? finish(tle, even, pseudo) : 0u;
         const uint64_t bits = __builtin_amdgcn_ballot_w64(well && ipr == 0xFFFFu && tcpr == 0xFFFFu);
         rx_store_mask(mrs, bits, ak, cnt, n, lane);
@@ -1249,7 +1301,7 @@ __device__ __forceinline__ void rx_run_lds(const uint8_t* __restrict__ base, con
 #pragma unroll
     for (int j = 0; j < (V6 ? 3 : 6); ++j) d[j] = sdw[w0 + j];
     if constexpr (V6) d[3] = d[4] = d[5] = 0u;
-    const uint64_t F = lds_range_sum(slot, p, e);  // the frame's weighted sum
+    const uint64_t F = lds_range_sum(slot, p, e, d[0], live);  // the frame's weighted sum
     auto opt = [&](uint32_t (&o)[10]) {
 #pragma unroll
         for (int j = 6; j < 16; ++j) o[j - 6] = sdw[w0 + j];
@@ -1310,8 +1362,14 @@ __device__ __forceinline__ void rx_runs_lds(const uint8_t* __restrict__ base, __
         uint32_t an = a + kRxRun;
         uint64_t n_off = load_off(an + lane, an < a_end && an + lane <= n);
         uint64_t n_end = load_off(an + lane + 1u, an < a_end && an + lane + 1u <= n);
+        // Enter the loop with nothing in flight (the first run's rows and offsets are read at its head anyway). With
+        // them pending, hipcc's wait-count pass merged the entry edge into the loop head and waited vmcnt(0) in
+        // every iteration before reading the next run's offsets — a wait on the previous run's result stores,
+        // ahead of the next run's row loads.
+        __builtin_amdgcn_s_waitcnt(kWaitVm0);
         for (;;) {
             lds_stage<kRxSlotRows>(slot, V, cur.span, lane);
+            lds_zero_tail(slot, cur.span, lane);
             Run nxt = geo(an, n_off, n_end);
             if (!nxt.lds) nxt.span = 0;  // the rows of a run that will be streamed are not staged: empty loads
             issue(nxt);
@@ -1635,7 +1693,7 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
         // in flight through its own header/sum/store phases (tools/probes/copy_layout.hip seg_swp vs seg).
         const bool mfast = (mhdr & 3u) == 0 && (mdb & 3u) == 0 && mdb >= mhdr && (mwire & 3u) == 0 &&
                            mwire <= 2u * kRow;
-        if ((pipe == 1 || pipe == 3) && (!OPT || staged) && __builtin_amdgcn_ballot_w64(!(mfast || lane >= cnt)) == 0) {
+        if (pipe == 1 && (!OPT || staged) && __builtin_amdgcn_ballot_w64(!(mfast || lane >= cnt)) == 0) {
             struct Rows {
                 u32x4 v[PS][2];
             };
@@ -1663,28 +1721,17 @@ __global__ __launch_bounds__(kBlock) void tcp_build_kernel(TcpHdrSoA h, const ui
                     u32x4 x = F.v[e][0];
                     if (OPT)  // image dwords [5, hdr/4): options and padding, not the source bytes under them
                         x = staged_opts<true>(od, kk, (__builtin_amdgcn_readlane(mhdr, kk) - 20u) >> 2, lane, x);
-                    if (pipe == 3) {
-                        // VERDICT r2 item 5, tried: the header dwords D0-D3 of segment kk pulled from lane kk by
-                        // ds_bpermute instead of four v_readlane broadcasts and their scalar copies (D4 stays a
-                        // readlane: the field's dword is needed as a scalar below)
-                        S.D4 = __builtin_amdgcn_readlane(mD4, kk);
-                        const uint32_t h0 = bperm(mD0, kk), h1 = bperm(mD1, kk);
-                        const uint32_t h2 = bperm(mD2, kk), h3 = bperm(mD3, kk);
-                        x.x = lane == 0 ? h0 : (lane == 1 ? S.D4 : x.x);
-                        x.y = lane == 0 ? h1 : x.y;
-                        x.z = lane == 0 ? h2 : x.z;
-                        x.w = lane == 0 ? h3 : x.w;
-                    } else {
-                        S.D0 = __builtin_amdgcn_readlane(mD0, kk);
-                        S.D1 = __builtin_amdgcn_readlane(mD1, kk);
-                        S.D2 = __builtin_amdgcn_readlane(mD2, kk);
-                        S.D3 = __builtin_amdgcn_readlane(mD3, kk);
-                        S.D4 = __builtin_amdgcn_readlane(mD4, kk);
-                        x.x = lane == 0 ? S.D0 : (lane == 1 ? S.D4 : x.x);
-                        x.y = lane == 0 ? S.D1 : x.y;
-                        x.z = lane == 0 ? S.D2 : x.z;
-                        x.w = lane == 0 ? S.D3 : x.w;
-                    }
+                    // header dwords broadcast from lane kk (pulling D0-D3 with ds_bpermute instead measured equal,
+                    // DESIGN.md §7 step 46)
+                    S.D0 = __builtin_amdgcn_readlane(mD0, kk);
+                    S.D1 = __builtin_amdgcn_readlane(mD1, kk);
+                    S.D2 = __builtin_amdgcn_readlane(mD2, kk);
+                    S.D3 = __builtin_amdgcn_readlane(mD3, kk);
+                    S.D4 = __builtin_amdgcn_readlane(mD4, kk);
+                    x.x = lane == 0 ? S.D0 : (lane == 1 ? S.D4 : x.x);
+                    x.y = lane == 0 ? S.D1 : x.y;
+                    x.z = lane == 0 ? S.D2 : x.z;
+                    x.w = lane == 0 ? S.D3 : x.w;
                     const u32x4 y = F.v[e][1];  // row 1: zeros past the image (range check), stores clipped likewise
                     const uint32_t raw = seg_raw(kk, fold32(sad4(y, sad4(x, 0u))));
                     // both rows leave once the sum is known, one store each: dword 4 (lane 1's first) carries the
@@ -2691,7 +2738,7 @@ hipError_t launch_tcp_build(const LaunchCfg& c, const TcpHdrSoA& h, const uint8_
     const uint64_t tasks = (n + group - 1) / group;
     const uint32_t grid = grid_for(tasks, max_blocks);
     const uint32_t clog = deal_clog(c.xcd_chunk, tasks, (uint64_t)group * 2u * wire);  // payload + image per segment
-    const int pipe = c.kernel == 2 ? 0 : c.kernel == 3 ? 2 : c.kernel == 4 ? 3 : 1;
+    const int pipe = c.kernel == 2 ? 0 : c.kernel == 3 ? 2 : 1;
     if (opt_off)
         hipLaunchKernelGGL((tcp_build_kernel<0, 0, 2, true>), dim3(grid), dim3(kBlock), 0, st, h, opts, opt_off, data,
                            data_off, data_bytes, partial, n, out, out_off, raw, group, clog, pipe);

@@ -22,7 +22,6 @@ HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "
 NSX_OK, NSX_EIO, NSX_ENOMEM, NSX_ENODEV, NSX_EINVAL = 0, -5, -12, -19, -22
 # nsx_tune.kernel (include/nsx_tune.h)
 KERNEL_HDR_THREAD, KERNEL_HDR_DENSE, KERNEL_BUILD_PLAIN, KERNEL_BUILD_GENERAL, KERNEL_SCAN_PLAIN = 1, 2, 2, 3, 2
-KERNEL_BUILD_BPERM = 4
 
 
 class Tune(ctypes.Structure):

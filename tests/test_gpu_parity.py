@@ -735,7 +735,7 @@ def test_tcp_build_uniform_batches(P, n):
     for lead in (20, 28, 0):  # lead 0: segment 0 has no 20 bytes before its payload (general path)
         fields, data, data_off, out_off, ps = _uniform_build_case(rng, n, P, lead)
         want, wraw = O.c_go_tcp_build(fields, data, data_off, out_off, ps)
-        for kern in (0, nsx.KERNEL_BUILD_GENERAL, nsx.KERNEL_BUILD_PLAIN, nsx.KERNEL_BUILD_BPERM):
+        for kern in (0, nsx.KERNEL_BUILD_GENERAL, nsx.KERNEL_BUILD_PLAIN):
             got, raw = _run_build(fields, data, data_off, out_off, ps, tune=dict(kernel=kern))
             assert np.array_equal(raw, wraw), (P, n, lead, kern)
             assert np.array_equal(got, want), (P, n, lead, kern)
@@ -838,7 +838,7 @@ def test_tcp_build_uniform_batches_with_options(opt, P):
         assert all(int(out_off[i + 1] - out_off[i]) >= len(want_wire[i]) for i in range(n))
         # offset=None: byte 12 computed on the device (computeOffset, tcp.go:59-66) from the option bytes
         for kern, comp in ((0, False), (nsx.KERNEL_BUILD_GENERAL, False), (nsx.KERNEL_BUILD_PLAIN, False),
-                           (nsx.KERNEL_BUILD_BPERM, False), (0, True), (nsx.KERNEL_BUILD_PLAIN, True)):
+                           (0, True), (nsx.KERNEL_BUILD_PLAIN, True)):
             out = torch.full((int(out_off[-1]),), 0xAB, dtype=torch.uint8, device="cuda")
             raw = torch.empty(n, dtype=torch.int16, device="cuda")
             nsx.tcp_build_dev(dict(fields, offset=None) if comp else fields, dev(data), dev(data_off.view(np.int64)),

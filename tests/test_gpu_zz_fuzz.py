@@ -121,7 +121,7 @@ def test_fuzz_tcp_build(case):
               "offset": np.full(n, 5, np.uint8), "control": rng.integers(0, 256, n).astype(np.uint8),
               "window": rng.integers(0, 1 << 16, n).astype(np.uint16),
               "urgent_ptr": rng.integers(0, 1 << 16, n).astype(np.uint16)}
-    tune = dict(kernel=int(rng.choice([0, nsx.KERNEL_BUILD_PLAIN, nsx.KERNEL_BUILD_GENERAL, nsx.KERNEL_BUILD_BPERM])),
+    tune = dict(kernel=int(rng.choice([0, nsx.KERNEL_BUILD_PLAIN, nsx.KERNEL_BUILD_GENERAL])),
                 blocks_per_cu=int(rng.choice([0, 1, 8])))
     want, wraw = O.c_go_tcp_build(fields, data, data_off, out_off, None)
     dt = {np.uint16: np.int16, np.uint32: np.int32, np.uint8: np.uint8}
@@ -188,7 +188,7 @@ def test_fuzz_tcp_build_options(case):
     data_off[1:] = np.cumsum([len(sg.data) for sg in segs])
     data_off += np.uint64(dlead)
     out_off = nsx.tcp_layout_host(data_off, opt_off)
-    tune = dict(kernel=int(rng.choice([0, nsx.KERNEL_BUILD_PLAIN, nsx.KERNEL_BUILD_GENERAL, nsx.KERNEL_BUILD_BPERM])),
+    tune = dict(kernel=int(rng.choice([0, nsx.KERNEL_BUILD_PLAIN, nsx.KERNEL_BUILD_GENERAL])),
                 blocks_per_cu=int(rng.choice([0, 1, 8])))
     col = lambda k, dt: _dev(np.array([getattr(sg, k) for sg in segs], dt).view(
         {np.uint16: np.int16, np.uint32: np.int32, np.uint8: np.uint8}[dt]))
