@@ -128,17 +128,25 @@ WORKLOADS = {
              metric="GiB/s fused receive verify (IPv6 pseudo-header + TCP checksum into a bitmask), packet bytes",
              name="f2 rx6 small: 8M IPv6/TCP packets per GPU, 60-120B (uniform, ACK-sized), densely packed "
                   "(odd starts), 1 in 1000 corrupted, verified into a validity bitmask, device-resident"),
+    # not a BASELINE config: ACK-dominated traffic with a few full frames — mean frame 125 B, just under the receive
+    # pass's small-frame line (equal-count wave ranges, LDS form), with 5% of the frames 12x the mean
+    17: dict(kind="rx", n=1 << 23, mix="ack_data", data_frac=0.05, seed=0x1080,
+             metric="GiB/s fused receive verify (IPv4 header + pseudo-header + TCP checksum into a bitmask), frame bytes",
+             name="f2+f3 rx ACK-heavy: 8M IPv4/TCP datagrams per GPU, 95% 40-66B ACKs and 5% 1500B data frames "
+                  "(random order), densely packed (odd starts), 1 in 1000 corrupted, verified into a validity "
+                  "bitmask, device-resident"),
 }
 
 
 def frame_lengths(cfg):
     """Per-unit byte lengths of a ragged / receive workload (the same on every rank; bytes differ by seed):
-    uniform on [lo, hi], or the bimodal ACK/data mix (half uniform on [40, 66], half 1500)."""
+    uniform on [lo, hi], or the bimodal ACK/data mix (uniform on [40, 66], a fraction data_frac (default half) of
+    1500)."""
     import numpy as np
     rng = np.random.default_rng(cfg["seed"])
     n = cfg["n"]
     if cfg.get("mix") == "ack_data":
-        return np.where(rng.random(n) < 0.5, rng.integers(40, 67, n), 1500).astype(np.uint64)
+        return np.where(rng.random(n) < 1.0 - cfg.get("data_frac", 0.5), rng.integers(40, 67, n), 1500).astype(np.uint64)
     return rng.integers(cfg["lo"], cfg["hi"] + 1, n).astype(np.uint64)
 
 
@@ -152,7 +160,7 @@ def parse_args(argv=None):
                          "8: f1 with 12 B options; 9: f3 verify into a bitmask; 10: fused receive pass (f2+f3); "
                          "11: the receive pass over IPv6; 12: f1 with 9000 B MTU segments; 13 / 16: the receive "
                          "pass over 8M ACK-sized IPv4 / IPv6 frames; 14: over a bimodal ACK/1500 B mix; 15: config 3's "
-                         "small-segment twin (8M x 64-128 B)")
+                         "small-segment twin (8M x 64-128 B); 17: 8M frames, 95% ACKs and 5% 1500 B")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--settle-s", type=float, default=0.5, help="device clock settle time before warmup (setup)")
     ap.add_argument("--tune", action="append", default=[], metavar="FIELD=V",

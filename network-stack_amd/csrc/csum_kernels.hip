@@ -610,6 +610,36 @@ __device__ __forceinline__ void seg_lower_bound2(__amdgpu_buffer_rsrc_t ofs, uin
         s[k] = lo[k] + (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(v[k] < t[k]));
 }
 
+// The units [a0, a_end) of wave g of W (a0, a_end multiples of `align`, except a_end = n for the last wave), and the
+// wave's bytes. Byte-balanced — wave g owns the units that start in the g-th of W equal byte slices, found by two
+// interleaved 64-ary searches over the offsets — unless the batch's mean unit is under small_mean bytes: then equal
+// unit counts, no search (§7 step 51). On batches of small frames the search's third round touches ~8 KB of
+// offsets lines per wave that are evicted again before the wave's runs read them (5-7% of the batch's bytes,
+// FETCH_SIZE), and its four dependent round trips hold every wave at the start; small units of similar size
+// balance well by count.
+struct WaveRange {
+    uint32_t a0, a_end;
+    uint64_t bytes;
+};
+__device__ __forceinline__ WaveRange wave_range(__amdgpu_buffer_rsrc_t ofs, uint32_t n, uint32_t g, uint32_t W,
+                                                uint32_t lane, uint32_t small_mean, uint32_t align) {
+    const uint64_t o_lo = ld_off(ofs, 0), o_hi = ld_off(ofs, n);
+    const uint64_t tot = o_hi - o_lo;
+    uint32_t s[2];
+    const bool by_count = tot < (uint64_t)small_mean * n;
+    if (by_count) {
+        s[0] = (uint32_t)((uint64_t)n * g / W);
+        s[1] = (uint32_t)((uint64_t)n * (g + 1) / W);
+    } else {
+        seg_lower_bound2(ofs, n, o_lo + tot * g / W, o_lo + tot * (g + 1) / W, lane, s);
+    }
+    WaveRange r;
+    r.a0 = g == 0 ? 0u : min((s[0] + align - 1u) / align * align, n);
+    r.a_end = g + 1 == W ? n : min((s[1] + align - 1u) / align * align, n);
+    r.bytes = by_count ? ld_off(ofs, r.a_end) - ld_off(ofs, r.a0) : tot * (g + 1) / W - tot * g / W;
+    return r;
+}
+
 // Stream the bytes [rbase + head, rbase + span) as 1 KiB rows of one wave (rbase 128-byte aligned, so a row
 // touches exactly 8 lines), R rows per load batch, and sample S (the weighted byte sum of the ragged scan
 // kernel, relative to rbase) at every lane's boundaries brel[k] (−1: none), k < NS: bval[k] = S(brel[k]). A
@@ -824,13 +854,14 @@ __device__ __forceinline__ void ragged_runs(const uint8_t* __restrict__ base, __
 // (Round-3 first form: both ends masked byte-wise with keep_bytes, ~56 VALU per run)
 __device__ __forceinline__ uint32_t lds_range_sum(const lds16* slot, uint32_t p, uint32_t e, uint32_t dq, bool live) {
     const uint32_t c0 = p >> 4, c1 = (e + 15u) >> 4, nch = c1 - c0;
-    // Blocks of 8 chunks, a wave-uniform trip count from the wave's longest range (an SGPR loop counter: a loop
-    // ending on a ballot left hipcc an undefined exit value that it read with v_readfirstlane from a register
-    // still being loaded — a vmcnt wait that drained the next run's rows before this run's sums began). A block
-    // reads chunks c0 + j0 .. c0 + j0 + 7 unclamped (one address, immediate offsets; the slot's pad keeps the
-    // reads past its last chunk inside it) and keeps those below nch. The first block is always read (its first
-    // chunk gives head and the neighbour's tail even for an empty range).
-    const uint32_t nblk = wave_max((nch + 7u) >> 3);
+    // A first block of 8 chunks, then blocks of 4 while the wave's longest range has more: a wave-uniform trip
+    // count (an SGPR loop counter: a loop ending on a ballot left hipcc an undefined exit value that it read with
+    // v_readfirstlane from a register still being loaded — a vmcnt wait that drained the next run's rows before this
+    // run's sums began). A block reads its chunks from c0 + j0 unclamped (one address, immediate offsets; the slot's
+    // pad keeps the reads past its last chunk inside it) and keeps those below nch. The first block is always read
+    // (its first chunk gives head and the neighbour's tail even for an empty range). Blocks of 4 after it: 64-128 B
+    // segments span up to 9 chunks, and a second block of 8 read 7 chunks for nothing in nearly every wave.
+    const uint32_t nmax = wave_max(nch);
     uint32_t acc;
     {
         u32x4 x[8];
@@ -854,13 +885,13 @@ __device__ __forceinline__ uint32_t lds_range_sum(const lds16* slot, uint32_t p,
             acc += j < nch ? s4 : 0u;
         }
     }
-    for (uint32_t j0 = 8; j0 < nblk * 8u; j0 += 8u) {
-        u32x4 x[8];
+    for (uint32_t j0 = 8; j0 < nmax; j0 += 4u) {
+        u32x4 x[4];
         const lds16* blk = slot + c0 + j0;
 #pragma unroll
-        for (uint32_t j = 0; j < 8u; ++j) x[j] = lds_get(blk, j);
+        for (uint32_t j = 0; j < 4u; ++j) x[j] = lds_get(blk, j);
 #pragma unroll
-        for (uint32_t j = 0; j < 8u; ++j) {
+        for (uint32_t j = 0; j < 4u; ++j) {
             const uint32_t s4 = sad4(x[j], 0u);
             acc += j0 + j < nch ? s4 : 0u;
         }
@@ -999,13 +1030,8 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
         const uint32_t b = blockIdx.x, W = nb * kWavesPerBlock;
         const uint32_t g = (nb >= 16 && (nb & 7) == 0) ? ((b & 7) * (nb >> 3) + (b >> 3)) * kWavesPerBlock + wave
                                                         : b * kWavesPerBlock + wave;
-        const uint64_t o_lo = ld_off(ofs, 0), o_hi = ld_off(ofs, n);
-        const uint64_t tot = o_hi - o_lo;
-        uint32_t s[2];
-        seg_lower_bound2(ofs, n, o_lo + tot * g / W, o_lo + tot * (g + 1) / W, lane, s);
-        a0 = g == 0 ? 0u : s[0];
-        a_end = g + 1 == W ? n : s[1];
-        wave_bytes = tot * (g + 1) / W - tot * g / W;
+        const WaveRange wr = wave_range(ofs, n, g, W, lane, kScanLdsSeg, 1u);
+        a0 = wr.a0, a_end = wr.a_end, wave_bytes = wr.bytes;
     }
     // Two sets per run suit segments of a few hundred bytes and up (config 3). A wave whose segments average under
     // kScanLdsSeg bytes sums them out of LDS (§7 step 44); under kScanSmallSeg it takes runs of four sets, so that
@@ -1416,13 +1442,8 @@ __global__ __launch_bounds__(kBlock, WPS) void rx_tcp_kernel(const uint8_t* __re
         const uint32_t b = blockIdx.x, W = nb * kWavesPerBlock;
         const uint32_t g = (nb >= 16 && (nb & 7) == 0) ? ((b & 7) * (nb >> 3) + (b >> 3)) * kWavesPerBlock + wave
                                                         : b * kWavesPerBlock + wave;
-        const uint64_t o_lo = ld_off(ofs, 0), o_hi = ld_off(ofs, n);
-        const uint64_t tot = o_hi - o_lo;
-        uint32_t s[2];
-        seg_lower_bound2(ofs, n, o_lo + tot * g / W, o_lo + tot * (g + 1) / W, lane, s);
-        a0 = g == 0 ? 0u : min((s[0] + 7u) & ~7u, n);
-        a_end = g + 1 == W ? n : min((s[1] + 7u) & ~7u, n);
-        wave_bytes = tot * (g + 1) / W - tot * g / W;
+        const WaveRange wr = wave_range(ofs, n, g, W, lane, kRxSmallFrame, 8u);
+        a0 = wr.a0, a_end = wr.a_end, wave_bytes = wr.bytes;
     }
     const bool small = sets == 2 || (sets == 0 && wave_bytes < (uint64_t)kRxSmallFrame * (a_end - a0));
     if (small) {

@@ -127,6 +127,18 @@ RAGGED_TUNES = [dict(kernel=k, rows=r, run_segs=rs, blocks_per_cu=b)  # pipeline
                 for rs in (0, 1, 16, 63) for b in (0, 1, 8) for k in (0, nsx.KERNEL_SCAN_PLAIN)]
 
 
+def test_ragged_small_segment_bench_workload_full_size():
+    """Bench workload 15 at full size (8M ragged segments of 64-128 B, equal-count wave ranges, the LDS form): every
+    raw sum equals the C oracle's (16 threads)."""
+    import bench
+    cfg = bench.WORKLOADS[15]
+    w = bench.build_workload(cfg, 0, torch.device("cuda", 0))
+    w["step"]()
+    got = u16(w["out"])
+    want = O.c_batch(host(w["buf"]), cfg["n"], offsets=w["offsets"], threads=16)
+    assert np.array_equal(got, want)
+
+
 @pytest.mark.parametrize("n", [1, 126, 252, 253, 30_001, 400_003])
 def test_ragged_small_segments_runs_of_four_sets(n):
     """Segments of 0-200 B (mean ~100): waves whose segments average under 256 B take the LDS form (DESIGN.md §7

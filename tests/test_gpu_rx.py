@@ -122,10 +122,11 @@ def test_rx_small_frames_300K_every_set_form_vs_oracle(ipver):
             assert bad.size == 0, (what, tune, bad[:5])
 
 
-@pytest.mark.parametrize("config", [13, 14, 16])
+@pytest.mark.parametrize("config", [13, 14, 16, 17])
 def test_rx_small_frame_bench_workloads_full_size(config):
     """The bench's small-frame receive workloads at full size (13: 8M IPv4 frames of 40-100 B; 14: 2M frames, half
-    40-66 B ACKs and half 1500 B; 16: 8M IPv6 packets of 60-120 B): the device mask equals the oracle's on every
+    40-66 B ACKs and half 1500 B; 16: 8M IPv6 packets of 60-120 B; 17: 8M frames, 95% ACKs and 5% 1500 B — equal-count
+    wave ranges with runs too wide for the LDS slot among LDS runs): the device mask equals the oracle's on every
     frame, and exactly the corrupted frames fail."""
     import bench
     cfg = bench.WORKLOADS[config]
