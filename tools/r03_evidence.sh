@@ -23,7 +23,7 @@ step() {  # step <name> <timeout> cmd...
 case $mode in
   prof)
     mkdir -p gpurun_out/profiles
-    for c in ${1:-2 3 10 11 13 14 15 16}; do
+    for c in ${1:-2 3 10 11 13 14 15 16 17}; do
       GROUPS_ONLY="kt fetch write" bash tools/profile.sh $c r03 || exit 1
       python3 tools/prof_summary.py r03 $c > /dev/null || exit 1
       cp profiles/r03_config${c}.md profiles/r03_config${c}_kernel_stats.csv profiles/traffic_config${c}.json \
@@ -42,7 +42,7 @@ case $mode in
     step bench_c3 300 python bench.py --config 3 --cpu-seconds 5
     step bench_c4 300 python bench.py --config 4 --steps 50 --cpu-seconds 5
     step bench_c5 300 python bench.py --config 5 --steps 20 --cpu-seconds 0
-    for c in 6 7 8 9 10 11 13 14 15 16; do
+    for c in 6 7 8 9 10 11 13 14 15 16 17; do
       step bench_c$c 300 python bench.py --config $c --steps 100 --cpu-seconds 5
     done
     step bench_c12 300 python bench.py --config 12 --steps 50 --cpu-seconds 5
@@ -56,7 +56,7 @@ case $mode in
     done
     ;;
   same)
-    bash tools/same_run_profile.sh r03 ${1:-2 3 4 5 6 7 8 9 10 11 12 13 14 15 16} || exit $?
+    bash tools/same_run_profile.sh r03 ${1:-2 3 4 5 6 7 8 9 10 11 12 13 14 15 16 17} || exit $?
     ;;
 esac
 echo done
