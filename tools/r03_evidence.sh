@@ -32,20 +32,21 @@ case $mode in
       echo "profiled config $c"
     done
     ;;
-  bench)
+  bench)  # tools/r03_evidence.sh bench "tests 2 3 ..." — "tests" runs the -m gpu suite and smoke first
     { nproc; python3 -c "import os; print('affinity', len(os.sched_getaffinity(0)), 'cpu_count', os.cpu_count())";
       cat /sys/fs/cgroup/cpu.max 2>/dev/null; echo "OMP_NUM_THREADS=${OMP_NUM_THREADS:-}";
       lscpu | grep -E "Model name|^CPU\(s\)|Thread|Core|Socket"; } > gpurun_out/r03ev/host.txt 2>&1
-    step pytest_gpu 900 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider
-    step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-    step bench_c2 300 python bench.py
-    step bench_c3 300 python bench.py --config 3 --cpu-seconds 5
-    step bench_c4 300 python bench.py --config 4 --steps 50 --cpu-seconds 5
-    step bench_c5 300 python bench.py --config 5 --steps 20 --cpu-seconds 0
-    for c in 6 7 8 9 10 11 13 14 15 16 17; do
-      step bench_c$c 300 python bench.py --config $c --steps 100 --cpu-seconds 5
+    for c in ${1:-tests 2 3 4 5 6 7 8 9 10 11 12 13 14 15 16 17}; do
+      case $c in
+        tests) step pytest_gpu 900 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider
+               step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+        2) step bench_c2 300 python bench.py ;;
+        3) step bench_c3 300 python bench.py --config 3 --cpu-seconds 5 ;;
+        4|12) step bench_c$c 300 python bench.py --config $c --steps 50 --cpu-seconds 5 ;;
+        5) step bench_c5 300 python bench.py --config 5 --steps 20 --cpu-seconds 0 ;;
+        *) step bench_c$c 300 python bench.py --config $c --steps 100 --cpu-seconds 5 ;;
+      esac
     done
-    step bench_c12 300 python bench.py --config 12 --steps 50 --cpu-seconds 5
     ;;
   host)
     step e2e_host 600 python tools/e2e_host.py

@@ -47,5 +47,27 @@ def main(save):
               f"**{r['frac']:.3f}** | {tr} | {cpu} | {cpu1} |")
 
 
+def traffic():
+    """DESIGN §5 traffic rows: PMC HBM bytes per launch (profiles/traffic_config<N>.json) against the bench line's
+    algorithmic bytes, and the profile's mean kernel duration against the bench's HIP-event mean."""
+    import re
+    print("| workload | HBM bytes per launch | algorithmic | traffic / alg | rocprofv3 mean | bench event mean |")
+    print("|---|---|---|---|---|---|")
+    for c in sorted(NAMES):
+        d = line(c)
+        tp = os.path.join(ROOT, "profiles", f"traffic_config{c}.json")
+        md = os.path.join(ROOT, "profiles", f"r03_config{c}.md")
+        if d is None or not os.path.exists(tp) or not os.path.exists(md):
+            continue
+        t = json.load(open(tp))
+        alg = d["roofline"]["alg_bytes_per_launch"]
+        m = re.search(r"per-launch durations \(µs, trace order\): median [0-9.]+, mean ([0-9.]+)", open(md).read())
+        print(f"| {c} | {t['bytes_per_launch'] / 1e9:.4f} GB | {alg / 1e9:.4f} GB | {t['bytes_per_launch'] / alg:.4f} | "
+              f"{m.group(1) if m else '—'} µs | {d['kernel_ms_mean'] * 1000:.1f} µs |")
+
+
 if __name__ == "__main__":
-    main("--save" in sys.argv)
+    if "--traffic" in sys.argv:
+        traffic()
+    else:
+        main("--save" in sys.argv)
