@@ -1372,16 +1372,21 @@ __device__ __forceinline__ void rx_runs_lds(const uint8_t* __restrict__ base, __
     // outer loop. (Kept apart so that the streaming form's loads still in flight at its end — its pipeline issues
     // one empty batch past the run — never merge into the LDS loop's wait counts: at a merge hipcc waits
     // vmcnt(0) before reusing such a register, which drained the next run's rows right after their issue.)
+    // The offsets of the outer loop's next run are always loaded one run ahead (before a streamed run, or by the LDS
+    // loop), so that a switch between the forms does not wait for them (§7 step 53).
     uint32_t a = a0;
+    uint64_t c_off = load_off(a + lane, a < a_end && a + lane <= n);
+    uint64_t c_end = load_off(a + lane + 1u, a < a_end && a + lane + 1u <= n);
     while (a < a_end) {
-        uint64_t c_off = load_off(a + lane, a + lane <= n);
-        uint64_t c_end = load_off(a + lane + 1u, a + lane + 1u <= n);
         Run cur = geo(a, c_off, c_end);
         if (!cur.lds) {  // a run too wide for the slot: the streaming form
+            const uint32_t as = a + kRxRun;
+            const uint64_t s_off = load_off(as + lane, as < a_end && as + lane <= n);
+            const uint64_t s_end = load_off(as + lane + 1u, as < a_end && as + lane + 1u <= n);
             uint32_t cnt1[1] = {cur.cnt};
             uint64_t o1[1] = {c_off}, e1[1] = {c_end};
             rx_run_stream<R, V6, 1>(base, a, cnt1, o1, e1, 0u, n, lane, mrs, irs, trs);
-            a += kRxRun;
+            a = as, c_off = s_off, c_end = s_end;
             continue;
         }
         issue(cur);
@@ -1404,9 +1409,10 @@ __device__ __forceinline__ void rx_runs_lds(const uint8_t* __restrict__ base, __
             const uint64_t p_end = load_off(an2 + lane + 1u, an2 < a_end && an2 + lane + 1u <= n);
             rx_run_lds<V6>(base, cur.rbase, a, cur.cnt, c_off, c_end, n, lane, slot, mrs, irs, trs);
             a = an;
+            c_off = n_off, c_end = n_end;
             if (!nxt.lds) break;  // the end of the wave's range, or a run for the outer loop
             cur = nxt;
-            c_off = n_off, c_end = n_end, n_off = p_off, n_end = p_end;
+            n_off = p_off, n_end = p_end;
             an = an2;
         }
     }
