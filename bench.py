@@ -135,6 +135,12 @@ WORKLOADS = {
              name="f2+f3 rx ACK-heavy: 8M IPv4/TCP datagrams per GPU, 95% 40-66B ACKs and 5% 1500B data frames "
                   "(random order), densely packed (odd starts), 1 in 1000 corrupted, verified into a validity "
                   "bitmask, device-resident"),
+    # not a BASELINE config: frames between the ACK and the full-frame regimes (mean 220 B), the receive pass's
+    # 15-row prefix form
+    18: dict(kind="rx", n=1 << 23, lo=40, hi=400, seed=0x1081,
+             metric="GiB/s fused receive verify (IPv4 header + pseudo-header + TCP checksum into a bitmask), frame bytes",
+             name="f2+f3 rx mid: 8M IPv4/TCP datagrams per GPU, 40-400B (uniform), densely packed (odd starts), "
+                  "1 in 1000 corrupted, verified into a validity bitmask, device-resident"),
 }
 
 

@@ -1006,6 +1006,201 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
     }
 }
 
+// ---------------------------------------------------------------------------
+// The prefix form: per-unit work that does not grow with the unit. The LDS forms
+// (ragged_runs_lds above, rx_runs_lds below) sum each unit chunk by chunk in its own lane, so a run holding one
+// 1500 B frame among ACKs waits ~94 chunk reads for that lane, and a run wider than the 8 KiB slot is streamed. The
+// receive pass uses this form (rx_runs_pfx); on the ragged checksum, whose streamed four-set runs hold 0.74-0.82 at
+// every segment size, it measured 2-13% slower everywhere and is not built (§7 step 56). Here the staging pass also writes the run's chunk PREFIX SUMS: per staged row,
+// each lane's 16 B chunk sum (v_sad_u16 ×4) and an inclusive wave scan (DPP) plus the rows before it give I[c] = the
+// weighted sum of the slot's bytes below chunk c. A unit starting at slot position p then has S(p) = I[p/16] + the
+// bytes of chunk p/16 below p (its dword prefix sums and the low p mod 4 bytes of the dword holding p — no byte
+// masks), and its sum is S(end) − S(p) with S(end) = the next lane's S(start) (one DPP shift; the piece's last lane
+// takes the staged total, the bytes past the piece's end being zeroed at staging). Per lane: one ds_read_b128 and
+// two ds_read_b32 at any unit size. Sums of a slot's bytes stay below 2^32 (ROWS·512 halves of < 2^16).
+//
+// Pieces instead of runs: a piece is the units of a 64-unit run from lane s on whose bytes fit the slot, cut at a
+// multiple of ALIGN units (the receive pass: 8, whole mask bytes) unless it reaches the run's end. A run of ACKs fits
+// whole; a run holding large frames goes as 2-3 pieces, each still one pass of cheap lanes (cutting runs cost 28% in
+// the LDS form, §7 step 52, only because a lane then summed a 1500 B frame alone). Only a piece whose first ALIGN
+// units exceed the slot (units of several KB) is streamed. The next piece's rows are loaded while this one is summed.
+//
+// Slot per wave: ROWS rows of data + 64 B (a header window read past the data) + I[0 .. 64·ROWS] (I[0] = 0).
+constexpr uint32_t kPfxRun = 64;
+template <uint32_t ROWS>
+struct PfxSlot {
+    static constexpr uint32_t kData = ROWS * kRow;
+    static constexpr uint32_t kPrefix = kData + 64u;  // byte offset of I
+    static constexpr uint32_t kBytes = (kPrefix + (ROWS * kWave + 1u) * 4u + 15u) & ~15u;
+};
+// 4 blocks/CU: 7 rows (16 × 9040 B = 141 KiB of the CU's 160); 3 blocks/CU: 10 rows; 2 blocks/CU: 15 rows.
+constexpr uint32_t pfx_rows_for(uint32_t blocks_per_cu) { return blocks_per_cu >= 4 ? 7u : blocks_per_cu == 3 ? 10u : 15u; }
+// The hybrid loop's direct pieces: a whole run in the LDS form's 8 rows (+ 256 B pad, kScanSlot = kRxSlot).
+constexpr uint32_t kPfxDirectRows = 8;
+constexpr uint32_t kPfxDirectSlot = kPfxDirectRows * kRow + 256;
+// Units up to this long may be summed lane by lane in direct pieces: 17 chunks.
+constexpr uint32_t kPfxDirectMax = 256;
+
+// Stage a piece's rows [0, span) into the slot (the rows already in V, all loaded) with their chunk prefix sums;
+// returns S(span), the weighted sum of the staged bytes. The chunk holding byte `span` keeps only its bytes below
+// it (the row loads read whole dwords up to 4·ceil(span/4): up to 3 bytes of the next unit). I[0] = 0 is written
+// every time: the hybrid loop's direct pieces stage whole 8 KiB runs over it.
+template <uint32_t ROWS, uint32_t VR>
+__device__ __forceinline__ uint32_t pfx_stage(lds16* slot, u32x4 (&V)[VR], uint32_t span, uint32_t lane) {
+    static_assert(ROWS <= VR, "rows in registers");
+    uint32_t* I = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(slot) + PfxSlot<ROWS>::kPrefix);
+#pragma unroll
+    for (uint32_t r = 0; r < VR; ++r) asm volatile("" : "+v"(V[r]));
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t rows = __builtin_amdgcn_readfirstlane((span + kRow - 1u) / kRow);  // ≤ ROWS (scalar)
+    const uint32_t zr = span / kRow, zc = (span / 16u) & (kWave - 1u);
+    const int32_t zk = (int32_t)(span & 15u);
+    if (lane == 0) I[0] = 0u;
+    uint32_t carry = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < ROWS; ++r) {
+        if (r < rows) {
+            u32x4 v = V[r];
+            if (r == zr) v = lane == zc ? keep_bytes(v, 0, zk) : v;
+            slot[r * kWave + lane] = lds16{v.x, v.y, v.z, v.w};
+            const uint32_t incl = wave_incl_scan(sad4(v, 0u));
+            I[r * kWave + lane + 1u] = carry + incl;
+            carry += __builtin_amdgcn_readlane(incl, 63);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    return carry;
+}
+
+// A wave's units [a0, a_end) in runs of 64 (from a0), as pieces of the prefix form with ROWS-row slots. Unit a + l =
+// bytes [offsets[a + l], offsets[a + l + 1]), lanes holding both ends. HYB (the hybrid loop, §7 step 55): a whole run
+// whose bytes fit 8 rows and whose units are all ≤ kPfxDirectMax bytes is a DIRECT piece instead — staged without
+// prefix sums and summed lane by lane (lds_range_sum, the LDS form, 3-6% faster on runs of ACKs alone: no per-row
+// scans); the slot (PfxSlot<7>, 9040 B) holds either layout.
+//   out(F, p, d0, live, a, s, cnt, off, end)  the results of units [a + s, a + s + cnt) (lane l = unit a + l):
+//                                      F = the unit's weighted sum, p its slot position, d0 = the slot dword at p/4;
+//   stream(a, s, rem, off, end)        units [a + s, a + s + rem) of the run at a in the streaming form (lane l of
+//                                      off / end = unit a + l).
+template <uint32_t ROWS, bool HYB, uint32_t ALIGN, typename Out, typename Stream>
+__device__ __forceinline__ void pfx_runs(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
+                                         uint32_t a0, uint32_t a_end, uint32_t lane, lds16* slot, Out&& out,
+                                         Stream&& stream) {
+    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+    constexpr uint32_t kCap = ROWS * kRow;
+    constexpr uint32_t VR = HYB && ROWS < kPfxDirectRows ? kPfxDirectRows : ROWS;  // rows in flight per piece
+    static_assert(!HYB || PfxSlot<ROWS>::kBytes >= kPfxDirectSlot, "a direct piece's 8 rows + pad fit the slot");
+    auto load_off = [&](uint32_t i, bool live) -> uint64_t {
+        const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, live ? i * 8 : kOOB, 0, 0);
+        return ((uint64_t)x.y << 32) | x.x;
+    };
+    const uint32_t* sdw = reinterpret_cast<const uint32_t*>(slot);
+    const uint32_t* I = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(slot) + PfxSlot<ROWS>::kPrefix);
+    struct Piece {
+        uint32_t a, s, cnt, rem;  // units [a + s, a + s + cnt) of the run at a; rem = the run's units from s on
+        const uint8_t* rbase;     // 128-aligned, at or below the piece's first byte
+        uint32_t span;            // bytes from rbase to the piece's end
+        bool direct;              // HYB: a whole run summed lane by lane
+    };
+    // Wave-uniform geometry of the piece of run a from lane s (off/end: that run's offsets, lane l = unit a + l).
+    auto geo = [&](uint32_t a, uint32_t s, uint64_t off, uint64_t end) {
+        Piece g{a, s, 0u, 0u, base, 0u, false};
+        const uint32_t rc = a < a_end ? min(kPfxRun, a_end - a) : 0u;
+        if (s < rc) {
+            g.rem = rc - s;
+            g.rbase = reinterpret_cast<const uint8_t*>(((uintptr_t)(base + readlane64(off, s))) & ~(uintptr_t)127);
+            const uint64_t lim = (uint64_t)(g.rbase - base) + kCap;  // units ending at or below fit the slot
+            if constexpr (HYB) {
+                if (s == 0) {
+                    const uint64_t span = (uint64_t)((base + readlane64(end, rc - 1u)) - g.rbase);
+                    const bool big = __builtin_amdgcn_ballot_w64(lane < rc && end - off > kPfxDirectMax) != 0;
+                    if (span <= (uint64_t)kPfxDirectRows * kRow && !big) {
+                        g.cnt = rc, g.span = (uint32_t)span, g.direct = true;
+                        return g;
+                    }
+                }
+            }
+            const uint64_t over = __builtin_amdgcn_ballot_w64(lane >= s && lane < rc && end > lim);
+            uint32_t fit = over ? (uint32_t)__builtin_ctzll(over) - s : g.rem;
+            if (fit < g.rem) fit &= ~(ALIGN - 1u);
+            g.cnt = fit;
+            if (fit) g.span = (uint32_t)((base + readlane64(end, s + fit - 1u)) - g.rbase);
+        }
+        return g;
+    };
+    u32x4 V[VR];
+    auto issue = [&](const Piece& g) {  // rows past the piece: out of the descriptor's range, 0, no traffic
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(g.rbase, g.cnt ? (g.span + 3u) & ~3u : 0u);
+#pragma unroll
+        for (uint32_t r = 0; r < VR; ++r) V[r] = bld16<true>(rs, r * kRow + lane * 16u);
+    };
+    auto live_of = [&](const Piece& g) { return lane >= g.s && lane < g.s + g.cnt; };
+    uint32_t a = a0;
+    uint64_t c_off = load_off(a + lane, a < a_end && a + lane <= n);
+    uint64_t c_end = load_off(a + lane + 1u, a < a_end && a + lane + 1u <= n);
+    uint64_t n_off = load_off(a + kPfxRun + lane, a + kPfxRun < a_end && a + kPfxRun + lane <= n);
+    uint64_t n_end = load_off(a + kPfxRun + lane + 1u, a + kPfxRun < a_end && a + kPfxRun + lane + 1u <= n);
+    Piece cur = geo(a, 0u, c_off, c_end);
+    issue(cur);
+    __builtin_amdgcn_s_waitcnt(kWaitVm0);  // nothing in flight at the loop's entry (rx_runs_lds, §7 step 50)
+    while (cur.rem) {
+        if (!cur.cnt) {
+            // The first ALIGN units from s exceed the slot: stream the run's units from s on.
+            stream(a, cur.s, cur.rem, c_off, c_end);
+            a += kPfxRun;
+            c_off = n_off, c_end = n_end;
+            n_off = load_off(a + kPfxRun + lane, a + kPfxRun < a_end && a + kPfxRun + lane <= n);
+            n_end = load_off(a + kPfxRun + lane + 1u, a + kPfxRun < a_end && a + kPfxRun + lane + 1u <= n);
+            cur = geo(a, 0u, c_off, c_end);
+            issue(cur);
+            __builtin_amdgcn_s_waitcnt(kWaitVm0);
+            continue;
+        }
+        uint32_t total = 0;
+        if (HYB && cur.direct) {
+            lds_stage<VR>(slot, V, cur.span, lane);
+            lds_zero_tail(slot, cur.span, lane);
+        } else {
+            total = pfx_stage<ROWS, VR>(slot, V, cur.span, lane);
+        }
+        // The next piece: the rest of this run, or the next run (whose offsets are already loaded).
+        const bool adv = cur.cnt == cur.rem;
+        Piece nxt;
+        if (adv) nxt = geo(a + kPfxRun, 0u, n_off, n_end);
+        else nxt = geo(a, cur.s + cur.cnt, c_off, c_end);
+        issue(nxt);
+        const uint32_t ap = a + 2u * kPfxRun;
+        const uint64_t p_off = load_off(ap + lane, adv && ap < a_end && ap + lane <= n);
+        const uint64_t p_end = load_off(ap + lane + 1u, adv && ap < a_end && ap + lane + 1u <= n);
+        {
+            const bool live = live_of(cur);
+            const uint32_t p = live ? (uint32_t)((base + c_off) - cur.rbase) : 0u;
+            const uint32_t d0 = sdw[p >> 2];
+            uint64_t F;
+            if (HYB && cur.direct) {
+                const uint32_t e = live ? (uint32_t)((base + c_end) - cur.rbase) : 0u;
+                F = lds_range_sum(slot, p, e, d0, live);
+            } else {
+                const lds16 x = slot[p >> 4];
+                const uint32_t pre1 = __builtin_amdgcn_sad_u16(x.x, 0u, 0u);
+                const uint32_t pre2 = __builtin_amdgcn_sad_u16(x.y, 0u, pre1);
+                const uint32_t pre3 = __builtin_amdgcn_sad_u16(x.z, 0u, pre2);
+                const uint32_t q = (p >> 2) & 3u;
+                const uint32_t pq = q == 0u ? 0u : q == 1u ? pre1 : q == 2u ? pre2 : pre3;
+                const uint32_t sp = I[p >> 4] + __builtin_amdgcn_sad_u16(d0 & ((1u << (8u * (p & 3u))) - 1u), 0u, pq);
+                const uint32_t sn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sp, 0x130, 0xF, 0xF, false);  // wave_shl:1
+                F = (uint32_t)((lane == cur.s + cur.cnt - 1u ? total : sn) - sp);
+            }
+            out(F, p, d0, live, a, cur.s, cur.cnt, c_off, c_end);
+        }
+        if (adv) {
+            a += kPfxRun;
+            c_off = n_off, c_end = n_end;
+            n_off = p_off, n_end = p_end;
+        }
+        cur = nxt;
+    }
+}
+
 template <int R, bool VERIFY, bool PIPE, int NS>
 __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, uint32_t n,
@@ -1077,12 +1272,14 @@ constexpr uint32_t kRxRun = 64;
 // A run's validity ballot (frames [a, a + cnt), a a multiple of 8) as mask bytes a/8 ..: one byte per lane
 // (lanes 0-7), so wave ranges need only be cut at multiples of 8 frames, not at whole 64-bit words; the
 // batch's last run also zero-fills the rest of the mask's last word.
+// A piece of the run (the prefix form's frames [a + s, a + s + cnt), s a multiple of 8, bits still indexed by lane
+// = frame − a) writes only its own bytes s/8 ...
 __device__ __forceinline__ void rx_store_mask(__amdgpu_buffer_rsrc_t mrs, uint64_t bits, uint32_t a, uint32_t cnt,
-                                              uint32_t n, uint32_t lane) {
-    const uint32_t nbytes = (uint64_t)a + cnt >= n ? (uint32_t)((((uint64_t)n + 63u) / 64u) * 8u - a / 8u)
-                                                   : (cnt + 7u) / 8u;
+                                              uint32_t n, uint32_t lane, uint32_t s = 0) {
+    const uint32_t nbytes = (uint64_t)a + s + cnt >= n ? (uint32_t)((((uint64_t)n + 63u) / 64u) * 8u - a / 8u)
+                                                       : (s + cnt + 7u) / 8u;
     const uint32_t v = lane < 8u ? (uint32_t)(bits >> (8u * lane)) & 0xFFu : 0u;
-    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, mrs, lane < nbytes ? a / 8u + lane : kOOB, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, mrs, lane >= s / 8u && lane < nbytes ? a / 8u + lane : kOOB, 0, 0);
 }
 
 // V6: IPv6 packets (RFC 8200 §3: fixed 40-byte header, Next Header 6 = TCP directly). There is no header
@@ -1108,7 +1305,7 @@ template <bool V6, typename OptFn>
 __device__ __forceinline__ void rx_frame_out(uint64_t F, const uint32_t (&d)[6], uint32_t hd, uint64_t flen, bool even,
                                              bool live, uint32_t ak, uint32_t cnt, uint32_t n, uint32_t lane,
                                              __amdgpu_buffer_rsrc_t mrs, __amdgpu_buffer_rsrc_t irs,
-                                             __amdgpu_buffer_rsrc_t trs, OptFn&& opt) {
+                                             __amdgpu_buffer_rsrc_t trs, OptFn&& opt, uint32_t s = 0) {
     if constexpr (V6) {
         const uint32_t H0 = __builtin_amdgcn_alignbyte(d[1], d[0], hd);  // version, class, flow label
         const uint32_t H1 = __builtin_amdgcn_alignbyte(d[2], d[1], hd);  // payload length, next header
@@ -1122,7 +1319,7 @@ __device__ __forceinline__ void rx_frame_out(uint64_t F, const uint32_t (&d)[6],
         const uint32_t tle = fold32((uint32_t)T) + fold32((uint32_t)(T >> 32));
         const uint32_t tcpr = well ? finish(tle, even, plen + 6u) : 0u;
         const uint64_t bits = __builtin_amdgcn_ballot_w64(well && tcpr == 0xFFFFu);
-        rx_store_mask(mrs, bits, ak, cnt, n, lane);
+        rx_store_mask(mrs, bits, ak, cnt, n, lane, s);
         __builtin_amdgcn_raw_buffer_store_b16((uint16_t)tcpr, trs, live ? (ak + lane) * 2u : kOOB, 0, 0);
     } else {
         // IPv4 header fields (RFC 791 §3.1): header dword m = bytes 4m..4m+3, little-endian view.
@@ -1168,7 +1365,7 @@ __device__ __forceinline__ void rx_frame_out(uint64_t F, const uint32_t (&d)[6],
             __builtin_amdgcn_sad_u16(__builtin_amdgcn_alignbyte(H3, H3, 1u), 0u, 6u + ((total - hlen) & 0xFFFFu)));
         const uint32_t tcpr = well ? finish(tle, even, pseudo) : 0u;
         const uint64_t bits = __builtin_amdgcn_ballot_w64(well && ipr == 0xFFFFu && tcpr == 0xFFFFu);
-        rx_store_mask(mrs, bits, ak, cnt, n, lane);
+        rx_store_mask(mrs, bits, ak, cnt, n, lane, s);
         __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ipr, irs, live ? (ak + lane) * 2u : kOOB, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b16((uint16_t)tcpr, trs, live ? (ak + lane) * 2u : kOOB, 0, 0);
     }
@@ -1418,12 +1615,53 @@ __device__ __forceinline__ void rx_runs_lds(const uint8_t* __restrict__ base, __
     }
 }
 
+// The receive pass in the prefix form (pfx_runs: pieces cut at whole mask bytes; the header window from the slot).
+template <int R, bool V6, uint32_t ROWS, bool HYB>
+__device__ __forceinline__ void rx_runs_pfx(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
+                                            uint32_t a0, uint32_t a_end, uint32_t lane, lds16* slot,
+                                            __amdgpu_buffer_rsrc_t mrs, __amdgpu_buffer_rsrc_t irs,
+                                            __amdgpu_buffer_rsrc_t trs) {
+    static_assert(kPfxRun == kRxRun && kPfxDirectSlot == kRxSlot, "the receive pass's runs and direct slot");
+    const uint32_t* sdw = reinterpret_cast<const uint32_t*>(slot);
+    auto out = [&](uint64_t F, uint32_t p, uint32_t d0, bool live, uint32_t a, uint32_t s, uint32_t cnt, uint64_t off,
+                   uint64_t end) {
+        const uint32_t w0 = p >> 2;
+        uint32_t d[6];
+        d[0] = d0;
+#pragma unroll
+        for (int j = 1; j < (V6 ? 3 : 6); ++j) d[j] = sdw[w0 + j];
+        if constexpr (V6) d[3] = d[4] = d[5] = 0u;
+        auto opt = [&](uint32_t (&o)[10]) {
+#pragma unroll
+            for (int j = 6; j < 16; ++j) o[j - 6] = sdw[w0 + j];
+        };
+        rx_frame_out<V6>(F, d, p & 3u, end - off, (p & 1u) == 0, live, a, cnt, n, lane, mrs, irs, trs, opt, s);
+    };
+    auto stream = [&](uint32_t a, uint32_t s, uint32_t rem, uint64_t off, uint64_t end) {  // lanes shifted by s
+        uint32_t cnt1[1] = {rem};
+        uint64_t o1[1] = {(uint64_t)__shfl_down((unsigned long long)off, s)};
+        uint64_t e1[1] = {(uint64_t)__shfl_down((unsigned long long)end, s)};
+        rx_run_stream<R, V6, 1>(base, a + s, cnt1, o1, e1, 0u, n, lane, mrs, irs, trs);
+    };
+    pfx_runs<ROWS, HYB, 8u>(base, ofs, n, a0, a_end, lane, slot, out, stream);
+}
+
+// The receive pass's grids by the batch's mean frame m (tools/r03_pfx_sweep.sh): m <
+// kRxPfxMean: four waves per block, the hybrid loop (direct pieces for runs of small frames that fit 8 KiB, prefix
+// pieces of ≤ 7 KiB otherwise); kRxPfxMean ≤ m < kRxBigMean: the prefix form with 15-row slots on two waves per
+// block (8 waves per CU, ~19 KB of LDS each); m ≥ kRxBigMean: streamed runs on 3 blocks per CU.
+constexpr uint32_t kRxPfxMean = 112;
+
 // sets: 0 = by the wave's mean frame size (the LDS form below kRxSmallFrame, else streamed runs of one 64-frame
-// set); 1 = force the streamed runs; 2 = force the LDS form. (Round 2's streamed runs of four sets for small
-// frames, §7 step 41, were removed: the LDS form beat them by 30-40% on every small-frame mix, §7 step 43.)
+// set); 1 = force the streamed runs; 2 = force the LDS form; 3 = the prefix form (PF rows per slot). (Round 2's
+// streamed runs of four sets for small frames, §7 step 41, were removed: the LDS form beat them by 30-40% on every
+// small-frame mix, §7 step 43.)
 // WPS: waves per SIMD the registers must allow (__launch_bounds__'s second argument): 1 = no constraint (158 VGPRs,
 // 3 waves per SIMD at the default 3 blocks/CU); 4 = the 4-blocks/CU instantiation (≤ 128 VGPRs).
-template <int R, bool V6, int WPS>
+// PF: 0 = no prefix form compiled in; > 0 = the prefix form with PF-row slots when sets == 3; -1 = the default
+// grid's kernel (4 blocks/CU, PfxSlot<15> × 2 of LDS per block): sets 0 = by the batch's mean frame (kRxPfxMean,
+// kRxBigMean above), 1 = streamed runs, 5 = the hybrid loop on four waves, 6 = the 15-row prefix form on waves 0-1.
+template <int R, bool V6, int WPS, int PF = 0>
 __global__ __launch_bounds__(kBlock, WPS) void rx_tcp_kernel(const uint8_t* __restrict__ base,
                                                              const uint64_t* __restrict__ offsets, uint32_t n,
                                                              uint64_t* __restrict__ mask,
@@ -1436,24 +1674,54 @@ __global__ __launch_bounds__(kBlock, WPS) void rx_tcp_kernel(const uint8_t* __re
     const __amdgpu_buffer_rsrc_t mrs = make_rsrc(mask, (((uint64_t)n + 63) / 64) * 8);
     const __amdgpu_buffer_rsrc_t irs = make_rsrc(ip_raw, ip_raw ? (uint64_t)n * 2 : 0);
     const __amdgpu_buffer_rsrc_t trs = make_rsrc(tcp_raw, tcp_raw ? (uint64_t)n * 2 : 0);
+    extern __shared__ lds16 lds_rx[];
     // Byte-balanced wave ranges (as csum_ragged_scan_kernel), cut at multiples of 8 frames. Cut at whole mask
     // words (64 frames, ~50 KB) instead, a wave streamed up to one run more than the mean, and the launch
     // waited ~20 µs for those waves at any batch size.
+    // XCD-contiguous numbering of the blocks; wpb of each block's waves take ranges.
+    auto range = [&](uint32_t nb, uint32_t wpb, uint32_t w) {
+        const uint32_t b = blockIdx.x, W = nb * wpb;
+        const uint32_t g = (nb >= 16 && (nb & 7) == 0) ? ((b & 7) * (nb >> 3) + (b >> 3)) * wpb + w : b * wpb + w;
+        return wave_range(ofs, n, g, W, lane, kRxSmallFrame, 8u);
+    };
+    if constexpr (PF < 0) {
+        int mode = sets;
+        if (sets == 0) {
+            const uint64_t tot = ld_off(ofs, n) - ld_off(ofs, 0);
+            mode = tot >= (uint64_t)kRxBigMean * n ? 1 : tot >= (uint64_t)kRxPfxMean * n ? 6 : 5;
+        }
+        if (mode == 6) {  // two waves per block, 15-row slots (waves 0-1: as fast as 0-1 / 2-3 by block parity
+                          // and as 2 blocks/CU of four waves)
+            if (wave >= 2u) return;
+            const WaveRange wr = range(gridDim.x, 2u, wave);
+            rx_runs_pfx<R, V6, 15, false>(base, ofs, n, wr.a0, wr.a_end, lane,
+                                          lds_rx + wave * (PfxSlot<15>::kBytes / 16u), mrs, irs, trs);
+        } else if (mode == 5) {  // four waves per block, the hybrid loop
+            const WaveRange wr = range(gridDim.x, kWavesPerBlock, wave);
+            rx_runs_pfx<R, V6, 7, true>(base, ofs, n, wr.a0, wr.a_end, lane, lds_rx + wave * (PfxSlot<7>::kBytes / 16u),
+                                        mrs, irs, trs);
+        } else {  // streamed runs; a batch of large frames on 3 of the 4 blocks per CU
+            const uint32_t nb = active_blocks(ofs, n, kRxBigMean, sets == 0 ? 3u : 0u);
+            if (blockIdx.x >= nb) return;
+            const WaveRange wr = range(nb, kWavesPerBlock, wave);
+            rx_runs<R, V6, 1>(base, ofs, n, wr.a0, wr.a_end, lane, mrs, irs, trs);
+        }
+        return;
+    }
     // The grid is sized for small frames (4 blocks/CU); a batch of large ones streams on big_keep of them.
     const uint32_t nb = active_blocks(ofs, n, kRxBigMean, big_keep);
     if (blockIdx.x >= nb) return;
-    uint32_t a0, a_end;
-    uint64_t wave_bytes;
-    {
-        const uint32_t b = blockIdx.x, W = nb * kWavesPerBlock;
-        const uint32_t g = (nb >= 16 && (nb & 7) == 0) ? ((b & 7) * (nb >> 3) + (b >> 3)) * kWavesPerBlock + wave
-                                                        : b * kWavesPerBlock + wave;
-        const WaveRange wr = wave_range(ofs, n, g, W, lane, kRxSmallFrame, 8u);
-        a0 = wr.a0, a_end = wr.a_end, wave_bytes = wr.bytes;
+    const WaveRange wr = range(nb, kWavesPerBlock, wave);
+    const uint32_t a0 = wr.a0, a_end = wr.a_end;
+    if constexpr (PF > 0) {
+        if (sets == 3) {
+            rx_runs_pfx<R, V6, (uint32_t)PF, false>(base, ofs, n, a0, a_end, lane,
+                                                    lds_rx + wave * (PfxSlot<(uint32_t)PF>::kBytes / 16u), mrs, irs, trs);
+            return;
+        }
     }
-    const bool small = sets == 2 || (sets == 0 && wave_bytes < (uint64_t)kRxSmallFrame * (a_end - a0));
+    const bool small = sets == 2 || (sets == 0 && wr.bytes < (uint64_t)kRxSmallFrame * (a_end - a0));
     if (small) {
-        extern __shared__ lds16 lds_rx[];
         rx_runs_lds<R, V6>(base, ofs, n, a0, a_end, lane, lds_rx + wave * (kRxSlot / 16u), mrs, irs, trs);
     } else {
         rx_runs<R, V6, 1>(base, ofs, n, a0, a_end, lane, mrs, irs, trs);
@@ -2673,17 +2941,71 @@ hipError_t launch_rx_tcp(const LaunchCfg& c, int ipver, const void* d_base, cons
     // 0.1305 for batches of 4 rows, 0.1348 for single batches of 8 rows, 0.145 for 2 rows at 2 blocks/CU, 0.136
     // at 4); launches of ≤ 2^27 frames (a multiple of 64, so every launch starts on a mask word)
     const int rows = (c.rows == 2 || c.rows == 4 || c.rows == 8 || c.rows == 16) ? c.rows : 2;
-    // 64-frame sets per run: by each wave's mean frame size, or forced by segs_per_wave 1 / 4 (tests)
+    // Non-default shapes (below the default grid): per wave the LDS form or streamed runs of 64 frames, by each
+    // wave's mean frame size or forced by segs_per_wave 1 / 2; blocks_per_cu runs exactly that grid (default 3;
+    // the register-capped instantiation from 4 blocks/CU up).
     const int sets = c.segs_per_wave == 1 || c.segs_per_wave == 2 ? c.segs_per_wave : 0;
     const size_t lds = (size_t)kRxSlot * kWavesPerBlock;  // the LDS form's per-wave slots (3 blocks/CU: 100 KB)
-    // Default grid: 4 blocks/CU with the register-capped instantiation (≤ 128 VGPRs, four waves per SIMD), of
-    // which a batch of frames averaging ≥ kRxBigMean uses 3 (active_blocks; workload 10 keeps its 3 blocks/CU).
-    // A blocks_per_cu override runs exactly that grid (the capped instantiation from 4 blocks/CU up).
-    const bool pick = c.blocks_per_cu == 0 && rows == 2 && sets == 0;
-    const uint32_t mb = pick ? (uint32_t)c.cus * 4u : max_blocks_of(c, 3);
-    const uint32_t keep = pick ? 3u : 0u;
+    const uint32_t mb = max_blocks_of(c, 3);
+    const uint32_t keep = 0u;
     const bool w4 = rows == 2 && mb >= (uint32_t)c.cus * 4u;
     const uint8_t* base = static_cast<const uint8_t*>(d_base);
+    // The default shape (and the forms it picks, forced by segs_per_wave 5 / 6 for tests and A/B): the
+    // PF = -1 kernel at 4 blocks/CU, each block with two 15-row prefix slots of LDS (its four 7-row slots fit the
+    // same 38.5 KB), the mode chosen in-kernel by the batch's mean frame.
+    const bool auto_grid = rows == 2 && c.blocks_per_cu == 0 &&
+                           (c.segs_per_wave == 0 || c.segs_per_wave == 5 || c.segs_per_wave == 6);
+    if (auto_grid) {
+        constexpr size_t la = (size_t)PfxSlot<15>::kBytes * 2;
+        static_assert(la >= (size_t)PfxSlot<7>::kBytes * kWavesPerBlock && la * 4 <= 163840, "4 blocks per CU");
+        for (uint64_t c0 = 0; c0 < n; c0 += kRaggedChunk) {
+            const uint32_t cn = (uint32_t)(n - c0 < kRaggedChunk ? n - c0 : kRaggedChunk);
+            const uint32_t grid = grid_for((cn + kRxRun - 1) / kRxRun, (uint32_t)c.cus * 4u);
+            uint16_t* ic = ip_raw ? ip_raw + c0 : nullptr;
+            uint16_t* tc = tcp_raw ? tcp_raw + c0 : nullptr;
+            if (ipver == 6)
+                hipLaunchKernelGGL((rx_tcp_kernel<2, true, 4, -1>), dim3(grid), dim3(kBlock), la, st, base, d_offsets + c0,
+                                   cn, mask + c0 / 64, nullptr, tc, c.segs_per_wave, 0u);
+            else
+                hipLaunchKernelGGL((rx_tcp_kernel<2, false, 4, -1>), dim3(grid), dim3(kBlock), la, st, base,
+                                   d_offsets + c0, cn, mask + c0 / 64, ic, tc, c.segs_per_wave, 0u);
+            const hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
+    if (c.segs_per_wave == 3) {  // the prefix form: 4 / 3 / 2 blocks per CU with slots of 7 / 10 / 15 rows
+        const int bpc = c.blocks_per_cu == 2 || c.blocks_per_cu == 3 ? c.blocks_per_cu : 4;
+        for (uint64_t c0 = 0; c0 < n; c0 += kRaggedChunk) {
+            const uint32_t cn = (uint32_t)(n - c0 < kRaggedChunk ? n - c0 : kRaggedChunk);
+            const uint32_t grid = grid_for((cn + kRxRun - 1) / kRxRun, (uint32_t)(c.cus * bpc));
+            uint16_t* ic = ip_raw ? ip_raw + c0 : nullptr;
+            uint16_t* tc = tcp_raw ? tcp_raw + c0 : nullptr;
+#define NSX_RXP(B_)                                                                                                \
+            if (bpc == B_) {                                                                                       \
+                constexpr int pr = (int)pfx_rows_for(B_);                                                          \
+                const size_t lp = (size_t)PfxSlot<(uint32_t)pr>::kBytes * kWavesPerBlock;                                    \
+                if (ipver == 6) {                                                                                  \
+                    if (lp > 65536)                                                                        \
+                        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&rx_tcp_kernel<2, true, B_, pr>),   \
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lp);            \
+                    hipLaunchKernelGGL((rx_tcp_kernel<2, true, B_, pr>), dim3(grid), dim3(kBlock), lp, st, base,   \
+                                       d_offsets + c0, cn, mask + c0 / 64, nullptr, tc, 3, 0u);                                        \
+                } else {                                                                                           \
+                    if (lp > 65536)                                                                        \
+                        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&rx_tcp_kernel<2, false, B_, pr>),   \
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lp);            \
+                    hipLaunchKernelGGL((rx_tcp_kernel<2, false, B_, pr>), dim3(grid), dim3(kBlock), lp, st, base,   \
+                                       d_offsets + c0, cn, mask + c0 / 64, ic, tc, 3, 0u);                                             \
+                }                                                                                                  \
+            }
+            NSX_RXP(2) NSX_RXP(3) NSX_RXP(4)
+#undef NSX_RXP
+            const hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
     for (uint64_t c0 = 0; c0 < n; c0 += kRaggedChunk) {
         const uint32_t cn = (uint32_t)(n - c0 < kRaggedChunk ? n - c0 : kRaggedChunk);
         const uint32_t grid = grid_for((cn + kRxRun - 1) / kRxRun, mb);

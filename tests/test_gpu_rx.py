@@ -48,15 +48,22 @@ def test_rx_mixed_batches(n, lead):
     rng = np.random.default_rng(n * 4 + lead)
     buf, offs, kinds = _rx.batch(rng, n, lead=lead, max_payload=1460)
     want = O.c_rx_ipv4_tcp(buf, offs)
-    got = run_rx(buf, offs)
-    for w, g, what in zip(want, got, ("mask", "ip_raw", "tcp_raw")):
-        assert np.array_equal(w, g), (what, n, lead)
+    for tune in [None] + PFX:
+        got = run_rx(buf, offs, tune)
+        for w, g, what in zip(want, got, ("mask", "ip_raw", "tcp_raw")):
+            assert np.array_equal(w, g), (what, n, lead, tune)
 
 
 TUNES = [dict(rows=2), dict(rows=4), dict(rows=16), dict(blocks_per_cu=1), dict(blocks_per_cu=8), dict(rows=16, blocks_per_cu=1),
          dict(segs_per_wave=1), dict(segs_per_wave=1, rows=4), dict(segs_per_wave=1, blocks_per_cu=4),  # streamed runs
          dict(segs_per_wave=2), dict(segs_per_wave=2, blocks_per_cu=1), dict(segs_per_wave=2, blocks_per_cu=4),
-         dict(segs_per_wave=2, blocks_per_cu=8), dict(blocks_per_cu=4)]  # LDS form; 4 blocks/CU = the capped kernel
+         dict(segs_per_wave=2, blocks_per_cu=8), dict(blocks_per_cu=4),  # LDS form; 4 blocks/CU = the capped kernel
+         dict(segs_per_wave=3), dict(segs_per_wave=3, blocks_per_cu=3), dict(segs_per_wave=3, blocks_per_cu=2),  # prefix
+         dict(segs_per_wave=5), dict(segs_per_wave=6)]  # the default grid's modes, forced
+# the prefix form at each forced grid, and the default grid's modes forced (5 hybrid loop on four waves, 6 the
+# 15-row prefix form on two waves per block)
+PFX = [dict(segs_per_wave=3), dict(segs_per_wave=3, blocks_per_cu=3), dict(segs_per_wave=3, blocks_per_cu=2),
+       dict(segs_per_wave=5), dict(segs_per_wave=6)]
 
 
 @pytest.mark.parametrize("n", [1, 255, 256, 257, 1000, 30_001])
@@ -68,7 +75,7 @@ def test_rx_small_frames_runs_of_four_sets(n, lead):
     rng = np.random.default_rng(n * 2 + lead)
     buf, offs, _ = _rx.batch(rng, n, lead=lead, max_payload=40)
     want = O.c_rx_ipv4_tcp(buf, offs)
-    for tune in (None, dict(segs_per_wave=1), dict(segs_per_wave=2), dict(blocks_per_cu=3)):
+    for tune in [None, dict(segs_per_wave=1), dict(segs_per_wave=2), dict(blocks_per_cu=3)] + PFX:
         got = run_rx(buf, offs, tune)
         for w, g, what in zip(want, got, ("mask", "ip_raw", "tcp_raw")):
             assert np.array_equal(w, g), (what, n, lead, tune)
@@ -115,14 +122,14 @@ def test_rx_small_frames_300K_every_set_form_vs_oracle(ipver):
     assert 0.85 * n < bits.sum() < 0.985 * n  # mostly valid, every kind of failure present
     for tune in (None, dict(segs_per_wave=1), dict(segs_per_wave=2), dict(blocks_per_cu=1), dict(blocks_per_cu=3),
                  dict(blocks_per_cu=1, segs_per_wave=1), dict(blocks_per_cu=1, segs_per_wave=2),
-                 dict(blocks_per_cu=4, segs_per_wave=1)):
+                 dict(blocks_per_cu=4, segs_per_wave=1), *PFX):
         got = run_rx(buf_h, offs, tune) if ipver == 4 else run_rx6(buf_h, offs, tune)
         for wv, g, what in zip(want, got, ("mask", "ip_raw", "tcp_raw") if ipver == 4 else ("mask", "tcp_raw")):
             bad = np.nonzero(wv != g)[0]
             assert bad.size == 0, (what, tune, bad[:5])
 
 
-@pytest.mark.parametrize("config", [13, 14, 16, 17])
+@pytest.mark.parametrize("config", [13, 14, 16, 17, 18])
 def test_rx_small_frame_bench_workloads_full_size(config):
     """The bench's small-frame receive workloads at full size (13: 8M IPv4 frames of 40-100 B; 14: 2M frames, half
     40-66 B ACKs and half 1500 B; 16: 8M IPv6 packets of 60-120 B; 17: 8M frames, 95% ACKs and 5% 1500 B — equal-count
@@ -142,6 +149,24 @@ def test_rx_small_frame_bench_workloads_full_size(config):
     pad = np.zeros((n + 63) // 64 * 64, np.uint8)
     pad[:n] = valid
     assert np.array_equal(got, np.packbits(pad, bitorder="little").view(np.uint64))
+
+
+@pytest.mark.parametrize("config", [10, 13, 14, 16, 17, 18])
+def test_rx_prefix_form_bench_workloads_full_size(config):
+    """The prefix form on the bench's receive workloads at full size, at each of its grids
+    (4 / 3 / 2 blocks per CU with 7 / 10 / 15-row slots): pieces cut at every multiple of 8 frames, whole runs, the
+    streamed fallback; mask and raw sums against the oracle on every frame."""
+    import bench
+    cfg = bench.WORKLOADS[config]
+    w = bench.build_workload(cfg, 0, torch.device("cuda", 0))
+    buf_h = host(w["buf"])
+    v6 = cfg.get("ipver") == 6
+    want = (O.c_rx_ipv6_tcp if v6 else O.c_rx_ipv4_tcp)(buf_h, w["offsets"])
+    for tune in PFX:
+        got = run_rx6(buf_h, w["offsets"], tune) if v6 else run_rx(buf_h, w["offsets"], tune)
+        for wv, g, what in zip(want, got, ("mask", "tcp_raw") if v6 else ("mask", "ip_raw", "tcp_raw")):
+            bad = np.nonzero(wv != g)[0]
+            assert bad.size == 0, (what, config, tune, bad[:5])
 
 
 @pytest.mark.parametrize("tune", TUNES, ids=lambda t: ",".join(f"{k}={v}" for k, v in t.items()))
@@ -173,9 +198,10 @@ def test_rx_mostly_valid_large_frames_and_junk():
     offs[1:] = np.cumsum([len(f) for f in frames])
     buf = np.frombuffer(b"".join(frames) + bytes(3), np.uint8)
     want = O.c_rx_ipv4_tcp(buf, offs)
-    got = run_rx(buf, offs)
-    for w, g in zip(want, got):
-        assert np.array_equal(w, g)
+    for tune in [None] + PFX:  # the prefix form streams the pieces whose first 8 frames exceed its slot
+        got = run_rx(buf, offs, tune)
+        for w, g in zip(want, got):
+            assert np.array_equal(w, g), tune
     bits = np.unpackbits(want[0].view(np.uint8), bitorder="little")
     assert bits[:len(frames)].sum() == sum(1 for i, f in enumerate(frames) if len(f) and i != 350)
 
@@ -240,9 +266,10 @@ def test_rx6_mixed_batches(n, lead):
     rng = np.random.default_rng(n * 8 + lead + 1)
     buf, offs, kinds = _rx.batch(rng, n, kinds=_rx.KINDS6, lead=lead, max_payload=1440, ip=6)
     want = O.c_rx_ipv6_tcp(buf, offs)
-    got = run_rx6(buf, offs)
-    for w, g, what in zip(want, got, ("mask", "tcp_raw")):
-        assert np.array_equal(w, g), (what, n, lead)
+    for tune in [None] + PFX:
+        got = run_rx6(buf, offs, tune)
+        for w, g, what in zip(want, got, ("mask", "tcp_raw")):
+            assert np.array_equal(w, g), (what, n, lead, tune)
 
 
 @pytest.mark.parametrize("tune", TUNES, ids=lambda t: ",".join(f"{k}={v}" for k, v in t.items()))
@@ -273,9 +300,10 @@ def test_rx6_maximum_packets_and_junk():
     offs[1:] = np.cumsum([len(f) for f in frames])
     buf = np.frombuffer(b"".join(frames) + bytes(3), np.uint8)
     want = O.c_rx_ipv6_tcp(buf, offs)
-    got = run_rx6(buf, offs)
-    for w, g in zip(want, got):
-        assert np.array_equal(w, g)
+    for tune in [None] + PFX:
+        got = run_rx6(buf, offs, tune)
+        for w, g in zip(want, got):
+            assert np.array_equal(w, g), tune
     bits = np.unpackbits(want[0].view(np.uint8), bitorder="little")
     assert bits[:len(frames)].sum() == sum(1 for i, f in enumerate(frames) if len(f) and i != 250)
 

@@ -41,7 +41,7 @@ def main():
         cfg["n"] = a.n
     for kv in a.set:
         k, _, v = kv.partition("=")
-        cfg[k] = int(v)
+        cfg[k] = float(v) if "." in v else int(v)
     w = bench.build_workload(cfg, 0, torch.device("cuda", 0))
     variants = []
     for item in a.variants.split(";"):

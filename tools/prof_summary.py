@@ -78,7 +78,7 @@ def main(tag, cfg, kernel_substr="csum"):
 
 
 KERNEL_OF_CONFIG = {6: "tcp_build", 7: "ipv4_hdr", 8: "tcp_build", 9: "ipv4_hdr", 10: "rx_tcp", 11: "rx_tcp", 12: "tcp_build",
-                    13: "rx_tcp", 14: "rx_tcp", 16: "rx_tcp", 17: "rx_tcp"}  # bench.py workloads beyond the checksum configs
+                    13: "rx_tcp", 14: "rx_tcp", 16: "rx_tcp", 17: "rx_tcp", 18: "rx_tcp"}  # bench.py workloads beyond the checksum configs
 
 if __name__ == "__main__":
     c = int(sys.argv[2])

@@ -23,7 +23,7 @@ step() {  # step <name> <timeout> cmd...
 case $mode in
   prof)
     mkdir -p gpurun_out/profiles
-    for c in ${1:-2 3 10 11 13 14 15 16 17}; do
+    for c in ${1:-2 3 10 11 13 14 15 16 17 18}; do
       GROUPS_ONLY="kt fetch write" bash tools/profile.sh $c r03 || exit 1
       python3 tools/prof_summary.py r03 $c > /dev/null || exit 1
       cp profiles/r03_config${c}.md profiles/r03_config${c}_kernel_stats.csv profiles/traffic_config${c}.json \
@@ -36,7 +36,7 @@ case $mode in
     { nproc; python3 -c "import os; print('affinity', len(os.sched_getaffinity(0)), 'cpu_count', os.cpu_count())";
       cat /sys/fs/cgroup/cpu.max 2>/dev/null; echo "OMP_NUM_THREADS=${OMP_NUM_THREADS:-}";
       lscpu | grep -E "Model name|^CPU\(s\)|Thread|Core|Socket"; } > gpurun_out/r03ev/host.txt 2>&1
-    for c in ${1:-tests 2 3 4 5 6 7 8 9 10 11 12 13 14 15 16 17}; do
+    for c in ${1:-tests 2 3 4 5 6 7 8 9 10 11 12 13 14 15 16 17 18}; do
       case $c in
         tests) step pytest_gpu 900 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider
                step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
@@ -57,7 +57,7 @@ case $mode in
     done
     ;;
   same)
-    bash tools/same_run_profile.sh r03 ${1:-2 3 4 5 6 7 8 9 10 11 12 13 14 15 16 17} || exit $?
+    bash tools/same_run_profile.sh r03 ${1:-2 3 4 5 6 7 8 9 10 11 12 13 14 15 16 17 18} || exit $?
     ;;
 esac
 echo done
