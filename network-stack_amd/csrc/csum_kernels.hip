@@ -1297,15 +1297,21 @@ constexpr uint32_t kRxSmallFrame = 128;
 // 170 B mean, 3.4% at 320 B, 0.4% at 520 B; 3 blocks 2.9% faster at workload 10's 770 B)
 constexpr uint32_t kRxBigMean = 640;
 
-// Per-frame verdict of the receive pass, shared by the streaming and the LDS forms. F = the frame's weighted byte
-// sum (exact; weights 1 / 256 at even / odd addresses, the LE half-sum rule); d[0..5] = the dwords from the
-// frame's start rounded down to 4 B (hd = start & 3; IPv6 reads d[0..2]); opt(o) fills the IPv4 option dwords
-// 6..15, called only when some lane has IHL > 5. Writes the run's mask bytes and the raw sums.
+// Per-frame verdict of the receive pass, shared by every form, in two halves: rx_hdr parses the frame's header
+// window and sums its header (what a form must take while the window is at hand), rx_verdict takes the frame's
+// weighted byte sum F (exact; weights 1 / 256 at even / odd addresses, the LE half-sum rule) and writes the run's
+// mask bytes and the raw sums. d[0..5] = the dwords from the frame's start rounded down to 4 B (hd = start & 3;
+// IPv6 reads d[0..2]); opt(o) fills the IPv4 option dwords 6..15, called only when some lane has IHL > 5.
+struct RxHdr {
+    uint32_t hs;   // the header's weighted sum (IPv6: bytes 0-7), subtracted from F when hdr_ok
+    uint32_t aux;  // the pseudo-header's words not in F: IPv4 src + dst + 6 + TCP length; IPv6 payload length + 6
+    uint32_t ipr;  // IPv4 header raw sum (0 unless hdr_ok)
+    bool hdr_ok, well;
+};
+
 template <bool V6, typename OptFn>
-__device__ __forceinline__ void rx_frame_out(uint64_t F, const uint32_t (&d)[6], uint32_t hd, uint64_t flen, bool even,
-                                             bool live, uint32_t ak, uint32_t cnt, uint32_t n, uint32_t lane,
-                                             __amdgpu_buffer_rsrc_t mrs, __amdgpu_buffer_rsrc_t irs,
-                                             __amdgpu_buffer_rsrc_t trs, OptFn&& opt, uint32_t s = 0) {
+__device__ __forceinline__ RxHdr rx_hdr(const uint32_t (&d)[6], uint32_t hd, uint64_t flen, bool even, bool live,
+                                        OptFn&& opt) {
     if constexpr (V6) {
         const uint32_t H0 = __builtin_amdgcn_alignbyte(d[1], d[0], hd);  // version, class, flow label
         const uint32_t H1 = __builtin_amdgcn_alignbyte(d[2], d[1], hd);  // payload length, next header
@@ -1315,12 +1321,7 @@ __device__ __forceinline__ void rx_frame_out(uint64_t F, const uint32_t (&d)[6],
         const uint32_t rot = hd & 1u;  // see the IPv4 header sum below
         const uint32_t h8 = __builtin_amdgcn_sad_u16(__builtin_amdgcn_alignbyte(H1, H1, rot), 0u,
                                                      __builtin_amdgcn_sad_u16(__builtin_amdgcn_alignbyte(H0, H0, rot), 0u, 0u));
-        const uint64_t T = F - h8;  // addresses ‖ segment
-        const uint32_t tle = fold32((uint32_t)T) + fold32((uint32_t)(T >> 32));
-        const uint32_t tcpr = well ? finish(tle, even, plen + 6u) : 0u;
-        const uint64_t bits = __builtin_amdgcn_ballot_w64(well && tcpr == 0xFFFFu);
-        rx_store_mask(mrs, bits, ak, cnt, n, lane, s);
-        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)tcpr, trs, live ? (ak + lane) * 2u : kOOB, 0, 0);
+        return RxHdr{h8, plen + 6u, 0u, true, well};  // F − h8 = addresses ‖ segment
     } else {
         // IPv4 header fields (RFC 791 §3.1): header dword m = bytes 4m..4m+3, little-endian view.
         const uint32_t H0 = __builtin_amdgcn_alignbyte(d[1], d[0], hd);
@@ -1356,19 +1357,35 @@ __device__ __forceinline__ void rx_frame_out(uint64_t F, const uint32_t (&d)[6],
             }
         }
         const uint32_t ipr = hdr_ok ? finish(hs, even, 0u) : 0u;
-        const uint64_t T = F - (hdr_ok ? hs : 0u);  // the TCP segment's weighted sum
-        const uint32_t tle = fold32((uint32_t)T) + fold32((uint32_t)(T >> 32));
         // Pseudo-header source and destination (header dwords 3-4) as BE words: Σ bswap16(half) = the v_sad_u16
         // of the dword rotated one byte.
         const uint32_t pseudo = __builtin_amdgcn_sad_u16(
             __builtin_amdgcn_alignbyte(H4, H4, 1u), 0u,
             __builtin_amdgcn_sad_u16(__builtin_amdgcn_alignbyte(H3, H3, 1u), 0u, 6u + ((total - hlen) & 0xFFFFu)));
-        const uint32_t tcpr = well ? finish(tle, even, pseudo) : 0u;
-        const uint64_t bits = __builtin_amdgcn_ballot_w64(well && ipr == 0xFFFFu && tcpr == 0xFFFFu);
-        rx_store_mask(mrs, bits, ak, cnt, n, lane, s);
-        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ipr, irs, live ? (ak + lane) * 2u : kOOB, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)tcpr, trs, live ? (ak + lane) * 2u : kOOB, 0, 0);
+        return RxHdr{hs, pseudo, ipr, hdr_ok, well};
     }
+}
+
+template <bool V6>
+__device__ __forceinline__ void rx_verdict(uint64_t F, const RxHdr& h, bool even, bool live, uint32_t ak, uint32_t cnt,
+                                           uint32_t n, uint32_t lane, __amdgpu_buffer_rsrc_t mrs,
+                                           __amdgpu_buffer_rsrc_t irs, __amdgpu_buffer_rsrc_t trs, uint32_t s) {
+    const uint64_t T = F - (h.hdr_ok ? h.hs : 0u);  // the TCP segment's weighted sum (IPv6: addresses ‖ segment)
+    const uint32_t tle = fold32((uint32_t)T) + fold32((uint32_t)(T >> 32));
+    const uint32_t tcpr = h.well ? finish(tle, even, h.aux) : 0u;
+    const uint64_t bits = __builtin_amdgcn_ballot_w64(h.well && (V6 || h.ipr == 0xFFFFu) && tcpr == 0xFFFFu);
+    rx_store_mask(mrs, bits, ak, cnt, n, lane, s);
+    if constexpr (!V6)
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)h.ipr, irs, live ? (ak + lane) * 2u : kOOB, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)tcpr, trs, live ? (ak + lane) * 2u : kOOB, 0, 0);
+}
+
+template <bool V6, typename OptFn>
+__device__ __forceinline__ void rx_frame_out(uint64_t F, const uint32_t (&d)[6], uint32_t hd, uint64_t flen, bool even,
+                                             bool live, uint32_t ak, uint32_t cnt, uint32_t n, uint32_t lane,
+                                             __amdgpu_buffer_rsrc_t mrs, __amdgpu_buffer_rsrc_t irs,
+                                             __amdgpu_buffer_rsrc_t trs, OptFn&& opt, uint32_t s = 0) {
+    rx_verdict<V6>(F, rx_hdr<V6>(d, hd, flen, even, live, opt), even, live, ak, cnt, n, lane, mrs, irs, trs, s);
 }
 
 // One run of NS sets of ≤ 64 frames in the streaming form: frame a + 64k + lane = [my_off[k], my_end[k]) for
