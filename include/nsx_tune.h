@@ -45,10 +45,9 @@ typedef struct nsx_tune {
                                   else streamed runs on 3 blocks/CU; 5 / 6 force the hybrid loop / the
                                   two-wave prefix form on that grid. With rows or blocks_per_cu set (the
                                   pre-prefix shapes): 0 = per wave the LDS form (mean < 128 B) or streamed
-                                  runs, 1 = streamed runs, 2 = the LDS form, 3 = the prefix form with the
-                                  grid's slot (blocks_per_cu 4 / 3 / 2: 7 / 10 / 15 KiB, default 4). (A run
-                                  that does not fit the LDS form's 8 KiB slot, or a piece whose first 8
-                                  frames exceed the prefix form's slot, is streamed.) */
+                                  runs, 1 = streamed runs, 2 = the LDS form. (A run that does not fit the
+                                  LDS form's 8 KiB slot, or a piece whose first 8 frames exceed the prefix
+                                  form's slot, is streamed.) */
     int32_t block_mode;        /* 0 auto (a block per segment when n < 4 * CUs), 1 never, 2 always */
     int32_t rows;              /* ragged scan / receive kernels: 1 KiB rows per load batch (4, 8, 16) */
     int32_t run_segs;          /* segments per wave task: ragged scan kernel 1..63, TCP build 1..64 */

@@ -1033,8 +1033,8 @@ struct PfxSlot {
     static constexpr uint32_t kPrefix = kData + 64u;  // byte offset of I
     static constexpr uint32_t kBytes = (kPrefix + (ROWS * kWave + 1u) * 4u + 15u) & ~15u;
 };
-// 4 blocks/CU: 7 rows (16 × 9040 B = 141 KiB of the CU's 160); 3 blocks/CU: 10 rows; 2 blocks/CU: 15 rows.
-constexpr uint32_t pfx_rows_for(uint32_t blocks_per_cu) { return blocks_per_cu >= 4 ? 7u : blocks_per_cu == 3 ? 10u : 15u; }
+// The default receive grid (4 blocks/CU, §7 step 55) holds four 7-row slots (9040 B) or two 15-row slots (19280 B)
+// per block.
 // The hybrid loop's direct pieces: a whole run in the LDS form's 8 rows (+ 256 B pad, kScanSlot = kRxSlot).
 constexpr uint32_t kPfxDirectRows = 8;
 constexpr uint32_t kPfxDirectSlot = kPfxDirectRows * kRow + 256;
@@ -1669,15 +1669,16 @@ __device__ __forceinline__ void rx_runs_pfx(const uint8_t* __restrict__ base, __
 // block (8 waves per CU, ~19 KB of LDS each); m ≥ kRxBigMean: streamed runs on 3 blocks per CU.
 constexpr uint32_t kRxPfxMean = 112;
 
-// sets: 0 = by the wave's mean frame size (the LDS form below kRxSmallFrame, else streamed runs of one 64-frame
-// set); 1 = force the streamed runs; 2 = force the LDS form; 3 = the prefix form (PF rows per slot). (Round 2's
-// streamed runs of four sets for small frames, §7 step 41, were removed: the LDS form beat them by 30-40% on every
-// small-frame mix, §7 step 43.)
+// PF = -1: the default grid's kernel (4 blocks/CU, PfxSlot<15> × 2 of LDS per block): sets 0 = by the batch's mean
+// frame (kRxPfxMean, kRxBigMean above), 1 = streamed runs, 5 = the hybrid loop on four waves, 6 = the 15-row prefix
+// form on waves 0-1. (The prefix form at 3 and 2 blocks per CU, forced by sets 3 in §7 step 54, was removed once
+// the default grid held both of its slots.)
+// PF = 0: the shapes set by rows / blocks_per_cu: sets 0 = by the wave's mean frame size (the LDS form below
+// kRxSmallFrame, else streamed runs of one 64-frame set); 1 = force the streamed runs; 2 = force the LDS form.
+// (Round 2's streamed runs of four sets for small frames, §7 step 41, were removed: the LDS form beat them by
+// 30-40% on every small-frame mix, §7 step 43.)
 // WPS: waves per SIMD the registers must allow (__launch_bounds__'s second argument): 1 = no constraint (158 VGPRs,
-// 3 waves per SIMD at the default 3 blocks/CU); 4 = the 4-blocks/CU instantiation (≤ 128 VGPRs).
-// PF: 0 = no prefix form compiled in; > 0 = the prefix form with PF-row slots when sets == 3; -1 = the default
-// grid's kernel (4 blocks/CU, PfxSlot<15> × 2 of LDS per block): sets 0 = by the batch's mean frame (kRxPfxMean,
-// kRxBigMean above), 1 = streamed runs, 5 = the hybrid loop on four waves, 6 = the 15-row prefix form on waves 0-1.
+// 3 waves per SIMD at the default 3 blocks/CU); 4 = the 4-blocks/CU instantiations (≤ 128 VGPRs).
 template <int R, bool V6, int WPS, int PF = 0>
 __global__ __launch_bounds__(kBlock, WPS) void rx_tcp_kernel(const uint8_t* __restrict__ base,
                                                              const uint64_t* __restrict__ offsets, uint32_t n,
@@ -1730,13 +1731,6 @@ __global__ __launch_bounds__(kBlock, WPS) void rx_tcp_kernel(const uint8_t* __re
     if (blockIdx.x >= nb) return;
     const WaveRange wr = range(nb, kWavesPerBlock, wave);
     const uint32_t a0 = wr.a0, a_end = wr.a_end;
-    if constexpr (PF > 0) {
-        if (sets == 3) {
-            rx_runs_pfx<R, V6, (uint32_t)PF, false>(base, ofs, n, a0, a_end, lane,
-                                                    lds_rx + wave * (PfxSlot<(uint32_t)PF>::kBytes / 16u), mrs, irs, trs);
-            return;
-        }
-    }
     const bool small = sets == 2 || (sets == 0 && wr.bytes < (uint64_t)kRxSmallFrame * (a_end - a0));
     if (small) {
         rx_runs_lds<R, V6>(base, ofs, n, a0, a_end, lane, lds_rx + wave * (kRxSlot / 16u), mrs, irs, trs);
@@ -2986,38 +2980,6 @@ hipError_t launch_rx_tcp(const LaunchCfg& c, int ipver, const void* d_base, cons
             else
                 hipLaunchKernelGGL((rx_tcp_kernel<2, false, 4, -1>), dim3(grid), dim3(kBlock), la, st, base,
                                    d_offsets + c0, cn, mask + c0 / 64, ic, tc, c.segs_per_wave, 0u);
-            const hipError_t e = hipGetLastError();
-            if (e != hipSuccess) return e;
-        }
-        return hipSuccess;
-    }
-    if (c.segs_per_wave == 3) {  // the prefix form: 4 / 3 / 2 blocks per CU with slots of 7 / 10 / 15 rows
-        const int bpc = c.blocks_per_cu == 2 || c.blocks_per_cu == 3 ? c.blocks_per_cu : 4;
-        for (uint64_t c0 = 0; c0 < n; c0 += kRaggedChunk) {
-            const uint32_t cn = (uint32_t)(n - c0 < kRaggedChunk ? n - c0 : kRaggedChunk);
-            const uint32_t grid = grid_for((cn + kRxRun - 1) / kRxRun, (uint32_t)(c.cus * bpc));
-            uint16_t* ic = ip_raw ? ip_raw + c0 : nullptr;
-            uint16_t* tc = tcp_raw ? tcp_raw + c0 : nullptr;
-#define NSX_RXP(B_)                                                                                                \
-            if (bpc == B_) {                                                                                       \
-                constexpr int pr = (int)pfx_rows_for(B_);                                                          \
-                const size_t lp = (size_t)PfxSlot<(uint32_t)pr>::kBytes * kWavesPerBlock;                                    \
-                if (ipver == 6) {                                                                                  \
-                    if (lp > 65536)                                                                        \
-                        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&rx_tcp_kernel<2, true, B_, pr>),   \
-                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lp);            \
-                    hipLaunchKernelGGL((rx_tcp_kernel<2, true, B_, pr>), dim3(grid), dim3(kBlock), lp, st, base,   \
-                                       d_offsets + c0, cn, mask + c0 / 64, nullptr, tc, 3, 0u);                                        \
-                } else {                                                                                           \
-                    if (lp > 65536)                                                                        \
-                        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&rx_tcp_kernel<2, false, B_, pr>),   \
-                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lp);            \
-                    hipLaunchKernelGGL((rx_tcp_kernel<2, false, B_, pr>), dim3(grid), dim3(kBlock), lp, st, base,   \
-                                       d_offsets + c0, cn, mask + c0 / 64, ic, tc, 3, 0u);                                             \
-                }                                                                                                  \
-            }
-            NSX_RXP(2) NSX_RXP(3) NSX_RXP(4)
-#undef NSX_RXP
             const hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }

@@ -58,12 +58,9 @@ TUNES = [dict(rows=2), dict(rows=4), dict(rows=16), dict(blocks_per_cu=1), dict(
          dict(segs_per_wave=1), dict(segs_per_wave=1, rows=4), dict(segs_per_wave=1, blocks_per_cu=4),  # streamed runs
          dict(segs_per_wave=2), dict(segs_per_wave=2, blocks_per_cu=1), dict(segs_per_wave=2, blocks_per_cu=4),
          dict(segs_per_wave=2, blocks_per_cu=8), dict(blocks_per_cu=4),  # LDS form; 4 blocks/CU = the capped kernel
-         dict(segs_per_wave=3), dict(segs_per_wave=3, blocks_per_cu=3), dict(segs_per_wave=3, blocks_per_cu=2),  # prefix
          dict(segs_per_wave=5), dict(segs_per_wave=6)]  # the default grid's modes, forced
-# the prefix form at each forced grid, and the default grid's modes forced (5 hybrid loop on four waves, 6 the
-# 15-row prefix form on two waves per block)
-PFX = [dict(segs_per_wave=3), dict(segs_per_wave=3, blocks_per_cu=3), dict(segs_per_wave=3, blocks_per_cu=2),
-       dict(segs_per_wave=5), dict(segs_per_wave=6)]
+# the default grid's modes forced (5 the hybrid loop on four waves, 6 the 15-row prefix form on two waves per block)
+PFX = [dict(segs_per_wave=5), dict(segs_per_wave=6)]
 
 
 @pytest.mark.parametrize("n", [1, 255, 256, 257, 1000, 30_001])
@@ -153,9 +150,10 @@ def test_rx_small_frame_bench_workloads_full_size(config):
 
 @pytest.mark.parametrize("config", [10, 13, 14, 16, 17, 18])
 def test_rx_prefix_form_bench_workloads_full_size(config):
-    """The prefix form on the bench's receive workloads at full size, at each of its grids
-    (4 / 3 / 2 blocks per CU with 7 / 10 / 15-row slots): pieces cut at every multiple of 8 frames, whole runs, the
-    streamed fallback; mask and raw sums against the oracle on every frame."""
+    """The default grid's forms forced on the bench's receive workloads at full size:
+    the hybrid loop (direct runs and 7-row prefix pieces) and the 15-row prefix form on two waves per block —
+    pieces cut at every multiple of 8 frames, whole runs, the streamed fallback; mask and raw sums against the
+    oracle on every frame."""
     import bench
     cfg = bench.WORKLOADS[config]
     w = bench.build_workload(cfg, 0, torch.device("cuda", 0))
