@@ -39,11 +39,12 @@ typedef struct nsx_tune {
                                   in every wave. Only the default pipelined 2-row shape has more than one
                                   set: with kernel = SCAN_PLAIN or rows != 2 a 4 gives runs of one set.
                                   Receive kernels: 0 auto = the default grid (4 blocks/CU) choosing by the
-                                  batch's mean frame: < 112 B the hybrid loop (whole runs of <= 256 B
-                                  frames that fit 8 KiB in the LDS form, else prefix-form pieces of <= 7
-                                  KiB), < 640 B the prefix form with 15 KiB slots on two waves per block,
-                                  else streamed runs on 3 blocks/CU; 5 / 6 force the hybrid loop / the
-                                  two-wave prefix form on that grid. With rows or blocks_per_cu set (the
+                                  batch's mean frame: < 112 B the LDS form for whole runs of <= 256 B
+                                  frames that fit 8 KiB, switching at the first other run to the hybrid
+                                  loop (such runs as prefix-form pieces of <= 7 KiB), < 640 B the prefix
+                                  form with 15 KiB slots on two waves per block, else streamed runs on 3
+                                  blocks/CU; 5 / 6 / 7 force the small-frame mode / the two-wave prefix
+                                  form / the hybrid loop throughout on that grid. With rows or blocks_per_cu set (the
                                   pre-prefix shapes): 0 = per wave the LDS form (mean < 128 B) or streamed
                                   runs, 1 = streamed runs, 2 = the LDS form. (A run that does not fit the
                                   LDS form's 8 KiB slot, or a piece whose first 8 frames exceed the prefix

@@ -1526,6 +1526,37 @@ __device__ __forceinline__ void rx_runs(const uint8_t* __restrict__ base, __amdg
 constexpr uint32_t kRxSlotRows = 8;
 constexpr uint32_t kRxSlot = kRxSlotRows * kRow + 256;  // + pad: a header window or chunk block read past the end
 
+// The receive pass in the prefix form (pfx_runs: pieces cut at whole mask bytes; the header window from the slot).
+template <int R, bool V6, uint32_t ROWS, bool HYB>
+__device__ __forceinline__ void rx_runs_pfx(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
+                                            uint32_t a0, uint32_t a_end, uint32_t lane, lds16* slot,
+                                            __amdgpu_buffer_rsrc_t mrs, __amdgpu_buffer_rsrc_t irs,
+                                            __amdgpu_buffer_rsrc_t trs) {
+    static_assert(kPfxRun == kRxRun && kPfxDirectSlot == kRxSlot, "the receive pass's runs and direct slot");
+    const uint32_t* sdw = reinterpret_cast<const uint32_t*>(slot);
+    auto out = [&](uint64_t F, uint32_t p, uint32_t d0, bool live, uint32_t a, uint32_t s, uint32_t cnt, uint64_t off,
+                   uint64_t end) {
+        const uint32_t w0 = p >> 2;
+        uint32_t d[6];
+        d[0] = d0;
+#pragma unroll
+        for (int j = 1; j < (V6 ? 3 : 6); ++j) d[j] = sdw[w0 + j];
+        if constexpr (V6) d[3] = d[4] = d[5] = 0u;
+        auto opt = [&](uint32_t (&o)[10]) {
+#pragma unroll
+            for (int j = 6; j < 16; ++j) o[j - 6] = sdw[w0 + j];
+        };
+        rx_frame_out<V6>(F, d, p & 3u, end - off, (p & 1u) == 0, live, a, cnt, n, lane, mrs, irs, trs, opt, s);
+    };
+    auto stream = [&](uint32_t a, uint32_t s, uint32_t rem, uint64_t off, uint64_t end) {  // lanes shifted by s
+        uint32_t cnt1[1] = {rem};
+        uint64_t o1[1] = {(uint64_t)__shfl_down((unsigned long long)off, s)};
+        uint64_t e1[1] = {(uint64_t)__shfl_down((unsigned long long)end, s)};
+        rx_run_stream<R, V6, 1>(base, a + s, cnt1, o1, e1, 0u, n, lane, mrs, irs, trs);
+    };
+    pfx_runs<ROWS, HYB, 8u>(base, ofs, n, a0, a_end, lane, slot, out, stream);
+}
+
 template <bool V6>
 __device__ __forceinline__ void rx_run_lds(const uint8_t* __restrict__ base, const uint8_t* rbase, uint32_t a,
                                            uint32_t cnt, uint64_t my_off, uint64_t my_end, uint32_t n, uint32_t lane,
@@ -1550,7 +1581,10 @@ __device__ __forceinline__ void rx_run_lds(const uint8_t* __restrict__ base, con
 }
 
 // A wave's runs [a0, a_end) in the LDS form (runs of 64 frames from a multiple of 8, as rx_runs).
-template <int R, bool V6>
+// SW (the default grid's small-frame mode, §7 step 59): a run that is not a direct run — too wide for the slot, or
+// holding a frame over kPfxDirectMax bytes, which one lane would sum alone — hands the rest of the wave's range to the
+// hybrid loop (rx_runs_pfx<·, 7, true>) instead of being streamed; waves of ACKs alone stay in this tighter loop.
+template <int R, bool V6, bool SW = false>
 __device__ __forceinline__ void rx_runs_lds(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
                                             uint32_t a0, uint32_t a_end, uint32_t lane, lds16* slot,
                                             __amdgpu_buffer_rsrc_t mrs, __amdgpu_buffer_rsrc_t irs,
@@ -1573,6 +1607,7 @@ __device__ __forceinline__ void rx_runs_lds(const uint8_t* __restrict__ base, __
             g.rbase = reinterpret_cast<const uint8_t*>(((uintptr_t)(base + lo)) & ~(uintptr_t)127);
             g.span = (uint64_t)((base + hi) - g.rbase);
             g.lds = g.span <= (uint64_t)kRxSlotRows * kRow;
+            if constexpr (SW) g.lds = g.lds && !__builtin_amdgcn_ballot_w64(lane < g.cnt && end - off > kPfxDirectMax);
         }
         return g;
     };
@@ -1593,6 +1628,10 @@ __device__ __forceinline__ void rx_runs_lds(const uint8_t* __restrict__ base, __
     uint64_t c_end = load_off(a + lane + 1u, a < a_end && a + lane + 1u <= n);
     while (a < a_end) {
         Run cur = geo(a, c_off, c_end);
+        if (SW && !cur.lds) {
+            rx_runs_pfx<R, V6, 7, true>(base, ofs, n, a, a_end, lane, slot, mrs, irs, trs);
+            return;
+        }
         if (!cur.lds) {  // a run too wide for the slot: the streaming form
             const uint32_t as = a + kRxRun;
             const uint64_t s_off = load_off(as + lane, as < a_end && as + lane <= n);
@@ -1632,46 +1671,17 @@ __device__ __forceinline__ void rx_runs_lds(const uint8_t* __restrict__ base, __
     }
 }
 
-// The receive pass in the prefix form (pfx_runs: pieces cut at whole mask bytes; the header window from the slot).
-template <int R, bool V6, uint32_t ROWS, bool HYB>
-__device__ __forceinline__ void rx_runs_pfx(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
-                                            uint32_t a0, uint32_t a_end, uint32_t lane, lds16* slot,
-                                            __amdgpu_buffer_rsrc_t mrs, __amdgpu_buffer_rsrc_t irs,
-                                            __amdgpu_buffer_rsrc_t trs) {
-    static_assert(kPfxRun == kRxRun && kPfxDirectSlot == kRxSlot, "the receive pass's runs and direct slot");
-    const uint32_t* sdw = reinterpret_cast<const uint32_t*>(slot);
-    auto out = [&](uint64_t F, uint32_t p, uint32_t d0, bool live, uint32_t a, uint32_t s, uint32_t cnt, uint64_t off,
-                   uint64_t end) {
-        const uint32_t w0 = p >> 2;
-        uint32_t d[6];
-        d[0] = d0;
-#pragma unroll
-        for (int j = 1; j < (V6 ? 3 : 6); ++j) d[j] = sdw[w0 + j];
-        if constexpr (V6) d[3] = d[4] = d[5] = 0u;
-        auto opt = [&](uint32_t (&o)[10]) {
-#pragma unroll
-            for (int j = 6; j < 16; ++j) o[j - 6] = sdw[w0 + j];
-        };
-        rx_frame_out<V6>(F, d, p & 3u, end - off, (p & 1u) == 0, live, a, cnt, n, lane, mrs, irs, trs, opt, s);
-    };
-    auto stream = [&](uint32_t a, uint32_t s, uint32_t rem, uint64_t off, uint64_t end) {  // lanes shifted by s
-        uint32_t cnt1[1] = {rem};
-        uint64_t o1[1] = {(uint64_t)__shfl_down((unsigned long long)off, s)};
-        uint64_t e1[1] = {(uint64_t)__shfl_down((unsigned long long)end, s)};
-        rx_run_stream<R, V6, 1>(base, a + s, cnt1, o1, e1, 0u, n, lane, mrs, irs, trs);
-    };
-    pfx_runs<ROWS, HYB, 8u>(base, ofs, n, a0, a_end, lane, slot, out, stream);
-}
 
 // The receive pass's grids by the batch's mean frame m (tools/r03_pfx_sweep.sh): m <
-// kRxPfxMean: four waves per block, the hybrid loop (direct pieces for runs of small frames that fit 8 KiB, prefix
-// pieces of ≤ 7 KiB otherwise); kRxPfxMean ≤ m < kRxBigMean: the prefix form with 15-row slots on two waves per
+// kRxPfxMean: four waves per block, the LDS loop for runs of small frames that fit 8 KiB, handing over at the first
+// other run to the hybrid loop (direct pieces for such runs, prefix pieces of ≤ 7 KiB otherwise; §7 step 59);
+// kRxPfxMean ≤ m < kRxBigMean: the prefix form with 15-row slots on two waves per
 // block (8 waves per CU, ~19 KB of LDS each); m ≥ kRxBigMean: streamed runs on 3 blocks per CU.
 constexpr uint32_t kRxPfxMean = 112;
 
 // PF = -1: the default grid's kernel (4 blocks/CU, PfxSlot<15> × 2 of LDS per block): sets 0 = by the batch's mean
-// frame (kRxPfxMean, kRxBigMean above), 1 = streamed runs, 5 = the hybrid loop on four waves, 6 = the 15-row prefix
-// form on waves 0-1. (The prefix form at 3 and 2 blocks per CU, forced by sets 3 in §7 step 54, was removed once
+// frame (kRxPfxMean, kRxBigMean above), 1 = streamed runs, 5 = the small-frame mode (LDS loop, then the hybrid
+// loop), 6 = the 15-row prefix form on waves 0-1, 7 = the hybrid loop throughout. (The prefix form at 3 and 2 blocks per CU, forced by sets 3 in §7 step 54, was removed once
 // the default grid held both of its slots.)
 // PF = 0: the shapes set by rows / blocks_per_cu: sets 0 = by the wave's mean frame size (the LDS form below
 // kRxSmallFrame, else streamed runs of one 64-frame set); 1 = force the streamed runs; 2 = force the LDS form.
@@ -1714,10 +1724,12 @@ __global__ __launch_bounds__(kBlock, WPS) void rx_tcp_kernel(const uint8_t* __re
             const WaveRange wr = range(gridDim.x, 2u, wave);
             rx_runs_pfx<R, V6, 15, false>(base, ofs, n, wr.a0, wr.a_end, lane,
                                           lds_rx + wave * (PfxSlot<15>::kBytes / 16u), mrs, irs, trs);
-        } else if (mode == 5) {  // four waves per block, the hybrid loop
+        } else if (mode == 5 || mode == 7) {  // four waves per block: the LDS loop until a run needs the hybrid
+                                              // loop (5), or the hybrid loop throughout (7)
             const WaveRange wr = range(gridDim.x, kWavesPerBlock, wave);
-            rx_runs_pfx<R, V6, 7, true>(base, ofs, n, wr.a0, wr.a_end, lane, lds_rx + wave * (PfxSlot<7>::kBytes / 16u),
-                                        mrs, irs, trs);
+            lds16* slot = lds_rx + wave * (PfxSlot<7>::kBytes / 16u);
+            if (mode == 5) rx_runs_lds<R, V6, true>(base, ofs, n, wr.a0, wr.a_end, lane, slot, mrs, irs, trs);
+            else rx_runs_pfx<R, V6, 7, true>(base, ofs, n, wr.a0, wr.a_end, lane, slot, mrs, irs, trs);
         } else {  // streamed runs; a batch of large frames on 3 of the 4 blocks per CU
             const uint32_t nb = active_blocks(ofs, n, kRxBigMean, sets == 0 ? 3u : 0u);
             if (blockIdx.x >= nb) return;
@@ -2965,7 +2977,8 @@ hipError_t launch_rx_tcp(const LaunchCfg& c, int ipver, const void* d_base, cons
     // PF = -1 kernel at 4 blocks/CU, each block with two 15-row prefix slots of LDS (its four 7-row slots fit the
     // same 38.5 KB), the mode chosen in-kernel by the batch's mean frame.
     const bool auto_grid = rows == 2 && c.blocks_per_cu == 0 &&
-                           (c.segs_per_wave == 0 || c.segs_per_wave == 5 || c.segs_per_wave == 6);
+                           (c.segs_per_wave == 0 || c.segs_per_wave == 5 || c.segs_per_wave == 6 ||
+                            c.segs_per_wave == 7);
     if (auto_grid) {
         constexpr size_t la = (size_t)PfxSlot<15>::kBytes * 2;
         static_assert(la >= (size_t)PfxSlot<7>::kBytes * kWavesPerBlock && la * 4 <= 163840, "4 blocks per CU");

@@ -223,7 +223,7 @@ def test_fuzz_rx(case):
                              max_payload=int(rng.choice([64, 600, 1460, 9000])))
     want_m, want_i, want_t = O.c_rx_ipv4_tcp(buf, offs)
     tune = dict(rows=int(rng.choice([0, 2, 4, 8, 16])), blocks_per_cu=int(rng.choice([0, 1, 2, 4, 8])),
-                segs_per_wave=int(rng.choice([0, 1, 2, 5, 6])))  # auto / streamed / LDS / prefix / default-grid modes
+                segs_per_wave=int(rng.choice([0, 1, 2, 5, 6, 7])))  # auto / streamed / LDS / prefix / default-grid modes
     mask = torch.empty((n + 63) // 64, dtype=torch.int64, device="cuda")
     ipr, tcpr = torch.empty(n, dtype=torch.int16, device="cuda"), torch.empty(n, dtype=torch.int16, device="cuda")
     nsx.rx_ipv4_tcp_verify_dev(_dev(buf), _dev(offs.view(np.int64)), mask=mask, ip_raw=ipr, tcp_raw=tcpr, tune=tune)
@@ -247,7 +247,7 @@ def test_fuzz_rx6(case):
                              max_payload=int(rng.choice([64, 600, 1440, 9000])), ip=6)
     want_m, want_t = O.c_rx_ipv6_tcp(buf, offs)
     tune = dict(rows=int(rng.choice([0, 2, 4, 8, 16])), blocks_per_cu=int(rng.choice([0, 1, 2, 4, 8])),
-                segs_per_wave=int(rng.choice([0, 1, 2, 5, 6])))
+                segs_per_wave=int(rng.choice([0, 1, 2, 5, 6, 7])))
     mask = torch.empty((n + 63) // 64, dtype=torch.int64, device="cuda")
     tcpr = torch.empty(n, dtype=torch.int16, device="cuda")
     nsx.rx_ipv6_tcp_verify_dev(_dev(buf), _dev(offs.view(np.int64)), mask=mask, tcp_raw=tcpr, tune=tune)
