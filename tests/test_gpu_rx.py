@@ -168,6 +168,32 @@ def test_rx_prefix_form_bench_workloads_full_size(config):
             assert bad.size == 0, (what, config, tune, bad[:5])
 
 
+def test_rx_batch_past_the_launch_chunk():
+    """n > 2^27 ACK-sized frames (7.1 GB): the receive pass splits the batch into launches of 2^27 frames, each
+    starting on a mask word and choosing its form by its own mean frame. The mask is the expected pattern on every
+    frame (exactly the corrupted ones fail), the last word's bits past n are 0, and the raw sums of the frames either
+    side of the split and at the end equal the oracle's."""
+    import bench
+    cfg = dict(kind="rx", n=(1 << 27) + 999, lo=40, hi=66, seed=0x27)
+    w = bench.build_rx_frames(cfg, cfg["seed"], torch.device("cuda", 0))
+    n, offs = cfg["n"], w["offsets"]
+    mask = torch.full(((n + 63) // 64,), 0x5A5A5A5A5A5A5A5A, dtype=torch.int64, device="cuda")
+    ipr = torch.empty(n, dtype=torch.int16, device="cuda")
+    tcpr = torch.empty(n, dtype=torch.int16, device="cuda")
+    nsx.rx_ipv4_tcp_verify_dev(w["buf"], w["d_offs"], mask=mask, ip_raw=ipr, tcp_raw=tcpr)
+    got = host(mask).view(np.uint64)
+    valid = np.ones(n, bool)
+    valid[::1000] = False
+    pad = np.zeros((n + 63) // 64 * 64, np.uint8)
+    pad[:n] = valid
+    assert np.array_equal(got, np.packbits(pad, bitorder="little").view(np.uint64))
+    for lo, hi in (((1 << 27) - 70, (1 << 27) + 70), (n - 100, n)):
+        o0 = int(offs[lo])
+        sub = host(w["buf"][o0:int(offs[hi])])
+        _, want_i, want_t = O.c_rx_ipv4_tcp(sub, offs[lo:hi + 1] - np.uint64(o0))
+        assert np.array_equal(u16(ipr[lo:hi]), want_i) and np.array_equal(u16(tcpr[lo:hi]), want_t), (lo, hi)
+
+
 @pytest.mark.parametrize("tune", TUNES, ids=lambda t: ",".join(f"{k}={v}" for k, v in t.items()))
 def test_rx_launch_shapes(tune):
     rng = np.random.default_rng(0x7E)
