@@ -9,7 +9,7 @@ GPU (torchrun), each checksumming its own batch: the path shards with no
 exchange, so there is no data-path collective and scaling is
 weak. value = Σ bytes over all ranks ÷ max over ranks of the timed region.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2-16]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2-18] [--no-pseudo]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 `--gpus N` with N > 1 and no WORLD_SIZE in the environment launches the N rank
@@ -23,7 +23,12 @@ list with n_gpus = distinct devices, and RCCL ranks that landed on fewer distinc
 GPUs than ranks exit 3 instead of printing a line.
 
 Configs 2-5 are BASELINE.json's device-resident configurations (2 is the
-headline and the default). Configs 6 and 7 measure SURVEY.md §8's next rows to
+headline and the default). Configs 2 and 5 checksum every segment over its own
+IPv4 pseudo-header, given as the N x u32 partials SURVEY.md §8d specifies
+(tcp.go:72-73's ipPseudoHeader prefix; generated on the device by
+nsx_pseudo_ipv4_partial_dev from random addresses, proto 6, length 1500) and
+counted in the algorithmic bytes (+4 B per segment); --no-pseudo measures the
+same batch without them. Configs 6 and 7 measure SURVEY.md §8's next rows to
 the same bar, each with its own metric string: 6 = the fused sender pass
 (nsx_tcp_build_dev: segment.bytes() + computeChecksum + field write,
 tcp.go:98-128/:68-71) over 1M 1500 B wire images; 7 = IPv4 header checksum
@@ -34,7 +39,8 @@ workload 7 verified straight into a validity bitmask (nsx_ipv4_hdr_verify_mask_d
 (nsx_rx_ipv4_tcp_verify_dev / nsx_rx_ipv6_tcp_verify_dev); 12 = config 6 with
 9000 B MTU segments; 13 / 16 = the receive pass over 8M ACK-sized (40-100 B IPv4 /
 60-120 B IPv6) frames; 14 = over a bimodal mix of ACKs and 1500 B data frames;
-15 = config 3's small-segment twin (8M ragged 64-128 B segments).
+15 = config 3's small-segment twin (8M ragged 64-128 B segments); 17 / 18 = the
+receive pass over 8M frames, 95% ACKs and 5% 1500 B / 40-400 B.
 
 Printed by rank 0: one JSON line with the contract fields plus
   roofline     — dominant kernel: algorithmic bytes per launch ÷ its mean
@@ -45,7 +51,14 @@ Printed by rank 0: one JSON line with the contract fields plus
   cpu_baseline — the Go-faithful CPU restatement (oracle) timed on a bounded
                  sample of the same workload (rank 0, N=1 only) on every host
                  core this process may use (`cores`), with the 1-thread rate
-                 beside it.
+                 beside it;
+  per_gpu      — every rank's own rate (BASELINE config 5: "per-GPU and
+                 aggregate GiB/s"): its device, its bytes ÷ its own timed wall,
+                 its kernel mean and roofline fraction, so a slow GPU shows in
+                 the line itself; value_per_gpu_mean = value / ranks.
+
+The product library is brought up to date (`make -C network-stack_amd`, a no-op
+when nothing changed) before it is loaded, so a stale pushed binary never runs.
 """
 from __future__ import annotations
 
@@ -67,14 +80,16 @@ GIB = float(1 << 30)
 
 # Workloads (BASELINE.json configs; per GPU). "kind" picks the entry point.
 WORKLOADS = {
-    2: dict(kind="fixed", n=1 << 20, seg_len=1500, stride=1500, seed=0x1071,
-            name="config2: 1M x 1500B fixed-stride TCP segments per GPU, device-resident"),
+    2: dict(kind="fixed", n=1 << 20, seg_len=1500, stride=1500, seed=0x1071, pseudo=True,
+            name="config2: 1M x 1500B fixed-stride TCP segments per GPU, each over its IPv4 pseudo-header "
+                 "(N x u32 partials), device-resident"),
     3: dict(kind="ragged", n=1 << 20, lo=64, hi=9000, seed=0x1072,
             name="config3: 1M ragged 64-9000B segments per GPU, densely packed (odd starts), device-resident"),
     4: dict(kind="fixed", n=1 << 18, seg_len=65536, stride=65536, seed=0x1073,
             name="config4: 256K x 64KiB TSO-size segments per GPU, device-resident"),
-    5: dict(kind="fixed", n=1 << 24, seg_len=1500, stride=1500, seed=0x1071,
-            name="config5: 16M x 1500B per GPU (128M x 1500B over 8 GPUs), device-resident"),
+    5: dict(kind="fixed", n=1 << 24, seg_len=1500, stride=1500, seed=0x1071, pseudo=True,
+            name="config5: 16M x 1500B per GPU (128M x 1500B over 8 GPUs), each over its IPv4 pseudo-header "
+                 "(N x u32 partials), device-resident"),
     # SURVEY.md §8(f) rows measured to the same bar (not the headline metric):
     6: dict(kind="tcp_build", n=1 << 20, payload=1480, seed=0x1074,
             metric="GiB/s fused TCP segment build (serialize + checksum + field write), wire bytes",
@@ -166,11 +181,17 @@ def parse_args(argv=None):
                          "8: f1 with 12 B options; 9: f3 verify into a bitmask; 10: fused receive pass (f2+f3); "
                          "11: the receive pass over IPv6; 12: f1 with 9000 B MTU segments; 13 / 16: the receive "
                          "pass over 8M ACK-sized IPv4 / IPv6 frames; 14: over a bimodal ACK/1500 B mix; 15: config 3's "
-                         "small-segment twin (8M x 64-128 B); 17: 8M frames, 95% ACKs and 5% 1500 B")
+                         "small-segment twin (8M x 64-128 B); 17: 8M frames, 95% ACKs and 5% 1500 B; 18: 8M "
+                         "IPv4 frames of 40-400 B")
+    ap.add_argument("--no-pseudo", action="store_true",
+                    help="configs 2 and 5: checksum the segments without their pseudo-header partials")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--settle-s", type=float, default=0.5, help="device clock settle time before warmup (setup)")
     ap.add_argument("--tune", action="append", default=[], metavar="FIELD=V",
                     help="per-call launch override (include/nsx_tune.h nsx_tune field), e.g. blocks_per_cu=2")
+    ap.add_argument("--no-build", action="store_true",
+                    help="load the library as it is (default: `make -C network-stack_amd` first, a no-op when "
+                         "up to date)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: each rank's step is the CPU oracle on a small batch (exercises the launcher, "
                          "rendezvous and the timing/reduction logic; the value is not a measurement)")
@@ -304,11 +325,25 @@ def device_fields(idents: list) -> dict:
             "devices": [{k: d[k] for k in ("host", "local_device", "pci", "uuid")} for d in idents]}
 
 
+def per_gpu_entries(rank_stats, *, steps, bytes_per_rank_step, alg_bytes_per_launch, launches=1) -> list:
+    """Each rank's own rate from its own clock (rank_stats: every rank's {rank, device, wall_s, step_ms}, rank
+    order): bytes ÷ its timed wall, its kernel mean per launch and that launch's roofline fraction."""
+    out = []
+    for r in rank_stats:
+        k_ms = None if r.get("step_ms") is None else r["step_ms"] / launches
+        frac = None if not k_ms else alg_bytes_per_launch / launches / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS
+        out.append({"rank": r["rank"], "device": r.get("device"),
+                    "gib_s": round(bytes_per_rank_step * steps / r["wall_s"] / GIB, 3),
+                    "wall_s": round(r["wall_s"], 6), "kernel_ms": None if k_ms is None else round(k_ms, 5),
+                    "roofline_frac": None if frac is None else round(frac, 4)})
+    return out
+
+
 def result_line(*, world, steps, warmup, wall_max, bytes_per_rank_step, units_total, workload, cfg, launch_ms,
                 alg_bytes_per_launch, cpu_baseline, traffic, dtype="u16", metric=METRIC, launches=1,
-                n_gpus=None) -> dict:
+                n_gpus=None, rank_stats=None) -> dict:
     """world = ranks (each processed bytes_per_rank_step per step); n_gpus = distinct physical GPUs behind
-    them (default: one per rank)."""
+    them (default: one per rank); rank_stats = every rank's own timing (per_gpu_entries)."""
     total_bytes = bytes_per_rank_step * world * steps
     # launch_ms: mean device time of one step over the timed region; a step of `launches` back-to-back
     # launches is reported per launch (alg bytes and duration divided evenly, the gaps between launches
@@ -320,7 +355,7 @@ def result_line(*, world, steps, warmup, wall_max, bytes_per_rank_step, units_to
         "metric": metric,
         "value": round(total_bytes / wall_max / GIB, 3),
         "unit": "GiB/s",
-        "value_per_gpu": round(total_bytes / wall_max / GIB / world, 3),
+        "value_per_gpu_mean": round(total_bytes / wall_max / GIB / world, 3),
         "n_gpus": world if n_gpus is None else n_gpus,
         "ranks": world,
         "steps": steps,
@@ -341,6 +376,9 @@ def result_line(*, world, steps, warmup, wall_max, bytes_per_rank_step, units_to
             "traffic": None if traffic is None else traffic.get("bytes_per_launch"),
             "traffic_source": None if traffic is None else traffic.get("source"),
             "alg_bytes_per_launch": alg_bytes_per_launch, "launches_per_step": launches},
+        "per_gpu": None if rank_stats is None else per_gpu_entries(
+            rank_stats, steps=steps, bytes_per_rank_step=bytes_per_rank_step,
+            alg_bytes_per_launch=alg_bytes_per_launch, launches=launches),
         "cpu_baseline": cpu_baseline,
     }
 
@@ -360,6 +398,9 @@ def parse_tune(items) -> dict:
 
 
 def build_workload(cfg, rank, device, tune=None):
+    """One rank's device-resident batch and its step (one call of the entry point). cfg["pseudo"]: every
+    fixed-stride segment over its own IPv4 pseudo-header (random src/dst, proto 6, TCP length = seg_len),
+    passed as the N x u32 partials nsx_pseudo_ipv4_partial_dev makes."""
     import numpy as np
     import torch
     import nsx
@@ -370,9 +411,17 @@ def build_workload(cfg, rank, device, tune=None):
         buf = torch.empty((n - 1) * S + L, dtype=torch.uint8, device=device)
         nsx.fill_splitmix64_dev(buf, seed)
         out = torch.empty(n, dtype=torch.int16, device=device)
+        part = addrs = None
+        if cfg.get("pseudo"):
+            g = torch.Generator(device=device).manual_seed(seed)
+            addrs = torch.randint(0, 256, (2, n, 4), generator=g, device=device, dtype=torch.int64).to(torch.uint8)
+            part = nsx.pseudo_ipv4_partial_dev(addrs[0].reshape(-1), addrs[1].reshape(-1),
+                                               torch.full((n,), L, dtype=torch.int32, device=device), 6)
         # launches per step: the library's own count of its back-to-back windows (config 5: 16)
-        w.update(buf=buf, out=out, bytes=n * L, alg=n * L + 2 * n, launches=nsx.fixed_launch_count(S, L, n, tune),
-                 step_for=lambda t: lambda: nsx.fixed_dev(buf, S, L, n, out=out, tune=t))
+        w.update(buf=buf, out=out, part=part, addrs=addrs, bytes=n * L,
+                 alg=n * L + 2 * n + (4 * n if part is not None else 0),
+                 launches=nsx.fixed_launch_count(S, L, n, tune),
+                 step_for=lambda t: lambda: nsx.fixed_dev(buf, S, L, n, partial=part, out=out, tune=t))
     elif cfg["kind"] == "tcp_build":
         n, P, OL = cfg["n"], cfg["payload"], cfg.get("opt", 0)
         W = P + 20 + OL  # OL ≡ 0 mod 4: tcp.go:118-121 pads nothing
@@ -579,10 +628,23 @@ def cpu_baseline(cfg, w, seconds: float) -> dict:
         gpu = w["out"][:m].cpu().numpy().view(np.uint16)
         out = np.empty(m, np.uint16)
         bounds = [m * t // T for t in range(T + 1)]
+        part = None
+        if w.get("addrs") is not None:  # each segment's own 12 B IPv4 pseudo-header, as a Go caller passes it
+            a = w["addrs"][:, :m].cpu().numpy()
+            pseudo = np.ascontiguousarray(np.concatenate(
+                [a[0], a[1], np.tile(np.array([0, 6, L >> 8, L & 0xFF], np.uint8), (m, 1))], 1))
+            part = np.ascontiguousarray(w["part"][:m].cpu().numpy().view(np.uint32))
 
-        def go(lo, hi):
-            lib.oracle_go_batch_fixed(_ptr(sample, lo * S), S, L, hi - lo, None, 0, _ptr(out, lo))
-        nbytes, desc = m * L, f"first {m} segments x {L}B of rank 0's batch"
+            def go(lo, hi):
+                lib.oracle_go_batch_fixed_pseudo(_ptr(sample, lo * S), S, L, hi - lo, _ptr(pseudo, lo * 12), 12,
+                                                 _ptr(out, lo))
+        else:
+            def go(lo, hi):
+                lib.oracle_go_batch_fixed(_ptr(sample, lo * S), S, L, hi - lo, None, 0, _ptr(out, lo))
+        nbytes = m * L
+        desc = (f"first {m} segments x {L}B of rank 0's batch"
+                + (", each over its 12 B IPv4 pseudo-header (computeChecksum(ipPseudoHeader))" if part is not None
+                   else ""))
         check["segments"] = lambda: np.array_equal(out, gpu)
     elif cfg["kind"] == "tcp_build":
         n, P, OL = cfg["n"], cfg["payload"], cfg.get("opt", 0)
@@ -687,7 +749,7 @@ def cpu_baseline(cfg, w, seconds: float) -> dict:
     reps_1, dt_1 = _run_for(lambda: go(0, bounds[-1]), seconds / 2)
     ok_1 = all(f() for f in check.values())
     if cfg["kind"] == "fixed":
-        extra = cpu_extra_lines(sample, S, L, m, out, max(1.0, seconds / 4), T)
+        extra = cpu_extra_lines(sample, S, L, m, out, max(1.0, seconds / 4), T, part)
     return {"value": round(reps_t * nbytes / dt_t / GIB, 4), "unit": "GiB/s", "cores": T, "kind": "port",
             "sample": f"{desc}, {reps_t} pass(es) on {T} threads (Go-faithful loop, contiguous shards)",
             "seconds": round(dt_t, 2),
@@ -696,23 +758,25 @@ def cpu_baseline(cfg, w, seconds: float) -> dict:
             "sample_parity_vs_gpu": bool(ok_t and ok_1), "host": cores, "extra": extra}
 
 
-def cpu_extra_lines(sample, S, L, m, want, seconds, threads):
+def cpu_extra_lines(sample, S, L, m, want, seconds, threads, part=None):
     """The honest best-CPU line beside the Go-faithful one: a vectorised u64-accumulate
-    restatement (oracle/csum_cpu_fast.c) on 1 and `threads` threads, same sample; each result is
-    checked against the Go-faithful output."""
+    restatement (oracle/csum_cpu_fast.c) on 1 and `threads` threads, same sample (with the same pseudo-header
+    partials as the GPU's when it has them); each result is checked against the Go-faithful output."""
     import numpy as np
     from oracle import csum_oracle as O
     fast = O.c_fast()
     out = np.empty(m, np.uint16)
     ptr = sample.ctypes.data
+    pp = None if part is None else part.ctypes.data
 
     def run(fn):
         reps, dt = _run_for(fn, seconds)
         return {"value": round(reps * m * L / dt / GIB, 3), "unit": "GiB/s", "parity": bool(np.array_equal(out, want))}
 
-    res = {"optimized_1_thread": dict(run(lambda: fast.cpu_fast_batch_fixed(ptr, S, L, m, out.ctypes.data, 1)), cores=1),
-           "optimized_threads": dict(run(lambda: fast.cpu_fast_batch_fixed(ptr, S, L, m, out.ctypes.data, threads)),
-                                     cores=threads),
+    res = {"optimized_1_thread": dict(run(lambda: fast.cpu_fast_batch_fixed(ptr, S, L, m, pp, out.ctypes.data, 1)),
+                                      cores=1),
+           "optimized_threads": dict(run(lambda: fast.cpu_fast_batch_fixed(ptr, S, L, m, pp, out.ctypes.data,
+                                                                           threads)), cores=threads),
            "note": "optimized = oracle/csum_cpu_fast.c (8-byte loads, u64 accumulators, -O3 x86-64-v3): the best-CPU "
                    "line; the baseline value is the reference's algorithm as written"}
     return res
@@ -740,10 +804,11 @@ def dry_run(args) -> int:
     wall_max = dist.max(wall)
     idents = dist.gather({"host": socket.gethostname(), "local_device": None, "pci": None, "uuid": None,
                           "key": None})
+    stats = dist.gather({"rank": dist.rank, "device": None, "wall_s": wall, "step_ms": None})
     line = result_line(world=dist.world, steps=args.steps, warmup=args.warmup, wall_max=wall_max,
                        bytes_per_rank_step=n * L, units_total=n * dist.world, workload="dry run", cfg={"n": n, "seed": 0x1071},
                        launch_ms=launch_ms, alg_bytes_per_launch=n * L + 2 * n, cpu_baseline=None, traffic=None,
-                       n_gpus=0)
+                       n_gpus=0, rank_stats=stats)
     # no GPU behind any rank: n_gpus 0, the rank count separate
     line.update(dry_run=True, data="dry run: the CPU oracle stands in for the GPU kernel; not a measurement",
                 backend="gloo", rehearsal=True, distinct_devices=0,
@@ -754,9 +819,21 @@ def dry_run(args) -> int:
     return 0
 
 
+def build_library() -> None:
+    """Bring libnsx_csum.so up to date before it is loaded (incremental make: a no-op when the pushed binary
+    matches its sources; ~35 s for a full rebuild). A failed build is an error, never a stale library."""
+    r = subprocess.run(["make", "-s", "-j16", "-C", os.path.join(ROOT, "network-stack_amd")],
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise SystemExit(f"bench.py: building network-stack_amd failed:\n{r.stdout[-4000:]}")
+
+
 def main(argv=None) -> int:
     argv = sys.argv[1:] if argv is None else list(argv)
     args = parse_args(argv)
+    if not args.dry_run and not args.no_build and os.environ.get("NSX_BENCH_BUILT") != "1":
+        build_library()  # once, in the launching process, before any rank starts
+        os.environ["NSX_BENCH_BUILT"] = "1"
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return launch_ranks(args.gpus, argv)  # before anything touches a GPU
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -793,7 +870,11 @@ def main(argv=None) -> int:
         return 3
     tune = parse_tune(args.tune) or None
 
-    cfg = WORKLOADS[args.config]
+    cfg = dict(WORKLOADS[args.config])
+    if args.no_pseudo and cfg.get("pseudo"):
+        cfg["pseudo"] = False
+        cfg["name"] = cfg["name"].replace(", each over its IPv4 pseudo-header (N x u32 partials)", "") + \
+            " (no pseudo-header partials)"
     w = build_workload(cfg, dist.rank, device, tune)
     torch.cuda.synchronize()
     # Setup, not measurement: after data generation the GPU's clocks sit in an
@@ -813,6 +894,8 @@ def main(argv=None) -> int:
     wall, launch_ms = timed_loop(w["step"], torch.cuda.synchronize, lambda: dist.barrier(dev_id),
                                  args.steps, args.warmup, ev_pair)
     wall_max = dist.max(wall, device)
+    stats = dist.gather({"rank": dist.rank, "device": "%s/%s" % (socket.gethostname(), devf["devices"][dist.rank]["pci"]),
+                         "wall_s": wall, "step_ms": launch_ms[0] if launch_ms else None})
     cpu = None
     if dist.world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(cfg, w, args.cpu_seconds)
@@ -821,7 +904,7 @@ def main(argv=None) -> int:
                        cfg=cfg, launch_ms=launch_ms, alg_bytes_per_launch=w["alg"], cpu_baseline=cpu,
                        # the committed PMC traffic was profiled at the default launch shape
                        traffic=None if tune else load_traffic(args.config), metric=cfg.get("metric", METRIC),
-                       launches=w.get("launches", 1), n_gpus=devf["n_gpus"])
+                       launches=w.get("launches", 1), n_gpus=devf["n_gpus"], rank_stats=stats)
     line["backend"] = backend if dist.on else None
     line.update({k: v for k, v in devf.items() if k != "n_gpus"})
     if devf["distinct_devices"] < dist.world:  # gloo rehearsal: ranks share a GPU; n_gpus counts GPUs

@@ -72,7 +72,8 @@ func pseudoPartial(ph []byte) uint32 {
 
 // Checksum returns the raw sum of every segment in the batch, each over
 // pseudo[i] ‖ segment i when pseudo is non-nil (len(pseudo) == segments):
-// the batch form of computeChecksum (tcp.go:72-95). numGPUs 0 = all visible.
+// the batch form of computeChecksum (tcp.go:72-95). numGPUs 0 = auto: one GPU
+// per 64 MiB of batch, up to all visible (nsx_csum.h, host-resident batches).
 func (b *PinnedBatch) Checksum(pseudo [][]byte, numGPUs int) ([]uint16, error) {
 	n := len(b.offsets) - 1
 	out := make([]uint16, n)

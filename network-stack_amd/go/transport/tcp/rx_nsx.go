@@ -22,7 +22,8 @@ import (
 // VerifyDatagrams reports, per received datagram, whether it is a well-formed
 // unfragmented IPv4 datagram carrying a TCP segment of at least
 // minSegmentLength bytes (tcp.go:131) whose header and TCP checksums both
-// verify. numGPUs 0 = all visible GPUs.
+// verify. numGPUs 0 = auto: one GPU per 64 MiB of batch, up to all visible
+// (nsx_csum.h, host-resident batches).
 func VerifyDatagrams(frames [][]byte, numGPUs int) ([]bool, error) {
 	return verifyFrames(frames, numGPUs, 4)
 }

@@ -22,8 +22,9 @@ static inline uint32_t fold(uint64_t s) {
     return (uint32_t)s;
 }
 
-/* Raw sum of seg[0, len) as a stream starting at an even position. */
-static uint16_t fast_one(const uint8_t* p, size_t len) {
+/* Raw sum of prefix ‖ seg[0, len) as a stream starting at an even position, the
+ * prefix given as its BE-word partial (the d_prefix_partial convention). */
+static uint16_t fast_one(const uint8_t* p, size_t len, uint32_t partial) {
     uint64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
     size_t i = 0;
     for (; i + 32 <= len; i += 32) {
@@ -38,27 +39,28 @@ static uint16_t fast_one(const uint8_t* p, size_t len) {
     for (; i + 2 <= len; i += 2) s += (uint64_t)p[i] | ((uint64_t)p[i + 1] << 8);  /* LE halves */
     if (i < len) s += p[i];  /* odd tail: low byte of an LE half = high byte of its BE word */
     uint32_t le = fold(s);
-    return (uint16_t)(((le & 0xFFu) << 8) | (le >> 8)); /* LE sum → BE sum */
+    return (uint16_t)fold((uint64_t)(((le & 0xFFu) << 8) | (le >> 8)) + partial); /* LE sum → BE sum */
 }
 
 typedef struct {
-    const uint8_t* base; uint64_t stride; uint32_t seg_len; uint64_t lo, hi; uint16_t* out;
+    const uint8_t* base; uint64_t stride; uint32_t seg_len; uint64_t lo, hi; const uint32_t* partial; uint16_t* out;
 } fast_arg;
 
 static void* fast_run(void* a_) {
     fast_arg* a = (fast_arg*)a_;
-    for (uint64_t i = a->lo; i < a->hi; i++) a->out[i] = fast_one(a->base + i * a->stride, a->seg_len);
+    for (uint64_t i = a->lo; i < a->hi; i++) a->out[i] = fast_one(a->base + i * a->stride, a->seg_len, a->partial ? a->partial[i] : 0u);
     return NULL;
 }
 
+/* partial (nullable): per-segment pseudo-header partials, as nsx_csum_fixed_dev takes them. */
 FAST_EXPORT void cpu_fast_batch_fixed(const uint8_t* base, uint64_t stride, uint32_t seg_len, uint64_t n,
-                                      uint16_t* out, int threads) {
+                                      const uint32_t* partial, uint16_t* out, int threads) {
     if (threads < 1) threads = 1;
     if (threads > 256) threads = 256;
     pthread_t th[256];
     fast_arg args[256];
     for (int t = 0; t < threads; t++) {
-        args[t] = (fast_arg){base, stride, seg_len, n * t / threads, n * (t + 1) / threads, out};
+        args[t] = (fast_arg){base, stride, seg_len, n * t / threads, n * (t + 1) / threads, partial, out};
         pthread_create(&th[t], NULL, fast_run, &args[t]);
     }
     for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);

@@ -114,6 +114,15 @@ ORACLE_EXPORT void oracle_go_batch_fixed(const uint8_t* base, uint64_t stride, u
         out[i] = (uint16_t)oracle_go_checksum(prefix, prefix_len, base + i * stride, seg_len);
 }
 
+/* The same with a pseudo-header of its own per segment (tcp.go:72-73: a caller
+ * passes each segment's ipPseudoHeader): prefix i = pseudo[i*plen, (i+1)*plen). */
+ORACLE_EXPORT void oracle_go_batch_fixed_pseudo(const uint8_t* base, uint64_t stride, uint32_t seg_len,
+                                                uint64_t n, const uint8_t* pseudo, size_t plen,
+                                                uint16_t* out) {
+    for (uint64_t i = 0; i < n; i++)
+        out[i] = (uint16_t)oracle_go_checksum(pseudo + i * plen, plen, base + i * stride, seg_len);
+}
+
 /* The same over a ragged batch: segment i = base[offsets[i], offsets[i+1]). */
 ORACLE_EXPORT void oracle_go_batch_ragged(const uint8_t* base, const uint64_t* offsets, uint64_t n,
                                           const uint8_t* prefix, size_t prefix_len, uint16_t* out) {

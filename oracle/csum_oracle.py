@@ -357,6 +357,8 @@ def c_oracle():
                                         u8p, u8p, ctypes.c_int]
         lib.oracle_go_batch_fixed.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
                                               u8p, ctypes.c_size_t, u8p]
+        lib.oracle_go_batch_fixed_pseudo.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+                                                     u8p, ctypes.c_size_t, u8p]
         lib.oracle_go_batch_ragged.argtypes = [u8p, u8p, ctypes.c_uint64, u8p, ctypes.c_size_t, u8p]
         lib.oracle_go_rx_ipv4_tcp.argtypes = [u8p, u8p, ctypes.c_uint64, u8p, u8p, u8p]
         lib.oracle_go_rx_ipv6_tcp.argtypes = [u8p, u8p, ctypes.c_uint64, u8p, u8p]
@@ -383,7 +385,7 @@ def c_fast():
             build_c_oracle(force=True)
         lib = ctypes.CDLL(FAST_PATH)
         lib.cpu_fast_batch_fixed.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
-                                             ctypes.c_void_p, ctypes.c_int]
+                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         lib.cpu_fast_batch_fixed.restype = None
         _fast = lib
     return _fast

@@ -20,9 +20,9 @@ def pytest_configure(config):
 
 
 def pytest_sessionstart(session):
-    # Build the checker (oracle) and the product library in-tree if missing.
+    # Bring the checker (oracle) and the product library up to date in-tree before any test loads them. make is
+    # incremental: a no-op when the built files match their sources, so a stale pushed .so never runs and an
+    # up-to-date one is not rebuilt.
     import subprocess
-    if not os.path.exists(os.path.join(ROOT, "oracle", "build", "libnsx_oracle.so")):
-        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
-    if not os.path.exists(os.path.join(ROOT, "network-stack_amd", "lib", "libnsx_csum.so")):
-        subprocess.check_call(["make", "-s", "-j8", "-C", os.path.join(ROOT, "network-stack_amd")])
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+    subprocess.check_call(["make", "-s", "-j8", "-C", os.path.join(ROOT, "network-stack_amd")])

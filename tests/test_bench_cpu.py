@@ -36,6 +36,27 @@ def test_gpus_2_launches_two_ranks_itself():
     assert line["ranks"] == 2 and line["dry_run"] and line["rehearsal"]
     assert line["n_gpus"] == 0 and line["distinct_devices"] == 0 and len(line["devices"]) == 2
     assert line["config"]["units_per_step_all_gpus"] == 2 * line["config"]["units_per_gpu"]
+    # each rank's own rate (BASELINE config 5: per-GPU and aggregate GiB/s): one entry per rank, its own wall
+    per = line["per_gpu"]
+    assert [p["rank"] for p in per] == [0, 1]
+    for p in per:
+        assert set(p) == {"rank", "device", "gib_s", "wall_s", "kernel_ms", "roofline_frac"}
+        assert p["gib_s"] > 0 and p["wall_s"] > 0
+    assert line["value_per_gpu_mean"] == pytest.approx(line["value"] / 2, abs=1e-3)
+    assert min(p["gib_s"] for p in per) >= line["value"] / 2 - 1e-3  # the aggregate uses the slowest wall
+
+
+def test_per_gpu_entries_show_a_slow_gpu():
+    """a SCALE reader must see a slow GPU from the line alone."""
+    stats = [{"rank": r, "device": f"h/{r}", "wall_s": 1.0 if r != 2 else 1.25, "step_ms": 0.2 if r != 2 else 0.25}
+             for r in range(4)]
+    line = bench.result_line(world=4, steps=10, warmup=1, wall_max=1.25, bytes_per_rank_step=1 << 30,
+                             units_total=4, workload="w", cfg={"n": 1, "seed": 1}, launch_ms=[0.2],
+                             alg_bytes_per_launch=1 << 30, cpu_baseline=None, traffic=None, rank_stats=stats)
+    per = line["per_gpu"]
+    assert [p["gib_s"] for p in per] == [10.0, 10.0, 8.0, 10.0]
+    assert per[2]["roofline_frac"] < per[0]["roofline_frac"]
+    assert line["value"] == pytest.approx(32.0)  # 4 GiB x 10 steps / the slowest rank's 1.25 s
 
 
 def test_device_fields_count_distinct_gpus():

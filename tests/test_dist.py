@@ -47,10 +47,11 @@ def _worker(rank, world, port, q):
 
         wall, launch_ms = bench.timed_loop(step, lambda: None, d.barrier, steps=4, warmup=1)
         wmax = d.max(wall)
+        stats = d.gather({"rank": rank, "device": f"cpu{rank}", "wall_s": wall, "step_ms": 0.5 + rank})
         line = bench.result_line(world=world, steps=4, warmup=1, wall_max=wmax, bytes_per_rank_step=n * L,
                                  units_total=n * world, workload="gloo-test", cfg={"n": n, "seed": 0x1071},
                                  launch_ms=launch_ms, alg_bytes_per_launch=n * L + 2 * n, cpu_baseline=None,
-                                 traffic=None)
+                                 traffic=None, rank_stats=stats)
         # Sharded host batch: a ragged batch split by byte count, each rank does its shard.
         rng = np.random.default_rng(0x1072)
         lens = rng.integers(64, 9001, 3001).astype(np.uint64)
@@ -66,7 +67,7 @@ def _worker(rank, world, port, q):
         full = O.c_batch(rb, lens.size, offsets=offs)
         stitched = [x for _, _, part in sorted(gathered) for x in part]
         q.put(json.dumps({"rank": rank, "wall": wall, "wmax": wmax, "value": line["value"],
-                          "value_per_gpu": line["value_per_gpu"],
+                          "value_per_gpu_mean": line["value_per_gpu_mean"], "per_gpu": line["per_gpu"],
                           "n_gpus": line["n_gpus"], "stitched_ok": stitched == full.tolist(),
                           "sizes": [int(offs[b2] - offs[b1]) for b1, b2 in zip(bounds[:-1], bounds[1:])]}))
         d.close()
@@ -93,7 +94,15 @@ def test_bench_dist_logic_gloo_ws2():
         assert r["wmax"] == pytest.approx(wmax)      # MAX over ranks, identical everywhere
         assert r["n_gpus"] == 2
         assert r["value"] == pytest.approx(round(2 * 512 * 1500 * 4 / wmax / GIB, 3))  # whole-job bytes
-        assert r["value_per_gpu"] == pytest.approx(r["value"] / 2, abs=1e-3)           # per-GPU beside it (3 decimals)
+        assert r["value_per_gpu_mean"] == pytest.approx(r["value"] / 2, abs=1e-3)      # mean per GPU (3 decimals)
+        # every rank's own rate from its own clock, in rank order (BASELINE config 5: per-GPU and aggregate)
+        per = r["per_gpu"]
+        assert [p["rank"] for p in per] == [0, 1] and [p["device"] for p in per] == ["cpu0", "cpu1"]
+        for p in per:
+            assert p["gib_s"] == pytest.approx(512 * 1500 * 4 / by[p["rank"]]["wall"] / GIB, rel=1e-3)
+            assert p["gib_s"] >= r["value"] / 2 - 1e-3                               # no rank slower than the max
+        assert per[0]["kernel_ms"] == 0.5 and per[1]["kernel_ms"] == 1.5
+        assert per[0]["roofline_frac"] == pytest.approx((512 * 1502) / 0.5e-3 / 1e9 / 8000, abs=1e-4)
         assert r["stitched_ok"]                      # shards cover the batch exactly once
     sizes = by[0]["sizes"]
     assert abs(sizes[0] - sizes[1]) <= 9000          # byte-balanced split

@@ -176,18 +176,54 @@ def test_reference_TestSegmentCodec_on_device(pseudo):
 
 # ------------------------------------------------------------------ BASELINE configs at full size
 
+def ipv4_pseudo_partials(addrs: np.ndarray, tcp_len: int) -> np.ndarray:
+    """The BE-word sum of each segment's 12 B IPv4 pseudo-header src(4) dst(4) 0 6 len(2) (RFC 9293 §3.1;
+    ip.Addr.Raw(), network/ip/v4/ipv4.go:15; ip.NextProtoTCP, protocols.go:8), from (2, n, 4) address bytes."""
+    a = addrs.astype(np.uint32)
+    return ((a[..., 0] << 8) + a[..., 1] + (a[..., 2] << 8) + a[..., 3]).sum(0).astype(np.uint32) + 6 + tcp_len
+
+
+def pseudo_headers(addrs: np.ndarray, tcp_len: int) -> np.ndarray:
+    """(n, 12) pseudo-header bytes, as a Go caller would pass ipPseudoHeader (tcp.go:72-73)."""
+    n = addrs.shape[1]
+    return np.ascontiguousarray(np.concatenate(
+        [addrs[0], addrs[1], np.tile(np.array([0, 6, tcp_len >> 8, tcp_len & 0xFF], np.uint8), (n, 1))], 1))
+
+
 def test_config2_1M_x_1500_full():
+    """Config 2 exactly as bench.py times it (bench.build_workload): 1M x 1500 B, each segment over its own IPv4
+    pseudo-header given as the N x u32 partials SURVEY.md §8d specifies (tcp.go:72-73), generated on the device
+    by nsx_pseudo_ipv4_partial_dev. Every segment against the oracle fed partials computed on the host from the
+    same addresses; a sample against the Go-faithful loop over the 12 B pseudo-header bytes themselves; then
+    the same batch without partials."""
+    import bench
     n, L = 1 << 20, 1500
-    t = torch.empty(n * L, dtype=torch.uint8, device="cuda")
-    nsx.fill_splitmix64_dev(t, 0x1071)
+    w = bench.build_workload(bench.WORKLOADS[2], 0, torch.device("cuda"))
+    t = w["buf"]
+    assert w["alg"] == n * L + 2 * n + 4 * n and w["part"] is not None
     h = host(t)
     assert np.array_equal(h[:4096], O.c_splitmix64(0x1071, 4096))
     assert np.array_equal(h[-4096:], O.c_splitmix64(0x1071, 4096, n * L - 4096))
+    addrs = host(w["addrs"])
+    part = ipv4_pseudo_partials(addrs, L)
+    assert np.array_equal(np.array([O.fold(int(x)) for x in host(w["part"]).view(np.uint32)[:4096]]),
+                          np.array([O.fold(int(x)) for x in part[:4096]]))
+    w["step"]()
+    got = u16(w["out"])
+    want = O.c_batch(h, n, stride=L, seg_len=L, partial=part, threads=16)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, (bad[:8], got[bad[:8]], want[bad[:8]])
+    # the Go-faithful loop over the pseudo-header bytes (allocate, concatenate, serial compare-carry) on a sample
+    m = 20000
+    go = np.empty(m, np.uint16)
+    ph = pseudo_headers(addrs[:, :m], L)
+    O.c_oracle().oracle_go_batch_fixed_pseudo(h.ctypes.data, L, L, m, ph.ctypes.data, 12, go.ctypes.data)
+    assert np.array_equal(go, got[:m])
+    w["step"]()
+    assert np.array_equal(u16(w["out"]), got)  # idempotent
+    # the partial-less form over the same bytes
     out = nsx.fixed_dev(t, L, L, n, out=torch.empty(n, dtype=torch.int16, device="cuda"))
-    got = u16(out)
-    assert np.array_equal(got, O.c_batch(h, n, stride=L, seg_len=L, threads=16))
-    out2 = nsx.fixed_dev(t, L, L, n, out=torch.empty(n, dtype=torch.int16, device="cuda"))
-    assert np.array_equal(u16(out2), got)  # idempotent
+    assert np.array_equal(u16(out), O.c_batch(h, n, stride=L, seg_len=L, threads=16))
 
 
 def test_config3_1M_ragged_full():
@@ -205,7 +241,7 @@ def test_config3_1M_ragged_full():
         assert np.array_equal(u16(out), want), tune
 
 
-def oracle_fixed_chunked(t, n, L, S, seed=None, chunk=1 << 30):
+def oracle_fixed_chunked(t, n, L, S, seed=None, chunk=1 << 30, partial=None):
     """The C oracle (O.c_batch, 16 threads) over EVERY segment of a device-resident fixed-stride batch too large
     to copy whole: ~1 GiB of segments at a time comes back to the host and is checked there. With `seed`, each
     chunk's first and last 4 KiB are also compared with the counter-based splitmix64 stream (the batch is the
@@ -220,7 +256,8 @@ def oracle_fixed_chunked(t, n, L, S, seed=None, chunk=1 << 30):
             k = min(4096, hi - lo)
             assert np.array_equal(h[:k], O.c_splitmix64(seed, k, lo)), i0
             assert np.array_equal(h[-k:], O.c_splitmix64(seed, k, hi - k)), i0
-        want[i0:i1] = O.c_batch(h, i1 - i0, stride=S, seg_len=L, threads=16)
+        want[i0:i1] = O.c_batch(h, i1 - i0, stride=S, seg_len=L, threads=16,
+                                partial=None if partial is None else partial[i0:i1])
         del h
     return want
 
@@ -254,26 +291,34 @@ def test_config4_256K_x_64KiB_full_oracle_and_roundtrip():
 
 
 def test_config5_16M_x_1500_per_gpu_full_oracle():
-    """Config 5's per-GPU batch (16M x 1500 B = 23.4 GiB, SURVEY.md §8d, run as 16 back-to-back windows):
-    every segment against the oracle (chunked D2H; bytes checked against the counter-based stream at every
-    chunk edge), including both sides of every 8-way shard boundary and every window boundary; the one-launch
-    and block-per-segment forms agree on every segment as extra properties."""
+    """Config 5's per-GPU batch as bench.py times it on rank 3 (16M x 1500 B = 23.4 GiB, each segment over its
+    IPv4 pseudo-header partial, SURVEY.md §8d, run as 16 back-to-back windows): every segment against the oracle
+    (chunked D2H; bytes checked against the counter-based stream at every chunk edge), including both sides of
+    every 8-way shard boundary and every window boundary; the one-launch and block-per-segment forms agree on
+    every segment as extra properties (without partials)."""
+    import bench
     n, L, seed = 1 << 24, 1500, 0x1071 + 3  # the rank-3 seed
-    t = torch.empty(n * L, dtype=torch.uint8, device="cuda")
-    nsx.fill_splitmix64_dev(t, seed)
-    assert nsx.fixed_launch_count(L, L, n) == 16
-    got = u16(nsx.fixed_dev(t, L, L, n, out=torch.empty(n, dtype=torch.int16, device="cuda")))
-    want = oracle_fixed_chunked(t, n, L, L, seed)
+    w = bench.build_workload(bench.WORKLOADS[5], 3, torch.device("cuda"))
+    t = w["buf"]
+    assert nsx.fixed_launch_count(L, L, n) == 16 == w["launches"]
+    part = ipv4_pseudo_partials(host(w["addrs"]), L)
+    del w["addrs"]
+    w["step"]()
+    got = u16(w["out"])
+    want = oracle_fixed_chunked(t, n, L, L, seed, partial=part)
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, (bad[:8], got[bad[:8]], want[bad[:8]])
     edges = set()
     for b in list(nsx.shard_plan(n, 8)[1:-1]) + [k * (n // 16) for k in range(1, 16)]:
         edges |= {int(b) - 1, int(b)}
     for i in sorted(edges)[:8] + [n - 1]:  # the edges from the seed alone, independent of the D2H
-        assert got[i] == O.c_fold_checksum(b"", O.c_splitmix64(seed, L, i * L).tobytes()), i
+        assert got[i] == O.fold(O.be_word_sum(O.c_splitmix64(seed, L, i * L).tobytes()) + int(part[i])), i
+    plain = u16(nsx.fixed_dev(t, L, L, n, out=torch.empty(n, dtype=torch.int16, device="cuda")))
     one = u16(nsx.fixed_dev(t, L, L, n, out=torch.empty(n, dtype=torch.int16, device="cuda"),
                             tune=dict(window_bytes=-1)))
-    assert np.array_equal(one, got)
+    assert np.array_equal(one, plain)
     alt = u16(nsx.fixed_dev(t, L, L, n, out=torch.empty(n, dtype=torch.int16, device="cuda"),
                             tune=dict(block_mode=2)))
-    assert np.array_equal(alt, got)
+    assert np.array_equal(alt, plain)
+    for i in sorted(edges)[:8] + [n - 1]:
+        assert plain[i] == O.c_fold_checksum(b"", O.c_splitmix64(seed, L, i * L).tobytes()), i

@@ -238,10 +238,20 @@ def test_cpu_fast_line_matches_go_checksum():
         buf = rng.integers(0, 256, n * (L + 3) + 1, dtype=np.uint8)
         buf[: L + 3] = 0xFF
         out = np.empty(n, np.uint16)
-        O.c_fast().cpu_fast_batch_fixed(buf[1:].ctypes.data, L + 3, L, n, out.ctypes.data, 4)
+        O.c_fast().cpu_fast_batch_fixed(buf[1:].ctypes.data, L + 3, L, n, None, out.ctypes.data, 4)
         for i in range(n):
             seg = buf[1 + i * (L + 3):1 + i * (L + 3) + L].tobytes()
             assert out[i] == O.c_go_checksum(b"", seg), (L, i)
+        # with per-segment IPv4 pseudo-headers given as partials (config 2's headline form)
+        ph = rng.integers(0, 256, (n, 12), dtype=np.uint8)
+        part = np.array([O.be_word_sum(p.tobytes()) for p in ph], np.uint32)
+        O.c_fast().cpu_fast_batch_fixed(buf[1:].ctypes.data, L + 3, L, n, part.ctypes.data, out.ctypes.data, 4)
+        go = np.empty(n, np.uint16)
+        O.c_oracle().oracle_go_batch_fixed_pseudo(buf[1:].ctypes.data, L + 3, L, n, ph.ctypes.data, 12,
+                                                  go.ctypes.data)
+        for i in range(n):
+            seg = buf[1 + i * (L + 3):1 + i * (L + 3) + L].tobytes()
+            assert out[i] == go[i] == O.go_checksum(ph[i].tobytes(), seg), (L, i)
 
 
 # --- fused receive check (SURVEY.md §8 f2 + f3): Python vs C restatement, fixtures, per-kind rules ---
