@@ -782,7 +782,9 @@ def cpu_extra_lines(sample, S, L, m, want, seconds, threads, part=None):
     return res
 
 
-def load_traffic(config_id: int):
+def load_traffic(config_id):
+    """The committed PMC traffic of a workload (profiles/traffic_config<id>.json; id 2n = config 2 without its
+    pseudo-header partials)."""
     p = os.path.join(ROOT, "profiles", f"traffic_config{config_id}.json")
     if not os.path.exists(p):
         return None
@@ -903,7 +905,8 @@ def main(argv=None) -> int:
                        bytes_per_rank_step=w["bytes"], units_total=cfg["n"] * dist.world, workload=cfg["name"],
                        cfg=cfg, launch_ms=launch_ms, alg_bytes_per_launch=w["alg"], cpu_baseline=cpu,
                        # the committed PMC traffic was profiled at the default launch shape
-                       traffic=None if tune else load_traffic(args.config), metric=cfg.get("metric", METRIC),
+                       traffic=None if tune else load_traffic(
+                           f"{args.config}n" if args.no_pseudo and WORKLOADS[args.config].get("pseudo") else args.config), metric=cfg.get("metric", METRIC),
                        launches=w.get("launches", 1), n_gpus=devf["n_gpus"], rank_stats=stats)
     line["backend"] = backend if dist.on else None
     line.update({k: v for k, v in devf.items() if k != "n_gpus"})

@@ -621,12 +621,15 @@ struct WaveRange {
     uint32_t a0, a_end;
     uint64_t bytes;
 };
+// count_align (nonzero): the alignment of equal-count ranges instead of `align`.
 __device__ __forceinline__ WaveRange wave_range(__amdgpu_buffer_rsrc_t ofs, uint32_t n, uint32_t g, uint32_t W,
-                                                uint32_t lane, uint32_t small_mean, uint32_t align) {
+                                                uint32_t lane, uint32_t small_mean, uint32_t align,
+                                                uint32_t count_align = 0) {
     const uint64_t o_lo = ld_off(ofs, 0), o_hi = ld_off(ofs, n);
     const uint64_t tot = o_hi - o_lo;
     uint32_t s[2];
     const bool by_count = tot < (uint64_t)small_mean * n;
+    if (by_count && count_align) align = count_align;
     if (by_count) {
         s[0] = (uint32_t)((uint64_t)n * g / W);
         s[1] = (uint32_t)((uint64_t)n * (g + 1) / W);
@@ -929,14 +932,25 @@ __device__ __forceinline__ void lds_stage(lds16* slot, u32x4 (&V)[ROWS], uint64_
 constexpr uint32_t kScanSlotRows = 8;
 constexpr uint32_t kScanSlot = kScanSlotRows * kRow + 256;  // + pad: lds_range_sum's chunk blocks read past the end
 
-template <int R, bool VERIFY, bool PIPE>
+// XV (experiment, tools/evidence.sh ab): bit 0 = runs of 64 segments, each lane loading both of its segment's
+// offsets (the receive pass's form: no cross-lane shift for the end, and a run's 64 results are one whole 128 B
+// line when the wave range starts at a multiple of 64); bit 1 = write-through (sc1) result stores.
+template <int R, bool VERIFY, bool PIPE, int XV = 0>
 __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
                                                 __amdgpu_buffer_rsrc_t prs, __amdgpu_buffer_rsrc_t ors,
                                                 __amdgpu_buffer_rsrc_t oks, uint32_t run, uint32_t a0, uint32_t a_end,
                                                 uint32_t lane, lds16* slot) {
     typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+    constexpr bool R64 = (XV & 1) != 0;
+    constexpr int kSt = (XV & 2) ? kStoreSc1 : 0;
+    if constexpr (R64) run = kWave;
     auto load_offs = [&](uint32_t a) -> uint64_t {  // lane l ≤ run length: offsets[a + l]
         const uint32_t voff = (a < a_end && lane <= run && a + lane <= n) ? (a + lane) * 8 : kOOB;
+        const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, voff, 0, 0);
+        return ((uint64_t)x.y << 32) | x.x;
+    };
+    auto load_ends = [&](uint32_t a) -> uint64_t {  // R64: lane l < run length: offsets[a + l + 1]
+        const uint32_t voff = (a < a_end && a + lane + 1u <= n) ? (a + lane + 1u) * 8 : kOOB;
         const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, voff, 0, 0);
         return ((uint64_t)x.y << 32) | x.x;
     };
@@ -946,10 +960,11 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
         uint32_t cnt;
         bool lds;
     };
-    auto geo = [&](uint32_t a, uint64_t off) {  // wave-uniform geometry of run a (boundaries in lanes 0..cnt)
+    auto geo = [&](uint32_t a, uint64_t off, uint64_t end) {  // wave-uniform geometry of run a
         Run g{base, 0, a < a_end ? min(run, a_end - a) : 0u, false};
         if (g.cnt) {
-            const uint64_t lo = readlane64(off, 0), hi = readlane64(off, g.cnt);
+            // boundaries in lanes 0..cnt of off (R64: starts in off, ends in end, lanes 0..cnt-1)
+            const uint64_t lo = readlane64(off, 0), hi = R64 ? readlane64(end, g.cnt - 1u) : readlane64(off, g.cnt);
             g.rbase = reinterpret_cast<const uint8_t*>(((uintptr_t)(base + lo)) & ~(uintptr_t)127);
             g.span = (uint64_t)((base + hi) - g.rbase);
             g.lds = g.span <= (uint64_t)kScanSlotRows * kRow;
@@ -967,41 +982,54 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
     // loop's wait counts.
     uint32_t a = a0;
     while (a < a_end) {
-        uint64_t c_off = load_offs(a);
-        Run cur = geo(a, c_off);
+        uint64_t c_off = load_offs(a), c_end = R64 ? load_ends(a) : 0;
+        Run cur = geo(a, c_off, c_end);
         if (!cur.lds) {  // too wide for the slot: the streaming form
             const uint32_t part = __builtin_amdgcn_raw_buffer_load_b32(prs, lane < cur.cnt ? (a + lane) * 4 : kOOB, 0, 0);
-            const uint32_t cnt1[1] = {cur.cnt}, part1[1] = {part};
-            const uint64_t o1[1] = {c_off};
-            ragged_run_stream<R, VERIFY, PIPE, 1>(base, a, run, cnt1, o1, part1, ors, oks, lane);
+            if constexpr (R64) {  // the stream takes ≤ 63 segments (boundaries in lanes 0..cnt): 63, then the last
+                const uint32_t c1 = min(cur.cnt, kScanRun), c2 = cur.cnt - c1;
+                const uint32_t cnt1[1] = {c1}, part1[1] = {part};
+                const uint64_t o1[1] = {lane == c1 ? readlane64(c_end, c1 - 1u) : c_off};
+                ragged_run_stream<R, VERIFY, PIPE, 1>(base, a, kScanRun, cnt1, o1, part1, ors, oks, lane);
+                if (c2) {
+                    const uint32_t cnt2[1] = {c2}, part2[1] = {(uint32_t)__shfl_down((int)part, c1)};
+                    const uint64_t o2[1] = {lane == 0 ? readlane64(c_off, c1) : readlane64(c_end, c1)};
+                    ragged_run_stream<R, VERIFY, PIPE, 1>(base, a + c1, kScanRun, cnt2, o2, part2, ors, oks, lane);
+                }
+            } else {
+                const uint32_t cnt1[1] = {cur.cnt}, part1[1] = {part};
+                const uint64_t o1[1] = {c_off};
+                ragged_run_stream<R, VERIFY, PIPE, 1>(base, a, run, cnt1, o1, part1, ors, oks, lane);
+            }
             a += run;
             continue;
         }
         issue(cur);
-        uint64_t n_off = load_offs(a + run);
+        uint64_t n_off = load_offs(a + run), n_end = R64 ? load_ends(a + run) : 0;
         __builtin_amdgcn_s_waitcnt(kWaitVm0);  // as in rx_runs_lds: nothing in flight at the loop's entry
         for (;;) {
             const uint32_t part = __builtin_amdgcn_raw_buffer_load_b32(prs, lane < cur.cnt ? (a + lane) * 4 : kOOB, 0, 0);
             lds_stage<kScanSlotRows>(slot, V, cur.span, lane);
             lds_zero_tail(slot, cur.span, lane);
-            Run nxt = geo(a + run, n_off);
+            Run nxt = geo(a + run, n_off, n_end);
             if (!nxt.lds) nxt.span = 0;  // a run that will be streamed is not staged: empty loads
             issue(nxt);
-            const uint64_t p_off = load_offs(a + 2u * run);
+            const uint64_t p_off = load_offs(a + 2u * run), p_end = R64 ? load_ends(a + 2u * run) : 0;
             // segment a + lane = [boundary lane, boundary lane + 1)
-            const uint64_t e_off = (uint64_t)__shfl_down((unsigned long long)c_off, 1);
+            const uint64_t e_off = R64 ? c_end : (uint64_t)__shfl_down((unsigned long long)c_off, 1);
             const bool mine = lane < cur.cnt;
             const uint32_t p = mine ? (uint32_t)((base + c_off) - cur.rbase) : 0u;
             const uint32_t e = mine ? (uint32_t)((base + e_off) - cur.rbase) : 0u;
             const uint32_t dq = reinterpret_cast<const uint32_t*>(slot)[p >> 2];
             const uint32_t res = finish(fold32(lds_range_sum(slot, p, e, dq, mine)), (p & 1u) == 0, part);
-            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, mine ? (a + lane) * 2 : kOOB, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, mine ? (a + lane) * 2 : kOOB, 0, kSt);
             if constexpr (VERIFY)
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(res == 0xFFFFu), oks, mine ? a + lane : kOOB, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(res == 0xFFFFu), oks, mine ? a + lane : kOOB, 0, kSt);
             a += run;
             if (!nxt.lds) break;  // the end of the wave's range, or a run for the outer loop
             cur = nxt;
             c_off = n_off, n_off = p_off;
+            c_end = n_end, n_end = p_end;
         }
     }
 }
@@ -1201,7 +1229,7 @@ __device__ __forceinline__ void pfx_runs(const uint8_t* __restrict__ base, __amd
     }
 }
 
-template <int R, bool VERIFY, bool PIPE, int NS>
+template <int R, bool VERIFY, bool PIPE, int NS, int XV = 0>
 __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, uint32_t n,
     const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t run, int sets,
@@ -1225,7 +1253,7 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
         const uint32_t b = blockIdx.x, W = nb * kWavesPerBlock;
         const uint32_t g = (nb >= 16 && (nb & 7) == 0) ? ((b & 7) * (nb >> 3) + (b >> 3)) * kWavesPerBlock + wave
                                                         : b * kWavesPerBlock + wave;
-        const WaveRange wr = wave_range(ofs, n, g, W, lane, kScanLdsSeg, 1u);
+        const WaveRange wr = wave_range(ofs, n, g, W, lane, kScanLdsSeg, 1u, (XV & 1) ? kWave : 0u);
         a0 = wr.a0, a_end = wr.a_end, wave_bytes = wr.bytes;
     }
     // Two sets per run suit segments of a few hundred bytes and up (config 3). A wave whose segments average under
@@ -1233,8 +1261,8 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
     // each run still streams tens of KB (§7 step 42).
     if (sets == 2 || (NS == 2 && sets == 0 && wave_bytes < (uint64_t)kScanLdsSeg * (a_end - a0))) {
         extern __shared__ lds16 lds_scan[];
-        ragged_runs_lds<R, VERIFY, PIPE>(base, ofs, n, prs, ors, oks, run, a0, a_end, lane,
-                                         lds_scan + wave * (kScanSlot / 16u));
+        ragged_runs_lds<R, VERIFY, PIPE, XV>(base, ofs, n, prs, ors, oks, run, a0, a_end, lane,
+                                             lds_scan + wave * (kScanSlot / 16u));
     } else if (NS == 2 && (sets == 4 || (sets == 0 && wave_bytes < (uint64_t)kScanSmallSeg * (a_end - a0)))) {
         ragged_runs<R, VERIFY, PIPE, 4>(base, ofs, n, prs, ors, oks, run, a0, a_end, lane);
     } else {
@@ -2906,6 +2934,8 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
     // batches of 3 or 4 rows, 0.93 for 1 row). kernel 2 (NSX_TUNE_KERNEL_SCAN_PLAIN):
     // single batches of 4, 8 (default) or 16 rows.
     const bool pipe = c.kernel != 2;
+    // kernel 4..6: experiment variants of the LDS form (XV 1..3, ragged_runs_lds)
+    const int xv = c.kernel >= 4 && c.kernel <= 6 ? c.kernel - 3 : 0;
     const int rows = pipe ? (c.rows == 2 || c.rows == 4 || c.rows == 8 ? c.rows : 2)
                           : (c.rows == 4 || c.rows == 8 || c.rows == 16 ? c.rows : 8);
     const uint32_t run = (c.run_segs >= 1 && c.run_segs <= (int)kScanRun) ? (uint32_t)c.run_segs : kScanRun;
@@ -2931,10 +2961,26 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
         if (rows == R_ && pipe == P_ && ns == NS_)                                                              \
             hipLaunchKernelGGL((csum_ragged_scan_kernel<R_, VERIFY, P_, NS_>), dim3(grid), dim3(kBlock), lds, st,\
                                base, offsets + c0, cn, pc, oc, kc, run, sets, keep);
-        NSX_RSCAN(2, true, 1) NSX_RSCAN(4, true, 1) NSX_RSCAN(8, true, 1)
+        NSX_RSCAN(4, true, 1) NSX_RSCAN(8, true, 1)
         NSX_RSCAN(4, false, 1) NSX_RSCAN(8, false, 1) NSX_RSCAN(16, false, 1)
-        NSX_RSCAN(2, true, 2)
 #undef NSX_RSCAN
+        if (rows == 2 && pipe && ns == 1)
+            hipLaunchKernelGGL((csum_ragged_scan_kernel<2, VERIFY, true, 1>), dim3(grid), dim3(kBlock), lds, st, base,
+                               offsets + c0, cn, pc, oc, kc, run, sets, keep);
+        if (rows == 2 && pipe && ns == 2) {
+            switch (xv) {
+#define NSX_RSCAN_XV(X_)                                                                                          \
+                case X_:                                                                                           \
+                    hipLaunchKernelGGL((csum_ragged_scan_kernel<2, VERIFY, true, 2, X_>), dim3(grid), dim3(kBlock), \
+                                       lds, st, base, offsets + c0, cn, pc, oc, kc, run, sets, keep);              \
+                    break;
+                NSX_RSCAN_XV(1) NSX_RSCAN_XV(2) NSX_RSCAN_XV(3)
+#undef NSX_RSCAN_XV
+                default:
+                    hipLaunchKernelGGL((csum_ragged_scan_kernel<2, VERIFY, true, 2>), dim3(grid), dim3(kBlock), lds, st,
+                                       base, offsets + c0, cn, pc, oc, kc, run, sets, keep);
+            }
+        }
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

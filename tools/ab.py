@@ -54,6 +54,21 @@ def main():
             step = (lambda t: lambda: nsx.ragged_dev(w["buf"], w["d_offs"], out=rout, tune=t))(tune)
         variants.append((name, step, __import__("nsx").fixed_launch_count(
             cfg["stride"], cfg["seg_len"], cfg["n"], tune) if cfg["kind"] == "fixed" else 1))
+    # every variant must give the first one's results on this batch (they differ only in launch shape or code path)
+    ref = None
+    for name, step, _ in variants:
+        if cfg["kind"] == "rx" and name.startswith("scan"):
+            continue
+        w["out"].zero_()
+        step()
+        torch.cuda.synchronize()
+        got = w["out"].clone()
+        if ref is None:
+            ref = got
+        same = bool(torch.equal(got, ref))
+        print(f"parity {name}: {'same as first' if same else 'MISMATCH'}", flush=True)
+        if not same:
+            raise SystemExit(f"variant {name} differs from the first variant")
     t_end = time.perf_counter() + 1.0
     while time.perf_counter() < t_end:  # settle
         for _, step, _ in variants:

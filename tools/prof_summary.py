@@ -52,7 +52,7 @@ def main(tag, cfg, kernel_substr="csum"):
     with open(os.path.join(dst, f"traffic_config{cfg}.json"), "w") as f:
         json.dump(traffic, f, indent=1)
     lines = [f"# rocprofv3 summary — {tag}, bench.py --config {cfg}", "",
-             f"Command: `tools/profile.sh {cfg} {tag}` (bench.py --config {cfg} --steps 50 --warmup 5 under "
+             f"Command: `tools/profile.sh {cfg} {tag}` (bench.py --config {cfg} --steps 50 --warmup 5 (2n: --no-pseudo) under "
              "`rocprofv3 --kernel-trace --stats`, then one `--pmc` pass per counter group).", "",
              "## Kernel stats (rocprofv3 --stats)", "", "| kernel | calls | avg µs | min µs | max µs |",
              "|---|---|---|---|---|"]
@@ -81,5 +81,5 @@ KERNEL_OF_CONFIG = {6: "tcp_build", 7: "ipv4_hdr", 8: "tcp_build", 9: "ipv4_hdr"
                     13: "rx_tcp", 14: "rx_tcp", 16: "rx_tcp", 17: "rx_tcp", 18: "rx_tcp"}  # bench.py workloads beyond the checksum configs
 
 if __name__ == "__main__":
-    c = int(sys.argv[2])
-    main(sys.argv[1], c, *(sys.argv[3:4] or [KERNEL_OF_CONFIG.get(c, "csum")]))
+    c = sys.argv[2]  # a workload number, or a label such as 2n (config 2 with --no-pseudo; tools/evidence.sh)
+    main(sys.argv[1], c, *(sys.argv[3:4] or [KERNEL_OF_CONFIG.get(int(c.rstrip("n")), "csum")]))

@@ -1,13 +1,14 @@
 #!/bin/bash
 # rocprofv3 evidence for one bench workload: kernel-trace stats, then each PMC
 # group in its own pass (never combined with other trace domains).
-# usage: [GROUPS_ONLY="kt fetch write sq sq2 tlb tcc"] tools/profile.sh <config> [tag]
+# usage: [GROUPS_ONLY="kt fetch write sq sq2 tlb tcc"] [BENCH_EXTRA="--no-pseudo"] tools/profile.sh <config> [tag] [label]
+# (label names the output directory, default the config number: e.g. 2n for config 2 with --no-pseudo)
 set -u
-cfg=${1:-2}; tag=${2:-r01}
-out=gpurun_out/prof_${tag}_c${cfg}
+cfg=${1:-2}; tag=${2:-r01}; label=${3:-$cfg}
+out=gpurun_out/prof_${tag}_c${label}
 mkdir -p "$out"
 export TMPDIR=/tmp
-B="bench.py --config $cfg --steps 50 --warmup 5 --cpu-seconds 0"
+B="bench.py --config $cfg --steps 50 --warmup 5 --cpu-seconds 0 ${BENCH_EXTRA:-}"
 run() {  # run <name> <timeout> rocprofv3-args...
   local name=$1 t=$2; shift 2
   echo "=== $name"
