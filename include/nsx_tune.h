@@ -31,7 +31,10 @@ typedef struct nsx_tune {
     int32_t blocks_per_cu;     /* persistent grid: 1..8 blocks of 256 threads per CU. Default of the ragged
                                   scan and receive kernels: 4 per CU, of which a batch whose mean segment /
                                   frame is >= 2048 B / 640 B uses 2 / 3 (the rest return at once); a value
-                                  here runs exactly that grid */
+                                  here launches exactly that grid. A shape that may take an LDS form (the
+                                  ragged scan's and receive pass's small-unit forms: ~34 KB of LDS per
+                                  block) has at most 4 of its blocks resident per CU at a time (160 KB of
+                                  LDS); forced streamed shapes (segs_per_wave 1 or 4) allocate no LDS */
     int32_t segs_per_wave;     /* fixed batches of <= 4 KiB segments: segments per wave task (1, 2, 4, 8).
                                   Ragged scan, per wave: 0 auto (the LDS form in waves whose segments
                                   average < 128 B, streamed runs of four 63-segment sets < 2048 B, else runs
@@ -44,7 +47,8 @@ typedef struct nsx_tune {
                                   loop (such runs as prefix-form pieces of <= 7 KiB), < 640 B the prefix
                                   form with 15 KiB slots on two waves per block, else streamed runs on 3
                                   blocks/CU; 5 / 6 / 7 force the small-frame mode / the two-wave prefix
-                                  form / the hybrid loop throughout on that grid. With rows or blocks_per_cu set (the
+                                  form / the hybrid loop throughout on that grid (NSX_EINVAL with rows
+                                  other than 0 / 2 or with blocks_per_cu set). With rows or blocks_per_cu set (the
                                   pre-prefix shapes): 0 = per wave the LDS form (mean < 128 B) or streamed
                                   runs, 1 = streamed runs, 2 = the LDS form. (A run that does not fit the
                                   LDS form's 8 KiB slot, or a piece whose first 8 frames exceed the prefix

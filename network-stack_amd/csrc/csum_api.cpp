@@ -216,7 +216,9 @@ int nsx_rx_ipv4_tcp_verify_dev_tuned(const void* d_base, const uint64_t* d_offse
     if (n > ((uint64_t)1 << 40)) return NSX_EINVAL;
     const int dev = current_device();
     if (dev < 0) return NSX_ENODEV;
-    return map_err(nsx::launch_rx_tcp(make_cfg(dev, tune), 4, d_base, d_offsets, n, d_mask, d_ip_raw, d_tcp_raw,
+    const nsx::LaunchCfg cfg = make_cfg(dev, tune);
+    if (!nsx::rx_tune_valid(cfg)) return NSX_EINVAL;
+    return map_err(nsx::launch_rx_tcp(cfg, 4, d_base, d_offsets, n, d_mask, d_ip_raw, d_tcp_raw,
                                       static_cast<hipStream_t>(stream)));
 }
 
@@ -232,7 +234,9 @@ int nsx_rx_ipv6_tcp_verify_dev_tuned(const void* d_base, const uint64_t* d_offse
     if (n > ((uint64_t)1 << 40)) return NSX_EINVAL;
     const int dev = current_device();
     if (dev < 0) return NSX_ENODEV;
-    return map_err(nsx::launch_rx_tcp(make_cfg(dev, tune), 6, d_base, d_offsets, n, d_mask, nullptr, d_tcp_raw,
+    const nsx::LaunchCfg cfg = make_cfg(dev, tune);
+    if (!nsx::rx_tune_valid(cfg)) return NSX_EINVAL;
+    return map_err(nsx::launch_rx_tcp(cfg, 6, d_base, d_offsets, n, d_mask, nullptr, d_tcp_raw,
                                       static_cast<hipStream_t>(stream)));
 }
 

@@ -860,10 +860,13 @@ __device__ __forceinline__ uint32_t lds_range_sum(const lds16* slot, uint32_t p,
     // A first block of 8 chunks, then blocks of 4 while the wave's longest range has more: a wave-uniform trip
     // count (an SGPR loop counter: a loop ending on a ballot left hipcc an undefined exit value that it read with
     // v_readfirstlane from a register still being loaded — a vmcnt wait that drained the next run's rows before this
-    // run's sums began). A block reads its chunks from c0 + j0 unclamped (one address, immediate offsets; the slot's
-    // pad keeps the reads past its last chunk inside it) and keeps those below nch. The first block is always read
-    // (its first chunk gives head and the neighbour's tail even for an empty range). Blocks of 4 after it: 64-128 B
-    // segments span up to 9 chunks, and a second block of 8 read 7 chunks for nothing in nearly every wave.
+    // run's sums began). A block reads its chunks from one address with immediate offsets and keeps those below nch.
+    // The first block is always read (its first chunk gives head and the neighbour's tail even for an empty range);
+    // it reads chunks c0 .. c0 + 7, at most 7 past the range's last chunk, which the slot's 256 B pad holds. Blocks
+    // of 4 after it: 64-128 B segments span up to 9 chunks, and a second block of 8 read 7 chunks for nothing in
+    // nearly every wave. A lane whose range has ended (j0 ≥ nch) reads its block from c0 again instead of c0 + j0,
+    // so no lane reads more than 3 chunks past its range: in a run that mixes a several-KB unit with small ones, j0
+    // runs up to the long unit's chunk count, and c0 + j0 would leave the slot.
     const uint32_t nmax = wave_max(nch);
     uint32_t acc;
     {
@@ -890,7 +893,7 @@ __device__ __forceinline__ uint32_t lds_range_sum(const lds16* slot, uint32_t p,
     }
     for (uint32_t j0 = 8; j0 < nmax; j0 += 4u) {
         u32x4 x[4];
-        const lds16* blk = slot + c0 + j0;
+        const lds16* blk = slot + c0 + (j0 < nch ? j0 : 0u);
 #pragma unroll
         for (uint32_t j = 0; j < 4u; ++j) x[j] = lds_get(blk, j);
 #pragma unroll
@@ -2945,7 +2948,10 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
     const int ns = (pipe && rows == 2 && c.segs_per_wave != 1) ? 2 : 1;
     // force runs of four sets (4) or the LDS form (2; tests and A/B); 0: by mean segment size
     const int sets = c.segs_per_wave == 4 || c.segs_per_wave == 2 ? c.segs_per_wave : 0;
-    const size_t lds = (size_t)kScanSlot * kWavesPerBlock;  // the LDS form's per-wave slots
+    // the LDS form's per-wave slots, only when the kernel may choose that form (forced streamed shapes allocate none,
+    // so more of their blocks fit a CU: 33.8 KB of LDS per block caps a launch at 4 resident blocks per CU)
+    const bool lds_form = sets == 2 || (ns == 2 && sets == 0);
+    const size_t lds = lds_form ? (size_t)kScanSlot * kWavesPerBlock : 0;
     // Default grid: 4 blocks/CU, of which a batch of segments averaging ≥ kScanBigMean uses 2 (active_blocks;
     // config 3 keeps its 2 blocks/CU). A blocks_per_cu override runs exactly that grid.
     const bool pick = c.blocks_per_cu == 0 && pipe && rows == 2 && sets == 0;
@@ -3004,8 +3010,16 @@ hipError_t launch_ragged(const LaunchCfg& c, const void* d_base, const uint64_t*
     return launch_ragged_scan<false>(c, base, d_offsets, n, partial, out, nullptr, st);
 }
 
+bool rx_tune_valid(const LaunchCfg& c) {
+    // segs_per_wave 5 / 6 / 7 force a mode of the default grid; they mean nothing on the shapes rows / blocks_per_cu
+    // select (silently running the auto shape there made fuzz cases test another form than they named)
+    const bool grid_mode = c.segs_per_wave == 5 || c.segs_per_wave == 6 || c.segs_per_wave == 7;
+    return !grid_mode || ((c.rows == 0 || c.rows == 2) && c.blocks_per_cu == 0);
+}
+
 hipError_t launch_rx_tcp(const LaunchCfg& c, int ipver, const void* d_base, const uint64_t* d_offsets, uint64_t n,
                          uint64_t* mask, uint16_t* ip_raw, uint16_t* tcp_raw, hipStream_t st) {
+    if (!rx_tune_valid(c)) return hipErrorInvalidValue;
     // Double-buffered batches of 2 rows, 3 blocks/CU (tools/ab.py --config 10, same process: 0.1294 ms against
     // 0.1305 for batches of 4 rows, 0.1348 for single batches of 8 rows, 0.145 for 2 rows at 2 blocks/CU, 0.136
     // at 4); launches of ≤ 2^27 frames (a multiple of 64, so every launch starts on a mask word)
@@ -3014,7 +3028,8 @@ hipError_t launch_rx_tcp(const LaunchCfg& c, int ipver, const void* d_base, cons
     // wave's mean frame size or forced by segs_per_wave 1 / 2; blocks_per_cu runs exactly that grid (default 3;
     // the register-capped instantiation from 4 blocks/CU up).
     const int sets = c.segs_per_wave == 1 || c.segs_per_wave == 2 ? c.segs_per_wave : 0;
-    const size_t lds = (size_t)kRxSlot * kWavesPerBlock;  // the LDS form's per-wave slots (3 blocks/CU: 100 KB)
+    // the LDS form's per-wave slots (3 blocks/CU: 100 KB), unless streamed runs are forced (sets 1)
+    const size_t lds = sets == 1 ? 0 : (size_t)kRxSlot * kWavesPerBlock;
     const uint32_t mb = max_blocks_of(c, 3);
     const uint32_t keep = 0u;
     const bool w4 = rows == 2 && mb >= (uint32_t)c.cus * 4u;

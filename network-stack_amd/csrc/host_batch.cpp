@@ -388,6 +388,7 @@ static int rx_host(int ipver, const uint8_t* h_base, const uint64_t* h_offsets, 
                    int num_gpus, const nsx_tune* tune) {
     if (n == 0) return NSX_OK;
     if (!h_mask || !h_offsets || !h_base) return NSX_EINVAL;
+    if (!nsx::rx_tune_valid(nsx::launch_cfg(1, tune))) return NSX_EINVAL;
     for (uint64_t i = 0; i < n; ++i)
         if (h_offsets[i + 1] < h_offsets[i]) return NSX_EINVAL;
     return run_sharded(h_base, 0, 0, h_offsets, n, nullptr, nullptr, h_mask, ipver, num_gpus, tune);

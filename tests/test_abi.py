@@ -333,3 +333,17 @@ def test_tcp_wire_len_and_layout_match_reference_bytes():
     want = np.zeros(len(segs) + 1, np.uint64)
     want[1:] = np.cumsum([(len(s.bytes()) + 3) & ~3 for s in segs])
     assert np.array_equal(out_off, want)
+
+
+def test_receive_grid_modes_off_the_default_grid_are_einval():
+    """segs_per_wave 5 / 6 / 7 force a mode of the receive pass's default grid; with rows 4-16 or
+    blocks_per_cu set they name no shape and are refused (NSX_EINVAL) instead of silently running the auto shape.
+    The host entry points check before touching a device, so this runs on any host."""
+    offs = np.array([0, 40], np.uint64)
+    buf = np.zeros(40, np.uint8)
+    for mode in (5, 6, 7):
+        for bad in (dict(blocks_per_cu=2), dict(rows=4), dict(rows=16, blocks_per_cu=1)):
+            for fn in (nsx.rx_ipv4_tcp_verify_host, nsx.rx_ipv6_tcp_verify_host):
+                with pytest.raises(nsx.NsxError) as e:
+                    fn(buf, offs, tune=dict(bad, segs_per_wave=mode))
+                assert e.value.code == nsx.NSX_EINVAL, (mode, bad)

@@ -210,6 +210,16 @@ def test_fuzz_tcp_build_options(case):
         assert not got[o + len(want[i]):int(out_off[i + 1])].any(), (case, i)
 
 
+def rx_fuzz_tune(rng) -> dict:
+    """A random receive-pass launch shape: one of the default grid's modes (segs_per_wave 0 auto, 5 small-frame,
+    6 two-wave prefix, 7 hybrid; rows 0 or 2, no blocks_per_cu), or one of the older shapes rows / blocks_per_cu
+    select (segs_per_wave 0 auto, 1 streamed, 2 LDS) — never a mode on a grid it does not exist on."""
+    if rng.random() < 0.5:
+        return dict(rows=int(rng.choice([0, 2])), segs_per_wave=int(rng.choice([0, 5, 6, 7])))
+    return dict(rows=int(rng.choice([0, 2, 4, 8, 16])), blocks_per_cu=int(rng.choice([1, 2, 4, 8])),
+                segs_per_wave=int(rng.choice([0, 1, 2])))
+
+
 @pytest.mark.parametrize("case", range(40 * SCALE))
 def test_fuzz_rx(case):
     """Random received-datagram batches (every frame kind of tests/_rx.py in random proportions, random start
@@ -222,8 +232,7 @@ def test_fuzz_rx(case):
     buf, offs, _ = _rx.batch(rng, n, weights=w / w.sum(), lead=int(rng.integers(0, 8)),
                              max_payload=int(rng.choice([64, 600, 1460, 9000])))
     want_m, want_i, want_t = O.c_rx_ipv4_tcp(buf, offs)
-    tune = dict(rows=int(rng.choice([0, 2, 4, 8, 16])), blocks_per_cu=int(rng.choice([0, 1, 2, 4, 8])),
-                segs_per_wave=int(rng.choice([0, 1, 2, 5, 6, 7])))  # auto / streamed / LDS / prefix / default-grid modes
+    tune = rx_fuzz_tune(rng)
     mask = torch.empty((n + 63) // 64, dtype=torch.int64, device="cuda")
     ipr, tcpr = torch.empty(n, dtype=torch.int16, device="cuda"), torch.empty(n, dtype=torch.int16, device="cuda")
     nsx.rx_ipv4_tcp_verify_dev(_dev(buf), _dev(offs.view(np.int64)), mask=mask, ip_raw=ipr, tcp_raw=tcpr, tune=tune)
@@ -246,8 +255,7 @@ def test_fuzz_rx6(case):
     buf, offs, _ = _rx.batch(rng, n, kinds=_rx.KINDS6, weights=w / w.sum(), lead=int(rng.integers(0, 8)),
                              max_payload=int(rng.choice([64, 600, 1440, 9000])), ip=6)
     want_m, want_t = O.c_rx_ipv6_tcp(buf, offs)
-    tune = dict(rows=int(rng.choice([0, 2, 4, 8, 16])), blocks_per_cu=int(rng.choice([0, 1, 2, 4, 8])),
-                segs_per_wave=int(rng.choice([0, 1, 2, 5, 6, 7])))
+    tune = rx_fuzz_tune(rng)
     mask = torch.empty((n + 63) // 64, dtype=torch.int64, device="cuda")
     tcpr = torch.empty(n, dtype=torch.int16, device="cuda")
     nsx.rx_ipv6_tcp_verify_dev(_dev(buf), _dev(offs.view(np.int64)), mask=mask, tcp_raw=tcpr, tune=tune)
