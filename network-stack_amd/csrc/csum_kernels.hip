@@ -1037,6 +1037,110 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
     }
 }
 
+// XV bit 2 (experiment, with runs of 64): TWO runs in flight per wave instead of one — two row register sets used in
+// turn, each restaged and reissued in its own step (stage run k from set k mod 2, then load run k + 2 into it while
+// run k + 1 is still arriving in the other). Every value a step waits for was issued before the rows still in
+// flight (vmcnt counts in issue order): run k's partials are loaded just before run k's rows, and the offsets of
+// run k + 3 before run k + 2's rows. 64 more VGPRs: launched at 3 blocks/CU.
+template <int R, bool VERIFY, bool PIPE, int XV>
+__device__ __forceinline__ void ragged_runs_lds_deep(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs,
+                                                     uint32_t n, __amdgpu_buffer_rsrc_t prs, __amdgpu_buffer_rsrc_t ors,
+                                                     __amdgpu_buffer_rsrc_t oks, uint32_t a0, uint32_t a_end,
+                                                     uint32_t lane, lds16* slot) {
+    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+    constexpr uint32_t run = kWave;
+    constexpr int kSt = (XV & 2) ? kStoreSc1 : 0;
+    auto ld64 = [&](uint32_t i, bool live) -> uint64_t {
+        const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, live ? i * 8 : kOOB, 0, 0);
+        return ((uint64_t)x.y << 32) | x.x;
+    };
+    struct Offs {
+        uint64_t off, end;  // lane l: offsets[a + l], offsets[a + l + 1]
+    };
+    auto load_offs = [&](uint32_t a) {
+        return Offs{ld64(a + lane, a < a_end && a + lane <= n), ld64(a + lane + 1u, a < a_end && a + lane + 1u <= n)};
+    };
+    struct Run {
+        const uint8_t* rbase;
+        uint64_t span;
+        uint32_t cnt;
+        bool lds;
+    };
+    auto geo = [&](uint32_t a, const Offs& o) {
+        Run g{base, 0, a < a_end ? min(run, a_end - a) : 0u, false};
+        if (g.cnt) {
+            const uint64_t lo = readlane64(o.off, 0), hi = readlane64(o.end, g.cnt - 1u);
+            g.rbase = reinterpret_cast<const uint8_t*>(((uintptr_t)(base + lo)) & ~(uintptr_t)127);
+            g.span = (uint64_t)((base + hi) - g.rbase);
+            g.lds = g.span <= (uint64_t)kScanSlotRows * kRow;
+        }
+        return g;
+    };
+    auto load_part = [&](uint32_t a, const Run& g) {
+        return __builtin_amdgcn_raw_buffer_load_b32(prs, lane < g.cnt ? (a + lane) * 4 : kOOB, 0, 0);
+    };
+    u32x4 VA[kScanSlotRows], VB[kScanSlotRows];
+    auto issue = [&](const Run& g, u32x4 (&V)[kScanSlotRows]) {
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(g.rbase, (g.span + 3) & ~3ull);
+#pragma unroll
+        for (uint32_t r = 0; r < kScanSlotRows; ++r) V[r] = bld16<true>(rs, r * kRow + lane * 16u);
+    };
+    uint32_t a = a0;
+    while (a < a_end) {
+        Offs oc = load_offs(a), on = load_offs(a + run), op = load_offs(a + 2u * run);
+        __builtin_amdgcn_s_waitcnt(kWaitVm0);
+        Run cur = geo(a, oc);
+        if (!cur.lds) {  // too wide for the slot: streamed as 63 + 1 segments (ragged_runs_lds)
+            const uint32_t part = load_part(a, cur);
+            const uint32_t c1 = min(cur.cnt, kScanRun), c2 = cur.cnt - c1;
+            const uint32_t cnt1[1] = {c1}, part1[1] = {part};
+            const uint64_t o1[1] = {lane == c1 ? readlane64(oc.end, c1 - 1u) : oc.off};
+            ragged_run_stream<R, VERIFY, PIPE, 1>(base, a, kScanRun, cnt1, o1, part1, ors, oks, lane);
+            if (c2) {
+                const uint32_t cnt2[1] = {c2}, part2[1] = {(uint32_t)__shfl_down((int)part, c1)};
+                const uint64_t o2[1] = {lane == 0 ? readlane64(oc.off, c1) : readlane64(oc.end, c1)};
+                ragged_run_stream<R, VERIFY, PIPE, 1>(base, a + c1, kScanRun, cnt2, o2, part2, ors, oks, lane);
+            }
+            a += run;
+            continue;
+        }
+        Run nxt = geo(a + run, on);
+        if (!nxt.lds) nxt.span = 0;
+        uint32_t pc = load_part(a, cur);
+        issue(cur, VA);
+        uint32_t pn = load_part(a + run, nxt);
+        issue(nxt, VB);
+        // One step: run `cur` (rows in V) staged and summed; run cur + 2 loaded into V.
+        auto step = [&](u32x4 (&V)[kScanSlotRows]) -> bool {
+            lds_stage<kScanSlotRows>(slot, V, cur.span, lane);
+            lds_zero_tail(slot, cur.span, lane);
+            const Offs oq = load_offs(a + 3u * run);  // before run + 2's rows
+            Run nn = nxt.lds ? geo(a + 2u * run, op) : Run{base, 0, 0u, false};
+            if (!nn.lds) nn.span = 0;
+            const uint32_t pnn = load_part(a + 2u * run, nn);
+            issue(nn, V);
+            const bool mine = lane < cur.cnt;
+            const uint32_t p = mine ? (uint32_t)((base + oc.off) - cur.rbase) : 0u;
+            const uint32_t e = mine ? (uint32_t)((base + oc.end) - cur.rbase) : 0u;
+            const uint32_t dq = reinterpret_cast<const uint32_t*>(slot)[p >> 2];
+            const uint32_t res = finish(fold32(lds_range_sum(slot, p, e, dq, mine)), (p & 1u) == 0, pc);
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, mine ? (a + lane) * 2 : kOOB, 0, kSt);
+            if constexpr (VERIFY)
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(res == 0xFFFFu), oks, mine ? a + lane : kOOB, 0, kSt);
+            a += run;
+            if (!nxt.lds) return false;  // the end of the range, or a run for the outer loop
+            cur = nxt, nxt = nn;
+            pc = pn, pn = pnn;
+            oc = on, on = op, op = oq;
+            return true;
+        };
+        for (;;) {
+            if (!step(VA)) break;
+            if (!step(VB)) break;
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // The prefix form: per-unit work that does not grow with the unit. The LDS forms
 // (ragged_runs_lds above, rx_runs_lds below) sum each unit chunk by chunk in its own lane, so a run holding one
@@ -1256,7 +1360,7 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
         const uint32_t b = blockIdx.x, W = nb * kWavesPerBlock;
         const uint32_t g = (nb >= 16 && (nb & 7) == 0) ? ((b & 7) * (nb >> 3) + (b >> 3)) * kWavesPerBlock + wave
                                                         : b * kWavesPerBlock + wave;
-        const WaveRange wr = wave_range(ofs, n, g, W, lane, kScanLdsSeg, 1u, (XV & 1) ? kWave : 0u);
+        const WaveRange wr = wave_range(ofs, n, g, W, lane, kScanLdsSeg, 1u, (XV & 5) ? kWave : 0u);
         a0 = wr.a0, a_end = wr.a_end, wave_bytes = wr.bytes;
     }
     // Two sets per run suit segments of a few hundred bytes and up (config 3). A wave whose segments average under
@@ -1264,8 +1368,12 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
     // each run still streams tens of KB (§7 step 42).
     if (sets == 2 || (NS == 2 && sets == 0 && wave_bytes < (uint64_t)kScanLdsSeg * (a_end - a0))) {
         extern __shared__ lds16 lds_scan[];
-        ragged_runs_lds<R, VERIFY, PIPE, XV>(base, ofs, n, prs, ors, oks, run, a0, a_end, lane,
-                                             lds_scan + wave * (kScanSlot / 16u));
+        if constexpr ((XV & 4) != 0)
+            ragged_runs_lds_deep<R, VERIFY, PIPE, XV>(base, ofs, n, prs, ors, oks, a0, a_end, lane,
+                                                      lds_scan + wave * (kScanSlot / 16u));
+        else
+            ragged_runs_lds<R, VERIFY, PIPE, XV>(base, ofs, n, prs, ors, oks, run, a0, a_end, lane,
+                                                 lds_scan + wave * (kScanSlot / 16u));
     } else if (NS == 2 && (sets == 4 || (sets == 0 && wave_bytes < (uint64_t)kScanSmallSeg * (a_end - a0)))) {
         ragged_runs<R, VERIFY, PIPE, 4>(base, ofs, n, prs, ors, oks, run, a0, a_end, lane);
     } else {
@@ -2937,8 +3045,8 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
     // batches of 3 or 4 rows, 0.93 for 1 row). kernel 2 (NSX_TUNE_KERNEL_SCAN_PLAIN):
     // single batches of 4, 8 (default) or 16 rows.
     const bool pipe = c.kernel != 2;
-    // kernel 4..6: experiment variants of the LDS form (XV 1..3, ragged_runs_lds)
-    const int xv = c.kernel >= 4 && c.kernel <= 6 ? c.kernel - 3 : 0;
+    // kernel 4..8: experiment variants of the LDS form (XV 1, 2, 3, 5, 7: ragged_runs_lds, ragged_runs_lds_deep)
+    const int xv = c.kernel >= 4 && c.kernel <= 6 ? c.kernel - 3 : c.kernel == 7 ? 5 : c.kernel == 8 ? 7 : 0;
     const int rows = pipe ? (c.rows == 2 || c.rows == 4 || c.rows == 8 ? c.rows : 2)
                           : (c.rows == 4 || c.rows == 8 || c.rows == 16 ? c.rows : 8);
     const uint32_t run = (c.run_segs >= 1 && c.run_segs <= (int)kScanRun) ? (uint32_t)c.run_segs : kScanRun;
@@ -2980,7 +3088,7 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
                     hipLaunchKernelGGL((csum_ragged_scan_kernel<2, VERIFY, true, 2, X_>), dim3(grid), dim3(kBlock), \
                                        lds, st, base, offsets + c0, cn, pc, oc, kc, run, sets, keep);              \
                     break;
-                NSX_RSCAN_XV(1) NSX_RSCAN_XV(2) NSX_RSCAN_XV(3)
+                NSX_RSCAN_XV(1) NSX_RSCAN_XV(2) NSX_RSCAN_XV(3) NSX_RSCAN_XV(5) NSX_RSCAN_XV(7)
 #undef NSX_RSCAN_XV
                 default:
                     hipLaunchKernelGGL((csum_ragged_scan_kernel<2, VERIFY, true, 2>), dim3(grid), dim3(kBlock), lds, st,
