@@ -937,7 +937,8 @@ constexpr uint32_t kScanSlot = kScanSlotRows * kRow + 256;  // + pad: lds_range_
 
 // XV (experiment, tools/evidence.sh ab): bit 0 = runs of 64 segments, each lane loading both of its segment's
 // offsets (the receive pass's form: no cross-lane shift for the end, and a run's 64 results are one whole 128 B
-// line when the wave range starts at a multiple of 64); bit 1 = write-through (sc1) result stores.
+// line when the wave range starts at a multiple of 64); bit 1 = write-through (sc1) result stores. Diagnostics (wrong
+// results, A/B only): bit 3 = no partial load, bit 4 = no result store, bit 5 = no LDS sum (the dword at p instead).
 template <int R, bool VERIFY, bool PIPE, int XV = 0>
 __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
                                                 __amdgpu_buffer_rsrc_t prs, __amdgpu_buffer_rsrc_t ors,
@@ -1011,7 +1012,8 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
         uint64_t n_off = load_offs(a + run), n_end = R64 ? load_ends(a + run) : 0;
         __builtin_amdgcn_s_waitcnt(kWaitVm0);  // as in rx_runs_lds: nothing in flight at the loop's entry
         for (;;) {
-            const uint32_t part = __builtin_amdgcn_raw_buffer_load_b32(prs, lane < cur.cnt ? (a + lane) * 4 : kOOB, 0, 0);
+            const uint32_t part =
+                (XV & 8) ? 0u : __builtin_amdgcn_raw_buffer_load_b32(prs, lane < cur.cnt ? (a + lane) * 4 : kOOB, 0, 0);
             lds_stage<kScanSlotRows>(slot, V, cur.span, lane);
             lds_zero_tail(slot, cur.span, lane);
             Run nxt = geo(a + run, n_off, n_end);
@@ -1024,8 +1026,10 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
             const uint32_t p = mine ? (uint32_t)((base + c_off) - cur.rbase) : 0u;
             const uint32_t e = mine ? (uint32_t)((base + e_off) - cur.rbase) : 0u;
             const uint32_t dq = reinterpret_cast<const uint32_t*>(slot)[p >> 2];
-            const uint32_t res = finish(fold32(lds_range_sum(slot, p, e, dq, mine)), (p & 1u) == 0, part);
-            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, mine ? (a + lane) * 2 : kOOB, 0, kSt);
+            const uint32_t sum = (XV & 32) ? dq + e : lds_range_sum(slot, p, e, dq, mine);
+            const uint32_t res = finish(fold32(sum), (p & 1u) == 0, part);
+            if constexpr ((XV & 16) == 0)
+                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, mine ? (a + lane) * 2 : kOOB, 0, kSt);
             if constexpr (VERIFY)
                 __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(res == 0xFFFFu), oks, mine ? a + lane : kOOB, 0, kSt);
             a += run;
@@ -3046,7 +3050,9 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
     // single batches of 4, 8 (default) or 16 rows.
     const bool pipe = c.kernel != 2;
     // kernel 4..8: experiment variants of the LDS form (XV 1, 2, 3, 5, 7: ragged_runs_lds, ragged_runs_lds_deep)
-    const int xv = c.kernel >= 4 && c.kernel <= 6 ? c.kernel - 3 : c.kernel == 7 ? 5 : c.kernel == 8 ? 7 : 0;
+    // (kernel 100 + XV for the diagnostic variants 8, 9, 16, 32, 48)
+    const int xv = c.kernel >= 4 && c.kernel <= 6 ? c.kernel - 3 : c.kernel == 7 ? 5 : c.kernel == 8 ? 7
+                 : c.kernel >= 100 ? c.kernel - 100 : 0;
     const int rows = pipe ? (c.rows == 2 || c.rows == 4 || c.rows == 8 ? c.rows : 2)
                           : (c.rows == 4 || c.rows == 8 || c.rows == 16 ? c.rows : 8);
     const uint32_t run = (c.run_segs >= 1 && c.run_segs <= (int)kScanRun) ? (uint32_t)c.run_segs : kScanRun;
@@ -3089,6 +3095,7 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
                                        lds, st, base, offsets + c0, cn, pc, oc, kc, run, sets, keep);              \
                     break;
                 NSX_RSCAN_XV(1) NSX_RSCAN_XV(2) NSX_RSCAN_XV(3) NSX_RSCAN_XV(5) NSX_RSCAN_XV(7)
+                NSX_RSCAN_XV(8) NSX_RSCAN_XV(9) NSX_RSCAN_XV(16) NSX_RSCAN_XV(32) NSX_RSCAN_XV(48)
 #undef NSX_RSCAN_XV
                 default:
                     hipLaunchKernelGGL((csum_ragged_scan_kernel<2, VERIFY, true, 2>), dim3(grid), dim3(kBlock), lds, st,

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Same-process A/B of launch overrides (include/nsx_tune.h) on one bench workload.
+"""Same-process A/B of launch overrides (variants named x_* are diagnostics: no parity check) (include/nsx_tune.h) on one bench workload.
 
     python tools/ab.py --config 6 --variants "def:;b3:blocks_per_cu=3;b8:blocks_per_cu=8" [--rounds 7]
 
@@ -57,8 +57,8 @@ def main():
     # every variant must give the first one's results on this batch (they differ only in launch shape or code path)
     ref = None
     for name, step, _ in variants:
-        if cfg["kind"] == "rx" and name.startswith("scan"):
-            continue
+        if (cfg["kind"] == "rx" and name.startswith("scan")) or name.startswith("x_"):
+            continue  # another computation / a diagnostic variant whose results are wrong on purpose
         w["out"].zero_()
         step()
         torch.cuda.synchronize()
