@@ -939,6 +939,9 @@ constexpr uint32_t kScanSlot = kScanSlotRows * kRow + 256;  // + pad: lds_range_
 // offsets (the receive pass's form: no cross-lane shift for the end, and a run's 64 results are one whole 128 B
 // line when the wave range starts at a multiple of 64); bit 1 = write-through (sc1) result stores. Diagnostics (wrong
 // results, A/B only): bit 3 = no partial load, bit 4 = no result store, bit 5 = no LDS sum (the dword at p instead).
+// Bit 6 (with bit 0): results parked in LDS (1 KiB per wave after its slot) and written 8 runs at a time, one
+// 16 B store per lane (1 KiB contiguous) instead of one 2 B store per lane per run; a wave's partial last run and
+// the runs before a streamed one are written as before.
 template <int R, bool VERIFY, bool PIPE, int XV = 0>
 __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
                                                 __amdgpu_buffer_rsrc_t prs, __amdgpu_buffer_rsrc_t ors,
@@ -980,6 +983,20 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
         const __amdgpu_buffer_rsrc_t rs = make_rsrc(g.rbase, (g.span + 3) & ~3ull);
 #pragma unroll
         for (uint32_t r = 0; r < kScanSlotRows; ++r) V[r] = bld16<true>(rs, r * kRow + lane * 16u);
+    };
+    constexpr bool PARK = (XV & 64) != 0 && R64;
+    uint16_t* park = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(slot) + kScanSlot);
+    uint32_t parked = 0, a_park = 0;  // full runs parked, the first one's segment index
+    auto flush = [&]() {              // the parked runs' 64·parked results: lane l stores results 8l .. 8l + 7
+        if (parked) {
+            __builtin_amdgcn_wave_barrier();
+            const lds16 v = reinterpret_cast<const lds16*>(park)[lane];
+            typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+            __builtin_amdgcn_raw_buffer_store_b128(v4u{v.x, v.y, v.z, v.w}, ors,
+                                                   lane < 8u * parked ? (a_park + lane * 8u) * 2u : kOOB, 0, kSt);
+            __builtin_amdgcn_wave_barrier();
+            parked = 0;
+        }
     };
     // As rx_runs_lds: the LDS loop runs while consecutive runs fit the slot; a run that does not is streamed on
     // its own in the outer loop, so the streaming form's loads in flight at its end never merge into the LDS
@@ -1028,8 +1045,18 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
             const uint32_t dq = reinterpret_cast<const uint32_t*>(slot)[p >> 2];
             const uint32_t sum = (XV & 32) ? dq + e : lds_range_sum(slot, p, e, dq, mine);
             const uint32_t res = finish(fold32(sum), (p & 1u) == 0, part);
-            if constexpr ((XV & 16) == 0)
+            if constexpr (PARK) {
+                if (cur.cnt == kWave) {  // a full run: parked (wave-uniform)
+                    if (parked == 0) a_park = a;
+                    park[parked * kWave + lane] = (uint16_t)res;
+                    if (++parked == 8u) flush();
+                } else {
+                    flush();
+                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, mine ? (a + lane) * 2 : kOOB, 0, kSt);
+                }
+            } else if constexpr ((XV & 16) == 0) {
                 __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, mine ? (a + lane) * 2 : kOOB, 0, kSt);
+            }
             if constexpr (VERIFY)
                 __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(res == 0xFFFFu), oks, mine ? a + lane : kOOB, 0, kSt);
             a += run;
@@ -1038,6 +1065,7 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
             c_off = n_off, n_off = p_off;
             c_end = n_end, n_end = p_end;
         }
+        if constexpr (PARK) flush();
     }
 }
 
@@ -1377,7 +1405,7 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
                                                       lds_scan + wave * (kScanSlot / 16u));
         else
             ragged_runs_lds<R, VERIFY, PIPE, XV>(base, ofs, n, prs, ors, oks, run, a0, a_end, lane,
-                                                 lds_scan + wave * (kScanSlot / 16u));
+                                                 lds_scan + wave * ((kScanSlot + ((XV & 64) ? 1024u : 0u)) / 16u));
     } else if (NS == 2 && (sets == 4 || (sets == 0 && wave_bytes < (uint64_t)kScanSmallSeg * (a_end - a0)))) {
         ragged_runs<R, VERIFY, PIPE, 4>(base, ofs, n, prs, ors, oks, run, a0, a_end, lane);
     } else {
@@ -3065,7 +3093,7 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
     // the LDS form's per-wave slots, only when the kernel may choose that form (forced streamed shapes allocate none,
     // so more of their blocks fit a CU: 33.8 KB of LDS per block caps a launch at 4 resident blocks per CU)
     const bool lds_form = sets == 2 || (ns == 2 && sets == 0);
-    const size_t lds = lds_form ? (size_t)kScanSlot * kWavesPerBlock : 0;
+    const size_t lds = lds_form ? (size_t)(kScanSlot + (xv & 64 ? 1024u : 0u)) * kWavesPerBlock : 0;
     // Default grid: 4 blocks/CU, of which a batch of segments averaging ≥ kScanBigMean uses 2 (active_blocks;
     // config 3 keeps its 2 blocks/CU). A blocks_per_cu override runs exactly that grid.
     const bool pick = c.blocks_per_cu == 0 && pipe && rows == 2 && sets == 0;
@@ -3095,7 +3123,7 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
                                        lds, st, base, offsets + c0, cn, pc, oc, kc, run, sets, keep);              \
                     break;
                 NSX_RSCAN_XV(1) NSX_RSCAN_XV(2) NSX_RSCAN_XV(3) NSX_RSCAN_XV(5) NSX_RSCAN_XV(7)
-                NSX_RSCAN_XV(8) NSX_RSCAN_XV(9) NSX_RSCAN_XV(16) NSX_RSCAN_XV(32) NSX_RSCAN_XV(48)
+                NSX_RSCAN_XV(8) NSX_RSCAN_XV(9) NSX_RSCAN_XV(16) NSX_RSCAN_XV(32) NSX_RSCAN_XV(48) NSX_RSCAN_XV(65)
 #undef NSX_RSCAN_XV
                 default:
                     hipLaunchKernelGGL((csum_ragged_scan_kernel<2, VERIFY, true, 2>), dim3(grid), dim3(kBlock), lds, st,
