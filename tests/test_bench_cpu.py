@@ -155,3 +155,15 @@ def test_cpu_baseline_rx_frames():
     assert res["sample_parity_vs_gpu"] and res["value"] > 0
     w["out"][3] ^= 1 << 5
     assert not bench.cpu_baseline(cfg, w, 0.05)["sample_parity_vs_gpu"]
+
+
+def test_config2_pseudo_header_partials_in_the_workload_and_the_line():
+    """config 2 (and 5) are measured over N x u32 pseudo-header partials, counted
+    in the algorithmic bytes; --no-pseudo names the partial-less line and finds its own traffic profile."""
+    for c in (2, 5):
+        assert bench.WORKLOADS[c]["pseudo"] and "pseudo-header" in bench.WORKLOADS[c]["name"]
+    args = bench.parse_args(["--config", "2", "--no-pseudo"])
+    assert args.no_pseudo and not bench.parse_args([]).no_pseudo
+    assert bench.load_traffic("2")["bytes_per_launch"] > 0          # with partials (round 4 profile)
+    assert bench.load_traffic("2n")["source"].endswith("traffic_config2n.json")
+    assert bench.load_traffic("99") is None
