@@ -937,8 +937,8 @@ constexpr uint32_t kScanSlot = kScanSlotRows * kRow + 256;  // + pad: lds_range_
 
 // XV (experiment, tools/evidence.sh ab): bit 0 = runs of 64 segments, each lane loading both of its segment's
 // offsets (the receive pass's form: no cross-lane shift for the end, and a run's 64 results are one whole 128 B
-// line when the wave range starts at a multiple of 64); bit 1 = write-through (sc1) result stores. Diagnostics (wrong
-// results, A/B only): bit 3 = no partial load, bit 4 = no result store, bit 5 = no LDS sum (the dword at p instead).
+// line when the wave range starts at a multiple of 64); bit 1 = write-through (sc1) result stores; bit 3 = no
+// per-run partial load when the batch has none (has_part false).
 // Bit 6 (with bit 0): results parked in LDS (1 KiB per wave after its slot) and written 8 runs at a time, one
 // 16 B store per lane (1 KiB contiguous) instead of one 2 B store per lane per run; a wave's partial last run and
 // the runs before a streamed one are written as before.
@@ -946,7 +946,7 @@ template <int R, bool VERIFY, bool PIPE, int XV = 0>
 __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
                                                 __amdgpu_buffer_rsrc_t prs, __amdgpu_buffer_rsrc_t ors,
                                                 __amdgpu_buffer_rsrc_t oks, uint32_t run, uint32_t a0, uint32_t a_end,
-                                                uint32_t lane, lds16* slot) {
+                                                uint32_t lane, lds16* slot, bool has_part = true) {
     typedef uint32_t v2u __attribute__((ext_vector_type(2)));
     constexpr bool R64 = (XV & 1) != 0;
     constexpr int kSt = (XV & 2) ? kStoreSc1 : 0;
@@ -1029,8 +1029,9 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
         uint64_t n_off = load_offs(a + run), n_end = R64 ? load_ends(a + run) : 0;
         __builtin_amdgcn_s_waitcnt(kWaitVm0);  // as in rx_runs_lds: nothing in flight at the loop's entry
         for (;;) {
-            const uint32_t part =
-                (XV & 8) ? 0u : __builtin_amdgcn_raw_buffer_load_b32(prs, lane < cur.cnt ? (a + lane) * 4 : kOOB, 0, 0);
+            const uint32_t part = (XV & 8) && !has_part
+                                      ? 0u
+                                      : __builtin_amdgcn_raw_buffer_load_b32(prs, lane < cur.cnt ? (a + lane) * 4 : kOOB, 0, 0);
             lds_stage<kScanSlotRows>(slot, V, cur.span, lane);
             lds_zero_tail(slot, cur.span, lane);
             Run nxt = geo(a + run, n_off, n_end);
@@ -1043,8 +1044,7 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
             const uint32_t p = mine ? (uint32_t)((base + c_off) - cur.rbase) : 0u;
             const uint32_t e = mine ? (uint32_t)((base + e_off) - cur.rbase) : 0u;
             const uint32_t dq = reinterpret_cast<const uint32_t*>(slot)[p >> 2];
-            const uint32_t sum = (XV & 32) ? dq + e : lds_range_sum(slot, p, e, dq, mine);
-            const uint32_t res = finish(fold32(sum), (p & 1u) == 0, part);
+            const uint32_t res = finish(fold32(lds_range_sum(slot, p, e, dq, mine)), (p & 1u) == 0, part);
             if constexpr (PARK) {
                 if (cur.cnt == kWave) {  // a full run: parked (wave-uniform)
                     if (parked == 0) a_park = a;
@@ -1054,7 +1054,7 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
                     flush();
                     __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, mine ? (a + lane) * 2 : kOOB, 0, kSt);
                 }
-            } else if constexpr ((XV & 16) == 0) {
+            } else {
                 __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, mine ? (a + lane) * 2 : kOOB, 0, kSt);
             }
             if constexpr (VERIFY)
@@ -1405,7 +1405,8 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
                                                       lds_scan + wave * (kScanSlot / 16u));
         else
             ragged_runs_lds<R, VERIFY, PIPE, XV>(base, ofs, n, prs, ors, oks, run, a0, a_end, lane,
-                                                 lds_scan + wave * ((kScanSlot + ((XV & 64) ? 1024u : 0u)) / 16u));
+                                                 lds_scan + wave * ((kScanSlot + ((XV & 64) ? 1024u : 0u)) / 16u),
+                                                 partial != nullptr);
     } else if (NS == 2 && (sets == 4 || (sets == 0 && wave_bytes < (uint64_t)kScanSmallSeg * (a_end - a0)))) {
         ragged_runs<R, VERIFY, PIPE, 4>(base, ofs, n, prs, ors, oks, run, a0, a_end, lane);
     } else {
@@ -3078,7 +3079,7 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
     // single batches of 4, 8 (default) or 16 rows.
     const bool pipe = c.kernel != 2;
     // kernel 4..8: experiment variants of the LDS form (XV 1, 2, 3, 5, 7: ragged_runs_lds, ragged_runs_lds_deep)
-    // (kernel 100 + XV for the diagnostic variants 8, 9, 16, 32, 48)
+    // (kernel 100 + XV for the variants 8, 9, 65)
     const int xv = c.kernel >= 4 && c.kernel <= 6 ? c.kernel - 3 : c.kernel == 7 ? 5 : c.kernel == 8 ? 7
                  : c.kernel >= 100 ? c.kernel - 100 : 0;
     const int rows = pipe ? (c.rows == 2 || c.rows == 4 || c.rows == 8 ? c.rows : 2)
@@ -3123,7 +3124,7 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
                                        lds, st, base, offsets + c0, cn, pc, oc, kc, run, sets, keep);              \
                     break;
                 NSX_RSCAN_XV(1) NSX_RSCAN_XV(2) NSX_RSCAN_XV(3) NSX_RSCAN_XV(5) NSX_RSCAN_XV(7)
-                NSX_RSCAN_XV(8) NSX_RSCAN_XV(9) NSX_RSCAN_XV(16) NSX_RSCAN_XV(32) NSX_RSCAN_XV(48) NSX_RSCAN_XV(65)
+                NSX_RSCAN_XV(8) NSX_RSCAN_XV(9) NSX_RSCAN_XV(65)
 #undef NSX_RSCAN_XV
                 default:
                     hipLaunchKernelGGL((csum_ragged_scan_kernel<2, VERIFY, true, 2>), dim3(grid), dim3(kBlock), lds, st,

@@ -69,6 +69,10 @@ def main():
         print(f"parity {name}: {'same as first' if same else 'MISMATCH'}", flush=True)
         if not same:
             raise SystemExit(f"variant {name} differs from the first variant")
+    for name, step, _ in variants:  # one synchronised launch each first, so a hang names its variant
+        step()
+        torch.cuda.synchronize()
+        print(f"ran {name}", flush=True)
     t_end = time.perf_counter() + 1.0
     while time.perf_counter() < t_end:  # settle
         for _, step, _ in variants:
