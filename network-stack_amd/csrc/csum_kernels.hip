@@ -1414,6 +1414,28 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
     }
 }
 
+// Experiment: the LDS form alone in a kernel of its own (no streamed forms compiled beside it, no active_blocks),
+// register-capped like the receive pass's 4-blocks/CU kernel; equal-count wave ranges aligned to 64.
+template <bool VERIFY, int XV>
+__global__ __launch_bounds__(kBlock, 4) void csum_ragged_lds_kernel(
+    const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, uint32_t n,
+    const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, uint8_t* __restrict__ ok) {
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const __amdgpu_buffer_rsrc_t ofs = make_rsrc(offsets, ((uint64_t)n + 1) * 8);
+    const __amdgpu_buffer_rsrc_t prs = make_rsrc(partial, partial ? (uint64_t)n * 4 : 0);
+    const __amdgpu_buffer_rsrc_t ors = make_rsrc(out, out ? (uint64_t)n * 2 : 0);
+    const __amdgpu_buffer_rsrc_t oks = make_rsrc(ok, VERIFY ? (uint64_t)n : 0);
+    const uint32_t nb = gridDim.x, b = blockIdx.x, W = nb * kWavesPerBlock;
+    const uint32_t g = (nb >= 16 && (nb & 7) == 0) ? ((b & 7) * (nb >> 3) + (b >> 3)) * kWavesPerBlock + wave
+                                                    : b * kWavesPerBlock + wave;
+    const WaveRange wr = wave_range(ofs, n, g, W, lane, 0xFFFFFFFFu, 1u, kWave);
+    extern __shared__ lds16 lds_scan[];
+    ragged_runs_lds<2, VERIFY, true, XV>(base, ofs, n, prs, ors, oks, kWave, wr.a0, wr.a_end, lane,
+                                         lds_scan + wave * ((kScanSlot + ((XV & 64) ? 1024u : 0u)) / 16u),
+                                         partial != nullptr);
+}
+
 // ---------------------------------------------------------------------------
 // Fused receive pass (SURVEY.md §8 f2 + f3 in one launch): a batch of received
 // IPv4 datagrams carrying TCP, densely packed (frame i = base[offsets[i],
@@ -3081,7 +3103,7 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
     // kernel 4..8: experiment variants of the LDS form (XV 1, 2, 3, 5, 7: ragged_runs_lds, ragged_runs_lds_deep)
     // (kernel 100 + XV for the variants 8, 9, 65)
     const int xv = c.kernel >= 4 && c.kernel <= 6 ? c.kernel - 3 : c.kernel == 7 ? 5 : c.kernel == 8 ? 7
-                 : c.kernel >= 100 ? c.kernel - 100 : 0;
+                 : c.kernel >= 100 && c.kernel < 200 ? c.kernel - 100 : 0;
     const int rows = pipe ? (c.rows == 2 || c.rows == 4 || c.rows == 8 ? c.rows : 2)
                           : (c.rows == 4 || c.rows == 8 || c.rows == 16 ? c.rows : 8);
     const uint32_t run = (c.run_segs >= 1 && c.run_segs <= (int)kScanRun) ? (uint32_t)c.run_segs : kScanRun;
@@ -3113,10 +3135,19 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
         NSX_RSCAN(4, true, 1) NSX_RSCAN(8, true, 1)
         NSX_RSCAN(4, false, 1) NSX_RSCAN(8, false, 1) NSX_RSCAN(16, false, 1)
 #undef NSX_RSCAN
-        if (rows == 2 && pipe && ns == 1)
+        if (rows == 2 && pipe && ns == 1 && c.kernel < 200)
             hipLaunchKernelGGL((csum_ragged_scan_kernel<2, VERIFY, true, 1>), dim3(grid), dim3(kBlock), lds, st, base,
                                offsets + c0, cn, pc, oc, kc, run, sets, keep);
-        if (rows == 2 && pipe && ns == 2) {
+        if (c.kernel >= 200 && c.kernel < 300) {  // experiment: csum_ragged_lds_kernel<·, kernel − 200>
+            const uint32_t mb4 = (uint32_t)c.cus * 4u, g4 = grid_for((cn + 63) / 64, mb4);
+            const size_t l4 = (size_t)(kScanSlot + (c.kernel == 265 ? 1024u : 0u)) * kWavesPerBlock;
+            if (c.kernel == 265)
+                hipLaunchKernelGGL((csum_ragged_lds_kernel<VERIFY, 65>), dim3(g4), dim3(kBlock), l4, st, base,
+                                   offsets + c0, cn, pc, oc, kc);
+            else
+                hipLaunchKernelGGL((csum_ragged_lds_kernel<VERIFY, 9>), dim3(g4), dim3(kBlock), l4, st, base,
+                                   offsets + c0, cn, pc, oc, kc);
+        } else if (rows == 2 && pipe && ns == 2) {
             switch (xv) {
 #define NSX_RSCAN_XV(X_)                                                                                          \
                 case X_:                                                                                           \
