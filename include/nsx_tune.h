@@ -46,8 +46,8 @@ typedef struct nsx_tune {
                                   frames that fit 8 KiB, switching at the first other run to the hybrid
                                   loop (such runs as prefix-form pieces of <= 7 KiB), < 640 B the prefix
                                   form with 15 KiB slots on two waves per block, else streamed runs on 3
-                                  blocks/CU; 5 / 6 / 7 force the small-frame mode / the two-wave prefix
-                                  form / the hybrid loop throughout on that grid (NSX_EINVAL with rows
+                                  blocks/CU; 5 / 6 / 7 / 8 force the small-frame mode / the two-wave prefix
+                                  form / the hybrid loop throughout / the streamed runs (3 blocks/CU) on that grid (NSX_EINVAL with rows
                                   other than 0 / 2 or with blocks_per_cu set). With rows or blocks_per_cu set (the
                                   pre-prefix shapes): 0 = per wave the LDS form (mean < 128 B) or streamed
                                   runs, 1 = streamed runs, 2 = the LDS form. (A run that does not fit the

@@ -1925,7 +1925,8 @@ __global__ __launch_bounds__(kBlock, WPS) void rx_tcp_kernel(const uint8_t* __re
             if (mode == 5) rx_runs_lds<R, V6, true>(base, ofs, n, wr.a0, wr.a_end, lane, slot, mrs, irs, trs);
             else rx_runs_pfx<R, V6, 7, true>(base, ofs, n, wr.a0, wr.a_end, lane, slot, mrs, irs, trs);
         } else {  // streamed runs; a batch of large frames on 3 of the 4 blocks per CU
-            const uint32_t nb = active_blocks(ofs, n, kRxBigMean, sets == 0 ? 3u : 0u);
+            // (mode 8: the streamed runs forced, on the 3 of 4 blocks per CU the auto choice gives them)
+            const uint32_t nb = active_blocks(ofs, n, sets == 8 ? 0u : kRxBigMean, sets == 0 || sets == 8 ? 3u : 0u);
             if (blockIdx.x >= nb) return;
             const WaveRange wr = range(nb, kWavesPerBlock, wave);
             rx_runs<R, V6, 1>(base, ofs, n, wr.a0, wr.a_end, lane, mrs, irs, trs);
@@ -3188,7 +3189,7 @@ hipError_t launch_ragged(const LaunchCfg& c, const void* d_base, const uint64_t*
 bool rx_tune_valid(const LaunchCfg& c) {
     // segs_per_wave 5 / 6 / 7 force a mode of the default grid; they mean nothing on the shapes rows / blocks_per_cu
     // select (silently running the auto shape there made fuzz cases test another form than they named)
-    const bool grid_mode = c.segs_per_wave == 5 || c.segs_per_wave == 6 || c.segs_per_wave == 7;
+    const bool grid_mode = c.segs_per_wave == 5 || c.segs_per_wave == 6 || c.segs_per_wave == 7 || c.segs_per_wave == 8;
     return !grid_mode || ((c.rows == 0 || c.rows == 2) && c.blocks_per_cu == 0);
 }
 
@@ -3214,7 +3215,7 @@ hipError_t launch_rx_tcp(const LaunchCfg& c, int ipver, const void* d_base, cons
     // same 38.5 KB), the mode chosen in-kernel by the batch's mean frame.
     const bool auto_grid = rows == 2 && c.blocks_per_cu == 0 &&
                            (c.segs_per_wave == 0 || c.segs_per_wave == 5 || c.segs_per_wave == 6 ||
-                            c.segs_per_wave == 7);
+                            c.segs_per_wave == 7 || c.segs_per_wave == 8);
     if (auto_grid) {
         constexpr size_t la = (size_t)PfxSlot<15>::kBytes * 2;
         static_assert(la >= (size_t)PfxSlot<7>::kBytes * kWavesPerBlock && la * 4 <= 163840, "4 blocks per CU");
