@@ -3,9 +3,10 @@
 
     python tools/ab.py --config 6 --variants "def:;b3:blocks_per_cu=3;b8:blocks_per_cu=8" [--rounds 7]
 
-For config 10 (fused receive pass), a variant named scan* runs the plain ragged
+For the receive-pass configs, a variant named scan* runs the plain ragged
 checksum (nsx_csum_ragged_dev) over the same frames instead: the receive pass's
-own cost against the one-pass checksum it is built on.
+own cost against the one-pass checksum it is built on; raw* runs the receive pass
+also writing its 2 B TCP raw sums (the ragged checksum's output volume).
 
 Builds the workload once (bench.build_workload), settles the clocks, then runs
 the variants in interleaved rounds (each round: every variant, `--launches`
@@ -48,6 +49,11 @@ def main():
         name, _, kv = item.partition(":")
         tune = bench.parse_tune([x for x in kv.split(",") if x]) or None
         step = w["step_for"](tune)
+        if cfg["kind"] == "rx" and name.startswith("raw"):  # the receive pass also writing its 2 B TCP raw sums
+            import nsx
+            rxf = nsx.rx_ipv6_tcp_verify_dev if cfg.get("ipver") == 6 else nsx.rx_ipv4_tcp_verify_dev
+            traw = torch.empty(cfg["n"], dtype=torch.int16, device="cuda")
+            step = (lambda t: lambda: rxf(w["buf"], w["d_offs"], mask=w["out"], tcp_raw=traw, tune=t))(tune)
         if cfg["kind"] == "rx" and name.startswith("scan"):
             import nsx
             rout = torch.empty(cfg["n"], dtype=torch.int16, device="cuda")
