@@ -939,9 +939,9 @@ constexpr uint32_t kScanSlot = kScanSlotRows * kRow + 256;  // + pad: lds_range_
 // offsets (the receive pass's form: no cross-lane shift for the end, and a run's 64 results are one whole 128 B
 // line when the wave range starts at a multiple of 64); bit 1 = write-through (sc1) result stores; bit 3 = no
 // per-run partial load when the batch has none (has_part false).
-// Bit 6 (with bit 0): results parked in LDS (1 KiB per wave after its slot) and written 8 runs at a time, one
-// 16 B store per lane (1 KiB contiguous) instead of one 2 B store per lane per run; a wave's partial last run and
-// the runs before a streamed one are written as before.
+// Bit 6 (with bit 0): results parked in LDS (after the wave's slot) and written 8 runs at a time (bit 7: 32 runs,
+// 4 KiB per wave, which leaves room for 3 blocks per CU), 16 B per lane and store (1 KiB contiguous) instead of one
+// 2 B store per lane per run; a wave's partial last run and the runs before a streamed one are written as before.
 template <int R, bool VERIFY, bool PIPE, int XV = 0>
 __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
                                                 __amdgpu_buffer_rsrc_t prs, __amdgpu_buffer_rsrc_t ors,
@@ -985,15 +985,20 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
         for (uint32_t r = 0; r < kScanSlotRows; ++r) V[r] = bld16<true>(rs, r * kRow + lane * 16u);
     };
     constexpr bool PARK = (XV & 64) != 0 && R64;
+    constexpr uint32_t PR = (XV & 128) ? 32u : 8u;  // runs parked per flush
     uint16_t* park = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(slot) + kScanSlot);
     uint32_t parked = 0, a_park = 0;  // full runs parked, the first one's segment index
-    auto flush = [&]() {              // the parked runs' 64·parked results: lane l stores results 8l .. 8l + 7
+    auto flush = [&]() {              // the parked runs' 64·parked results: 16 B blocks of 8, 64 blocks per store
         if (parked) {
             __builtin_amdgcn_wave_barrier();
-            const lds16 v = reinterpret_cast<const lds16*>(park)[lane];
-            typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-            __builtin_amdgcn_raw_buffer_store_b128(v4u{v.x, v.y, v.z, v.w}, ors,
-                                                   lane < 8u * parked ? (a_park + lane * 8u) * 2u : kOOB, 0, kSt);
+#pragma unroll
+            for (uint32_t q = 0; q < PR / 8u; ++q) {
+                const uint32_t blk = q * kWave + lane;  // results 8·blk .. 8·blk + 7
+                const lds16 v = reinterpret_cast<const lds16*>(park)[blk];
+                typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+                __builtin_amdgcn_raw_buffer_store_b128(v4u{v.x, v.y, v.z, v.w}, ors,
+                                                       blk < 8u * parked ? (a_park + blk * 8u) * 2u : kOOB, 0, kSt);
+            }
             __builtin_amdgcn_wave_barrier();
             parked = 0;
         }
@@ -1049,7 +1054,7 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
                 if (cur.cnt == kWave) {  // a full run: parked (wave-uniform)
                     if (parked == 0) a_park = a;
                     park[parked * kWave + lane] = (uint16_t)res;
-                    if (++parked == 8u) flush();
+                    if (++parked == PR) flush();
                 } else {
                     flush();
                     __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, mine ? (a + lane) * 2 : kOOB, 0, kSt);
@@ -1405,7 +1410,7 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
                                                       lds_scan + wave * (kScanSlot / 16u));
         else
             ragged_runs_lds<R, VERIFY, PIPE, XV>(base, ofs, n, prs, ors, oks, run, a0, a_end, lane,
-                                                 lds_scan + wave * ((kScanSlot + ((XV & 64) ? 1024u : 0u)) / 16u),
+                                                 lds_scan + wave * ((kScanSlot + ((XV & 64) ? ((XV & 128) ? 4096u : 1024u) : 0u)) / 16u),
                                                  partial != nullptr);
     } else if (NS == 2 && (sets == 4 || (sets == 0 && wave_bytes < (uint64_t)kScanSmallSeg * (a_end - a0)))) {
         ragged_runs<R, VERIFY, PIPE, 4>(base, ofs, n, prs, ors, oks, run, a0, a_end, lane);
@@ -1432,7 +1437,7 @@ __global__ __launch_bounds__(kBlock, 4) void csum_ragged_lds_kernel(
     const WaveRange wr = wave_range(ofs, n, g, W, lane, 0xFFFFFFFFu, 1u, kWave);
     extern __shared__ lds16 lds_scan[];
     ragged_runs_lds<2, VERIFY, true, XV>(base, ofs, n, prs, ors, oks, kWave, wr.a0, wr.a_end, lane,
-                                         lds_scan + wave * ((kScanSlot + ((XV & 64) ? 1024u : 0u)) / 16u),
+                                         lds_scan + wave * ((kScanSlot + ((XV & 64) ? ((XV & 128) ? 4096u : 1024u) : 0u)) / 16u),
                                          partial != nullptr);
 }
 
@@ -3139,15 +3144,23 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
         if (rows == 2 && pipe && ns == 1 && c.kernel < 200)
             hipLaunchKernelGGL((csum_ragged_scan_kernel<2, VERIFY, true, 1>), dim3(grid), dim3(kBlock), lds, st, base,
                                offsets + c0, cn, pc, oc, kc, run, sets, keep);
-        if (c.kernel >= 200 && c.kernel < 300) {  // experiment: csum_ragged_lds_kernel<·, kernel − 200>
-            const uint32_t mb4 = (uint32_t)c.cus * 4u, g4 = grid_for((cn + 63) / 64, mb4);
-            const size_t l4 = (size_t)(kScanSlot + (c.kernel == 265 ? 1024u : 0u)) * kWavesPerBlock;
-            if (c.kernel == 265)
-                hipLaunchKernelGGL((csum_ragged_lds_kernel<VERIFY, 65>), dim3(g4), dim3(kBlock), l4, st, base,
-                                   offsets + c0, cn, pc, oc, kc);
-            else
-                hipLaunchKernelGGL((csum_ragged_lds_kernel<VERIFY, 9>), dim3(g4), dim3(kBlock), l4, st, base,
-                                   offsets + c0, cn, pc, oc, kc);
+        if (c.kernel >= 200 && c.kernel < 300) {  // experiment: csum_ragged_lds_kernel (209, 265, 267, 293, 295)
+            const int lx = c.kernel == 293 ? 193 : c.kernel == 295 ? 195 : c.kernel - 200;
+            const uint32_t pk = (lx & 64) ? ((lx & 128) ? 4096u : 1024u) : 0u;
+            const uint32_t g4 = grid_for((cn + 63) / 64, (uint32_t)c.cus * ((lx & 128) ? 3u : 4u));
+            const size_t l4 = (size_t)(kScanSlot + pk) * kWavesPerBlock;
+            switch (lx) {
+#define NSX_RLDS(X_)                                                                                          \
+                case X_:                                                                                       \
+                    hipLaunchKernelGGL((csum_ragged_lds_kernel<VERIFY, X_>), dim3(g4), dim3(kBlock), l4, st, base, \
+                                       offsets + c0, cn, pc, oc, kc);                                          \
+                    break;
+                NSX_RLDS(65) NSX_RLDS(67) NSX_RLDS(193) NSX_RLDS(195)
+#undef NSX_RLDS
+                default:
+                    hipLaunchKernelGGL((csum_ragged_lds_kernel<VERIFY, 9>), dim3(g4), dim3(kBlock), l4, st, base,
+                                       offsets + c0, cn, pc, oc, kc);
+            }
         } else if (rows == 2 && pipe && ns == 2) {
             switch (xv) {
 #define NSX_RSCAN_XV(X_)                                                                                          \
