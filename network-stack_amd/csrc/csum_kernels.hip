@@ -985,7 +985,8 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
         for (uint32_t r = 0; r < kScanSlotRows; ++r) V[r] = bld16<true>(rs, r * kRow + lane * 16u);
     };
     constexpr bool PARK = (XV & 64) != 0 && R64;
-    constexpr uint32_t PR = (XV & 128) ? 32u : 8u;  // runs parked per flush
+    constexpr uint32_t PR = (XV & 256) ? 64u : (XV & 128) ? 32u : 8u;  // runs parked per flush (bit 8: 64, 8 KiB)
+    constexpr int kFl = (XV & 512) ? 2 : kSt;  // flush stores' cache policy (bit 9: non-temporal)
     uint16_t* park = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(slot) + kScanSlot);
     uint32_t parked = 0, a_park = 0;  // full runs parked, the first one's segment index
     auto flush = [&]() {              // the parked runs' 64·parked results: 16 B blocks of 8, 64 blocks per store
@@ -997,7 +998,7 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
                 const lds16 v = reinterpret_cast<const lds16*>(park)[blk];
                 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
                 __builtin_amdgcn_raw_buffer_store_b128(v4u{v.x, v.y, v.z, v.w}, ors,
-                                                       blk < 8u * parked ? (a_park + blk * 8u) * 2u : kOOB, 0, kSt);
+                                                       blk < 8u * parked ? (a_park + blk * 8u) * 2u : kOOB, 0, kFl);
             }
             __builtin_amdgcn_wave_barrier();
             parked = 0;
@@ -1410,7 +1411,7 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
                                                       lds_scan + wave * (kScanSlot / 16u));
         else
             ragged_runs_lds<R, VERIFY, PIPE, XV>(base, ofs, n, prs, ors, oks, run, a0, a_end, lane,
-                                                 lds_scan + wave * ((kScanSlot + ((XV & 64) ? ((XV & 128) ? 4096u : 1024u) : 0u)) / 16u),
+                                                 lds_scan + wave * ((kScanSlot + ((XV & 64) ? ((XV & 256) ? 8192u : (XV & 128) ? 4096u : 1024u) : 0u)) / 16u),
                                                  partial != nullptr);
     } else if (NS == 2 && (sets == 4 || (sets == 0 && wave_bytes < (uint64_t)kScanSmallSeg * (a_end - a0)))) {
         ragged_runs<R, VERIFY, PIPE, 4>(base, ofs, n, prs, ors, oks, run, a0, a_end, lane);
@@ -1437,7 +1438,7 @@ __global__ __launch_bounds__(kBlock, 4) void csum_ragged_lds_kernel(
     const WaveRange wr = wave_range(ofs, n, g, W, lane, 0xFFFFFFFFu, 1u, kWave);
     extern __shared__ lds16 lds_scan[];
     ragged_runs_lds<2, VERIFY, true, XV>(base, ofs, n, prs, ors, oks, kWave, wr.a0, wr.a_end, lane,
-                                         lds_scan + wave * ((kScanSlot + ((XV & 64) ? ((XV & 128) ? 4096u : 1024u) : 0u)) / 16u),
+                                         lds_scan + wave * ((kScanSlot + ((XV & 64) ? ((XV & 256) ? 8192u : (XV & 128) ? 4096u : 1024u) : 0u)) / 16u),
                                          partial != nullptr);
 }
 
@@ -3145,9 +3146,10 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
             hipLaunchKernelGGL((csum_ragged_scan_kernel<2, VERIFY, true, 1>), dim3(grid), dim3(kBlock), lds, st, base,
                                offsets + c0, cn, pc, oc, kc, run, sets, keep);
         if (c.kernel >= 200 && c.kernel < 300) {  // experiment: csum_ragged_lds_kernel (209, 265, 267, 293, 295)
-            const int lx = c.kernel == 293 ? 193 : c.kernel == 295 ? 195 : c.kernel - 200;
-            const uint32_t pk = (lx & 64) ? ((lx & 128) ? 4096u : 1024u) : 0u;
-            const uint32_t g4 = grid_for((cn + 63) / 64, (uint32_t)c.cus * ((lx & 128) ? 3u : 4u));
+            const int lx = c.kernel == 293 ? 193 : c.kernel == 295 ? 195 : c.kernel == 296 ? 321
+                         : c.kernel == 297 ? 705 : c.kernel - 200;
+            const uint32_t pk = (lx & 64) ? ((lx & 256) ? 8192u : (lx & 128) ? 4096u : 1024u) : 0u;
+            const uint32_t g4 = grid_for((cn + 63) / 64, (uint32_t)c.cus * ((lx & 256) ? 2u : (lx & 128) ? 3u : 4u));
             const size_t l4 = (size_t)(kScanSlot + pk) * kWavesPerBlock;
             switch (lx) {
 #define NSX_RLDS(X_)                                                                                          \
@@ -3155,7 +3157,7 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
                     hipLaunchKernelGGL((csum_ragged_lds_kernel<VERIFY, X_>), dim3(g4), dim3(kBlock), l4, st, base, \
                                        offsets + c0, cn, pc, oc, kc);                                          \
                     break;
-                NSX_RLDS(65) NSX_RLDS(67) NSX_RLDS(193) NSX_RLDS(195)
+                NSX_RLDS(65) NSX_RLDS(67) NSX_RLDS(193) NSX_RLDS(195) NSX_RLDS(321) NSX_RLDS(705)
 #undef NSX_RLDS
                 default:
                     hipLaunchKernelGGL((csum_ragged_lds_kernel<VERIFY, 9>), dim3(g4), dim3(kBlock), l4, st, base,

@@ -124,7 +124,7 @@ RAGGED_TUNES = [dict(kernel=k, rows=r, run_segs=rs, blocks_per_cu=b)  # pipeline
                [dict(segs_per_wave=4, run_segs=rs, blocks_per_cu=b)  # runs of four sets
                 for rs in (0, 1, 16, 63) for b in (0, 1, 8)] + \
                [dict(segs_per_wave=2, run_segs=rs, blocks_per_cu=b, kernel=k)  # the LDS form (small segments' form)
-                for rs in (0, 1, 16, 63) for b in (0, 1, 8) for k in (0, nsx.KERNEL_SCAN_PLAIN, 4, 5, 6, 7, 8, 108, 109, 165, 209, 265, 267, 293, 295)]
+                for rs in (0, 1, 16, 63) for b in (0, 1, 8) for k in (0, nsx.KERNEL_SCAN_PLAIN, 4, 5, 6, 7, 8, 108, 109, 165, 209, 265, 267, 293, 295, 296, 297)]
 
 
 def test_ragged_small_segment_bench_workload_full_size():
@@ -134,7 +134,7 @@ def test_ragged_small_segment_bench_workload_full_size():
     cfg = bench.WORKLOADS[15]
     w = bench.build_workload(cfg, 0, torch.device("cuda", 0))
     want = O.c_batch(host(w["buf"]), cfg["n"], offsets=w["offsets"], threads=16)
-    for k in (0, 4, 5, 6, 7, 8, 108, 109, 165, 209, 265, 267, 293, 295):
+    for k in (0, 4, 5, 6, 7, 8, 108, 109, 165, 209, 265, 267, 293, 295, 296, 297):
         w["out"].zero_()
         w["step_for"](dict(kernel=k))()
         assert np.array_equal(u16(w["out"]), want), k
