@@ -36,10 +36,13 @@ typedef struct nsx_tune {
                                   block) has at most 4 of its blocks resident per CU at a time (160 KB of
                                   LDS); forced streamed shapes (segs_per_wave 1 or 4) allocate no LDS */
     int32_t segs_per_wave;     /* fixed batches of <= 4 KiB segments: segments per wave task (1, 2, 4, 8).
-                                  Ragged scan, per wave: 0 auto (the LDS form in waves whose segments
-                                  average < 128 B, streamed runs of four 63-segment sets < 2048 B, else runs
-                                  of two sets), 1 = runs of one set, 2 = the LDS form, 4 = runs of four sets
-                                  in every wave. Only the default pipelined 2-row shape has more than one
+                                  Ragged scan: 0 auto (a batch whose segments average < 128 B: the small-
+                                  segment mode — the LDS form on two waves per block, results parked and
+                                  written 8 KiB at a time; otherwise per wave: the LDS form in waves whose
+                                  segments average < 128 B, streamed runs of four 63-segment sets < 2048 B,
+                                  else runs of two sets), 1 = runs of one set, 2 = the small-segment mode,
+                                  3 = the LDS form in every wave (four per block, results stored per run),
+                                  4 = runs of four sets in every wave. Only the default pipelined 2-row shape has more than one
                                   set: with kernel = SCAN_PLAIN or rows != 2 a 4 gives runs of one set.
                                   Receive kernels: 0 auto = the default grid (4 blocks/CU) choosing by the
                                   batch's mean frame: < 112 B the LDS form for whole runs of <= 256 B

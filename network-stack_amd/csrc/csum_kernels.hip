@@ -929,38 +929,35 @@ __device__ __forceinline__ void lds_stage(lds16* slot, u32x4 (&V)[ROWS], uint64_
     __builtin_amdgcn_wave_barrier();
 }
 
-// The LDS form of the ragged checksum for waves of small segments, the receive pass's
-// (rx_runs_lds) applied to runs of ≤ run segments: lane l sums segment a + l out of the wave's slot. A run too
-// wide for the slot takes the streaming form (one set).
+// The LDS form of the ragged checksum for small segments, the receive pass's
+// (rx_runs_lds) applied to runs of ≤ run segments: lane l sums segment a + l out of the wave's slot, both of its
+// offsets loaded by the lane itself. A run too wide for the slot is streamed (as ≤ 63 + the rest).
+//
+// PARK (runs of 64, the default small-segment mode, §7 step 61): the runs' results are not stored run by run but
+// parked in LDS beside the slot and written 64 runs at a time — 8 KiB contiguous per wave, 16 B per lane and store.
+// A result store per run (128 B per wave every few microseconds, 2 B per segment: 1.8% of workload 15's bytes) cost
+// this loop 12-14% of its time: the receive pass over the same frames ran 14% slower when it also wrote its 2 B raw
+// sums, and parking 8 / 32 / 64 runs took the ragged form 2% / 6% / 12.6% faster (profiles/r04_ragged_park_*). The
+// park buffer is the second of the block's four 8.25 KiB slots, so the mode runs two waves per block (8 per CU).
+// The partial of each run is loaded only when the batch has partials. A wave's partial last run, and the runs before
+// a streamed one, are flushed (and stored) as they come.
 constexpr uint32_t kScanSlotRows = 8;
-constexpr uint32_t kScanSlot = kScanSlotRows * kRow + 256;  // + pad: lds_range_sum's chunk blocks read past the end
+constexpr uint32_t kScanSlot = kScanSlotRows * kRow + 256;  // + pad: lds_range_sum's first chunk block reads past the end
+constexpr uint32_t kParkRuns = 64;                          // runs parked per flush: 64 × 128 B = 8 KiB ≤ one slot
 
-// XV (experiment, tools/evidence.sh ab): bit 0 = runs of 64 segments, each lane loading both of its segment's
-// offsets (the receive pass's form: no cross-lane shift for the end, and a run's 64 results are one whole 128 B
-// line when the wave range starts at a multiple of 64); bit 1 = write-through (sc1) result stores; bit 3 = no
-// per-run partial load when the batch has none (has_part false).
-// Bit 6 (with bit 0): results parked in LDS (after the wave's slot) and written 8 runs at a time (bit 7: 32 runs,
-// 4 KiB per wave, which leaves room for 3 blocks per CU), 16 B per lane and store (1 KiB contiguous) instead of one
-// 2 B store per lane per run; a wave's partial last run and the runs before a streamed one are written as before.
-template <int R, bool VERIFY, bool PIPE, int XV = 0>
+template <int R, bool VERIFY, bool PIPE, bool PARK>
 __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
                                                 __amdgpu_buffer_rsrc_t prs, __amdgpu_buffer_rsrc_t ors,
                                                 __amdgpu_buffer_rsrc_t oks, uint32_t run, uint32_t a0, uint32_t a_end,
-                                                uint32_t lane, lds16* slot, bool has_part = true) {
+                                                uint32_t lane, lds16* slot, bool has_part) {
     typedef uint32_t v2u __attribute__((ext_vector_type(2)));
-    constexpr bool R64 = (XV & 1) != 0;
-    constexpr int kSt = (XV & 2) ? kStoreSc1 : 0;
-    if constexpr (R64) run = kWave;
-    auto load_offs = [&](uint32_t a) -> uint64_t {  // lane l ≤ run length: offsets[a + l]
-        const uint32_t voff = (a < a_end && lane <= run && a + lane <= n) ? (a + lane) * 8 : kOOB;
-        const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, voff, 0, 0);
+    auto ld64 = [&](uint32_t i, bool live) -> uint64_t {
+        const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, live ? i * 8 : kOOB, 0, 0);
         return ((uint64_t)x.y << 32) | x.x;
     };
-    auto load_ends = [&](uint32_t a) -> uint64_t {  // R64: lane l < run length: offsets[a + l + 1]
-        const uint32_t voff = (a < a_end && a + lane + 1u <= n) ? (a + lane + 1u) * 8 : kOOB;
-        const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, voff, 0, 0);
-        return ((uint64_t)x.y << 32) | x.x;
-    };
+    // lane l < run length: segment a + l = [offsets[a + l], offsets[a + l + 1])
+    auto load_offs = [&](uint32_t a) { return ld64(a + lane, a < a_end && lane < run && a + lane <= n); };
+    auto load_ends = [&](uint32_t a) { return ld64(a + lane + 1u, a < a_end && lane < run && a + lane + 1u <= n); };
     struct Run {
         const uint8_t* rbase;
         uint64_t span;
@@ -970,13 +967,15 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
     auto geo = [&](uint32_t a, uint64_t off, uint64_t end) {  // wave-uniform geometry of run a
         Run g{base, 0, a < a_end ? min(run, a_end - a) : 0u, false};
         if (g.cnt) {
-            // boundaries in lanes 0..cnt of off (R64: starts in off, ends in end, lanes 0..cnt-1)
-            const uint64_t lo = readlane64(off, 0), hi = R64 ? readlane64(end, g.cnt - 1u) : readlane64(off, g.cnt);
+            const uint64_t lo = readlane64(off, 0), hi = readlane64(end, g.cnt - 1u);
             g.rbase = reinterpret_cast<const uint8_t*>(((uintptr_t)(base + lo)) & ~(uintptr_t)127);
             g.span = (uint64_t)((base + hi) - g.rbase);
             g.lds = g.span <= (uint64_t)kScanSlotRows * kRow;
         }
         return g;
+    };
+    auto load_part = [&](uint32_t a, uint32_t cnt) {
+        return has_part ? __builtin_amdgcn_raw_buffer_load_b32(prs, lane < cnt ? (a + lane) * 4 : kOOB, 0, 0) : 0u;
     };
     u32x4 V[kScanSlotRows];
     auto issue = [&](const Run& g) {  // rows past the run: out of the descriptor's range, 0, no traffic
@@ -984,21 +983,18 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
 #pragma unroll
         for (uint32_t r = 0; r < kScanSlotRows; ++r) V[r] = bld16<true>(rs, r * kRow + lane * 16u);
     };
-    constexpr bool PARK = (XV & 64) != 0 && R64;
-    constexpr uint32_t PR = (XV & 256) ? 64u : (XV & 128) ? 32u : 8u;  // runs parked per flush (bit 8: 64, 8 KiB)
-    constexpr int kFl = (XV & 512) ? 2 : kSt;  // flush stores' cache policy (bit 9: non-temporal)
     uint16_t* park = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(slot) + kScanSlot);
     uint32_t parked = 0, a_park = 0;  // full runs parked, the first one's segment index
-    auto flush = [&]() {              // the parked runs' 64·parked results: 16 B blocks of 8, 64 blocks per store
-        if (parked) {
+    auto flush = [&]() {              // parked results 8·blk .. 8·blk + 7 (16 B) by lane blk mod 64
+        if (PARK && parked) {
             __builtin_amdgcn_wave_barrier();
 #pragma unroll
-            for (uint32_t q = 0; q < PR / 8u; ++q) {
-                const uint32_t blk = q * kWave + lane;  // results 8·blk .. 8·blk + 7
+            for (uint32_t q = 0; q < kParkRuns / 8u; ++q) {
+                const uint32_t blk = q * kWave + lane;
                 const lds16 v = reinterpret_cast<const lds16*>(park)[blk];
                 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
                 __builtin_amdgcn_raw_buffer_store_b128(v4u{v.x, v.y, v.z, v.w}, ors,
-                                                       blk < 8u * parked ? (a_park + blk * 8u) * 2u : kOOB, 0, kFl);
+                                                       blk < 8u * parked ? (a_park + blk * 8u) * 2u : kOOB, 0, 0);
             }
             __builtin_amdgcn_wave_barrier();
             parked = 0;
@@ -1009,173 +1005,56 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
     // loop's wait counts.
     uint32_t a = a0;
     while (a < a_end) {
-        uint64_t c_off = load_offs(a), c_end = R64 ? load_ends(a) : 0;
+        uint64_t c_off = load_offs(a), c_end = load_ends(a);
         Run cur = geo(a, c_off, c_end);
-        if (!cur.lds) {  // too wide for the slot: the streaming form
-            const uint32_t part = __builtin_amdgcn_raw_buffer_load_b32(prs, lane < cur.cnt ? (a + lane) * 4 : kOOB, 0, 0);
-            if constexpr (R64) {  // the stream takes ≤ 63 segments (boundaries in lanes 0..cnt): 63, then the last
-                const uint32_t c1 = min(cur.cnt, kScanRun), c2 = cur.cnt - c1;
-                const uint32_t cnt1[1] = {c1}, part1[1] = {part};
-                const uint64_t o1[1] = {lane == c1 ? readlane64(c_end, c1 - 1u) : c_off};
-                ragged_run_stream<R, VERIFY, PIPE, 1>(base, a, kScanRun, cnt1, o1, part1, ors, oks, lane);
-                if (c2) {
-                    const uint32_t cnt2[1] = {c2}, part2[1] = {(uint32_t)__shfl_down((int)part, c1)};
-                    const uint64_t o2[1] = {lane == 0 ? readlane64(c_off, c1) : readlane64(c_end, c1)};
-                    ragged_run_stream<R, VERIFY, PIPE, 1>(base, a + c1, kScanRun, cnt2, o2, part2, ors, oks, lane);
-                }
-            } else {
-                const uint32_t cnt1[1] = {cur.cnt}, part1[1] = {part};
-                const uint64_t o1[1] = {c_off};
-                ragged_run_stream<R, VERIFY, PIPE, 1>(base, a, run, cnt1, o1, part1, ors, oks, lane);
+        if (!cur.lds) {  // too wide for the slot: streamed (boundaries in lanes 0..cnt: ≤ 63 segments, then the rest)
+            flush();
+            const uint32_t part = load_part(a, cur.cnt);
+            const uint32_t c1 = min(cur.cnt, kScanRun), c2 = cur.cnt - c1;
+            const uint32_t cnt1[1] = {c1}, part1[1] = {part};
+            const uint64_t o1[1] = {lane == c1 ? readlane64(c_end, c1 - 1u) : c_off};
+            ragged_run_stream<R, VERIFY, PIPE, 1>(base, a, kScanRun, cnt1, o1, part1, ors, oks, lane);
+            if (c2) {
+                const uint32_t cnt2[1] = {c2}, part2[1] = {(uint32_t)__shfl_down((int)part, c1)};
+                const uint64_t o2[1] = {lane == 0 ? readlane64(c_off, c1) : readlane64(c_end, c1)};
+                ragged_run_stream<R, VERIFY, PIPE, 1>(base, a + c1, kScanRun, cnt2, o2, part2, ors, oks, lane);
             }
             a += run;
             continue;
         }
         issue(cur);
-        uint64_t n_off = load_offs(a + run), n_end = R64 ? load_ends(a + run) : 0;
+        uint64_t n_off = load_offs(a + run), n_end = load_ends(a + run);
         __builtin_amdgcn_s_waitcnt(kWaitVm0);  // as in rx_runs_lds: nothing in flight at the loop's entry
         for (;;) {
-            const uint32_t part = (XV & 8) && !has_part
-                                      ? 0u
-                                      : __builtin_amdgcn_raw_buffer_load_b32(prs, lane < cur.cnt ? (a + lane) * 4 : kOOB, 0, 0);
+            const uint32_t part = load_part(a, cur.cnt);
             lds_stage<kScanSlotRows>(slot, V, cur.span, lane);
             lds_zero_tail(slot, cur.span, lane);
             Run nxt = geo(a + run, n_off, n_end);
             if (!nxt.lds) nxt.span = 0;  // a run that will be streamed is not staged: empty loads
             issue(nxt);
-            const uint64_t p_off = load_offs(a + 2u * run), p_end = R64 ? load_ends(a + 2u * run) : 0;
-            // segment a + lane = [boundary lane, boundary lane + 1)
-            const uint64_t e_off = R64 ? c_end : (uint64_t)__shfl_down((unsigned long long)c_off, 1);
+            const uint64_t p_off = load_offs(a + 2u * run), p_end = load_ends(a + 2u * run);
             const bool mine = lane < cur.cnt;
             const uint32_t p = mine ? (uint32_t)((base + c_off) - cur.rbase) : 0u;
-            const uint32_t e = mine ? (uint32_t)((base + e_off) - cur.rbase) : 0u;
+            const uint32_t e = mine ? (uint32_t)((base + c_end) - cur.rbase) : 0u;
             const uint32_t dq = reinterpret_cast<const uint32_t*>(slot)[p >> 2];
             const uint32_t res = finish(fold32(lds_range_sum(slot, p, e, dq, mine)), (p & 1u) == 0, part);
-            if constexpr (PARK) {
-                if (cur.cnt == kWave) {  // a full run: parked (wave-uniform)
-                    if (parked == 0) a_park = a;
-                    park[parked * kWave + lane] = (uint16_t)res;
-                    if (++parked == PR) flush();
-                } else {
-                    flush();
-                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, mine ? (a + lane) * 2 : kOOB, 0, kSt);
-                }
+            if (PARK && cur.cnt == kWave) {  // a full run: parked (wave-uniform)
+                if (parked == 0) a_park = a;
+                park[parked * kWave + lane] = (uint16_t)res;
+                if (++parked == kParkRuns) flush();
             } else {
-                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, mine ? (a + lane) * 2 : kOOB, 0, kSt);
+                flush();
+                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, mine ? (a + lane) * 2 : kOOB, 0, 0);
             }
             if constexpr (VERIFY)
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(res == 0xFFFFu), oks, mine ? a + lane : kOOB, 0, kSt);
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(res == 0xFFFFu), oks, mine ? a + lane : kOOB, 0, 0);
             a += run;
             if (!nxt.lds) break;  // the end of the wave's range, or a run for the outer loop
             cur = nxt;
             c_off = n_off, n_off = p_off;
             c_end = n_end, n_end = p_end;
         }
-        if constexpr (PARK) flush();
-    }
-}
-
-// XV bit 2 (experiment, with runs of 64): TWO runs in flight per wave instead of one — two row register sets used in
-// turn, each restaged and reissued in its own step (stage run k from set k mod 2, then load run k + 2 into it while
-// run k + 1 is still arriving in the other). Every value a step waits for was issued before the rows still in
-// flight (vmcnt counts in issue order): run k's partials are loaded just before run k's rows, and the offsets of
-// run k + 3 before run k + 2's rows. 64 more VGPRs: launched at 3 blocks/CU.
-template <int R, bool VERIFY, bool PIPE, int XV>
-__device__ __forceinline__ void ragged_runs_lds_deep(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs,
-                                                     uint32_t n, __amdgpu_buffer_rsrc_t prs, __amdgpu_buffer_rsrc_t ors,
-                                                     __amdgpu_buffer_rsrc_t oks, uint32_t a0, uint32_t a_end,
-                                                     uint32_t lane, lds16* slot) {
-    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
-    constexpr uint32_t run = kWave;
-    constexpr int kSt = (XV & 2) ? kStoreSc1 : 0;
-    auto ld64 = [&](uint32_t i, bool live) -> uint64_t {
-        const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, live ? i * 8 : kOOB, 0, 0);
-        return ((uint64_t)x.y << 32) | x.x;
-    };
-    struct Offs {
-        uint64_t off, end;  // lane l: offsets[a + l], offsets[a + l + 1]
-    };
-    auto load_offs = [&](uint32_t a) {
-        return Offs{ld64(a + lane, a < a_end && a + lane <= n), ld64(a + lane + 1u, a < a_end && a + lane + 1u <= n)};
-    };
-    struct Run {
-        const uint8_t* rbase;
-        uint64_t span;
-        uint32_t cnt;
-        bool lds;
-    };
-    auto geo = [&](uint32_t a, const Offs& o) {
-        Run g{base, 0, a < a_end ? min(run, a_end - a) : 0u, false};
-        if (g.cnt) {
-            const uint64_t lo = readlane64(o.off, 0), hi = readlane64(o.end, g.cnt - 1u);
-            g.rbase = reinterpret_cast<const uint8_t*>(((uintptr_t)(base + lo)) & ~(uintptr_t)127);
-            g.span = (uint64_t)((base + hi) - g.rbase);
-            g.lds = g.span <= (uint64_t)kScanSlotRows * kRow;
-        }
-        return g;
-    };
-    auto load_part = [&](uint32_t a, const Run& g) {
-        return __builtin_amdgcn_raw_buffer_load_b32(prs, lane < g.cnt ? (a + lane) * 4 : kOOB, 0, 0);
-    };
-    u32x4 VA[kScanSlotRows], VB[kScanSlotRows];
-    auto issue = [&](const Run& g, u32x4 (&V)[kScanSlotRows]) {
-        const __amdgpu_buffer_rsrc_t rs = make_rsrc(g.rbase, (g.span + 3) & ~3ull);
-#pragma unroll
-        for (uint32_t r = 0; r < kScanSlotRows; ++r) V[r] = bld16<true>(rs, r * kRow + lane * 16u);
-    };
-    uint32_t a = a0;
-    while (a < a_end) {
-        Offs oc = load_offs(a), on = load_offs(a + run), op = load_offs(a + 2u * run);
-        __builtin_amdgcn_s_waitcnt(kWaitVm0);
-        Run cur = geo(a, oc);
-        if (!cur.lds) {  // too wide for the slot: streamed as 63 + 1 segments (ragged_runs_lds)
-            const uint32_t part = load_part(a, cur);
-            const uint32_t c1 = min(cur.cnt, kScanRun), c2 = cur.cnt - c1;
-            const uint32_t cnt1[1] = {c1}, part1[1] = {part};
-            const uint64_t o1[1] = {lane == c1 ? readlane64(oc.end, c1 - 1u) : oc.off};
-            ragged_run_stream<R, VERIFY, PIPE, 1>(base, a, kScanRun, cnt1, o1, part1, ors, oks, lane);
-            if (c2) {
-                const uint32_t cnt2[1] = {c2}, part2[1] = {(uint32_t)__shfl_down((int)part, c1)};
-                const uint64_t o2[1] = {lane == 0 ? readlane64(oc.off, c1) : readlane64(oc.end, c1)};
-                ragged_run_stream<R, VERIFY, PIPE, 1>(base, a + c1, kScanRun, cnt2, o2, part2, ors, oks, lane);
-            }
-            a += run;
-            continue;
-        }
-        Run nxt = geo(a + run, on);
-        if (!nxt.lds) nxt.span = 0;
-        uint32_t pc = load_part(a, cur);
-        issue(cur, VA);
-        uint32_t pn = load_part(a + run, nxt);
-        issue(nxt, VB);
-        // One step: run `cur` (rows in V) staged and summed; run cur + 2 loaded into V.
-        auto step = [&](u32x4 (&V)[kScanSlotRows]) -> bool {
-            lds_stage<kScanSlotRows>(slot, V, cur.span, lane);
-            lds_zero_tail(slot, cur.span, lane);
-            const Offs oq = load_offs(a + 3u * run);  // before run + 2's rows
-            Run nn = nxt.lds ? geo(a + 2u * run, op) : Run{base, 0, 0u, false};
-            if (!nn.lds) nn.span = 0;
-            const uint32_t pnn = load_part(a + 2u * run, nn);
-            issue(nn, V);
-            const bool mine = lane < cur.cnt;
-            const uint32_t p = mine ? (uint32_t)((base + oc.off) - cur.rbase) : 0u;
-            const uint32_t e = mine ? (uint32_t)((base + oc.end) - cur.rbase) : 0u;
-            const uint32_t dq = reinterpret_cast<const uint32_t*>(slot)[p >> 2];
-            const uint32_t res = finish(fold32(lds_range_sum(slot, p, e, dq, mine)), (p & 1u) == 0, pc);
-            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, mine ? (a + lane) * 2 : kOOB, 0, kSt);
-            if constexpr (VERIFY)
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(res == 0xFFFFu), oks, mine ? a + lane : kOOB, 0, kSt);
-            a += run;
-            if (!nxt.lds) return false;  // the end of the range, or a run for the outer loop
-            cur = nxt, nxt = nn;
-            pc = pn, pn = pnn;
-            oc = on, on = op, op = oq;
-            return true;
-        };
-        for (;;) {
-            if (!step(VA)) break;
-            if (!step(VB)) break;
-        }
+        flush();
     }
 }
 
@@ -1374,8 +1253,14 @@ __device__ __forceinline__ void pfx_runs(const uint8_t* __restrict__ base, __amd
     }
 }
 
-template <int R, bool VERIFY, bool PIPE, int NS, int XV = 0>
-__global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
+// sets (nsx_tune.segs_per_wave): 0 = by the batch's mean segment (below), 1 = runs of one set, 2 = the small-segment
+// mode (the LDS form with parked results, two waves per block), 3 = the LDS form in every wave of four per block
+// without parking (the form a wave of small segments takes in a batch of larger mean), 4 = runs of four sets.
+// run: segments per run (0 = default: 63 per boundary set, 64 per LDS run).
+// The default instantiation (NS = 2) is register-capped for 4 waves per SIMD (the default grid's 4 blocks per CU
+// must all be resident: their ranges are dealt assuming it); the forced single-set shapes are not.
+template <int R, bool VERIFY, bool PIPE, int NS>
+__global__ __launch_bounds__(kBlock, NS == 2 ? 4 : 1) void csum_ragged_scan_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, uint32_t n,
     const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t run, int sets,
     uint32_t big_keep) {
@@ -1385,6 +1270,29 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
     const __amdgpu_buffer_rsrc_t prs = make_rsrc(partial, partial ? (uint64_t)n * 4 : 0);
     const __amdgpu_buffer_rsrc_t ors = make_rsrc(out, out ? (uint64_t)n * 2 : 0);
     const __amdgpu_buffer_rsrc_t oks = make_rsrc(ok, VERIFY ? (uint64_t)n : 0);
+    extern __shared__ lds16 lds_scan[];
+    const uint32_t lds_run = run ? run : kWave, scan_run = run ? run : kScanRun;
+    // XCD-contiguous numbering of the blocks, wpb of each block's waves taking ranges
+    auto wave_no = [&](uint32_t nb, uint32_t wpb) {
+        const uint32_t b = blockIdx.x;
+        return (nb >= 16 && (nb & 7) == 0) ? ((b & 7) * (nb >> 3) + (b >> 3)) * wpb + wave : b * wpb + wave;
+    };
+    // The small-segment mode (§7 step 61): a batch whose mean segment is under kScanLdsSeg bytes is summed out of LDS
+    // by waves 0-1 of every block (equal-count ranges cut at multiples of 64 segments), each with two of the block's
+    // four slots — one for the run's rows, one for its parked results.
+    if (sets == 2 || (NS == 2 && sets == 0 && run == 0 &&
+                      ld_off(ofs, n) - ld_off(ofs, 0) < (uint64_t)kScanLdsSeg * n)) {
+        if (wave >= 2u) return;
+        const uint32_t nb = gridDim.x, W = nb * 2u;
+        const WaveRange wr = wave_range(ofs, n, wave_no(nb, 2u), W, lane, kScanLdsSeg, 1u, kWave);
+        if (lds_run == kWave)
+            ragged_runs_lds<R, VERIFY, PIPE, true>(base, ofs, n, prs, ors, oks, kWave, wr.a0, wr.a_end, lane,
+                                                   lds_scan + wave * (2u * kScanSlot / 16u), partial != nullptr);
+        else  // tune.run_segs (tests): shorter runs, stored run by run
+            ragged_runs_lds<R, VERIFY, PIPE, false>(base, ofs, n, prs, ors, oks, lds_run, wr.a0, wr.a_end, lane,
+                                                    lds_scan + wave * (2u * kScanSlot / 16u), partial != nullptr);
+        return;
+    }
     // The grid is sized for small segments (4 blocks/CU); a batch of large ones streams on big_keep of them.
     const uint32_t nb = active_blocks(ofs, n, kScanBigMean, big_keep);
     if (blockIdx.x >= nb) return;
@@ -1392,54 +1300,20 @@ __global__ __launch_bounds__(kBlock) void csum_ragged_scan_kernel(
     // a0 + NS·run, ... < a_end; a run never crosses a_end. Byte-balanced: wave g (XCD-contiguous numbering) owns
     // the segments that start in the g-th of W equal byte slices of the batch, so every wave streams the same
     // bytes (± one segment) and none is left running alone at the end of the launch.
-    uint32_t a0, a_end;
-    uint64_t wave_bytes;
-    {
-        const uint32_t b = blockIdx.x, W = nb * kWavesPerBlock;
-        const uint32_t g = (nb >= 16 && (nb & 7) == 0) ? ((b & 7) * (nb >> 3) + (b >> 3)) * kWavesPerBlock + wave
-                                                        : b * kWavesPerBlock + wave;
-        const WaveRange wr = wave_range(ofs, n, g, W, lane, kScanLdsSeg, 1u, (XV & 5) ? kWave : 0u);
-        a0 = wr.a0, a_end = wr.a_end, wave_bytes = wr.bytes;
-    }
-    // Two sets per run suit segments of a few hundred bytes and up (config 3). A wave whose segments average under
-    // kScanLdsSeg bytes sums them out of LDS (§7 step 44); under kScanSmallSeg it takes runs of four sets, so that
-    // each run still streams tens of KB (§7 step 42).
-    if (sets == 2 || (NS == 2 && sets == 0 && wave_bytes < (uint64_t)kScanLdsSeg * (a_end - a0))) {
-        extern __shared__ lds16 lds_scan[];
-        if constexpr ((XV & 4) != 0)
-            ragged_runs_lds_deep<R, VERIFY, PIPE, XV>(base, ofs, n, prs, ors, oks, a0, a_end, lane,
-                                                      lds_scan + wave * (kScanSlot / 16u));
-        else
-            ragged_runs_lds<R, VERIFY, PIPE, XV>(base, ofs, n, prs, ors, oks, run, a0, a_end, lane,
-                                                 lds_scan + wave * ((kScanSlot + ((XV & 64) ? ((XV & 256) ? 8192u : (XV & 128) ? 4096u : 1024u) : 0u)) / 16u),
-                                                 partial != nullptr);
+    const WaveRange wr = wave_range(ofs, n, wave_no(nb, kWavesPerBlock), nb * kWavesPerBlock, lane, kScanLdsSeg, 1u);
+    const uint32_t a0 = wr.a0, a_end = wr.a_end;
+    const uint64_t wave_bytes = wr.bytes;
+    // Two sets per run suit segments of a few hundred bytes and up (config 3). In a batch of larger mean, a wave
+    // whose own segments average under kScanLdsSeg bytes sums them out of LDS (§7 step 44); under kScanSmallSeg it
+    // takes runs of four sets, so that each run still streams tens of KB (§7 step 42).
+    if (sets == 3 || (NS == 2 && sets == 0 && wave_bytes < (uint64_t)kScanLdsSeg * (a_end - a0))) {
+        ragged_runs_lds<R, VERIFY, PIPE, false>(base, ofs, n, prs, ors, oks, lds_run, a0, a_end, lane,
+                                                lds_scan + wave * (kScanSlot / 16u), partial != nullptr);
     } else if (NS == 2 && (sets == 4 || (sets == 0 && wave_bytes < (uint64_t)kScanSmallSeg * (a_end - a0)))) {
-        ragged_runs<R, VERIFY, PIPE, 4>(base, ofs, n, prs, ors, oks, run, a0, a_end, lane);
+        ragged_runs<R, VERIFY, PIPE, 4>(base, ofs, n, prs, ors, oks, scan_run, a0, a_end, lane);
     } else {
-        ragged_runs<R, VERIFY, PIPE, NS>(base, ofs, n, prs, ors, oks, run, a0, a_end, lane);
+        ragged_runs<R, VERIFY, PIPE, NS>(base, ofs, n, prs, ors, oks, scan_run, a0, a_end, lane);
     }
-}
-
-// Experiment: the LDS form alone in a kernel of its own (no streamed forms compiled beside it, no active_blocks),
-// register-capped like the receive pass's 4-blocks/CU kernel; equal-count wave ranges aligned to 64.
-template <bool VERIFY, int XV>
-__global__ __launch_bounds__(kBlock, 4) void csum_ragged_lds_kernel(
-    const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, uint32_t n,
-    const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, uint8_t* __restrict__ ok) {
-    const uint32_t lane = threadIdx.x & (kWave - 1);
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const __amdgpu_buffer_rsrc_t ofs = make_rsrc(offsets, ((uint64_t)n + 1) * 8);
-    const __amdgpu_buffer_rsrc_t prs = make_rsrc(partial, partial ? (uint64_t)n * 4 : 0);
-    const __amdgpu_buffer_rsrc_t ors = make_rsrc(out, out ? (uint64_t)n * 2 : 0);
-    const __amdgpu_buffer_rsrc_t oks = make_rsrc(ok, VERIFY ? (uint64_t)n : 0);
-    const uint32_t nb = gridDim.x, b = blockIdx.x, W = nb * kWavesPerBlock;
-    const uint32_t g = (nb >= 16 && (nb & 7) == 0) ? ((b & 7) * (nb >> 3) + (b >> 3)) * kWavesPerBlock + wave
-                                                    : b * kWavesPerBlock + wave;
-    const WaveRange wr = wave_range(ofs, n, g, W, lane, 0xFFFFFFFFu, 1u, kWave);
-    extern __shared__ lds16 lds_scan[];
-    ragged_runs_lds<2, VERIFY, true, XV>(base, ofs, n, prs, ors, oks, kWave, wr.a0, wr.a_end, lane,
-                                         lds_scan + wave * ((kScanSlot + ((XV & 64) ? ((XV & 256) ? 8192u : (XV & 128) ? 4096u : 1024u) : 0u)) / 16u),
-                                         partial != nullptr);
 }
 
 // ---------------------------------------------------------------------------
@@ -3107,31 +2981,30 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
     // batches of 3 or 4 rows, 0.93 for 1 row). kernel 2 (NSX_TUNE_KERNEL_SCAN_PLAIN):
     // single batches of 4, 8 (default) or 16 rows.
     const bool pipe = c.kernel != 2;
-    // kernel 4..8: experiment variants of the LDS form (XV 1, 2, 3, 5, 7: ragged_runs_lds, ragged_runs_lds_deep)
-    // (kernel 100 + XV for the variants 8, 9, 65)
-    const int xv = c.kernel >= 4 && c.kernel <= 6 ? c.kernel - 3 : c.kernel == 7 ? 5 : c.kernel == 8 ? 7
-                 : c.kernel >= 100 && c.kernel < 200 ? c.kernel - 100 : 0;
     const int rows = pipe ? (c.rows == 2 || c.rows == 4 || c.rows == 8 ? c.rows : 2)
                           : (c.rows == 4 || c.rows == 8 || c.rows == 16 ? c.rows : 8);
-    const uint32_t run = (c.run_segs >= 1 && c.run_segs <= (int)kScanRun) ? (uint32_t)c.run_segs : kScanRun;
+    const uint32_t run = (c.run_segs >= 1 && c.run_segs <= (int)kScanRun) ? (uint32_t)c.run_segs : 0u;  // 0: default
+    const uint32_t task = run ? run : kScanRun;
     // 2 boundary sets per lane (runs of 126 segments) on the default shape: the per-run pipeline fill and drain
     // are paid half as often (config 3 0.684 → 0.682 ms, 40-1500 B frames 0.1320 → 0.1293; 4 sets: 0.683 /
     // 0.1308, more registers and phase-2 checks); segs_per_wave = 1 keeps one set.
     const int ns = (pipe && rows == 2 && c.segs_per_wave != 1) ? 2 : 1;
-    // force runs of four sets (4) or the LDS form (2; tests and A/B); 0: by mean segment size
-    const int sets = c.segs_per_wave == 4 || c.segs_per_wave == 2 ? c.segs_per_wave : 0;
-    // the LDS form's per-wave slots, only when the kernel may choose that form (forced streamed shapes allocate none,
-    // so more of their blocks fit a CU: 33.8 KB of LDS per block caps a launch at 4 resident blocks per CU)
-    const bool lds_form = sets == 2 || (ns == 2 && sets == 0);
-    const size_t lds = lds_form ? (size_t)(kScanSlot + (xv & 64 ? 1024u : 0u)) * kWavesPerBlock : 0;
+    // force the small-segment mode (2), the four-wave LDS form (3) or runs of four sets (4); 0: by mean segment size
+    const int sets = c.segs_per_wave >= 2 && c.segs_per_wave <= 4 ? c.segs_per_wave : 0;
+    // the LDS forms' slots (four per block; the small-segment mode gives two to each of its two waves), only when the
+    // kernel may choose an LDS form (forced streamed shapes allocate none, so more of their blocks fit a CU: 33.8 KB
+    // of LDS per block caps a launch at 4 resident blocks per CU)
+    const bool lds_form = sets == 2 || sets == 3 || (ns == 2 && sets == 0);
+    const size_t lds = lds_form ? (size_t)kScanSlot * kWavesPerBlock : 0;
     // Default grid: 4 blocks/CU, of which a batch of segments averaging ≥ kScanBigMean uses 2 (active_blocks;
-    // config 3 keeps its 2 blocks/CU). A blocks_per_cu override runs exactly that grid.
+    // config 3 keeps its 2 blocks/CU) and a batch averaging < kScanLdsSeg two waves per block (§7 step 61). A
+    // blocks_per_cu override runs exactly that grid.
     const bool pick = c.blocks_per_cu == 0 && pipe && rows == 2 && sets == 0;
     const uint32_t mb = pick ? (uint32_t)c.cus * 4u : max_blocks_of(c, 2);
     const uint32_t keep = pick ? 2u : 0u;
     for (uint64_t c0 = 0; c0 < n; c0 += kRaggedChunk) {
         const uint32_t cn = (uint32_t)(n - c0 < kRaggedChunk ? n - c0 : kRaggedChunk);
-        const uint32_t grid = grid_for((cn + run * ns - 1) / (run * ns), mb);
+        const uint32_t grid = grid_for((cn + task * ns - 1) / (task * ns), mb);
         const uint32_t* pc = partial ? partial + c0 : nullptr;
         uint16_t* oc = out ? out + c0 : nullptr;
         uint8_t* kc = ok ? ok + c0 : nullptr;
@@ -3139,45 +3012,10 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
         if (rows == R_ && pipe == P_ && ns == NS_)                                                              \
             hipLaunchKernelGGL((csum_ragged_scan_kernel<R_, VERIFY, P_, NS_>), dim3(grid), dim3(kBlock), lds, st,\
                                base, offsets + c0, cn, pc, oc, kc, run, sets, keep);
-        NSX_RSCAN(4, true, 1) NSX_RSCAN(8, true, 1)
+        NSX_RSCAN(2, true, 1) NSX_RSCAN(4, true, 1) NSX_RSCAN(8, true, 1)
         NSX_RSCAN(4, false, 1) NSX_RSCAN(8, false, 1) NSX_RSCAN(16, false, 1)
+        NSX_RSCAN(2, true, 2)
 #undef NSX_RSCAN
-        if (rows == 2 && pipe && ns == 1 && c.kernel < 200)
-            hipLaunchKernelGGL((csum_ragged_scan_kernel<2, VERIFY, true, 1>), dim3(grid), dim3(kBlock), lds, st, base,
-                               offsets + c0, cn, pc, oc, kc, run, sets, keep);
-        if (c.kernel >= 200 && c.kernel < 300) {  // experiment: csum_ragged_lds_kernel (209, 265, 267, 293, 295)
-            const int lx = c.kernel == 293 ? 193 : c.kernel == 295 ? 195 : c.kernel == 296 ? 321
-                         : c.kernel == 297 ? 705 : c.kernel - 200;
-            const uint32_t pk = (lx & 64) ? ((lx & 256) ? 8192u : (lx & 128) ? 4096u : 1024u) : 0u;
-            const uint32_t g4 = grid_for((cn + 63) / 64, (uint32_t)c.cus * ((lx & 256) ? 2u : (lx & 128) ? 3u : 4u));
-            const size_t l4 = (size_t)(kScanSlot + pk) * kWavesPerBlock;
-            switch (lx) {
-#define NSX_RLDS(X_)                                                                                          \
-                case X_:                                                                                       \
-                    hipLaunchKernelGGL((csum_ragged_lds_kernel<VERIFY, X_>), dim3(g4), dim3(kBlock), l4, st, base, \
-                                       offsets + c0, cn, pc, oc, kc);                                          \
-                    break;
-                NSX_RLDS(65) NSX_RLDS(67) NSX_RLDS(193) NSX_RLDS(195) NSX_RLDS(321) NSX_RLDS(705)
-#undef NSX_RLDS
-                default:
-                    hipLaunchKernelGGL((csum_ragged_lds_kernel<VERIFY, 9>), dim3(g4), dim3(kBlock), l4, st, base,
-                                       offsets + c0, cn, pc, oc, kc);
-            }
-        } else if (rows == 2 && pipe && ns == 2) {
-            switch (xv) {
-#define NSX_RSCAN_XV(X_)                                                                                          \
-                case X_:                                                                                           \
-                    hipLaunchKernelGGL((csum_ragged_scan_kernel<2, VERIFY, true, 2, X_>), dim3(grid), dim3(kBlock), \
-                                       lds, st, base, offsets + c0, cn, pc, oc, kc, run, sets, keep);              \
-                    break;
-                NSX_RSCAN_XV(1) NSX_RSCAN_XV(2) NSX_RSCAN_XV(3) NSX_RSCAN_XV(5) NSX_RSCAN_XV(7)
-                NSX_RSCAN_XV(8) NSX_RSCAN_XV(9) NSX_RSCAN_XV(65)
-#undef NSX_RSCAN_XV
-                default:
-                    hipLaunchKernelGGL((csum_ragged_scan_kernel<2, VERIFY, true, 2>), dim3(grid), dim3(kBlock), lds, st,
-                                       base, offsets + c0, cn, pc, oc, kc, run, sets, keep);
-            }
-        }
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

@@ -123,21 +123,27 @@ RAGGED_TUNES = [dict(kernel=k, rows=r, run_segs=rs, blocks_per_cu=b)  # pipeline
                 for rs in (0, 1, 16, 63) for b in (0, 1, 8)] + \
                [dict(segs_per_wave=4, run_segs=rs, blocks_per_cu=b)  # runs of four sets
                 for rs in (0, 1, 16, 63) for b in (0, 1, 8)] + \
-               [dict(segs_per_wave=2, run_segs=rs, blocks_per_cu=b, kernel=k)  # the LDS form (small segments' form)
-                for rs in (0, 1, 16, 63) for b in (0, 1, 8) for k in (0, nsx.KERNEL_SCAN_PLAIN, 4, 5, 6, 7, 8, 108, 109, 165, 209, 265, 267, 293, 295, 296, 297)]
+               [dict(segs_per_wave=sp, run_segs=rs, blocks_per_cu=b, kernel=k)  # the LDS forms: 2 = the small-segment
+                for sp in (2, 3) for rs in (0, 1, 16, 63) for b in (0, 1, 8)  # mode (parked results), 3 = four waves
+                for k in (0, nsx.KERNEL_SCAN_PLAIN)]
 
 
 def test_ragged_small_segment_bench_workload_full_size():
     """Bench workload 15 at full size (8M ragged segments of 64-128 B, equal-count wave ranges, the LDS form): every
-    raw sum equals the C oracle's (16 threads), in every form of the LDS loop."""
+    raw sum equals the C oracle's (16 threads): the default small-segment mode (runs of 64 parked and written 8 KiB
+    at a time), the four-wave LDS form, the streamed runs, and the default with partials."""
     import bench
     cfg = bench.WORKLOADS[15]
     w = bench.build_workload(cfg, 0, torch.device("cuda", 0))
     want = O.c_batch(host(w["buf"]), cfg["n"], offsets=w["offsets"], threads=16)
-    for k in (0, 4, 5, 6, 7, 8, 108, 109, 165, 209, 265, 267, 293, 295, 296, 297):
+    for tune in (None, dict(segs_per_wave=3), dict(segs_per_wave=4), dict(segs_per_wave=1)):
         w["out"].zero_()
-        w["step_for"](dict(kernel=k))()
-        assert np.array_equal(u16(w["out"]), want), k
+        w["step_for"](tune)()
+        assert np.array_equal(u16(w["out"]), want), tune
+    part = torch.randint(0, 1 << 31, (cfg["n"],), dtype=torch.int64, device="cuda").to(torch.int32)
+    want_p = O.c_batch(host(w["buf"]), cfg["n"], offsets=w["offsets"], partial=host(part).view(np.uint32), threads=16)
+    out = nsx.ragged_dev(w["buf"], w["d_offs"], partial=part, out=torch.empty_like(w["out"]))
+    assert np.array_equal(u16(out), want_p)
 
 
 @pytest.mark.parametrize("n", [1, 126, 252, 253, 30_001, 400_003])
@@ -158,10 +164,10 @@ def test_ragged_small_segments_runs_of_four_sets(n):
     want = O.c_batch(buf, n, offsets=offs, threads=16)
     want_p = O.c_batch(buf, n, offsets=offs, partial=part, threads=16)
     d, o, p = dev(buf), dev(offs.view(np.int64)), dev(part.view(np.int32))
-    tunes = [None, dict(segs_per_wave=1), dict(segs_per_wave=4), dict(segs_per_wave=2)]
-    tunes += [dict(segs_per_wave=2, kernel=k) for k in (4, 5, 6, 7, 8, 108, 109, 165)] + [dict(kernel=k) for k in (4, 5, 6, 7, 8, 108, 109, 165)]
+    tunes = [None, dict(segs_per_wave=1), dict(segs_per_wave=4), dict(segs_per_wave=2), dict(segs_per_wave=3)]
     tunes += [dict(block_mode=1, blocks_per_cu=1, run_segs=rs, **sp)
-              for rs in (0, 1, 16) for sp in ({}, dict(segs_per_wave=1), dict(segs_per_wave=4), dict(segs_per_wave=2))]
+              for rs in (0, 1, 16) for sp in ({}, dict(segs_per_wave=1), dict(segs_per_wave=4), dict(segs_per_wave=2),
+                                              dict(segs_per_wave=3))]
     for tune in tunes:
         out = torch.empty(n, dtype=torch.int16, device="cuda")
         nsx.ragged_dev(d, o, out=out, tune=tune)
