@@ -4,6 +4,7 @@
 #
 #   bash tools/lib_ab.sh build [ref]          # here (CPU): builds <ref> (default HEAD) into network-stack_amd/lib_base/libnsx_csum.so
 #   bash tools/lib_ab.sh run "10 11" [pairs]  # on the GPU box: new, base, new, base, ... for each workload
+#   AB_EXTRA="--set hi=256" bash tools/lib_ab.sh run 15   # extra tools/ab.py arguments (a workload variant)
 #
 # Both builds share include/ and the ABI of the working tree; only use it for kernel-internal changes.
 set -eu
@@ -29,7 +30,7 @@ case "${1:-}" in
       for k in new base; do
         if [ "$k" = base ]; then cp network-stack_amd/lib_base/libnsx_csum.so "$lib"; else cp /tmp/lib_ab_new.so "$lib"; fi
         for c in $configs; do
-          timeout -k 10 200 python tools/ab.py --config "$c" --variants "$k:" --rounds 5 2>/dev/null | grep AB
+          timeout -k 10 200 python tools/ab.py --config "$c" --variants "$k:" --rounds 5 ${AB_EXTRA:-} 2>/dev/null | grep AB
         done
       done
     done
