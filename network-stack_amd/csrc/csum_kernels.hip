@@ -765,13 +765,76 @@ __device__ __forceinline__ uint32_t active_blocks(__amdgpu_buffer_rsrc_t ofs, ui
     return k ? k : nb;
 }
 
+// Results parked in LDS and written in bulk. A 2-byte raw sum per segment is a small write
+// stream beside a large read stream, and written as it is produced (128 B per wave and run) it cost far more than
+// its bytes: 12-14% of the small-segment LDS form's time, 5-16% of the streamed form's with frames of 160-620 B
+// (profiles/r04_ragged_park_*, r04_rawstream_ab.txt). Parked, a wave's results go out up to 8 KiB at a time, 16 B
+// per lane and store. buf[i] holds the result of segment base + i, base chosen so that out + base is 16 B aligned
+// (al = the output's misalignment in results; base may wrap below 0: only differences of indices are compared);
+// [lo, hi) is parked. A wave parks in increasing segment order and flushes when the next set is not contiguous
+// or would not fit, and at its end. Off (buf null): stored directly.
+constexpr uint32_t kParkCap = 4096;  // results per park buffer: 8 KiB of a wave's 8.25 KiB LDS slot
+struct ResultPark {
+    uint16_t* buf;
+    uint32_t al, base, lo, hi;
+    __device__ __forceinline__ void rebase(uint32_t a) {
+        base = ((a + al) & ~7u) - al;
+        lo = hi = a;
+    }
+};
+
+__device__ __forceinline__ ResultPark make_park(uint16_t* buf, uint32_t out_al, uint32_t a0) {
+    ResultPark pk{buf, out_al, 0, 0, 0};
+    pk.rebase(a0);
+    return pk;
+}
+
+__device__ __forceinline__ void park_flush(ResultPark& pk, __amdgpu_buffer_rsrc_t ors, uint32_t lane) {
+    if (!pk.buf || pk.hi == pk.lo) return;
+    __builtin_amdgcn_wave_barrier();
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const uint32_t l = pk.lo - pk.base, h = pk.hi - pk.base;  // parked: buf[l, h), 0 ≤ l < h ≤ kParkCap
+    const uint32_t b0 = l / 8u, b1 = (h + 7u) / 8u;             // the 8-result blocks touched
+    const bool head_full = 8u * b0 == l, tail_full = 8u * b1 == h;
+    for (uint32_t q = b0; q < b1; q += kWave) {  // whole blocks: one 16 B store each
+        const uint32_t blk = q + lane;
+        const bool full = blk < b1 && (blk != b0 || head_full) && (blk != b1 - 1u || tail_full);
+        const lds16 v = reinterpret_cast<const lds16*>(pk.buf)[blk < kParkCap / 8u ? blk : 0u];
+        __builtin_amdgcn_raw_buffer_store_b128(v4u{v.x, v.y, v.z, v.w}, ors, full ? (pk.base + 8u * blk) * 2u : kOOB,
+                                               0, 0);
+    }
+    // the results of a partial first / last block, one lane each (lanes 0-7: block b0, 8-15: block b1 − 1)
+    const uint32_t i = (lane < 8u ? 8u * b0 : 8u * (b1 - 1u)) + (lane & 7u);
+    const bool st = lane < 16u && (lane < 8u ? !head_full : !tail_full) && i >= l && i < h;
+    const uint16_t r = pk.buf[st ? i : 0u];
+    __builtin_amdgcn_raw_buffer_store_b16(r, ors, st ? (pk.base + i) * 2u : kOOB, 0, 0);
+    __builtin_amdgcn_wave_barrier();
+    pk.rebase(pk.hi);
+}
+
+// Segment a + lane's result (lanes < cnt): parked, or stored directly when parking is off.
+__device__ __forceinline__ void park_put(ResultPark& pk, __amdgpu_buffer_rsrc_t ors, uint32_t a, uint32_t cnt,
+                                         uint32_t lane, uint32_t res) {
+    if (!pk.buf) {
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, lane < cnt ? (a + lane) * 2u : kOOB, 0, 0);
+        return;
+    }
+    if (pk.hi != a || a + cnt - pk.base > kParkCap) {  // not contiguous, or would overflow: flush, rebase at a
+        park_flush(pk, ors, lane);
+        pk.rebase(a);
+    }
+    if (lane < cnt) pk.buf[a + lane - pk.base] = (uint16_t)res;
+    pk.hi = a + cnt;
+}
+
 // One run of NS sets of ≤ run segments in the streaming form: set k = segments [a + k·run, + cnt[k]), lane l ≤
-// cnt[k] holds boundary my_off[k] = offsets[a + k·run + l] and (l < cnt[k]) the partial my_part[k].
+// cnt[k] holds boundary my_off[k] = offsets[a + k·run + l] and (l < cnt[k]) the partial my_part[k]. Results into
+// the wave's park (ResultPark).
 template <int R, bool VERIFY, bool PIPE, int NS>
 __device__ __forceinline__ void ragged_run_stream(const uint8_t* __restrict__ base, uint32_t a, uint32_t run,
                                                   const uint32_t (&cnt)[NS], const uint64_t (&my_off)[NS],
                                                   const uint32_t (&my_part)[NS], __amdgpu_buffer_rsrc_t ors,
-                                                  __amdgpu_buffer_rsrc_t oks, uint32_t lane) {
+                                                  __amdgpu_buffer_rsrc_t oks, uint32_t lane, ResultPark& pk) {
     int64_t brel[NS];
     uint64_t bval[NS];
     // the run's last boundary: set kl = the last set with segments, its lane cnt
@@ -805,7 +868,7 @@ __device__ __forceinline__ void ragged_run_stream(const uint8_t* __restrict__ ba
         const uint32_t res = finish(le, even, my_part[k]);
         const bool mine = lane < cnt[k];
         const uint32_t ak = a + k * run;
-        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, mine ? (ak + lane) * 2 : kOOB, 0, 0);
+        if (cnt[k]) park_put(pk, ors, ak, cnt[k], lane, res);
         if constexpr (VERIFY)
             __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(res == 0xFFFFu), oks, mine ? ak + lane : kOOB, 0, 0);
     }
@@ -816,7 +879,8 @@ template <int R, bool VERIFY, bool PIPE, int NS>
 __device__ __forceinline__ void ragged_runs(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
                                             __amdgpu_buffer_rsrc_t prs, __amdgpu_buffer_rsrc_t ors,
                                             __amdgpu_buffer_rsrc_t oks, uint32_t run, uint32_t a0, uint32_t a_end,
-                                            uint32_t lane) {
+                                            uint32_t lane, uint16_t* park_buf, uint32_t out_al) {
+    ResultPark pk = make_park(park_buf, out_al, a0);
     typedef uint32_t v2u __attribute__((ext_vector_type(2)));
     const uint32_t a_step = run * NS;
     auto load_offs = [&](uint32_t a) -> uint64_t {  // lane l ≤ run length: offsets[a + l]
@@ -838,8 +902,9 @@ __device__ __forceinline__ void ragged_runs(const uint8_t* __restrict__ base, __
             nxt_off[k] = load_offs(a + a_step + k * run);
             my_part[k] = __builtin_amdgcn_raw_buffer_load_b32(prs, lane < cnt[k] ? (ak + lane) * 4 : kOOB, 0, 0);
         }
-        ragged_run_stream<R, VERIFY, PIPE, NS>(base, a, run, cnt, my_off, my_part, ors, oks, lane);
+        ragged_run_stream<R, VERIFY, PIPE, NS>(base, a, run, cnt, my_off, my_part, ors, oks, lane, pk);
     }
+    park_flush(pk, ors, lane);
 }
 
 // Sum of the bytes [p, e) of a wave's LDS slot for the lanes' consecutive ranges of one run (p, e slot positions;
@@ -943,13 +1008,12 @@ __device__ __forceinline__ void lds_stage(lds16* slot, u32x4 (&V)[ROWS], uint64_
 // a streamed one, are flushed (and stored) as they come.
 constexpr uint32_t kScanSlotRows = 8;
 constexpr uint32_t kScanSlot = kScanSlotRows * kRow + 256;  // + pad: lds_range_sum's first chunk block reads past the end
-constexpr uint32_t kParkRuns = 64;                          // runs parked per flush: 64 × 128 B = 8 KiB ≤ one slot
 
 template <int R, bool VERIFY, bool PIPE, bool PARK>
 __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
                                                 __amdgpu_buffer_rsrc_t prs, __amdgpu_buffer_rsrc_t ors,
                                                 __amdgpu_buffer_rsrc_t oks, uint32_t run, uint32_t a0, uint32_t a_end,
-                                                uint32_t lane, lds16* slot, bool has_part) {
+                                                uint32_t lane, lds16* slot, bool has_part, uint32_t out_al) {
     typedef uint32_t v2u __attribute__((ext_vector_type(2)));
     auto ld64 = [&](uint32_t i, bool live) -> uint64_t {
         const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, live ? i * 8 : kOOB, 0, 0);
@@ -983,23 +1047,9 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
 #pragma unroll
         for (uint32_t r = 0; r < kScanSlotRows; ++r) V[r] = bld16<true>(rs, r * kRow + lane * 16u);
     };
-    uint16_t* park = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(slot) + kScanSlot);
-    uint32_t parked = 0, a_park = 0;  // full runs parked, the first one's segment index
-    auto flush = [&]() {              // parked results 8·blk .. 8·blk + 7 (16 B) by lane blk mod 64
-        if (PARK && parked) {
-            __builtin_amdgcn_wave_barrier();
-#pragma unroll
-            for (uint32_t q = 0; q < kParkRuns / 8u; ++q) {
-                const uint32_t blk = q * kWave + lane;
-                const lds16 v = reinterpret_cast<const lds16*>(park)[blk];
-                typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-                __builtin_amdgcn_raw_buffer_store_b128(v4u{v.x, v.y, v.z, v.w}, ors,
-                                                       blk < 8u * parked ? (a_park + blk * 8u) * 2u : kOOB, 0, 0);
-            }
-            __builtin_amdgcn_wave_barrier();
-            parked = 0;
-        }
-    };
+    // PARK: the results parked in the slot after the run's (the small-segment mode gives each wave two)
+    ResultPark pk = make_park(PARK ? reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(slot) + kScanSlot) : nullptr,
+                              out_al, a0);
     // As rx_runs_lds: the LDS loop runs while consecutive runs fit the slot; a run that does not is streamed on
     // its own in the outer loop, so the streaming form's loads in flight at its end never merge into the LDS
     // loop's wait counts.
@@ -1008,16 +1058,15 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
         uint64_t c_off = load_offs(a), c_end = load_ends(a);
         Run cur = geo(a, c_off, c_end);
         if (!cur.lds) {  // too wide for the slot: streamed (boundaries in lanes 0..cnt: ≤ 63 segments, then the rest)
-            flush();
             const uint32_t part = load_part(a, cur.cnt);
             const uint32_t c1 = min(cur.cnt, kScanRun), c2 = cur.cnt - c1;
             const uint32_t cnt1[1] = {c1}, part1[1] = {part};
             const uint64_t o1[1] = {lane == c1 ? readlane64(c_end, c1 - 1u) : c_off};
-            ragged_run_stream<R, VERIFY, PIPE, 1>(base, a, kScanRun, cnt1, o1, part1, ors, oks, lane);
+            ragged_run_stream<R, VERIFY, PIPE, 1>(base, a, kScanRun, cnt1, o1, part1, ors, oks, lane, pk);
             if (c2) {
                 const uint32_t cnt2[1] = {c2}, part2[1] = {(uint32_t)__shfl_down((int)part, c1)};
                 const uint64_t o2[1] = {lane == 0 ? readlane64(c_off, c1) : readlane64(c_end, c1)};
-                ragged_run_stream<R, VERIFY, PIPE, 1>(base, a + c1, kScanRun, cnt2, o2, part2, ors, oks, lane);
+                ragged_run_stream<R, VERIFY, PIPE, 1>(base, a + c1, kScanRun, cnt2, o2, part2, ors, oks, lane, pk);
             }
             a += run;
             continue;
@@ -1038,14 +1087,7 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
             const uint32_t e = mine ? (uint32_t)((base + c_end) - cur.rbase) : 0u;
             const uint32_t dq = reinterpret_cast<const uint32_t*>(slot)[p >> 2];
             const uint32_t res = finish(fold32(lds_range_sum(slot, p, e, dq, mine)), (p & 1u) == 0, part);
-            if (PARK && cur.cnt == kWave) {  // a full run: parked (wave-uniform)
-                if (parked == 0) a_park = a;
-                park[parked * kWave + lane] = (uint16_t)res;
-                if (++parked == kParkRuns) flush();
-            } else {
-                flush();
-                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, mine ? (a + lane) * 2 : kOOB, 0, 0);
-            }
+            park_put(pk, ors, a, cur.cnt, lane, res);
             if constexpr (VERIFY)
                 __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(res == 0xFFFFu), oks, mine ? a + lane : kOOB, 0, 0);
             a += run;
@@ -1054,8 +1096,8 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
             c_off = n_off, n_off = p_off;
             c_end = n_end, n_end = p_end;
         }
-        flush();
     }
+    park_flush(pk, ors, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -1263,7 +1305,7 @@ template <int R, bool VERIFY, bool PIPE, int NS>
 __global__ __launch_bounds__(kBlock, NS == 2 ? 4 : 1) void csum_ragged_scan_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, uint32_t n,
     const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t run, int sets,
-    uint32_t big_keep) {
+    uint32_t big_keep, bool park) {
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const __amdgpu_buffer_rsrc_t ofs = make_rsrc(offsets, ((uint64_t)n + 1) * 8);
@@ -1272,6 +1314,7 @@ __global__ __launch_bounds__(kBlock, NS == 2 ? 4 : 1) void csum_ragged_scan_kern
     const __amdgpu_buffer_rsrc_t oks = make_rsrc(ok, VERIFY ? (uint64_t)n : 0);
     extern __shared__ lds16 lds_scan[];
     const uint32_t lds_run = run ? run : kWave, scan_run = run ? run : kScanRun;
+    const uint32_t out_al = (uint32_t)((uintptr_t)out >> 1) & 7u;  // the output's misalignment in results (ResultPark)
     // XCD-contiguous numbering of the blocks, wpb of each block's waves taking ranges
     auto wave_no = [&](uint32_t nb, uint32_t wpb) {
         const uint32_t b = blockIdx.x;
@@ -1287,10 +1330,10 @@ __global__ __launch_bounds__(kBlock, NS == 2 ? 4 : 1) void csum_ragged_scan_kern
         const WaveRange wr = wave_range(ofs, n, wave_no(nb, 2u), W, lane, kScanLdsSeg, 1u, kWave);
         if (lds_run == kWave)
             ragged_runs_lds<R, VERIFY, PIPE, true>(base, ofs, n, prs, ors, oks, kWave, wr.a0, wr.a_end, lane,
-                                                   lds_scan + wave * (2u * kScanSlot / 16u), partial != nullptr);
+                                                   lds_scan + wave * (2u * kScanSlot / 16u), partial != nullptr, out_al);
         else  // tune.run_segs (tests): shorter runs, stored run by run
             ragged_runs_lds<R, VERIFY, PIPE, false>(base, ofs, n, prs, ors, oks, lds_run, wr.a0, wr.a_end, lane,
-                                                    lds_scan + wave * (2u * kScanSlot / 16u), partial != nullptr);
+                                                    lds_scan + wave * (2u * kScanSlot / 16u), partial != nullptr, out_al);
         return;
     }
     // The grid is sized for small segments (4 blocks/CU); a batch of large ones streams on big_keep of them.
@@ -1306,13 +1349,15 @@ __global__ __launch_bounds__(kBlock, NS == 2 ? 4 : 1) void csum_ragged_scan_kern
     // Two sets per run suit segments of a few hundred bytes and up (config 3). In a batch of larger mean, a wave
     // whose own segments average under kScanLdsSeg bytes sums them out of LDS (§7 step 44); under kScanSmallSeg it
     // takes runs of four sets, so that each run still streams tens of KB (§7 step 42).
+    // The streamed forms park their results in the wave's unused LDS slot when the launch has one (park).
+    uint16_t* pbuf = park ? reinterpret_cast<uint16_t*>(lds_scan + wave * (kScanSlot / 16u)) : nullptr;
     if (sets == 3 || (NS == 2 && sets == 0 && wave_bytes < (uint64_t)kScanLdsSeg * (a_end - a0))) {
         ragged_runs_lds<R, VERIFY, PIPE, false>(base, ofs, n, prs, ors, oks, lds_run, a0, a_end, lane,
-                                                lds_scan + wave * (kScanSlot / 16u), partial != nullptr);
+                                                lds_scan + wave * (kScanSlot / 16u), partial != nullptr, out_al);
     } else if (NS == 2 && (sets == 4 || (sets == 0 && wave_bytes < (uint64_t)kScanSmallSeg * (a_end - a0)))) {
-        ragged_runs<R, VERIFY, PIPE, 4>(base, ofs, n, prs, ors, oks, scan_run, a0, a_end, lane);
+        ragged_runs<R, VERIFY, PIPE, 4>(base, ofs, n, prs, ors, oks, scan_run, a0, a_end, lane, pbuf, out_al);
     } else {
-        ragged_runs<R, VERIFY, PIPE, NS>(base, ofs, n, prs, ors, oks, scan_run, a0, a_end, lane);
+        ragged_runs<R, VERIFY, PIPE, NS>(base, ofs, n, prs, ors, oks, scan_run, a0, a_end, lane, pbuf, out_al);
     }
 }
 
@@ -3011,7 +3056,7 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
 #define NSX_RSCAN(R_, P_, NS_)                                                                                 \
         if (rows == R_ && pipe == P_ && ns == NS_)                                                              \
             hipLaunchKernelGGL((csum_ragged_scan_kernel<R_, VERIFY, P_, NS_>), dim3(grid), dim3(kBlock), lds, st,\
-                               base, offsets + c0, cn, pc, oc, kc, run, sets, keep);
+                               base, offsets + c0, cn, pc, oc, kc, run, sets, keep, lds_form);
         NSX_RSCAN(2, true, 1) NSX_RSCAN(4, true, 1) NSX_RSCAN(8, true, 1)
         NSX_RSCAN(4, false, 1) NSX_RSCAN(8, false, 1) NSX_RSCAN(16, false, 1)
         NSX_RSCAN(2, true, 2)

@@ -176,6 +176,39 @@ def test_ragged_small_segments_runs_of_four_sets(n):
         assert np.array_equal(u16(out), want_p), tune
 
 
+@pytest.mark.parametrize("shift", [0, 1, 3, 7])
+@pytest.mark.parametrize("mix", ["small", "mid", "wide_runs"])
+def test_ragged_parked_results_any_output_alignment(mix, shift):
+    """Parked results (ResultPark) go out in 16 B blocks aligned to the output buffer, with
+    the partial blocks at either end of a flush written result by result: outputs starting 0-7 results past a
+    16 B boundary, inside a sentinel-filled buffer, receive exactly the oracle's sums and nothing outside them is
+    written. Mixes: 64-128 B (the small-segment mode), 0-400 B (streamed runs of four sets), and segments of
+    0-200 B with scattered 20-60 KB ones (LDS runs interrupted by streamed ones: flushes mid-range)."""
+    rng = np.random.default_rng(900 + shift)
+    n = 300_003
+    lens = {"small": rng.integers(64, 129, n), "mid": rng.integers(0, 401, n),
+            "wide_runs": rng.integers(0, 201, n)}[mix].astype(np.uint64)
+    if mix == "wide_runs":
+        lens[rng.integers(0, n, 400)] = rng.integers(20_000, 60_000, 400).astype(np.uint64)
+    offs = np.zeros(n + 1, np.uint64)
+    offs[1:] = np.cumsum(lens)
+    offs += np.uint64(1)
+    buf = O.c_splitmix64(0x5A + shift, int(offs[-1]) + 3)
+    part = rng.integers(0, 1 << 31, n, dtype=np.uint32)
+    want = O.c_batch(buf, n, offsets=offs, threads=16)
+    want_p = O.c_batch(buf, n, offsets=offs, partial=part, threads=16)
+    d, o, p = dev(buf), dev(offs.view(np.int64)), dev(part.view(np.int32))
+    big = torch.empty(n + 64, dtype=torch.int16, device="cuda")
+    assert big.data_ptr() % 16 == 0
+    for tune in (None, dict(segs_per_wave=2), dict(segs_per_wave=3), dict(segs_per_wave=4), dict(segs_per_wave=1)):
+        for pt, w in ((None, want), (p, want_p)):
+            big.fill_(0x5A5A)
+            nsx.ragged_dev(d, o, partial=pt, out=big[shift:shift + n], tune=tune)
+            got = u16(big)
+            assert np.array_equal(got[shift:shift + n], w), (tune, pt is None)
+            assert (got[:shift] == 0x5A5A).all() and (got[shift + n:] == 0x5A5A).all(), tune
+
+
 def test_ragged_launch_shapes_bit_exact():
     rng = np.random.default_rng(1234)
     lens = rng.integers(0, 9001, 20000).astype(np.uint64)
