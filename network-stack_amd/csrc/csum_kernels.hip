@@ -1388,6 +1388,14 @@ __device__ __forceinline__ uint32_t bswap16u(uint32_t v) { return ((v & 0xFFu) <
 
 constexpr uint32_t kRxRun = 64;
 
+// The receive pass's outputs: the validity mask, and the optional IPv4 header / TCP raw sums. raw (wave-uniform):
+// either raw output is present; without one the per-frame raw stores are not issued at all (a store to an empty
+// descriptor is dropped, but still an instruction through the memory pipeline per frame set).
+struct RxOuts {
+    __amdgpu_buffer_rsrc_t mrs, irs, trs;
+    bool raw;
+};
+
 // A run's validity ballot (frames [a, a + cnt), a a multiple of 8) as mask bytes a/8 ..: one byte per lane
 // (lanes 0-7), so wave ranges need only be cut at multiples of 8 frames, not at whole 64-bit words; the
 // batch's last run also zero-fills the rest of the mask's last word.
@@ -1487,24 +1495,24 @@ __device__ __forceinline__ RxHdr rx_hdr(const uint32_t (&d)[6], uint32_t hd, uin
 
 template <bool V6>
 __device__ __forceinline__ void rx_verdict(uint64_t F, const RxHdr& h, bool even, bool live, uint32_t ak, uint32_t cnt,
-                                           uint32_t n, uint32_t lane, __amdgpu_buffer_rsrc_t mrs,
-                                           __amdgpu_buffer_rsrc_t irs, __amdgpu_buffer_rsrc_t trs, uint32_t s) {
+                                           uint32_t n, uint32_t lane, const RxOuts& ro, uint32_t s) {
     const uint64_t T = F - (h.hdr_ok ? h.hs : 0u);  // the TCP segment's weighted sum (IPv6: addresses ‖ segment)
     const uint32_t tle = fold32((uint32_t)T) + fold32((uint32_t)(T >> 32));
     const uint32_t tcpr = h.well ? finish(tle, even, h.aux) : 0u;
     const uint64_t bits = __builtin_amdgcn_ballot_w64(h.well && (V6 || h.ipr == 0xFFFFu) && tcpr == 0xFFFFu);
-    rx_store_mask(mrs, bits, ak, cnt, n, lane, s);
-    if constexpr (!V6)
-        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)h.ipr, irs, live ? (ak + lane) * 2u : kOOB, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)tcpr, trs, live ? (ak + lane) * 2u : kOOB, 0, 0);
+    rx_store_mask(ro.mrs, bits, ak, cnt, n, lane, s);
+    if (ro.raw) {
+        if constexpr (!V6)
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)h.ipr, ro.irs, live ? (ak + lane) * 2u : kOOB, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)tcpr, ro.trs, live ? (ak + lane) * 2u : kOOB, 0, 0);
+    }
 }
 
 template <bool V6, typename OptFn>
 __device__ __forceinline__ void rx_frame_out(uint64_t F, const uint32_t (&d)[6], uint32_t hd, uint64_t flen, bool even,
                                              bool live, uint32_t ak, uint32_t cnt, uint32_t n, uint32_t lane,
-                                             __amdgpu_buffer_rsrc_t mrs, __amdgpu_buffer_rsrc_t irs,
-                                             __amdgpu_buffer_rsrc_t trs, OptFn&& opt, uint32_t s = 0) {
-    rx_verdict<V6>(F, rx_hdr<V6>(d, hd, flen, even, live, opt), even, live, ak, cnt, n, lane, mrs, irs, trs, s);
+                                             const RxOuts& ro, OptFn&& opt, uint32_t s = 0) {
+    rx_verdict<V6>(F, rx_hdr<V6>(d, hd, flen, even, live, opt), even, live, ak, cnt, n, lane, ro, s);
 }
 
 // One run of NS sets of ≤ 64 frames in the streaming form: frame a + 64k + lane = [my_off[k], my_end[k]) for
@@ -1512,8 +1520,7 @@ __device__ __forceinline__ void rx_frame_out(uint64_t F, const uint32_t (&d)[6],
 template <int R, bool V6, int NS>
 __device__ __forceinline__ void rx_run_stream(const uint8_t* __restrict__ base, uint32_t a, const uint32_t (&cnt)[NS],
                                               const uint64_t (&my_off)[NS], const uint64_t (&my_end)[NS], uint32_t kl,
-                                              uint32_t n, uint32_t lane, __amdgpu_buffer_rsrc_t mrs,
-                                              __amdgpu_buffer_rsrc_t irs, __amdgpu_buffer_rsrc_t trs) {
+                                              uint32_t n, uint32_t lane, const RxOuts& ro) {
     {
         const uint64_t lo = readlane64(my_off[0], 0);
         uint64_t hi = 0;
@@ -1594,15 +1601,14 @@ __device__ __forceinline__ void rx_run_stream(const uint8_t* __restrict__ base, 
                 }
             };
             rx_frame_out<V6>(F, d[k], hd, my_end[k] - my_off[k], ((uintptr_t)fp & 1u) == 0, live, ak, cnt[k], n, lane,
-                             mrs, irs, trs, opt);
+                             ro, opt);
         }
     }
 }
 
 template <int R, bool V6, int NS>
 __device__ __forceinline__ void rx_runs(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
-                                        uint32_t a0, uint32_t a_end, uint32_t lane, __amdgpu_buffer_rsrc_t mrs,
-                                        __amdgpu_buffer_rsrc_t irs, __amdgpu_buffer_rsrc_t trs) {
+                                        uint32_t a0, uint32_t a_end, uint32_t lane, const RxOuts& ro) {
     typedef uint32_t v2u __attribute__((ext_vector_type(2)));
     auto load_off = [&](uint32_t i, bool live) -> uint64_t {
         const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, live ? i * 8 : kOOB, 0, 0);
@@ -1631,7 +1637,7 @@ __device__ __forceinline__ void rx_runs(const uint8_t* __restrict__ base, __amdg
             nxt_off[k] = load_off(an + lane, an < a_end && an + lane <= n);
             nxt_end[k] = load_off(an + lane + 1, an < a_end && an + lane + 1 <= n);
         }
-        rx_run_stream<R, V6, NS>(base, a, cnt, my_off, my_end, kl, n, lane, mrs, irs, trs);
+        rx_run_stream<R, V6, NS>(base, a, cnt, my_off, my_end, kl, n, lane, ro);
     }
 }
 
@@ -1649,8 +1655,7 @@ constexpr uint32_t kRxSlot = kRxSlotRows * kRow + 256;  // + pad: a header windo
 template <int R, bool V6, uint32_t ROWS, bool HYB>
 __device__ __forceinline__ void rx_runs_pfx(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
                                             uint32_t a0, uint32_t a_end, uint32_t lane, lds16* slot,
-                                            __amdgpu_buffer_rsrc_t mrs, __amdgpu_buffer_rsrc_t irs,
-                                            __amdgpu_buffer_rsrc_t trs) {
+                                            const RxOuts& ro) {
     static_assert(kPfxRun == kRxRun && kPfxDirectSlot == kRxSlot, "the receive pass's runs and direct slot");
     const uint32_t* sdw = reinterpret_cast<const uint32_t*>(slot);
     auto out = [&](uint64_t F, uint32_t p, uint32_t d0, bool live, uint32_t a, uint32_t s, uint32_t cnt, uint64_t off,
@@ -1665,13 +1670,13 @@ __device__ __forceinline__ void rx_runs_pfx(const uint8_t* __restrict__ base, __
 #pragma unroll
             for (int j = 6; j < 16; ++j) o[j - 6] = sdw[w0 + j];
         };
-        rx_frame_out<V6>(F, d, p & 3u, end - off, (p & 1u) == 0, live, a, cnt, n, lane, mrs, irs, trs, opt, s);
+        rx_frame_out<V6>(F, d, p & 3u, end - off, (p & 1u) == 0, live, a, cnt, n, lane, ro, opt, s);
     };
     auto stream = [&](uint32_t a, uint32_t s, uint32_t rem, uint64_t off, uint64_t end) {  // lanes shifted by s
         uint32_t cnt1[1] = {rem};
         uint64_t o1[1] = {(uint64_t)__shfl_down((unsigned long long)off, s)};
         uint64_t e1[1] = {(uint64_t)__shfl_down((unsigned long long)end, s)};
-        rx_run_stream<R, V6, 1>(base, a + s, cnt1, o1, e1, 0u, n, lane, mrs, irs, trs);
+        rx_run_stream<R, V6, 1>(base, a + s, cnt1, o1, e1, 0u, n, lane, ro);
     };
     pfx_runs<ROWS, HYB, 8u>(base, ofs, n, a0, a_end, lane, slot, out, stream);
 }
@@ -1679,8 +1684,7 @@ __device__ __forceinline__ void rx_runs_pfx(const uint8_t* __restrict__ base, __
 template <bool V6>
 __device__ __forceinline__ void rx_run_lds(const uint8_t* __restrict__ base, const uint8_t* rbase, uint32_t a,
                                            uint32_t cnt, uint64_t my_off, uint64_t my_end, uint32_t n, uint32_t lane,
-                                           const lds16* slot, __amdgpu_buffer_rsrc_t mrs, __amdgpu_buffer_rsrc_t irs,
-                                           __amdgpu_buffer_rsrc_t trs) {
+                                           const lds16* slot, const RxOuts& ro) {
     const uint32_t* sdw = reinterpret_cast<const uint32_t*>(slot);
     const bool live = lane < cnt;
     // frame position in the slot (rbase is 128-aligned, so the slot keeps every byte's address mod 128)
@@ -1696,7 +1700,7 @@ __device__ __forceinline__ void rx_run_lds(const uint8_t* __restrict__ base, con
 #pragma unroll
         for (int j = 6; j < 16; ++j) o[j - 6] = sdw[w0 + j];
     };
-    rx_frame_out<V6>(F, d, hd, my_end - my_off, (p & 1u) == 0, live, a, cnt, n, lane, mrs, irs, trs, opt);
+    rx_frame_out<V6>(F, d, hd, my_end - my_off, (p & 1u) == 0, live, a, cnt, n, lane, ro, opt);
 }
 
 // A wave's runs [a0, a_end) in the LDS form (runs of 64 frames from a multiple of 8, as rx_runs).
@@ -1706,8 +1710,7 @@ __device__ __forceinline__ void rx_run_lds(const uint8_t* __restrict__ base, con
 template <int R, bool V6, bool SW = false>
 __device__ __forceinline__ void rx_runs_lds(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
                                             uint32_t a0, uint32_t a_end, uint32_t lane, lds16* slot,
-                                            __amdgpu_buffer_rsrc_t mrs, __amdgpu_buffer_rsrc_t irs,
-                                            __amdgpu_buffer_rsrc_t trs) {
+                                            const RxOuts& ro) {
     typedef uint32_t v2u __attribute__((ext_vector_type(2)));
     auto load_off = [&](uint32_t i, bool live) -> uint64_t {
         const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, live ? i * 8 : kOOB, 0, 0);
@@ -1748,7 +1751,7 @@ __device__ __forceinline__ void rx_runs_lds(const uint8_t* __restrict__ base, __
     while (a < a_end) {
         Run cur = geo(a, c_off, c_end);
         if (SW && !cur.lds) {
-            rx_runs_pfx<R, V6, 7, true>(base, ofs, n, a, a_end, lane, slot, mrs, irs, trs);
+            rx_runs_pfx<R, V6, 7, true>(base, ofs, n, a, a_end, lane, slot, ro);
             return;
         }
         if (!cur.lds) {  // a run too wide for the slot: the streaming form
@@ -1757,7 +1760,7 @@ __device__ __forceinline__ void rx_runs_lds(const uint8_t* __restrict__ base, __
             const uint64_t s_end = load_off(as + lane + 1u, as < a_end && as + lane + 1u <= n);
             uint32_t cnt1[1] = {cur.cnt};
             uint64_t o1[1] = {c_off}, e1[1] = {c_end};
-            rx_run_stream<R, V6, 1>(base, a, cnt1, o1, e1, 0u, n, lane, mrs, irs, trs);
+            rx_run_stream<R, V6, 1>(base, a, cnt1, o1, e1, 0u, n, lane, ro);
             a = as, c_off = s_off, c_end = s_end;
             continue;
         }
@@ -1779,7 +1782,7 @@ __device__ __forceinline__ void rx_runs_lds(const uint8_t* __restrict__ base, __
             const uint32_t an2 = an + kRxRun;
             const uint64_t p_off = load_off(an2 + lane, an2 < a_end && an2 + lane <= n);
             const uint64_t p_end = load_off(an2 + lane + 1u, an2 < a_end && an2 + lane + 1u <= n);
-            rx_run_lds<V6>(base, cur.rbase, a, cur.cnt, c_off, c_end, n, lane, slot, mrs, irs, trs);
+            rx_run_lds<V6>(base, cur.rbase, a, cur.cnt, c_off, c_end, n, lane, slot, ro);
             a = an;
             c_off = n_off, c_end = n_end;
             if (!nxt.lds) break;  // the end of the wave's range, or a run for the outer loop
@@ -1818,9 +1821,8 @@ __global__ __launch_bounds__(kBlock, WPS) void rx_tcp_kernel(const uint8_t* __re
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const __amdgpu_buffer_rsrc_t ofs = make_rsrc(offsets, ((uint64_t)n + 1) * 8);
-    const __amdgpu_buffer_rsrc_t mrs = make_rsrc(mask, (((uint64_t)n + 63) / 64) * 8);
-    const __amdgpu_buffer_rsrc_t irs = make_rsrc(ip_raw, ip_raw ? (uint64_t)n * 2 : 0);
-    const __amdgpu_buffer_rsrc_t trs = make_rsrc(tcp_raw, tcp_raw ? (uint64_t)n * 2 : 0);
+    const RxOuts ro{make_rsrc(mask, (((uint64_t)n + 63) / 64) * 8), make_rsrc(ip_raw, ip_raw ? (uint64_t)n * 2 : 0),
+                    make_rsrc(tcp_raw, tcp_raw ? (uint64_t)n * 2 : 0), ip_raw != nullptr || tcp_raw != nullptr};
     extern __shared__ lds16 lds_rx[];
     // Byte-balanced wave ranges (as csum_ragged_scan_kernel), cut at multiples of 8 frames. Cut at whole mask
     // words (64 frames, ~50 KB) instead, a wave streamed up to one run more than the mean, and the launch
@@ -1842,19 +1844,19 @@ __global__ __launch_bounds__(kBlock, WPS) void rx_tcp_kernel(const uint8_t* __re
             if (wave >= 2u) return;
             const WaveRange wr = range(gridDim.x, 2u, wave);
             rx_runs_pfx<R, V6, 15, false>(base, ofs, n, wr.a0, wr.a_end, lane,
-                                          lds_rx + wave * (PfxSlot<15>::kBytes / 16u), mrs, irs, trs);
+                                          lds_rx + wave * (PfxSlot<15>::kBytes / 16u), ro);
         } else if (mode == 5 || mode == 7) {  // four waves per block: the LDS loop until a run needs the hybrid
                                               // loop (5), or the hybrid loop throughout (7)
             const WaveRange wr = range(gridDim.x, kWavesPerBlock, wave);
             lds16* slot = lds_rx + wave * (PfxSlot<7>::kBytes / 16u);
-            if (mode == 5) rx_runs_lds<R, V6, true>(base, ofs, n, wr.a0, wr.a_end, lane, slot, mrs, irs, trs);
-            else rx_runs_pfx<R, V6, 7, true>(base, ofs, n, wr.a0, wr.a_end, lane, slot, mrs, irs, trs);
+            if (mode == 5) rx_runs_lds<R, V6, true>(base, ofs, n, wr.a0, wr.a_end, lane, slot, ro);
+            else rx_runs_pfx<R, V6, 7, true>(base, ofs, n, wr.a0, wr.a_end, lane, slot, ro);
         } else {  // streamed runs; a batch of large frames on 3 of the 4 blocks per CU
             // (mode 8: the streamed runs forced, on the 3 of 4 blocks per CU the auto choice gives them)
             const uint32_t nb = active_blocks(ofs, n, sets == 8 ? 0u : kRxBigMean, sets == 0 || sets == 8 ? 3u : 0u);
             if (blockIdx.x >= nb) return;
             const WaveRange wr = range(nb, kWavesPerBlock, wave);
-            rx_runs<R, V6, 1>(base, ofs, n, wr.a0, wr.a_end, lane, mrs, irs, trs);
+            rx_runs<R, V6, 1>(base, ofs, n, wr.a0, wr.a_end, lane, ro);
         }
         return;
     }
@@ -1865,9 +1867,9 @@ __global__ __launch_bounds__(kBlock, WPS) void rx_tcp_kernel(const uint8_t* __re
     const uint32_t a0 = wr.a0, a_end = wr.a_end;
     const bool small = sets == 2 || (sets == 0 && wr.bytes < (uint64_t)kRxSmallFrame * (a_end - a0));
     if (small) {
-        rx_runs_lds<R, V6>(base, ofs, n, a0, a_end, lane, lds_rx + wave * (kRxSlot / 16u), mrs, irs, trs);
+        rx_runs_lds<R, V6>(base, ofs, n, a0, a_end, lane, lds_rx + wave * (kRxSlot / 16u), ro);
     } else {
-        rx_runs<R, V6, 1>(base, ofs, n, a0, a_end, lane, mrs, irs, trs);
+        rx_runs<R, V6, 1>(base, ofs, n, a0, a_end, lane, ro);
     }
 }
 
