@@ -29,8 +29,9 @@ extern "C" {
 
 typedef struct nsx_tune {
     int32_t blocks_per_cu;     /* persistent grid: 1..8 blocks of 256 threads per CU. Default of the ragged
-                                  scan and receive kernels: 4 per CU, of which a batch whose mean segment /
-                                  frame is >= 2048 B / 640 B uses 2 / 3 (the rest return at once); a value
+                                  scan and receive kernels: 4 per CU, of which a batch of segments averaging
+                                  >= 2048 B uses 2, a receive batch taking streamed runs 3 (the rest
+                                  return at once); a value
                                   here launches exactly that grid. A shape that may take an LDS form (the
                                   ragged scan's and receive pass's small-unit forms: ~34 KB of LDS per
                                   block) has at most 4 of its blocks resident per CU at a time (160 KB of
@@ -45,11 +46,12 @@ typedef struct nsx_tune {
                                   4 = runs of four sets in every wave. Only the default pipelined 2-row shape has more than one
                                   set: with kernel = SCAN_PLAIN or rows != 2 a 4 gives runs of one set.
                                   Receive kernels: 0 auto = the default grid (4 blocks/CU) choosing by the
-                                  batch's mean frame: < 112 B the LDS form for whole runs of <= 256 B
-                                  frames that fit 8 KiB, switching at the first other run to the hybrid
-                                  loop (such runs as prefix-form pieces of <= 7 KiB), < 640 B the prefix
-                                  form with 15 KiB slots on two waves per block, else streamed runs on 3
-                                  blocks/CU; 5 / 6 / 7 / 8 force the small-frame mode / the two-wave prefix
+                                  batch's mean frame and frame count: < 112 B the LDS form for whole runs
+                                  of <= 256 B frames that fit 8 KiB, switching at the first other run to
+                                  the hybrid loop (such runs as prefix-form pieces of <= 7 KiB); below the
+                                  streaming threshold (448 B in batches of < 2.5M frames, 768 B from 2.5M)
+                                  the prefix form with 15 KiB slots on two waves per block, else streamed
+                                  runs on 3 blocks/CU; 5 / 6 / 7 / 8 force the small-frame mode / the two-wave prefix
                                   form / the hybrid loop throughout / the streamed runs (3 blocks/CU) on that grid (NSX_EINVAL with rows
                                   other than 0 / 2 or with blocks_per_cu set). With rows or blocks_per_cu set (the
                                   pre-prefix shapes): 0 = per wave the LDS form (mean < 128 B) or streamed

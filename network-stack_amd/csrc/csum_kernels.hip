@@ -741,7 +741,7 @@ __device__ __forceinline__ void scan_span(const uint8_t* rbase, uint64_t span, u
         if (brel[k] >= (int64_t)(nrows * kRow)) bval[k] = carry;  // boundary at the very end of the rows
 }
 
-// Ragged scan forms by mean segment size (tools/r03_sweep.sh, profiles/r03_grid_sweep.txt): per wave, the LDS form
+// Ragged scan forms by mean segment size (profiles/r03_grid_sweep.txt): per wave, the LDS form
 // under kScanLdsSeg (runs of 63 such segments fit its 8 KiB slot), runs of four 63-segment sets under
 // kScanSmallSeg, else runs of two sets; per batch, 4 blocks/CU under kScanBigMean, else 2.
 constexpr uint32_t kScanSmallSeg = 2048;
@@ -1420,7 +1420,8 @@ __device__ __forceinline__ void rx_store_mask(__amdgpu_buffer_rsrc_t mrs, uint64
 // under kRxSmallFrame bytes takes the LDS form instead (rx_runs_lds, §7 step 43), which replaced round 2's runs of
 // four sets (§7 step 41).
 constexpr uint32_t kRxSmallFrame = 128;
-// 4 blocks/CU for batches whose mean frame is under kRxBigMean, else 3 (tools/r03_sweep.sh: 4 blocks 9% faster at a
+// The pre-prefix shapes (rows / blocks_per_cu set): 4 blocks/CU for batches whose mean frame is under kRxBigMean,
+// else 3 (profiles/r03_grid_sweep.txt: 4 blocks 9% faster at a
 // 170 B mean, 3.4% at 320 B, 0.4% at 520 B; 3 blocks 2.9% faster at workload 10's 770 B)
 constexpr uint32_t kRxBigMean = 640;
 
@@ -1794,15 +1795,23 @@ __device__ __forceinline__ void rx_runs_lds(const uint8_t* __restrict__ base, __
 }
 
 
-// The receive pass's grids by the batch's mean frame m (tools/r03_pfx_sweep.sh): m <
+// The receive pass's grids by the batch's mean frame m: m <
 // kRxPfxMean: four waves per block, the LDS loop for runs of small frames that fit 8 KiB, handing over at the first
 // other run to the hybrid loop (direct pieces for such runs, prefix pieces of ≤ 7 KiB otherwise; §7 step 59);
-// kRxPfxMean ≤ m < kRxBigMean: the prefix form with 15-row slots on two waves per
-// block (8 waves per CU, ~19 KB of LDS each); m ≥ kRxBigMean: streamed runs on 3 blocks per CU.
+// kRxPfxMean ≤ m < the streaming threshold: the prefix form with 15-row slots on two waves per block (8 waves per
+// CU, ~19 KB of LDS each); above it streamed runs on 3 blocks per CU.
+// The streaming threshold depends on the batch's frame count as well as its mean (DESIGN.md §7 step 63,
+// profiles/r04_rx_form_sweep.txt: n 1M-8M × means 200-900 B): in batches of up to 2M frames streamed runs win from
+// a 500 B mean (by 2-6% at 500-900 B) and lose by 1-23% at 200-400 B; from 3M frames the prefix form wins up to
+// a 750 B mean (by 1-3%), streamed runs from 800 B. The prefix form's time has a fixed part (~5-9 µs; its wave
+// ranges are equal-count, so their byte imbalance shrinks as the runs per wave grow) that large batches amortise.
 constexpr uint32_t kRxPfxMean = 112;
+constexpr uint32_t kRxStreamMeanSmallN = 448;      // the streaming threshold below kRxStreamBigN frames
+constexpr uint32_t kRxStreamMeanBigN = 768;        // ... and from kRxStreamBigN frames
+constexpr uint32_t kRxStreamBigN = 5u << 19;       // 2.5M frames
 
 // PF = -1: the default grid's kernel (4 blocks/CU, PfxSlot<15> × 2 of LDS per block): sets 0 = by the batch's mean
-// frame (kRxPfxMean, kRxBigMean above), 1 = streamed runs, 5 = the small-frame mode (LDS loop, then the hybrid
+// frame and frame count (above), 1 = streamed runs on every block, 8 = streamed runs on 3 blocks per CU, 5 = the small-frame mode (LDS loop, then the hybrid
 // loop), 6 = the 15-row prefix form on waves 0-1, 7 = the hybrid loop throughout. (The prefix form at 3 and 2 blocks per CU, forced by sets 3 in §7 step 54, was removed once
 // the default grid held both of its slots.)
 // PF = 0: the shapes set by rows / blocks_per_cu: sets 0 = by the wave's mean frame size (the LDS form below
@@ -1837,7 +1846,8 @@ __global__ __launch_bounds__(kBlock, WPS) void rx_tcp_kernel(const uint8_t* __re
         int mode = sets;
         if (sets == 0) {
             const uint64_t tot = ld_off(ofs, n) - ld_off(ofs, 0);
-            mode = tot >= (uint64_t)kRxBigMean * n ? 1 : tot >= (uint64_t)kRxPfxMean * n ? 6 : 5;
+            const uint64_t stream_mean = n >= kRxStreamBigN ? kRxStreamMeanBigN : kRxStreamMeanSmallN;
+            mode = tot >= stream_mean * n ? 1 : tot >= (uint64_t)kRxPfxMean * n ? 6 : 5;
         }
         if (mode == 6) {  // two waves per block, 15-row slots (waves 0-1: as fast as 0-1 / 2-3 by block parity
                           // and as 2 blocks/CU of four waves)
@@ -1851,9 +1861,9 @@ __global__ __launch_bounds__(kBlock, WPS) void rx_tcp_kernel(const uint8_t* __re
             lds16* slot = lds_rx + wave * (PfxSlot<7>::kBytes / 16u);
             if (mode == 5) rx_runs_lds<R, V6, true>(base, ofs, n, wr.a0, wr.a_end, lane, slot, ro);
             else rx_runs_pfx<R, V6, 7, true>(base, ofs, n, wr.a0, wr.a_end, lane, slot, ro);
-        } else {  // streamed runs; a batch of large frames on 3 of the 4 blocks per CU
-            // (mode 8: the streamed runs forced, on the 3 of 4 blocks per CU the auto choice gives them)
-            const uint32_t nb = active_blocks(ofs, n, sets == 8 ? 0u : kRxBigMean, sets == 0 || sets == 8 ? 3u : 0u);
+        } else {  // streamed runs on 3 of the 4 blocks per CU (the auto choice and mode 8, which forces it); mode 1:
+                  // on every block
+            const uint32_t nb = active_blocks(ofs, n, 0u, sets == 0 || sets == 8 ? 3u : 0u);
             if (blockIdx.x >= nb) return;
             const WaveRange wr = range(nb, kWavesPerBlock, wave);
             rx_runs<R, V6, 1>(base, ofs, n, wr.a0, wr.a_end, lane, ro);
