@@ -29,22 +29,25 @@ extern "C" {
 
 typedef struct nsx_tune {
     int32_t blocks_per_cu;     /* persistent grid: 1..8 blocks of 256 threads per CU. Default of the ragged
-                                  scan and receive kernels: 4 per CU, of which a batch of segments averaging
-                                  >= 2048 B uses 2, a receive batch taking streamed runs 3 (the rest
-                                  return at once); a value
+                                  scan and receive kernels: 4 per CU, of which a streamed batch uses 3
+                                  (a ragged batch of segments averaging >= 2048 B: 2; the rest return at
+                                  once); a value
                                   here launches exactly that grid. A shape that may take an LDS form (the
                                   ragged scan's and receive pass's small-unit forms: ~34 KB of LDS per
                                   block) has at most 4 of its blocks resident per CU at a time (160 KB of
-                                  LDS); forced streamed shapes (segs_per_wave 1 or 4) allocate no LDS */
+                                  LDS); above 4 blocks/CU forced streamed shapes allocate no LDS */
     int32_t segs_per_wave;     /* fixed batches of <= 4 KiB segments: segments per wave task (1, 2, 4, 8).
                                   Ragged scan: 0 auto (a batch whose segments average < 128 B: the small-
                                   segment mode — the LDS form on two waves per block, results parked and
                                   written 8 KiB at a time; otherwise per wave: the LDS form in waves whose
-                                  segments average < 128 B, streamed runs of four 63-segment sets < 2048 B,
-                                  else runs of two sets), 1 = runs of one set, 2 = the small-segment mode,
+                                  segments average < 128 B, else streamed runs of two 63-segment sets
+                                  < 256 B, else of one, on 3 blocks/CU, 2 from a 2048 B mean), 1 = runs
+                                  of one set on the uncapped single-set kernel, 2 = the small-segment mode,
                                   3 = the LDS form in every wave (four per block, results stored per run),
-                                  4 = runs of four sets in every wave. Only the default pipelined 2-row shape has more than one
-                                  set: with kernel = SCAN_PLAIN or rows != 2 a 4 gives runs of one set.
+                                  4 / 5 = runs of four / two sets in every wave. Only the default pipelined
+                                  2-row shape has more than one set: with kernel = SCAN_PLAIN or rows != 2
+                                  a 4 or 5 gives runs of one set. Grids of <= 4 blocks/CU park the streamed
+                                  forms' results in LDS and write them 8 KiB at a time.
                                   Receive kernels: 0 auto = the default grid (4 blocks/CU) choosing by the
                                   batch's mean frame and frame count: < 112 B the LDS form for whole runs
                                   of <= 256 B frames that fit 8 KiB, switching at the first other run to

@@ -741,11 +741,12 @@ __device__ __forceinline__ void scan_span(const uint8_t* rbase, uint64_t span, u
         if (brel[k] >= (int64_t)(nrows * kRow)) bval[k] = carry;  // boundary at the very end of the rows
 }
 
-// Ragged scan forms by mean segment size (profiles/r03_grid_sweep.txt): per wave, the LDS form
-// under kScanLdsSeg (runs of 63 such segments fit its 8 KiB slot), runs of four 63-segment sets under
-// kScanSmallSeg, else runs of two sets; per batch, 4 blocks/CU under kScanBigMean, else 2.
-constexpr uint32_t kScanSmallSeg = 2048;
+// Ragged scan forms by mean segment size (profiles/r04_ragged_form_sweep.txt): per batch, the small-segment mode
+// under kScanLdsSeg; else per wave the LDS form under kScanLdsSeg (runs of 63 such segments fit its 8 KiB slot),
+// else streamed runs of two 63-segment sets under kScanTwoSetSeg, else of one set, on 3 blocks/CU under
+// kScanBigMean, else 2.
 constexpr uint32_t kScanLdsSeg = 128;
+constexpr uint32_t kScanTwoSetSeg = 256;
 constexpr uint32_t kScanBigMean = 2048;
 
 // Blocks of this launch that take work. The persistent grids of the ragged scan and the receive pass are sized for
@@ -1297,7 +1298,8 @@ __device__ __forceinline__ void pfx_runs(const uint8_t* __restrict__ base, __amd
 
 // sets (nsx_tune.segs_per_wave): 0 = by the batch's mean segment (below), 1 = runs of one set, 2 = the small-segment
 // mode (the LDS form with parked results, two waves per block), 3 = the LDS form in every wave of four per block
-// without parking (the form a wave of small segments takes in a batch of larger mean), 4 = runs of four sets.
+// without parking (the form a wave of small segments takes in a batch of larger mean), 4 = runs of four sets,
+// 5 = runs of NS sets (two in the default instantiation) in every wave.
 // run: segments per run (0 = default: 63 per boundary set, 64 per LDS run).
 // The default instantiation (NS = 2) is register-capped for 4 waves per SIMD (the default grid's 4 blocks per CU
 // must all be resident: their ranges are dealt assuming it); the forced single-set shapes are not.
@@ -1336,8 +1338,10 @@ __global__ __launch_bounds__(kBlock, NS == 2 ? 4 : 1) void csum_ragged_scan_kern
                                                     lds_scan + wave * (2u * kScanSlot / 16u), partial != nullptr, out_al);
         return;
     }
-    // The grid is sized for small segments (4 blocks/CU); a batch of large ones streams on big_keep of them.
-    const uint32_t nb = active_blocks(ofs, n, kScanBigMean, big_keep);
+    // The grid is sized for small segments (4 blocks/CU); on the default grid (big_keep ≠ 0) streamed batches take
+    // 3 of them, batches averaging ≥ kScanBigMean bytes big_keep (2).
+    const uint64_t tot = ld_off(ofs, n) - ld_off(ofs, 0);
+    const uint32_t nb = active_blocks(ofs, n, 0u, big_keep == 0 ? 0u : tot >= (uint64_t)kScanBigMean * n ? big_keep : 3u);
     if (blockIdx.x >= nb) return;
     // The wave's tasks are runs of NS sets [a_k, a_k + cnt_k) of ≤ run segments each (a_k = a + k·run), a = a0,
     // a0 + NS·run, ... < a_end; a run never crosses a_end. Byte-balanced: wave g (XCD-contiguous numbering) owns
@@ -1346,18 +1350,20 @@ __global__ __launch_bounds__(kBlock, NS == 2 ? 4 : 1) void csum_ragged_scan_kern
     const WaveRange wr = wave_range(ofs, n, wave_no(nb, kWavesPerBlock), nb * kWavesPerBlock, lane, kScanLdsSeg, 1u);
     const uint32_t a0 = wr.a0, a_end = wr.a_end;
     const uint64_t wave_bytes = wr.bytes;
-    // Two sets per run suit segments of a few hundred bytes and up (config 3). In a batch of larger mean, a wave
-    // whose own segments average under kScanLdsSeg bytes sums them out of LDS (§7 step 44); under kScanSmallSeg it
-    // takes runs of four sets, so that each run still streams tens of KB (§7 step 42).
-    // The streamed forms park their results in the wave's unused LDS slot when the launch has one (park).
+    // A wave whose own segments average under kScanLdsSeg bytes sums them out of LDS (§7 step 44); the others stream
+    // runs of two 63-segment sets under kScanTwoSetSeg, else of one (§7 step 64: with results parked, one set beat
+    // four at every mean from 160 B to 4.5 KB, by up to 9%, and two from ~400 B; two sets ran 3-5% faster at a
+    // 160 B mean). The streamed forms park their results in the wave's unused LDS slot when the launch has one.
     uint16_t* pbuf = park ? reinterpret_cast<uint16_t*>(lds_scan + wave * (kScanSlot / 16u)) : nullptr;
     if (sets == 3 || (NS == 2 && sets == 0 && wave_bytes < (uint64_t)kScanLdsSeg * (a_end - a0))) {
         ragged_runs_lds<R, VERIFY, PIPE, false>(base, ofs, n, prs, ors, oks, lds_run, a0, a_end, lane,
                                                 lds_scan + wave * (kScanSlot / 16u), partial != nullptr, out_al);
-    } else if (NS == 2 && (sets == 4 || (sets == 0 && wave_bytes < (uint64_t)kScanSmallSeg * (a_end - a0)))) {
+    } else if (NS == 2 && sets == 4) {
         ragged_runs<R, VERIFY, PIPE, 4>(base, ofs, n, prs, ors, oks, scan_run, a0, a_end, lane, pbuf, out_al);
+    } else if (NS == 2 && (sets == 5 || (sets == 0 && wave_bytes < (uint64_t)kScanTwoSetSeg * (a_end - a0)))) {
+        ragged_runs<R, VERIFY, PIPE, 2>(base, ofs, n, prs, ors, oks, scan_run, a0, a_end, lane, pbuf, out_al);
     } else {
-        ragged_runs<R, VERIFY, PIPE, NS>(base, ofs, n, prs, ors, oks, scan_run, a0, a_end, lane, pbuf, out_al);
+        ragged_runs<R, VERIFY, PIPE, 1>(base, ofs, n, prs, ors, oks, scan_run, a0, a_end, lane, pbuf, out_al);
     }
 }
 
@@ -3042,21 +3048,23 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
                           : (c.rows == 4 || c.rows == 8 || c.rows == 16 ? c.rows : 8);
     const uint32_t run = (c.run_segs >= 1 && c.run_segs <= (int)kScanRun) ? (uint32_t)c.run_segs : 0u;  // 0: default
     const uint32_t task = run ? run : kScanRun;
-    // 2 boundary sets per lane (runs of 126 segments) on the default shape: the per-run pipeline fill and drain
-    // are paid half as often (config 3 0.684 → 0.682 ms, 40-1500 B frames 0.1320 → 0.1293; 4 sets: 0.683 /
-    // 0.1308, more registers and phase-2 checks); segs_per_wave = 1 keeps one set.
+    // The default shape's kernel (NS = 2: register-capped for 4 blocks/CU) holds every form: the small-segment mode,
+    // the LDS form, and streamed runs of one set (the default since §7 step 64), two (segs_per_wave 5; the round-2
+    // default, §7 step 33) or four (4). segs_per_wave = 1 runs the uncapped single-set instantiation.
     const int ns = (pipe && rows == 2 && c.segs_per_wave != 1) ? 2 : 1;
-    // force the small-segment mode (2), the four-wave LDS form (3) or runs of four sets (4); 0: by mean segment size
-    const int sets = c.segs_per_wave >= 2 && c.segs_per_wave <= 4 ? c.segs_per_wave : 0;
-    // the LDS forms' slots (four per block; the small-segment mode gives two to each of its two waves), only when the
-    // kernel may choose an LDS form (forced streamed shapes allocate none, so more of their blocks fit a CU: 33.8 KB
-    // of LDS per block caps a launch at 4 resident blocks per CU)
-    const bool lds_form = sets == 2 || sets == 3 || (ns == 2 && sets == 0);
+    // force the small-segment mode (2), the four-wave LDS form (3), runs of four sets (4) or of two sets (5); 0: by
+    // mean segment size
+    const int sets = c.segs_per_wave >= 2 && c.segs_per_wave <= 5 ? c.segs_per_wave : 0;
+    // the LDS slots (four per block: the LDS forms' rows, the streamed forms' parked results; the small-segment mode
+    // gives two to each of its two waves) whenever the kernel may choose an LDS form, and on grids of up to 4 blocks
+    // per CU (33.8 KB of LDS per block caps a launch at 4 resident blocks per CU): forced streamed shapes above 4
+    // blocks per CU allocate none and store their results directly
+    const bool lds_form = sets == 2 || sets == 3 || (ns == 2 && sets == 0) || c.blocks_per_cu <= 4;
     const size_t lds = lds_form ? (size_t)kScanSlot * kWavesPerBlock : 0;
     // Default grid: 4 blocks/CU, of which a batch of segments averaging ≥ kScanBigMean uses 2 (active_blocks;
     // config 3 keeps its 2 blocks/CU) and a batch averaging < kScanLdsSeg two waves per block (§7 step 61). A
     // blocks_per_cu override runs exactly that grid.
-    const bool pick = c.blocks_per_cu == 0 && pipe && rows == 2 && sets == 0;
+    const bool pick = c.blocks_per_cu == 0 && pipe && rows == 2;
     const uint32_t mb = pick ? (uint32_t)c.cus * 4u : max_blocks_of(c, 2);
     const uint32_t keep = pick ? 2u : 0u;
     for (uint64_t c0 = 0; c0 < n; c0 += kRaggedChunk) {

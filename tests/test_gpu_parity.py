@@ -116,16 +116,17 @@ def test_all_launch_shapes_bit_exact():
                 assert np.array_equal(u16(out), w), (tune, L, stride, n)
 
 
-RAGGED_TUNES = [dict(kernel=k, rows=r, run_segs=rs, blocks_per_cu=b)  # pipelined (rows 2/4/8) and plain (4/8/16)
+# Launch shapes of the ragged checksum: pipelined (rows 2/4/8) and plain (4/8/16) row batches; one boundary set
+# per lane (default: two); runs of four / two sets forced (blocks_per_cu 8 allocates no LDS: results stored
+# directly, else parked); the LDS forms (2 = the small-segment mode with parked results, 3 = four waves per block).
+RAGGED_TUNES = [dict(kernel=k, rows=r, run_segs=rs, blocks_per_cu=b)
                 for k, rows in ((0, (0, 4, 8)), (nsx.KERNEL_SCAN_PLAIN, (0, 4, 16))) for r in rows
                 for rs in (0, 1, 16, 63) for b in (0, 1, 8)] + \
-               [dict(segs_per_wave=1, run_segs=rs, blocks_per_cu=b)  # one boundary set per lane (default: two)
-                for rs in (0, 1, 16, 63) for b in (0, 1, 8)] + \
-               [dict(segs_per_wave=4, run_segs=rs, blocks_per_cu=b)  # runs of four sets
-                for rs in (0, 1, 16, 63) for b in (0, 1, 8)] + \
-               [dict(segs_per_wave=sp, run_segs=rs, blocks_per_cu=b, kernel=k)  # the LDS forms: 2 = the small-segment
-                for sp in (2, 3) for rs in (0, 1, 16, 63) for b in (0, 1, 8)  # mode (parked results), 3 = four waves
-                for k in (0, nsx.KERNEL_SCAN_PLAIN)]
+               [dict(segs_per_wave=1, run_segs=rs, blocks_per_cu=b) for rs in (0, 1, 16, 63) for b in (0, 1, 8)] + \
+               [dict(segs_per_wave=sp, run_segs=rs, blocks_per_cu=b)
+                for sp in (4, 5) for rs in (0, 1, 16, 63) for b in (0, 1, 8)] + \
+               [dict(segs_per_wave=sp, run_segs=rs, blocks_per_cu=b, kernel=k)
+                for sp in (2, 3) for rs in (0, 1, 16, 63) for b in (0, 1, 8) for k in (0, nsx.KERNEL_SCAN_PLAIN)]
 
 
 def test_ragged_small_segment_bench_workload_full_size():
@@ -200,7 +201,8 @@ def test_ragged_parked_results_any_output_alignment(mix, shift):
     d, o, p = dev(buf), dev(offs.view(np.int64)), dev(part.view(np.int32))
     big = torch.empty(n + 64, dtype=torch.int16, device="cuda")
     assert big.data_ptr() % 16 == 0
-    for tune in (None, dict(segs_per_wave=2), dict(segs_per_wave=3), dict(segs_per_wave=4), dict(segs_per_wave=1)):
+    for tune in (None, dict(segs_per_wave=2), dict(segs_per_wave=3), dict(segs_per_wave=4), dict(segs_per_wave=5),
+                 dict(segs_per_wave=1), dict(segs_per_wave=5, blocks_per_cu=3), dict(segs_per_wave=5, run_segs=16)):
         for pt, w in ((None, want), (p, want_p)):
             big.fill_(0x5A5A)
             nsx.ragged_dev(d, o, partial=pt, out=big[shift:shift + n], tune=tune)
