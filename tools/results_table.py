@@ -4,7 +4,8 @@
     python tools/results_table.py r04 > /tmp/table.md
 
 One row per workload: whole-job rate, kernel mean per launch, kernel rate and roofline fraction, HBM traffic over
-the algorithmic bytes (from the line's `roofline.traffic`, i.e. the committed traffic_config<W>.json), and the CPU
+the algorithmic bytes (this round's profiles/traffic_config<W>.json if there is one, else the line's
+`roofline.traffic`), and the CPU
 baseline (the Go-faithful loop on the box's CPU share and on one thread)."""
 import glob
 import json
@@ -13,6 +14,17 @@ import re
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LABELS = {
+    "2": "2: 1M × 1500 B, IPv4 pseudo-header partials (headline)", "2n": "2: the same without partials",
+    "3": "3: 1M ragged 64-9000 B", "4": "4: 256K × 64 KiB", "5": "5: 16M × 1500 B per GPU (23.4 GiB), partials",
+    "6": "6 (f1): 1M TCP builds, 1480 B payloads", "7": "7 (f3): 64M packed 20 B IPv4 headers",
+    "8": "8 (f1): 1M builds, 12 B options", "9": "9 (f3+f2): 64M headers into a bitmask",
+    "10": "10 (rx): 1M IPv4 datagrams, 40-1500 B", "11": "11 (rx6): 1M IPv6 packets, 60-1500 B",
+    "12": "12 (f1): 256K jumbo builds, 8960 B images", "13": "13 (rx): 8M IPv4 datagrams, 40-100 B",
+    "14": "14 (rx): 2M frames, half ACK / half 1500 B", "15": "15: 8M ragged 64-128 B",
+    "16": "16 (rx6): 8M IPv6 packets, 60-120 B", "17": "17 (rx): 8M frames, 95% ACK / 5% 1500 B",
+    "18": "18 (rx): 8M IPv4 datagrams, 40-400 B",
+}
 
 
 def order(path):
@@ -33,14 +45,15 @@ def main():
         lps = rf.get("launches_per_step", 1)
         kern = f"{d['kernel_ms_mean']:.4f} ms" + (f" (× {lps} per step)" if lps and lps > 1 else "")
         tr = rf.get("traffic")
+        tf = os.path.join(ROOT, "profiles", f"traffic_config{w}{suffix}.json")
+        if os.path.exists(tf) and json.load(open(tf)).get("profile", "").startswith(f"profiles/{tag}_"):
+            tr = json.load(open(tf))["bytes_per_launch"]  # this round's PMC pass, taken after the bench line
         ratio = f"{tr / rf['alg_bytes_per_launch']:.3f}" if tr else "—"
         cb = d.get("cpu_baseline") or {}
         cpu = f"{cb['value']:.1f} GiB/s" if cb.get("value") else "—"
         st = (cb.get("single_thread") or {}).get("value")
         cpu1 = f"{st:.2f} GiB/s" if st else "—"
-        name = d["config"]["workload"].split(":")[0]
-        label = f"{w}{' (no partials)' if suffix else ''}: {d['config']['workload'].split(':', 1)[1].split(',')[0].strip()}" \
-            if ":" in d["config"]["workload"] else name
+        label = LABELS.get(f"{w}{suffix}", d["config"]["workload"].split(",")[0])
         print(f"| {label} | {d['value']:.0f} GiB/s | {kern} | {rf['achieved'] / 1000:.2f} TB/s | **{rf['frac']:.3f}** "
               f"| {ratio} | {cpu} | {cpu1} |")
 
