@@ -327,11 +327,12 @@ def device_fields(idents: list) -> dict:
 
 def per_gpu_entries(rank_stats, *, steps, bytes_per_rank_step, alg_bytes_per_launch, launches=1) -> list:
     """Each rank's own rate from its own clock (rank_stats: every rank's {rank, device, wall_s, step_ms}, rank
-    order): bytes ÷ its timed wall, its kernel mean per launch and that launch's roofline fraction."""
+    order): bytes ÷ its timed wall, its kernel mean per launch (a step of `launches` launches, as config 5's
+    windows, split evenly) and that launch's roofline fraction (alg_bytes_per_launch: one launch's bytes)."""
     out = []
     for r in rank_stats:
         k_ms = None if r.get("step_ms") is None else r["step_ms"] / launches
-        frac = None if not k_ms else alg_bytes_per_launch / launches / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS
+        frac = None if not k_ms else alg_bytes_per_launch / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS
         out.append({"rank": r["rank"], "device": r.get("device"),
                     "gib_s": round(bytes_per_rank_step * steps / r["wall_s"] / GIB, 3),
                     "wall_s": round(r["wall_s"], 6), "kernel_ms": None if k_ms is None else round(k_ms, 5),

@@ -59,6 +59,19 @@ def test_per_gpu_entries_show_a_slow_gpu():
     assert line["value"] == pytest.approx(32.0)  # 4 GiB x 10 steps / the slowest rank's 1.25 s
 
 
+def test_per_gpu_roofline_of_a_windowed_step_matches_the_line():
+    """Config 5's steps are 16 back-to-back launches: each rank's roofline fraction is per launch, like the line's
+    (round 4's first 2-rank rehearsal printed the line's fraction divided by 16 again)."""
+    stats = [{"rank": r, "device": f"h/{r}", "wall_s": 0.036, "step_ms": 3.2} for r in range(2)]
+    line = bench.result_line(world=2, steps=10, warmup=1, wall_max=0.036, bytes_per_rank_step=16 * 1500,
+                             units_total=32, workload="w", cfg={"n": 16, "seed": 1}, launch_ms=[3.2],
+                             alg_bytes_per_launch=16 * 1600, cpu_baseline=None, traffic=None, launches=16,
+                             rank_stats=stats)
+    for p in line["per_gpu"]:
+        assert p["kernel_ms"] == pytest.approx(0.2)
+        assert p["roofline_frac"] == pytest.approx(line["roofline"]["frac"], abs=1e-4)
+
+
 def test_device_fields_count_distinct_gpus():
     """a SCALE reader must see from the line alone how many physical GPUs the ranks ran on."""
     a = {"host": "h", "local_device": 0, "pci": "0000:05:00", "uuid": "u0", "key": "h/0000:05:00/u0"}
