@@ -1809,8 +1809,8 @@ __device__ __forceinline__ void rx_runs_lds(const uint8_t* __restrict__ base, __
 // The streaming threshold depends on the batch's frame count as well as its mean (DESIGN.md §7 step 63,
 // profiles/r04_rx_form_sweep.txt: n 1M-8M × means 200-900 B): in batches of up to 2M frames streamed runs win from
 // a 500 B mean (by 2-6% at 500-900 B) and lose by 1-23% at 200-400 B; from 3M frames the prefix form wins up to
-// a 750 B mean (by 1-3%), streamed runs from 800 B. The prefix form's time has a fixed part (~5-9 µs; its wave
-// ranges are equal-count, so their byte imbalance shrinks as the runs per wave grow) that large batches amortise.
+// a 750 B mean (by 1-3%), streamed runs from 800 B. Fitted per batch size, the prefix form's time has a fixed
+// part of ~5-9 µs that large batches amortise (its source is not isolated); the streamed runs' rate is flat in n.
 constexpr uint32_t kRxPfxMean = 112;
 constexpr uint32_t kRxStreamMeanSmallN = 448;      // the streaming threshold below kRxStreamBigN frames
 constexpr uint32_t kRxStreamMeanBigN = 768;        // ... and from kRxStreamBigN frames
