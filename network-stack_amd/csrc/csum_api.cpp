@@ -179,6 +179,7 @@ int nsx_csum_ragged_dev_tuned(const void* d_base, const uint64_t* d_offsets, uin
     if (n == 0) return NSX_OK;
     if (!d_out || !d_offsets || !d_base) return NSX_EINVAL;
     if (n > ((uint64_t)1 << 40)) return NSX_EINVAL;
+    if (!nsx::ragged_tune_valid(nsx::launch_cfg(1, tune))) return NSX_EINVAL;
     const int dev = current_device();
     if (dev < 0) return NSX_ENODEV;
     return map_err(nsx::launch_ragged(make_cfg(dev, tune), d_base, d_offsets, n, d_prefix_partial, d_out, nullptr,
@@ -197,6 +198,7 @@ int nsx_verify_ragged_dev_tuned(const void* d_base, const uint64_t* d_offsets, u
     if (n == 0) return NSX_OK;
     if (!d_ok || !d_offsets || !d_base) return NSX_EINVAL;
     if (n > ((uint64_t)1 << 40)) return NSX_EINVAL;
+    if (!nsx::ragged_tune_valid(nsx::launch_cfg(1, tune))) return NSX_EINVAL;
     const int dev = current_device();
     if (dev < 0) return NSX_ENODEV;
     return map_err(nsx::launch_ragged(make_cfg(dev, tune), d_base, d_offsets, n, d_prefix_partial, d_raw, d_ok,

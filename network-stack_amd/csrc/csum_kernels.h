@@ -40,6 +40,7 @@ hipError_t launch_ragged(const LaunchCfg& c, const void* d_base, const uint64_t*
 // TCP checksum) per frame into a validity bitmask (ceil(n/64) words); ip_raw (IPv4 only) / tcp_raw nullable.
 // false for overrides that name no shape of the receive kernels (segs_per_wave 5-7 off the default grid): NSX_EINVAL
 bool rx_tune_valid(const LaunchCfg& c);
+bool ragged_tune_valid(const LaunchCfg& c);
 hipError_t launch_rx_tcp(const LaunchCfg& c, int ipver, const void* d_base, const uint64_t* d_offsets, uint64_t n,
                          uint64_t* mask, uint16_t* ip_raw, uint16_t* tcp_raw, hipStream_t st);
 hipError_t launch_pseudo_ipv4(const uint8_t* src, const uint8_t* dst, const uint32_t* len, uint8_t proto,

@@ -1298,8 +1298,9 @@ __device__ __forceinline__ void pfx_runs(const uint8_t* __restrict__ base, __amd
 
 // sets (nsx_tune.segs_per_wave): 0 = by the batch's mean segment (below), 1 = runs of one set, 2 = the small-segment
 // mode (the LDS form with parked results, two waves per block), 3 = the LDS form in every wave of four per block
-// without parking (the form a wave of small segments takes in a batch of larger mean), 4 = runs of four sets,
-// 5 = runs of NS sets (two in the default instantiation) in every wave.
+// without parking (the form a wave of small segments takes in a batch of larger mean), 5 = runs of NS sets (two in
+// the default instantiation) in every wave. (Runs of four sets, round 2's form for small segments, §7 step 42, lost
+// to one or two sets once results were parked, §7 step 64, and were removed.)
 // run: segments per run (0 = default: 63 per boundary set, 64 per LDS run).
 // The default instantiation (NS = 2) is register-capped for 4 waves per SIMD (the default grid's 4 blocks per CU
 // must all be resident: their ranges are dealt assuming it); the forced single-set shapes are not.
@@ -1358,8 +1359,6 @@ __global__ __launch_bounds__(kBlock, NS == 2 ? 4 : 1) void csum_ragged_scan_kern
     if (sets == 3 || (NS == 2 && sets == 0 && wave_bytes < (uint64_t)kScanLdsSeg * (a_end - a0))) {
         ragged_runs_lds<R, VERIFY, PIPE, false>(base, ofs, n, prs, ors, oks, lds_run, a0, a_end, lane,
                                                 lds_scan + wave * (kScanSlot / 16u), partial != nullptr, out_al);
-    } else if (NS == 2 && sets == 4) {
-        ragged_runs<R, VERIFY, PIPE, 4>(base, ofs, n, prs, ors, oks, scan_run, a0, a_end, lane, pbuf, out_al);
     } else if (NS == 2 && (sets == 5 || (sets == 0 && wave_bytes < (uint64_t)kScanTwoSetSeg * (a_end - a0)))) {
         ragged_runs<R, VERIFY, PIPE, 2>(base, ofs, n, prs, ors, oks, scan_run, a0, a_end, lane, pbuf, out_al);
     } else {
@@ -3049,12 +3048,12 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
     const uint32_t run = (c.run_segs >= 1 && c.run_segs <= (int)kScanRun) ? (uint32_t)c.run_segs : 0u;  // 0: default
     const uint32_t task = run ? run : kScanRun;
     // The default shape's kernel (NS = 2: register-capped for 4 blocks/CU) holds every form: the small-segment mode,
-    // the LDS form, and streamed runs of one set (the default since §7 step 64), two (segs_per_wave 5; the round-2
-    // default, §7 step 33) or four (4). segs_per_wave = 1 runs the uncapped single-set instantiation.
+    // the LDS form, and streamed runs of one set (the default since §7 step 64) or two (segs_per_wave 5; the round-2
+    // default, §7 step 33). segs_per_wave = 1 runs the uncapped single-set instantiation.
     const int ns = (pipe && rows == 2 && c.segs_per_wave != 1) ? 2 : 1;
-    // force the small-segment mode (2), the four-wave LDS form (3), runs of four sets (4) or of two sets (5); 0: by
-    // mean segment size
-    const int sets = c.segs_per_wave >= 2 && c.segs_per_wave <= 5 ? c.segs_per_wave : 0;
+    // force the small-segment mode (2), the four-wave LDS form (3) or runs of two sets (5); 0: by mean segment size
+    // (ragged_tune_valid rejects any other value but 1)
+    const int sets = c.segs_per_wave == 2 || c.segs_per_wave == 3 || c.segs_per_wave == 5 ? c.segs_per_wave : 0;
     // the LDS slots (four per block: the LDS forms' rows, the streamed forms' parked results; the small-segment mode
     // gives two to each of its two waves) whenever the kernel may choose an LDS form, and on grids of up to 4 blocks
     // per CU (33.8 KB of LDS per block caps a launch at 4 resident blocks per CU): forced streamed shapes above 4
@@ -3089,6 +3088,7 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
 
 hipError_t launch_ragged(const LaunchCfg& c, const void* d_base, const uint64_t* d_offsets, uint64_t n,
                          const uint32_t* partial, uint16_t* out, uint8_t* ok, hipStream_t st) {
+    if (!ragged_tune_valid(c)) return hipErrorInvalidValue;
     const uint8_t* base = static_cast<const uint8_t*>(d_base);
     if (use_block_mode(c, n)) {  // few segments: a block per segment
         const uint32_t grid = (uint32_t)std::min<uint64_t>(n, max_blocks_of(c, 8));
@@ -3102,6 +3102,13 @@ hipError_t launch_ragged(const LaunchCfg& c, const void* d_base, const uint64_t*
     }
     if (ok) return launch_ragged_scan<true>(c, base, d_offsets, n, partial, out, ok, st);
     return launch_ragged_scan<false>(c, base, d_offsets, n, partial, out, nullptr, st);
+}
+
+bool ragged_tune_valid(const LaunchCfg& c) {
+    // segs_per_wave: 0 auto, 1 the single-set kernel, 2 / 3 / 5 forced forms (4, runs of four sets, was removed in
+    // round 4: NSX_EINVAL rather than silently running another form)
+    const int s = c.segs_per_wave;
+    return s == 0 || s == 1 || s == 2 || s == 3 || s == 5;
 }
 
 bool rx_tune_valid(const LaunchCfg& c) {

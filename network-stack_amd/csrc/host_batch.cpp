@@ -374,6 +374,7 @@ int nsx_csum_ragged_host_tuned(const uint8_t* h_base, const uint64_t* h_offsets,
                                const nsx_tune* tune) {
     if (n == 0) return NSX_OK;
     if (!h_out || !h_offsets || !h_base) return NSX_EINVAL;
+    if (!nsx::ragged_tune_valid(nsx::launch_cfg(1, tune))) return NSX_EINVAL;
     for (uint64_t i = 0; i < n; ++i)
         if (h_offsets[i + 1] < h_offsets[i]) return NSX_EINVAL;
     return run_sharded(h_base, 0, 0, h_offsets, n, h_prefix_partial, h_out, nullptr, 0, num_gpus, tune);

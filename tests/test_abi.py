@@ -335,6 +335,18 @@ def test_tcp_wire_len_and_layout_match_reference_bytes():
     assert np.array_equal(out_off, want)
 
 
+def test_ragged_segs_per_wave_outside_its_forms_is_einval():
+    """Ragged checksum tunes: segs_per_wave 0 / 1 / 2 / 3 / 5 name its forms; 4 (runs of four sets, removed in round
+    4) and any other value are refused with NSX_EINVAL before a device is touched (host entry
+    point), instead of silently running the automatic form."""
+    offs = np.array([0, 40, 100], np.uint64)
+    buf = np.zeros(100, np.uint8)
+    for bad in (4, 6, 8, -1):
+        with pytest.raises(nsx.NsxError) as e:
+            nsx.ragged_host(buf, offs, tune=dict(segs_per_wave=bad))
+        assert e.value.code == nsx.NSX_EINVAL, bad
+
+
 def test_receive_grid_modes_off_the_default_grid_are_einval():
     """segs_per_wave 5 / 6 / 7 force a mode of the receive pass's default grid; with rows 4-16 or
     blocks_per_cu set they name no shape and are refused (NSX_EINVAL) instead of silently running the auto shape.

@@ -117,14 +117,13 @@ def test_all_launch_shapes_bit_exact():
 
 
 # Launch shapes of the ragged checksum: pipelined (rows 2/4/8) and plain (4/8/16) row batches; one boundary set
-# per lane (default: two); runs of four / two sets forced (blocks_per_cu 8 allocates no LDS: results stored
-# directly, else parked); the LDS forms (2 = the small-segment mode with parked results, 3 = four waves per block).
+# per lane; runs of two sets forced (blocks_per_cu 8 allocates no LDS: results stored directly, else parked); the
+# LDS forms (2 = the small-segment mode with parked results, 3 = four waves per block).
 RAGGED_TUNES = [dict(kernel=k, rows=r, run_segs=rs, blocks_per_cu=b)
                 for k, rows in ((0, (0, 4, 8)), (nsx.KERNEL_SCAN_PLAIN, (0, 4, 16))) for r in rows
                 for rs in (0, 1, 16, 63) for b in (0, 1, 8)] + \
                [dict(segs_per_wave=1, run_segs=rs, blocks_per_cu=b) for rs in (0, 1, 16, 63) for b in (0, 1, 8)] + \
-               [dict(segs_per_wave=sp, run_segs=rs, blocks_per_cu=b)
-                for sp in (4, 5) for rs in (0, 1, 16, 63) for b in (0, 1, 8)] + \
+               [dict(segs_per_wave=5, run_segs=rs, blocks_per_cu=b) for rs in (0, 1, 16, 63) for b in (0, 1, 8)] + \
                [dict(segs_per_wave=sp, run_segs=rs, blocks_per_cu=b, kernel=k)
                 for sp in (2, 3) for rs in (0, 1, 16, 63) for b in (0, 1, 8) for k in (0, nsx.KERNEL_SCAN_PLAIN)]
 
@@ -137,7 +136,7 @@ def test_ragged_small_segment_bench_workload_full_size():
     cfg = bench.WORKLOADS[15]
     w = bench.build_workload(cfg, 0, torch.device("cuda", 0))
     want = O.c_batch(host(w["buf"]), cfg["n"], offsets=w["offsets"], threads=16)
-    for tune in (None, dict(segs_per_wave=3), dict(segs_per_wave=4), dict(segs_per_wave=1)):
+    for tune in (None, dict(segs_per_wave=3), dict(segs_per_wave=5), dict(segs_per_wave=1)):
         w["out"].zero_()
         w["step_for"](tune)()
         assert np.array_equal(u16(w["out"]), want), tune
@@ -148,13 +147,13 @@ def test_ragged_small_segment_bench_workload_full_size():
 
 
 @pytest.mark.parametrize("n", [1, 126, 252, 253, 30_001, 400_003])
-def test_ragged_small_segments_runs_of_four_sets(n):
-    """Segments of 0-200 B (mean ~100): waves whose segments average under 256 B take the LDS form (DESIGN.md §7
-    step 44); it, the streamed runs of one and of four 63-segment sets (§7 step 42) and the automatic choice equal
-    the oracle, with and without partials.
+def test_ragged_small_segments_every_form(n):
+    """Segments of 0-200 B (mean ~100): the small-segment mode (2), the four-wave LDS form (3), the streamed runs
+    of one and of two 63-segment sets (1, 5) and the automatic choice equal the oracle, with
+    and without partials.
     block_mode=1 keeps even the smallest batches on the scan kernel, and short runs (run_segs 1, 16) at one block
-    per CU make every wave stream many runs, so all four sets, partial last sets and set-to-set frame ends run
-    (ADVICE r2); n = 400K reaches the four sets with the default run length too."""
+    per CU make every wave stream many runs, so both sets, partial last sets and set-to-set frame ends run
+    (ADVICE r2)."""
     rng = np.random.default_rng(n + 42)
     lens = rng.integers(0, 201, n).astype(np.uint64)
     offs = np.zeros(n + 1, np.uint64)
@@ -165,9 +164,9 @@ def test_ragged_small_segments_runs_of_four_sets(n):
     want = O.c_batch(buf, n, offsets=offs, threads=16)
     want_p = O.c_batch(buf, n, offsets=offs, partial=part, threads=16)
     d, o, p = dev(buf), dev(offs.view(np.int64)), dev(part.view(np.int32))
-    tunes = [None, dict(segs_per_wave=1), dict(segs_per_wave=4), dict(segs_per_wave=2), dict(segs_per_wave=3)]
+    tunes = [None, dict(segs_per_wave=1), dict(segs_per_wave=5), dict(segs_per_wave=2), dict(segs_per_wave=3)]
     tunes += [dict(block_mode=1, blocks_per_cu=1, run_segs=rs, **sp)
-              for rs in (0, 1, 16) for sp in ({}, dict(segs_per_wave=1), dict(segs_per_wave=4), dict(segs_per_wave=2),
+              for rs in (0, 1, 16) for sp in ({}, dict(segs_per_wave=1), dict(segs_per_wave=5), dict(segs_per_wave=2),
                                               dict(segs_per_wave=3))]
     for tune in tunes:
         out = torch.empty(n, dtype=torch.int16, device="cuda")
@@ -183,7 +182,7 @@ def test_ragged_parked_results_any_output_alignment(mix, shift):
     """Parked results (ResultPark) go out in 16 B blocks aligned to the output buffer, with
     the partial blocks at either end of a flush written result by result: outputs starting 0-7 results past a
     16 B boundary, inside a sentinel-filled buffer, receive exactly the oracle's sums and nothing outside them is
-    written. Mixes: 64-128 B (the small-segment mode), 0-400 B (streamed runs of four sets), and segments of
+    written. Mixes: 64-128 B (the small-segment mode), 0-400 B (streamed runs of one and two sets), and segments of
     0-200 B with scattered 20-60 KB ones (LDS runs interrupted by streamed ones: flushes mid-range)."""
     rng = np.random.default_rng(900 + shift)
     n = 300_003
@@ -201,7 +200,7 @@ def test_ragged_parked_results_any_output_alignment(mix, shift):
     d, o, p = dev(buf), dev(offs.view(np.int64)), dev(part.view(np.int32))
     big = torch.empty(n + 64, dtype=torch.int16, device="cuda")
     assert big.data_ptr() % 16 == 0
-    for tune in (None, dict(segs_per_wave=2), dict(segs_per_wave=3), dict(segs_per_wave=4), dict(segs_per_wave=5),
+    for tune in (None, dict(segs_per_wave=2), dict(segs_per_wave=3), dict(segs_per_wave=5),
                  dict(segs_per_wave=1), dict(segs_per_wave=5, blocks_per_cu=3), dict(segs_per_wave=5, run_segs=16)):
         for pt, w in ((None, want), (p, want_p)):
             big.fill_(0x5A5A)

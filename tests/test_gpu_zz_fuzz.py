@@ -27,7 +27,7 @@ RAGGED_KNOBS = [dict(), dict(rows=4), dict(rows=8), dict(run_segs=1), dict(run_s
                 dict(kernel=nsx.KERNEL_SCAN_PLAIN, rows=16, run_segs=5), dict(segs_per_wave=1),
                 dict(segs_per_wave=1, run_segs=7), dict(segs_per_wave=2), dict(segs_per_wave=2, run_segs=9), dict(segs_per_wave=3),
                 dict(segs_per_wave=3, run_segs=5),
-                dict(segs_per_wave=4, blocks_per_cu=1), dict(segs_per_wave=4), dict(segs_per_wave=5),
+                dict(segs_per_wave=5, blocks_per_cu=1), dict(segs_per_wave=5),
                 dict(segs_per_wave=5, run_segs=11, blocks_per_cu=2)]
 
 
