@@ -44,9 +44,10 @@ typedef struct nsx_tune {
                                   < 256 B, else of one, on 3 blocks/CU, 2 from a 2048 B mean), 1 = runs
                                   of one set on the uncapped single-set kernel, 2 = the small-segment mode,
                                   3 = the LDS form in every wave (four per block, results stored per run),
-                                  4 / 5 = runs of four / two sets in every wave. Only the default pipelined
-                                  2-row shape has more than one set: with kernel = SCAN_PLAIN or rows != 2
-                                  a 4 or 5 gives runs of one set. Grids of <= 4 blocks/CU park the streamed
+                                  5 = runs of two sets in every wave; any other value is NSX_EINVAL (4,
+                                  runs of four sets, was removed in round 4). Only the default pipelined
+                                  2-row shape has two sets: with kernel = SCAN_PLAIN or rows != 2 a 5
+                                  gives runs of one set. Grids of <= 4 blocks/CU park the streamed
                                   forms' results in LDS and write them 8 KiB at a time.
                                   Receive kernels: 0 auto = the default grid (4 blocks/CU) choosing by the
                                   batch's mean frame and frame count: < 112 B the LDS form for whole runs
