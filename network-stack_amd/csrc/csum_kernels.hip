@@ -804,9 +804,12 @@ __device__ __forceinline__ void park_flush(ResultPark& pk, __amdgpu_buffer_rsrc_
         __builtin_amdgcn_raw_buffer_store_b128(v4u{v.x, v.y, v.z, v.w}, ors, full ? (pk.base + 8u * blk) * 2u : kOOB,
                                                0, 0);
     }
-    // the results of a partial first / last block, one lane each (lanes 0-7: block b0, 8-15: block b1 − 1)
+    // the results of a partial first / last block, one lane each (lanes 0-7: block b0, 8-15: block b1 − 1 when it
+    // is another block; a block is partial when [l, h) does not cover it, as the full-block test above)
+    const bool one = b1 - 1u == b0;
+    const bool part0 = !head_full || (one && !tail_full), part1 = !one && !tail_full;
     const uint32_t i = (lane < 8u ? 8u * b0 : 8u * (b1 - 1u)) + (lane & 7u);
-    const bool st = lane < 16u && (lane < 8u ? !head_full : !tail_full) && i >= l && i < h;
+    const bool st = lane < 16u && (lane < 8u ? part0 : part1) && i >= l && i < h;
     const uint16_t r = pk.buf[st ? i : 0u];
     __builtin_amdgcn_raw_buffer_store_b16(r, ors, st ? (pk.base + i) * 2u : kOOB, 0, 0);
     __builtin_amdgcn_wave_barrier();
