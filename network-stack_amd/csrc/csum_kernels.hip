@@ -766,79 +766,110 @@ __device__ __forceinline__ uint32_t active_blocks(__amdgpu_buffer_rsrc_t ofs, ui
     return k ? k : nb;
 }
 
-// Results parked in LDS and written in bulk. A 2-byte raw sum per segment is a small write
-// stream beside a large read stream, and written as it is produced (128 B per wave and run) it cost far more than
-// its bytes: 12-14% of the small-segment LDS form's time, 5-16% of the streamed form's with frames of 160-620 B
-// (profiles/r04_ragged_park_*, r04_rawstream_ab.txt). Parked, a wave's results go out up to 8 KiB at a time, 16 B
-// per lane and store. buf[i] holds the result of segment base + i, base chosen so that out + base is 16 B aligned
-// (al = the output's misalignment in results; base may wrap below 0: only differences of indices are compared);
-// [lo, hi) is parked. A wave parks in increasing segment order and flushes when the next set is not contiguous
-// or would not fit, and at its end. Off (buf null): stored directly.
-constexpr uint32_t kParkCap = 4096;  // results per park buffer: 8 KiB of a wave's 8.25 KiB LDS slot
+// Results parked in LDS and written in bulk. A 2-byte raw sum (or a 1-byte verdict)
+// per segment is a small write stream beside a large read stream, and written as it is produced (128 B per wave and
+// run) it cost far more than its bytes: 12-14% of the small-segment LDS form's time, 5-16% of the streamed form's
+// with frames of 160-620 B (profiles/r04_ragged_park_*, r04_rawstream_ab.txt). Parked, a wave's results go out up to
+// 8 KiB at a time, 16 B per lane and store. T = the result type (uint16_t raw sums, uint8_t verdicts of the batch
+// verify); buf[i] holds the result of segment base + i, base chosen so that out + base is 16 B aligned (al = the
+// output's misalignment in results; base may wrap below 0: only differences of indices are compared); [lo, hi) is
+// parked. A wave parks in increasing segment order and flushes when the next set is not contiguous or would not
+// fit, and at its end. Off (buf null): stored directly.
+template <typename T>
 struct ResultPark {
-    uint16_t* buf;
+    static constexpr uint32_t kPer = 16u / sizeof(T);    // results per 16 B block
+    static constexpr uint32_t kCap = 8192u / sizeof(T);  // results per buffer: 8 KiB of a wave's 8.25 KiB LDS slot
+    T* buf;
+    __amdgpu_buffer_rsrc_t rs;  // the output
     uint32_t al, base, lo, hi;
     __device__ __forceinline__ void rebase(uint32_t a) {
-        base = ((a + al) & ~7u) - al;
+        base = ((a + al) & ~(kPer - 1u)) - al;
         lo = hi = a;
     }
 };
 
-__device__ __forceinline__ ResultPark make_park(uint16_t* buf, uint32_t out_al, uint32_t a0) {
-    ResultPark pk{buf, out_al, 0, 0, 0};
+template <typename T>
+__device__ __forceinline__ ResultPark<T> make_park(T* buf, __amdgpu_buffer_rsrc_t rs, const void* out, uint32_t a0) {
+    ResultPark<T> pk{buf, rs, (uint32_t)((uintptr_t)out / sizeof(T)) & (ResultPark<T>::kPer - 1u), 0, 0, 0};
     pk.rebase(a0);
     return pk;
 }
 
-__device__ __forceinline__ void park_flush(ResultPark& pk, __amdgpu_buffer_rsrc_t ors, uint32_t lane) {
+template <typename T>
+__device__ __forceinline__ void store_result(T v, __amdgpu_buffer_rsrc_t rs, uint32_t off) {
+    if constexpr (sizeof(T) == 2) __builtin_amdgcn_raw_buffer_store_b16(v, rs, off, 0, 0);
+    else __builtin_amdgcn_raw_buffer_store_b8(v, rs, off, 0, 0);
+}
+
+template <typename T>
+__device__ __forceinline__ void park_flush(ResultPark<T>& pk, uint32_t lane) {
+    constexpr uint32_t P = ResultPark<T>::kPer, C = ResultPark<T>::kCap;
     if (!pk.buf || pk.hi == pk.lo) return;
     __builtin_amdgcn_wave_barrier();
     typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-    const uint32_t l = pk.lo - pk.base, h = pk.hi - pk.base;  // parked: buf[l, h), 0 ≤ l < h ≤ kParkCap
-    const uint32_t b0 = l / 8u, b1 = (h + 7u) / 8u;             // the 8-result blocks touched
-    const bool head_full = 8u * b0 == l, tail_full = 8u * b1 == h;
+    const uint32_t l = pk.lo - pk.base, h = pk.hi - pk.base;  // parked: buf[l, h), 0 ≤ l < h ≤ C
+    const uint32_t b0 = l / P, b1 = (h + P - 1u) / P;           // the 16 B blocks touched
+    const bool head_full = P * b0 == l, tail_full = P * b1 == h;
     for (uint32_t q = b0; q < b1; q += kWave) {  // whole blocks: one 16 B store each
         const uint32_t blk = q + lane;
         const bool full = blk < b1 && (blk != b0 || head_full) && (blk != b1 - 1u || tail_full);
-        const lds16 v = reinterpret_cast<const lds16*>(pk.buf)[blk < kParkCap / 8u ? blk : 0u];
-        __builtin_amdgcn_raw_buffer_store_b128(v4u{v.x, v.y, v.z, v.w}, ors, full ? (pk.base + 8u * blk) * 2u : kOOB,
-                                               0, 0);
+        const lds16 v = reinterpret_cast<const lds16*>(pk.buf)[blk < C / P ? blk : 0u];
+        __builtin_amdgcn_raw_buffer_store_b128(v4u{v.x, v.y, v.z, v.w}, pk.rs,
+                                               full ? (pk.base + P * blk) * (uint32_t)sizeof(T) : kOOB, 0, 0);
     }
-    // the results of a partial first / last block, one lane each (lanes 0-7: block b0, 8-15: block b1 − 1 when it
-    // is another block; a block is partial when [l, h) does not cover it, as the full-block test above)
+    // the results of a partial first / last block, one lane each (lanes 0..P-1: block b0, P..2P-1: block b1 − 1
+    // when it is another block; a block is partial when [l, h) does not cover it, as the full-block test above)
     const bool one = b1 - 1u == b0;
     const bool part0 = !head_full || (one && !tail_full), part1 = !one && !tail_full;
-    const uint32_t i = (lane < 8u ? 8u * b0 : 8u * (b1 - 1u)) + (lane & 7u);
-    const bool st = lane < 16u && (lane < 8u ? part0 : part1) && i >= l && i < h;
-    const uint16_t r = pk.buf[st ? i : 0u];
-    __builtin_amdgcn_raw_buffer_store_b16(r, ors, st ? (pk.base + i) * 2u : kOOB, 0, 0);
+    const uint32_t i = (lane < P ? P * b0 : P * (b1 - 1u)) + (lane & (P - 1u));
+    const bool st = lane < 2u * P && (lane < P ? part0 : part1) && i >= l && i < h;
+    const T r = pk.buf[st ? i : 0u];
+    store_result<T>(r, pk.rs, st ? (pk.base + i) * (uint32_t)sizeof(T) : kOOB);
     __builtin_amdgcn_wave_barrier();
     pk.rebase(pk.hi);
 }
 
 // Segment a + lane's result (lanes < cnt): parked, or stored directly when parking is off.
-__device__ __forceinline__ void park_put(ResultPark& pk, __amdgpu_buffer_rsrc_t ors, uint32_t a, uint32_t cnt,
-                                         uint32_t lane, uint32_t res) {
+template <typename T>
+__device__ __forceinline__ void park_put(ResultPark<T>& pk, uint32_t a, uint32_t cnt, uint32_t lane, uint32_t res) {
     if (!pk.buf) {
-        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, lane < cnt ? (a + lane) * 2u : kOOB, 0, 0);
+        store_result<T>((T)res, pk.rs, lane < cnt ? (a + lane) * (uint32_t)sizeof(T) : kOOB);
         return;
     }
-    if (pk.hi != a || a + cnt - pk.base > kParkCap) {  // not contiguous, or would overflow: flush, rebase at a
-        park_flush(pk, ors, lane);
+    if (pk.hi != a || a + cnt - pk.base > ResultPark<T>::kCap) {  // not contiguous, or would overflow: flush, rebase
+        park_flush(pk, lane);
         pk.rebase(a);
     }
-    if (lane < cnt) pk.buf[a + lane - pk.base] = (uint16_t)res;
+    if (lane < cnt) pk.buf[a + lane - pk.base] = (T)res;
     pk.hi = a + cnt;
+}
+
+// The outputs of segments [a, a + cnt) (lane l: segment a + l): the raw sum parked (checksum), or — the batch verify
+// (VERIFY) — the 1-byte verdict parked and the raw sum, when asked for (raw), stored directly.
+template <bool VERIFY>
+using ScanPark = ResultPark<typename std::conditional<VERIFY, uint8_t, uint16_t>::type>;
+
+template <bool VERIFY>
+__device__ __forceinline__ void put_results(ScanPark<VERIFY>& pk, __amdgpu_buffer_rsrc_t ors, bool raw, uint32_t a,
+                                            uint32_t cnt, uint32_t lane, uint32_t res) {
+    if constexpr (VERIFY) {
+        if (raw) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)res, ors, lane < cnt ? (a + lane) * 2u : kOOB, 0, 0);
+        if (cnt) park_put(pk, a, cnt, lane, res == 0xFFFFu ? 1u : 0u);
+    } else {
+        (void)ors;
+        (void)raw;
+        if (cnt) park_put(pk, a, cnt, lane, res);
+    }
 }
 
 // One run of NS sets of ≤ run segments in the streaming form: set k = segments [a + k·run, + cnt[k]), lane l ≤
 // cnt[k] holds boundary my_off[k] = offsets[a + k·run + l] and (l < cnt[k]) the partial my_part[k]. Results into
-// the wave's park (ResultPark).
+// the wave's park (put_results).
 template <int R, bool VERIFY, bool PIPE, int NS>
 __device__ __forceinline__ void ragged_run_stream(const uint8_t* __restrict__ base, uint32_t a, uint32_t run,
                                                   const uint32_t (&cnt)[NS], const uint64_t (&my_off)[NS],
                                                   const uint32_t (&my_part)[NS], __amdgpu_buffer_rsrc_t ors,
-                                                  __amdgpu_buffer_rsrc_t oks, uint32_t lane, ResultPark& pk) {
+                                                  bool raw, uint32_t lane, ScanPark<VERIFY>& pk) {
     int64_t brel[NS];
     uint64_t bval[NS];
     // the run's last boundary: set kl = the last set with segments, its lane cnt
@@ -870,11 +901,7 @@ __device__ __forceinline__ void ragged_run_stream(const uint8_t* __restrict__ ba
         const uint32_t le = fold32((uint32_t)(d & 0xFFFFFFFFu)) + fold32((uint32_t)(d >> 32));
         const bool even = (((uintptr_t)base + my_off[k]) & 1u) == 0;
         const uint32_t res = finish(le, even, my_part[k]);
-        const bool mine = lane < cnt[k];
-        const uint32_t ak = a + k * run;
-        if (cnt[k]) park_put(pk, ors, ak, cnt[k], lane, res);
-        if constexpr (VERIFY)
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(res == 0xFFFFu), oks, mine ? ak + lane : kOOB, 0, 0);
+        put_results<VERIFY>(pk, ors, raw, a + k * run, cnt[k], lane, res);
     }
 }
 
@@ -883,8 +910,9 @@ template <int R, bool VERIFY, bool PIPE, int NS>
 __device__ __forceinline__ void ragged_runs(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
                                             __amdgpu_buffer_rsrc_t prs, __amdgpu_buffer_rsrc_t ors,
                                             __amdgpu_buffer_rsrc_t oks, uint32_t run, uint32_t a0, uint32_t a_end,
-                                            uint32_t lane, uint16_t* park_buf, uint32_t out_al) {
-    ResultPark pk = make_park(park_buf, out_al, a0);
+                                            uint32_t lane, void* park_buf, const void* out, bool raw) {
+    using T = typename std::conditional<VERIFY, uint8_t, uint16_t>::type;
+    ScanPark<VERIFY> pk = make_park<T>(static_cast<T*>(park_buf), VERIFY ? oks : ors, out, a0);
     typedef uint32_t v2u __attribute__((ext_vector_type(2)));
     const uint32_t a_step = run * NS;
     auto load_offs = [&](uint32_t a) -> uint64_t {  // lane l ≤ run length: offsets[a + l]
@@ -906,9 +934,9 @@ __device__ __forceinline__ void ragged_runs(const uint8_t* __restrict__ base, __
             nxt_off[k] = load_offs(a + a_step + k * run);
             my_part[k] = __builtin_amdgcn_raw_buffer_load_b32(prs, lane < cnt[k] ? (ak + lane) * 4 : kOOB, 0, 0);
         }
-        ragged_run_stream<R, VERIFY, PIPE, NS>(base, a, run, cnt, my_off, my_part, ors, oks, lane, pk);
+        ragged_run_stream<R, VERIFY, PIPE, NS>(base, a, run, cnt, my_off, my_part, ors, raw, lane, pk);
     }
-    park_flush(pk, ors, lane);
+    park_flush(pk, lane);
 }
 
 // Sum of the bytes [p, e) of a wave's LDS slot for the lanes' consecutive ranges of one run (p, e slot positions;
@@ -1017,7 +1045,7 @@ template <int R, bool VERIFY, bool PIPE, bool PARK>
 __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
                                                 __amdgpu_buffer_rsrc_t prs, __amdgpu_buffer_rsrc_t ors,
                                                 __amdgpu_buffer_rsrc_t oks, uint32_t run, uint32_t a0, uint32_t a_end,
-                                                uint32_t lane, lds16* slot, bool has_part, uint32_t out_al) {
+                                                uint32_t lane, lds16* slot, bool has_part, const void* out, bool raw) {
     typedef uint32_t v2u __attribute__((ext_vector_type(2)));
     auto ld64 = [&](uint32_t i, bool live) -> uint64_t {
         const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, live ? i * 8 : kOOB, 0, 0);
@@ -1052,8 +1080,9 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
         for (uint32_t r = 0; r < kScanSlotRows; ++r) V[r] = bld16<true>(rs, r * kRow + lane * 16u);
     };
     // PARK: the results parked in the slot after the run's (the small-segment mode gives each wave two)
-    ResultPark pk = make_park(PARK ? reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(slot) + kScanSlot) : nullptr,
-                              out_al, a0);
+    using T = typename std::conditional<VERIFY, uint8_t, uint16_t>::type;
+    ScanPark<VERIFY> pk = make_park<T>(PARK ? reinterpret_cast<T*>(reinterpret_cast<uint8_t*>(slot) + kScanSlot) : nullptr,
+                                       VERIFY ? oks : ors, out, a0);
     // As rx_runs_lds: the LDS loop runs while consecutive runs fit the slot; a run that does not is streamed on
     // its own in the outer loop, so the streaming form's loads in flight at its end never merge into the LDS
     // loop's wait counts.
@@ -1066,11 +1095,11 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
             const uint32_t c1 = min(cur.cnt, kScanRun), c2 = cur.cnt - c1;
             const uint32_t cnt1[1] = {c1}, part1[1] = {part};
             const uint64_t o1[1] = {lane == c1 ? readlane64(c_end, c1 - 1u) : c_off};
-            ragged_run_stream<R, VERIFY, PIPE, 1>(base, a, kScanRun, cnt1, o1, part1, ors, oks, lane, pk);
+            ragged_run_stream<R, VERIFY, PIPE, 1>(base, a, kScanRun, cnt1, o1, part1, ors, raw, lane, pk);
             if (c2) {
                 const uint32_t cnt2[1] = {c2}, part2[1] = {(uint32_t)__shfl_down((int)part, c1)};
                 const uint64_t o2[1] = {lane == 0 ? readlane64(c_off, c1) : readlane64(c_end, c1)};
-                ragged_run_stream<R, VERIFY, PIPE, 1>(base, a + c1, kScanRun, cnt2, o2, part2, ors, oks, lane, pk);
+                ragged_run_stream<R, VERIFY, PIPE, 1>(base, a + c1, kScanRun, cnt2, o2, part2, ors, raw, lane, pk);
             }
             a += run;
             continue;
@@ -1091,9 +1120,7 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
             const uint32_t e = mine ? (uint32_t)((base + c_end) - cur.rbase) : 0u;
             const uint32_t dq = reinterpret_cast<const uint32_t*>(slot)[p >> 2];
             const uint32_t res = finish(fold32(lds_range_sum(slot, p, e, dq, mine)), (p & 1u) == 0, part);
-            park_put(pk, ors, a, cur.cnt, lane, res);
-            if constexpr (VERIFY)
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(res == 0xFFFFu), oks, mine ? a + lane : kOOB, 0, 0);
+            put_results<VERIFY>(pk, ors, raw, a, cur.cnt, lane, res);
             a += run;
             if (!nxt.lds) break;  // the end of the wave's range, or a run for the outer loop
             cur = nxt;
@@ -1101,7 +1128,7 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
             c_end = n_end, n_end = p_end;
         }
     }
-    park_flush(pk, ors, lane);
+    park_flush(pk, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -1320,7 +1347,9 @@ __global__ __launch_bounds__(kBlock, NS == 2 ? 4 : 1) void csum_ragged_scan_kern
     const __amdgpu_buffer_rsrc_t oks = make_rsrc(ok, VERIFY ? (uint64_t)n : 0);
     extern __shared__ lds16 lds_scan[];
     const uint32_t lds_run = run ? run : kWave, scan_run = run ? run : kScanRun;
-    const uint32_t out_al = (uint32_t)((uintptr_t)out >> 1) & 7u;  // the output's misalignment in results (ResultPark)
+    // the parked output (the raw sums; the batch verify's verdicts) and whether the verify also writes raw sums
+    const void* pout = VERIFY ? static_cast<const void*>(ok) : static_cast<const void*>(out);
+    const bool raw = out != nullptr;
     // XCD-contiguous numbering of the blocks, wpb of each block's waves taking ranges
     auto wave_no = [&](uint32_t nb, uint32_t wpb) {
         const uint32_t b = blockIdx.x;
@@ -1336,10 +1365,10 @@ __global__ __launch_bounds__(kBlock, NS == 2 ? 4 : 1) void csum_ragged_scan_kern
         const WaveRange wr = wave_range(ofs, n, wave_no(nb, 2u), W, lane, kScanLdsSeg, 1u, kWave);
         if (lds_run == kWave)
             ragged_runs_lds<R, VERIFY, PIPE, true>(base, ofs, n, prs, ors, oks, kWave, wr.a0, wr.a_end, lane,
-                                                   lds_scan + wave * (2u * kScanSlot / 16u), partial != nullptr, out_al);
+                                                   lds_scan + wave * (2u * kScanSlot / 16u), partial != nullptr, pout, raw);
         else  // tune.run_segs (tests): shorter runs, stored run by run
             ragged_runs_lds<R, VERIFY, PIPE, false>(base, ofs, n, prs, ors, oks, lds_run, wr.a0, wr.a_end, lane,
-                                                    lds_scan + wave * (2u * kScanSlot / 16u), partial != nullptr, out_al);
+                                                    lds_scan + wave * (2u * kScanSlot / 16u), partial != nullptr, pout, raw);
         return;
     }
     // The grid is sized for small segments (4 blocks/CU); on the default grid (big_keep ≠ 0) streamed batches take
@@ -1358,14 +1387,14 @@ __global__ __launch_bounds__(kBlock, NS == 2 ? 4 : 1) void csum_ragged_scan_kern
     // runs of two 63-segment sets under kScanTwoSetSeg, else of one (§7 step 64: with results parked, one set beat
     // four at every mean from 160 B to 4.5 KB, by up to 9%, and two from ~400 B; two sets ran 3-5% faster at a
     // 160 B mean). The streamed forms park their results in the wave's unused LDS slot when the launch has one.
-    uint16_t* pbuf = park ? reinterpret_cast<uint16_t*>(lds_scan + wave * (kScanSlot / 16u)) : nullptr;
+    void* pbuf = park ? static_cast<void*>(lds_scan + wave * (kScanSlot / 16u)) : nullptr;
     if (sets == 3 || (NS == 2 && sets == 0 && wave_bytes < (uint64_t)kScanLdsSeg * (a_end - a0))) {
         ragged_runs_lds<R, VERIFY, PIPE, false>(base, ofs, n, prs, ors, oks, lds_run, a0, a_end, lane,
-                                                lds_scan + wave * (kScanSlot / 16u), partial != nullptr, out_al);
+                                                lds_scan + wave * (kScanSlot / 16u), partial != nullptr, pout, raw);
     } else if (NS == 2 && (sets == 5 || (sets == 0 && wave_bytes < (uint64_t)kScanTwoSetSeg * (a_end - a0)))) {
-        ragged_runs<R, VERIFY, PIPE, 2>(base, ofs, n, prs, ors, oks, scan_run, a0, a_end, lane, pbuf, out_al);
+        ragged_runs<R, VERIFY, PIPE, 2>(base, ofs, n, prs, ors, oks, scan_run, a0, a_end, lane, pbuf, pout, raw);
     } else {
-        ragged_runs<R, VERIFY, PIPE, 1>(base, ofs, n, prs, ors, oks, scan_run, a0, a_end, lane, pbuf, out_al);
+        ragged_runs<R, VERIFY, PIPE, 1>(base, ofs, n, prs, ors, oks, scan_run, a0, a_end, lane, pbuf, pout, raw);
     }
 }
 

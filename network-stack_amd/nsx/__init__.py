@@ -318,10 +318,12 @@ def ragged_dev(buf, offsets, partial=None, out=None, stream=None, tune=None):
     return out
 
 
-def verify_ragged_dev(buf, offsets, partial=None, raw=None, stream=None, tune=None):
+def verify_ragged_dev(buf, offsets, partial=None, raw=None, stream=None, tune=None, ok=None):
     import torch
     n = _count(offsets, "verify_ragged_dev offsets")
-    ok = torch.empty(max(n, 0), dtype=torch.uint8, device=offsets.device)
+    if ok is None:
+        ok = torch.empty(max(n, 0), dtype=torch.uint8, device=offsets.device)
+    _span(ok, n, "verify_ragged_dev ok")
     _span(buf, 0, "verify_ragged_dev buf")
     _span(partial, 4 * n, "verify_ragged_dev partial", elem=4)
     _span(raw, 2 * n, "verify_ragged_dev raw", elem=2)

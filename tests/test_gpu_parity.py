@@ -208,6 +208,27 @@ def test_ragged_parked_results_any_output_alignment(mix, shift):
             got = u16(big)
             assert np.array_equal(got[shift:shift + n], w), (tune, pt is None)
             assert (got[:shift] == 0x5A5A).all() and (got[shift + n:] == 0x5A5A).all(), tune
+    # the batch verify parks its 1-byte verdicts (16 per block): ok outputs 0-15 bytes past a 16 B boundary, with
+    # and without raw sums beside them
+    # partials that make about half the segments verify (the sum plus 0xFFFF - raw is 0xFFFF), so both verdicts occur
+    part_v = np.where(rng.random(n) < 0.5, (0xFFFF - want.astype(np.uint32)), part).astype(np.uint32)
+    want_v = O.c_batch(buf, n, offsets=offs, partial=part_v, threads=16)
+    assert 0.3 < (want_v == 0xFFFF).mean() < 0.7
+    pv = dev(part_v.view(np.int32))
+    okb = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    for tune in (None, dict(segs_per_wave=2), dict(segs_per_wave=3), dict(segs_per_wave=5), dict(segs_per_wave=1)):
+        for oshift in (0, shift, 9, 15):
+            for with_raw in (False, True):
+                okb.fill_(0xA5)
+                big.fill_(0x5A5A)
+                nsx.verify_ragged_dev(d, o, partial=pv, raw=big[shift:shift + n] if with_raw else None, tune=tune,
+                                      ok=okb[oshift:oshift + n])
+                gok = host(okb)
+                assert np.array_equal(gok[oshift:oshift + n].astype(bool), want_v == 0xFFFF), (tune, oshift)
+                assert set(np.unique(gok[oshift:oshift + n])) <= {0, 1}, (tune, oshift)
+                assert (gok[:oshift] == 0xA5).all() and (gok[oshift + n:] == 0xA5).all(), (tune, oshift)
+                if with_raw:
+                    assert np.array_equal(u16(big)[shift:shift + n], want_v), (tune, oshift)
 
 
 def test_ragged_launch_shapes_bit_exact():

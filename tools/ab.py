@@ -6,7 +6,8 @@
 For the receive-pass configs, a variant named scan* runs the plain ragged
 checksum (nsx_csum_ragged_dev) over the same frames instead: the receive pass's
 own cost against the one-pass checksum it is built on; raw* runs the receive pass
-also writing its 2 B TCP raw sums (the ragged checksum's output volume).
+also writing its 2 B TCP raw sums (the ragged checksum's output volume). For the ragged
+configs, verify* runs the batch verify (nsx_verify_ragged_dev: 1 B ok per segment) over the same segments.
 
 Builds the workload once (bench.build_workload), settles the clocks, then runs
 the variants in interleaved rounds (each round: every variant, `--launches`
@@ -54,6 +55,10 @@ def main():
             rxf = nsx.rx_ipv6_tcp_verify_dev if cfg.get("ipver") == 6 else nsx.rx_ipv4_tcp_verify_dev
             traw = torch.empty(cfg["n"], dtype=torch.int16, device="cuda")
             step = (lambda t: lambda: rxf(w["buf"], w["d_offs"], mask=w["out"], tcp_raw=traw, tune=t))(tune)
+        if cfg["kind"] == "ragged" and name.startswith("verify"):  # the batch verify (1 B ok per segment, no raw)
+            import nsx
+            vpart = w.get("partial")
+            step = (lambda t: lambda: nsx.verify_ragged_dev(w["buf"], w["d_offs"], partial=vpart, tune=t))(tune)
         if cfg["kind"] == "rx" and name.startswith("scan"):
             import nsx
             rout = torch.empty(cfg["n"], dtype=torch.int16, device="cuda")
@@ -63,7 +68,8 @@ def main():
     # every variant must give the first one's results on this batch (they differ only in launch shape or code path)
     ref = None
     for name, step, _ in variants:
-        if (cfg["kind"] == "rx" and name.startswith("scan")) or name.startswith("x_"):
+        if (cfg["kind"] == "rx" and name.startswith("scan")) or name.startswith("x_") or \
+                (cfg["kind"] == "ragged" and name.startswith("verify")):
             continue  # another computation / a diagnostic variant whose results are wrong on purpose
         w["out"].zero_()
         step()

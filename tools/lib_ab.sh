@@ -6,6 +6,7 @@
 #   bash tools/lib_ab.sh run "10 11" [pairs]  # on the GPU box: new, base, new, base, ... for each workload
 #   AB_EXTRA="--set hi=256" bash tools/lib_ab.sh run 15   # extra tools/ab.py arguments (a workload variant)
 #   AB_LIBS="new base x" bash tools/lib_ab.sh run 10       # more builds: x = network-stack_amd/lib_x/libnsx_csum.so
+#   AB_PREFIX=verify bash tools/lib_ab.sh run 15            # variant names prefixed (tools/ab.py: verify* = batch verify)
 #
 # Both builds share include/ and the ABI of the working tree; only use it for kernel-internal changes.
 set -eu
@@ -31,7 +32,7 @@ case "${1:-}" in
       for k in ${AB_LIBS:-new base}; do
         if [ "$k" = new ]; then cp /tmp/lib_ab_new.so "$lib"; else cp "network-stack_amd/lib_$k/libnsx_csum.so" "$lib"; fi
         for c in $configs; do
-          timeout -k 10 200 python tools/ab.py --config "$c" --variants "$k:" --rounds 5 ${AB_EXTRA:-} 2>/dev/null | grep AB
+          timeout -k 10 200 python tools/ab.py --config "$c" --variants "${AB_PREFIX:-}$k:" --rounds 5 ${AB_EXTRA:-} 2>/dev/null | grep AB
         done
       done
     done
