@@ -782,6 +782,7 @@ struct ResultPark {
     T* buf;
     __amdgpu_buffer_rsrc_t rs;  // the output
     uint32_t al, base, lo, hi;
+    uint32_t cap;  // results the buffer holds (≤ kCap, a multiple of kPer)
     __device__ __forceinline__ void rebase(uint32_t a) {
         base = ((a + al) & ~(kPer - 1u)) - al;
         lo = hi = a;
@@ -789,8 +790,9 @@ struct ResultPark {
 };
 
 template <typename T>
-__device__ __forceinline__ ResultPark<T> make_park(T* buf, __amdgpu_buffer_rsrc_t rs, const void* out, uint32_t a0) {
-    ResultPark<T> pk{buf, rs, (uint32_t)((uintptr_t)out / sizeof(T)) & (ResultPark<T>::kPer - 1u), 0, 0, 0};
+__device__ __forceinline__ ResultPark<T> make_park(T* buf, __amdgpu_buffer_rsrc_t rs, const void* out, uint32_t a0,
+                                                   uint32_t cap = ResultPark<T>::kCap) {
+    ResultPark<T> pk{buf, rs, (uint32_t)((uintptr_t)out / sizeof(T)) & (ResultPark<T>::kPer - 1u), 0, 0, 0, cap};
     pk.rebase(a0);
     return pk;
 }
@@ -803,17 +805,17 @@ __device__ __forceinline__ void store_result(T v, __amdgpu_buffer_rsrc_t rs, uin
 
 template <typename T>
 __device__ __forceinline__ void park_flush(ResultPark<T>& pk, uint32_t lane) {
-    constexpr uint32_t P = ResultPark<T>::kPer, C = ResultPark<T>::kCap;
+    constexpr uint32_t P = ResultPark<T>::kPer;
     if (!pk.buf || pk.hi == pk.lo) return;
     __builtin_amdgcn_wave_barrier();
     typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-    const uint32_t l = pk.lo - pk.base, h = pk.hi - pk.base;  // parked: buf[l, h), 0 ≤ l < h ≤ C
+    const uint32_t l = pk.lo - pk.base, h = pk.hi - pk.base;  // parked: buf[l, h), 0 ≤ l < h ≤ cap
     const uint32_t b0 = l / P, b1 = (h + P - 1u) / P;           // the 16 B blocks touched
     const bool head_full = P * b0 == l, tail_full = P * b1 == h;
     for (uint32_t q = b0; q < b1; q += kWave) {  // whole blocks: one 16 B store each
         const uint32_t blk = q + lane;
         const bool full = blk < b1 && (blk != b0 || head_full) && (blk != b1 - 1u || tail_full);
-        const lds16 v = reinterpret_cast<const lds16*>(pk.buf)[blk < C / P ? blk : 0u];
+        const lds16 v = reinterpret_cast<const lds16*>(pk.buf)[blk < pk.cap / P ? blk : 0u];
         __builtin_amdgcn_raw_buffer_store_b128(v4u{v.x, v.y, v.z, v.w}, pk.rs,
                                                full ? (pk.base + P * blk) * (uint32_t)sizeof(T) : kOOB, 0, 0);
     }
@@ -836,7 +838,7 @@ __device__ __forceinline__ void park_put(ResultPark<T>& pk, uint32_t a, uint32_t
         store_result<T>((T)res, pk.rs, lane < cnt ? (a + lane) * (uint32_t)sizeof(T) : kOOB);
         return;
     }
-    if (pk.hi != a || a + cnt - pk.base > ResultPark<T>::kCap) {  // not contiguous, or would overflow: flush, rebase
+    if (pk.hi != a || a + cnt - pk.base > pk.cap) {  // not contiguous, or would overflow: flush, rebase
         park_flush(pk, lane);
         pk.rebase(a);
     }
@@ -1431,7 +1433,17 @@ constexpr uint32_t kRxRun = 64;
 struct RxOuts {
     __amdgpu_buffer_rsrc_t mrs, irs, trs;
     bool raw;
+    // The streamed form's raw sums parked in the wave's LDS slot (§7 step 67; buf null in the LDS, hybrid and prefix
+    // forms, whose slots hold rows): IPv4 header sums and TCP sums, 2048 each (IPv6: TCP sums, 4096).
+    mutable ResultPark<uint16_t> ipk, tpk;
 };
+
+__device__ __forceinline__ RxOuts rx_outs(uint64_t* mask, uint16_t* ip_raw, uint16_t* tcp_raw, uint32_t n) {
+    const __amdgpu_buffer_rsrc_t irs = make_rsrc(ip_raw, ip_raw ? (uint64_t)n * 2 : 0);
+    const __amdgpu_buffer_rsrc_t trs = make_rsrc(tcp_raw, tcp_raw ? (uint64_t)n * 2 : 0);
+    return RxOuts{make_rsrc(mask, (((uint64_t)n + 63) / 64) * 8), irs, trs, ip_raw != nullptr || tcp_raw != nullptr,
+                  make_park<uint16_t>(nullptr, irs, ip_raw, 0), make_park<uint16_t>(nullptr, trs, tcp_raw, 0)};
+}
 
 // A run's validity ballot (frames [a, a + cnt), a a multiple of 8) as mask bytes a/8 ..: one byte per lane
 // (lanes 0-7), so wave ranges need only be cut at multiples of 8 frames, not at whole 64-bit words; the
@@ -1540,9 +1552,14 @@ __device__ __forceinline__ void rx_verdict(uint64_t F, const RxHdr& h, bool even
     const uint64_t bits = __builtin_amdgcn_ballot_w64(h.well && (V6 || h.ipr == 0xFFFFu) && tcpr == 0xFFFFu);
     rx_store_mask(ro.mrs, bits, ak, cnt, n, lane, s);
     if (ro.raw) {
-        if constexpr (!V6)
-            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)h.ipr, ro.irs, live ? (ak + lane) * 2u : kOOB, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)tcpr, ro.trs, live ? (ak + lane) * 2u : kOOB, 0, 0);
+        if (ro.tpk.buf) {  // parked (the streamed form: frames [ak, ak + cnt), live = lane < cnt)
+            if constexpr (!V6) park_put(ro.ipk, ak, cnt, lane, h.ipr);
+            park_put(ro.tpk, ak, cnt, lane, tcpr);
+        } else {
+            if constexpr (!V6)
+                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)h.ipr, ro.irs, live ? (ak + lane) * 2u : kOOB, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)tcpr, ro.trs, live ? (ak + lane) * 2u : kOOB, 0, 0);
+        }
     }
 }
 
@@ -1867,8 +1884,7 @@ __global__ __launch_bounds__(kBlock, WPS) void rx_tcp_kernel(const uint8_t* __re
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const __amdgpu_buffer_rsrc_t ofs = make_rsrc(offsets, ((uint64_t)n + 1) * 8);
-    const RxOuts ro{make_rsrc(mask, (((uint64_t)n + 63) / 64) * 8), make_rsrc(ip_raw, ip_raw ? (uint64_t)n * 2 : 0),
-                    make_rsrc(tcp_raw, tcp_raw ? (uint64_t)n * 2 : 0), ip_raw != nullptr || tcp_raw != nullptr};
+    const RxOuts ro = rx_outs(mask, ip_raw, tcp_raw, n);
     extern __shared__ lds16 lds_rx[];
     // Byte-balanced wave ranges (as csum_ragged_scan_kernel), cut at multiples of 8 frames. Cut at whole mask
     // words (64 frames, ~50 KB) instead, a wave streamed up to one run more than the mean, and the launch
@@ -1903,7 +1919,19 @@ __global__ __launch_bounds__(kBlock, WPS) void rx_tcp_kernel(const uint8_t* __re
             const uint32_t nb = active_blocks(ofs, n, 0u, sets == 0 || sets == 8 ? 3u : 0u);
             if (blockIdx.x >= nb) return;
             const WaveRange wr = range(nb, kWavesPerBlock, wave);
-            rx_runs<R, V6, 1>(base, ofs, n, wr.a0, wr.a_end, lane, ro);
+            // raw sums parked in the wave's (otherwise unused) 7-row slot, 8 KiB: IPv4 2 × 2048 results, IPv6 4096
+            static_assert(PfxSlot<7>::kBytes >= 8192, "two 4 KiB parks per wave slot");
+            RxOuts rp = ro;
+            if (ro.raw) {
+                uint16_t* pb = reinterpret_cast<uint16_t*>(lds_rx + wave * (PfxSlot<7>::kBytes / 16u));
+                rp.tpk = make_park<uint16_t>(pb, ro.trs, tcp_raw, wr.a0, V6 ? 4096u : 2048u);
+                if constexpr (!V6) rp.ipk = make_park<uint16_t>(pb + 2048, ro.irs, ip_raw, wr.a0, 2048u);
+            }
+            rx_runs<R, V6, 1>(base, ofs, n, wr.a0, wr.a_end, lane, rp);
+            if (ro.raw) {
+                park_flush(rp.tpk, lane);
+                if constexpr (!V6) park_flush(rp.ipk, lane);
+            }
         }
         return;
     }

@@ -362,3 +362,42 @@ def test_rx6_host_batches_sharded(shards):
     want, _ = O.c_rx_ipv6_tcp(buf, offs)
     got = nsx.rx_ipv6_tcp_verify_host(buf, offs, tune=dict(shards_per_device=shards))
     assert np.array_equal(got, want), shards
+
+
+@pytest.mark.parametrize("ipver", [4, 6])
+def test_rx_parked_raw_sums_any_output_alignment(ipver):
+    """The streamed form parks its raw sums in the wave's LDS slot and writes them in 16 B
+    blocks aligned to each output: raw outputs 0-7 sums past a 16 B boundary inside sentinel-filled buffers, either
+    one alone or both, get exactly the oracle's sums and nothing outside them is written; the mask is unaffected.
+    40-1500 B frames (mean ~770 B: the default takes streamed runs) and the forced streamed mode 8."""
+    rng = np.random.default_rng(0x67 + ipver)
+    n = 120_003
+    kinds = _rx.KINDS6 if ipver == 6 else _rx.KINDS
+    buf, offs, _ = _rx.batch(rng, n, kinds=kinds, lead=3, max_payload=1460, ip=ipver)
+    want = (O.c_rx_ipv6_tcp if ipver == 6 else O.c_rx_ipv4_tcp)(buf, offs)
+    want_m, want_t = want[0], want[-1]
+    want_i = want[1] if ipver == 4 else None
+    d, o = dev(buf), dev(offs.view(np.int64))
+    fn = nsx.rx_ipv6_tcp_verify_dev if ipver == 6 else nsx.rx_ipv4_tcp_verify_dev
+    ib = torch.empty(n + 32, dtype=torch.int16, device="cuda")
+    tb = torch.empty(n + 32, dtype=torch.int16, device="cuda")
+    for tune in (None, dict(segs_per_wave=8)):
+        for si, st in ((0, 0), (1, 7), (5, 3), (7, 0)):
+            for which in (("t",) if ipver == 6 else ("i", "t", "it")):
+                ib.fill_(0x5A5A)
+                tb.fill_(0x5A5A)
+                kw = {}
+                if "t" in which:
+                    kw["tcp_raw"] = tb[st:st + n]
+                if "i" in which:
+                    kw["ip_raw"] = ib[si:si + n]
+                mask = fn(d, o, tune=tune, **kw)
+                assert np.array_equal(host(mask).view(np.uint64), want_m), (tune, which)
+                if "t" in which:
+                    g = u16(tb)
+                    assert np.array_equal(g[st:st + n], want_t), (tune, which, st)
+                    assert (g[:st] == 0x5A5A).all() and (g[st + n:] == 0x5A5A).all(), (tune, which, st)
+                if "i" in which:
+                    g = u16(ib)
+                    assert np.array_equal(g[si:si + n], want_i), (tune, which, si)
+                    assert (g[:si] == 0x5A5A).all() and (g[si + n:] == 0x5A5A).all(), (tune, which, si)
