@@ -1850,7 +1850,7 @@ __device__ __forceinline__ void rx_runs_lds(const uint8_t* __restrict__ base, __
 
 
 // The receive pass's grids by the batch's mean frame m: m <
-// kRxPfxMean: four waves per block, the LDS loop for runs of small frames that fit 8 KiB, handing over at the first
+// kRxPfxMean: two waves per block (§7 step 68), the LDS loop for runs of small frames that fit 8 KiB, handing over at the first
 // other run to the hybrid loop (direct pieces for such runs, prefix pieces of ≤ 7 KiB otherwise; §7 step 59);
 // kRxPfxMean ≤ m < the streaming threshold: the prefix form with 15-row slots on two waves per block (8 waves per
 // CU, ~19 KB of LDS each); above it streamed runs on 3 blocks per CU.
@@ -1908,9 +1908,13 @@ __global__ __launch_bounds__(kBlock, WPS) void rx_tcp_kernel(const uint8_t* __re
             const WaveRange wr = range(gridDim.x, 2u, wave);
             rx_runs_pfx<R, V6, 15, false>(base, ofs, n, wr.a0, wr.a_end, lane,
                                           lds_rx + wave * (PfxSlot<15>::kBytes / 16u), ro);
-        } else if (mode == 5 || mode == 7) {  // four waves per block: the LDS loop until a run needs the hybrid
-                                              // loop (5), or the hybrid loop throughout (7)
-            const WaveRange wr = range(gridDim.x, kWavesPerBlock, wave);
+        } else if (mode == 5 || mode == 7) {  // two waves per block: the LDS loop until a run needs the hybrid loop
+                                              // (5), or the hybrid loop throughout (7). Four waves per block ran
+                                              // 2.5-4.4% slower on 40-120 B frames (workloads 13, 16; 17 −0.3%):
+                                              // with 8 waves per CU the VALU-heavy LDS loop queues less for issue
+                                              // 
+            if (wave >= 2u) return;
+            const WaveRange wr = range(gridDim.x, 2u, wave);
             lds16* slot = lds_rx + wave * (PfxSlot<7>::kBytes / 16u);
             if (mode == 5) rx_runs_lds<R, V6, true>(base, ofs, n, wr.a0, wr.a_end, lane, slot, ro);
             else rx_runs_pfx<R, V6, 7, true>(base, ofs, n, wr.a0, wr.a_end, lane, slot, ro);

@@ -60,7 +60,7 @@ TUNES = [dict(rows=2), dict(rows=4), dict(rows=16), dict(blocks_per_cu=1), dict(
          dict(segs_per_wave=2, blocks_per_cu=8), dict(blocks_per_cu=4),  # LDS form; 4 blocks/CU = the capped kernel
          dict(segs_per_wave=5), dict(segs_per_wave=6), dict(segs_per_wave=7), dict(segs_per_wave=8)]  # the default grid's modes
 # the default grid's modes forced (5 the LDS loop handing over to the hybrid loop, 7 the hybrid loop throughout, both
-# on four waves; 6 the 15-row prefix form on two waves per block)
+# on two waves per block; 6 the 15-row prefix form on two waves per block)
 PFX = [dict(segs_per_wave=5), dict(segs_per_wave=6), dict(segs_per_wave=7), dict(segs_per_wave=8)]
 
 
