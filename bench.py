@@ -285,7 +285,9 @@ def timed_loop(step, sync, barrier, steps: int, warmup: int, ev_pair=None):
     (Round 1 bracketed single launches; an event between two launches makes the
     next kernel wait for the event's completion and exposes its dispatch
     latency, which read 5-7% above the traced duration for 0.13 ms kernels.)
-    Returns (wall_s, [mean_step_ms]) ([] without ev_pair)."""
+    Returns (wall_s, [mean_step_ms] ([] without ev_pair), own_s): wall_s closes after the closing barrier, so it
+    is the slowest rank's time on every rank (the job's clock); own_s closes at this rank's own sync before that
+    barrier (its own clock, for its per-GPU rate — ADVICE r4: a rate from wall_s cannot show a slow GPU)."""
     for _ in range(warmup):
         step()
     sync()
@@ -300,10 +302,11 @@ def timed_loop(step, sync, barrier, steps: int, warmup: int, ev_pair=None):
     if ev:
         ev[1].record()
     sync()
+    own = time.perf_counter() - t0
     barrier()
     sync()
     wall = time.perf_counter() - t0
-    return wall, ([ev[0].elapsed_time(ev[1]) / steps] if ev else [])
+    return wall, ([ev[0].elapsed_time(ev[1]) / steps] if ev else []), own
 
 
 def device_identity(dev_id: int) -> dict:
@@ -326,16 +329,19 @@ def device_fields(idents: list) -> dict:
 
 
 def per_gpu_entries(rank_stats, *, steps, bytes_per_rank_step, alg_bytes_per_launch, launches=1) -> list:
-    """Each rank's own rate from its own clock (rank_stats: every rank's {rank, device, wall_s, step_ms}, rank
-    order): bytes ÷ its timed wall, its kernel mean per launch (a step of `launches` launches, as config 5's
+    """Each rank's own rate from its own clock (rank_stats: every rank's {rank, device, wall_s, own_s, step_ms},
+    rank order): bytes ÷ its own timed region (own_s: closed before the closing barrier, so a slow GPU shows;
+    wall_s, the barrier-closed job clock, when own_s is absent), its kernel mean per launch (a step of `launches` launches, as config 5's
     windows, split evenly) and that launch's roofline fraction (alg_bytes_per_launch: one launch's bytes)."""
     out = []
     for r in rank_stats:
         k_ms = None if r.get("step_ms") is None else r["step_ms"] / launches
         frac = None if not k_ms else alg_bytes_per_launch / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS
+        own = r.get("own_s") or r["wall_s"]
         out.append({"rank": r["rank"], "device": r.get("device"),
-                    "gib_s": round(bytes_per_rank_step * steps / r["wall_s"] / GIB, 3),
-                    "wall_s": round(r["wall_s"], 6), "kernel_ms": None if k_ms is None else round(k_ms, 5),
+                    "gib_s": round(bytes_per_rank_step * steps / own / GIB, 3),
+                    "own_s": round(own, 6), "wall_s": round(r["wall_s"], 6),
+                    "kernel_ms": None if k_ms is None else round(k_ms, 5),
                     "roofline_frac": None if frac is None else round(frac, 4)})
     return out
 
@@ -650,7 +656,7 @@ def cpu_baseline(cfg, w, seconds: float) -> dict:
     elif cfg["kind"] == "tcp_build":
         n, P, OL = cfg["n"], cfg["payload"], cfg.get("opt", 0)
         W = P + 20 + OL
-        m = min(n, 65536)  # sample: the first 64K segments (~94 MiB of wire)
+        m = min(n, max(1, (256 << 20) // W))  # sample: the first segments of ≤ 256 MiB of wire
         cols = [np.ascontiguousarray(w["fields"][k][:m].cpu().numpy().view(dt))
                 for k, dt in zip(O.TCP_FIELDS, O.TCP_FIELD_DTYPES)]
         data = w["data"][: m * P].cpu().numpy()
@@ -687,7 +693,7 @@ def cpu_baseline(cfg, w, seconds: float) -> dict:
         check["wire_images"] = lambda: np.array_equal(wire, gpu_wire)
     elif cfg["kind"] == "ipv4_hdr":
         n, H = cfg["n"], cfg["hdr"]
-        m = min(n, 1 << 22)
+        m = min(n, (256 << 20) // H // 64 * 64)  # sample: ≤ 256 MiB of headers, whole mask words
         sample = w["buf"][: m * H].cpu().numpy()
         mask = cfg.get("mask", False)
         gpu = (w["out"][: m // 64].cpu().numpy().view(np.uint64) if mask
@@ -730,7 +736,7 @@ def cpu_baseline(cfg, w, seconds: float) -> dict:
         check["mask"] = lambda: np.array_equal(cmask, gpu)
     else:
         offs_all = w["offsets"]
-        m = int(min(len(offs_all) - 1, 50000))
+        m = int(min(len(offs_all) - 1, max(1, np.searchsorted(offs_all, 256 << 20))))  # ≤ 256 MiB of segments
         hi_b = int(offs_all[m])
         sample = w["buf"][:hi_b].cpu().numpy()
         offs = np.ascontiguousarray(offs_all[: m + 1])
@@ -742,21 +748,60 @@ def cpu_baseline(cfg, w, seconds: float) -> dict:
             lib.oracle_go_batch_ragged(_ptr(sample), _ptr(offs, lo), hi - lo, None, 0, _ptr(out, lo))
         nbytes, desc = hi_b, f"first {m} ragged segments of rank 0's batch"
         check["segments"] = lambda: np.array_equal(out, gpu)
+    busy = []  # (thread, seconds) of every shard call in the all-threads leg
+
+    def timed_go(t):
+        t0 = time.perf_counter()
+        go(bounds[t], bounds[t + 1])
+        busy.append(time.perf_counter() - t0)
+    thr0 = cgroup_throttling()
     with ThreadPoolExecutor(T) as ex:
         def all_cores():
-            list(ex.map(lambda t: go(bounds[t], bounds[t + 1]), range(T)))
+            list(ex.map(timed_go, range(T)))
         reps_t, dt_t = _run_for(all_cores, seconds / 2)
         ok_t = all(f() for f in check.values())
+    thr1 = cgroup_throttling()
     reps_1, dt_1 = _run_for(lambda: go(0, bounds[-1]), seconds / 2)
     ok_1 = all(f() for f in check.values())
     if cfg["kind"] == "fixed":
         extra = cpu_extra_lines(sample, S, L, m, out, max(1.0, seconds / 4), T, part)
-    return {"value": round(reps_t * nbytes / dt_t / GIB, 4), "unit": "GiB/s", "cores": T, "kind": "port",
-            "sample": f"{desc}, {reps_t} pass(es) on {T} threads (Go-faithful loop, contiguous shards)",
+    v_t, v_1 = reps_t * nbytes / dt_t / GIB, reps_1 * nbytes / dt_1 / GIB
+    eff = v_t / (T * v_1) if v_1 else None
+    # why the all-threads leg falls short of T x the 1-thread rate, when it does: the shard calls' busy time against
+    # T x the wall time (threads waiting to run) and the per-thread rate inside the calls (threads running slower
+    # than alone: allocator or memory contention), plus any CPU-quota throttling the cgroup recorded meanwhile
+    busy_frac = sum(busy) / (T * dt_t) if dt_t else None
+    in_call = (nbytes * reps_t / T) / (sum(busy) / T) / GIB if busy else None
+    diag = {"busy_fraction": None if busy_frac is None else round(busy_frac, 3),
+            "per_thread_gib_s_in_call": None if in_call is None else round(in_call, 4),
+            "cgroup_throttled_ms": None if thr0 is None or thr1 is None else round((thr1[1] - thr0[1]) / 1e3, 1),
+            "cgroup_throttled_periods": None if thr0 is None or thr1 is None else thr1[0] - thr0[0]}
+    why = ""
+    if eff is not None and eff < 0.5:
+        if diag["cgroup_throttled_ms"]:
+            why = f"; below 0.5 parallel efficiency: the cgroup's CPU quota throttled the process {diag['cgroup_throttled_ms']} ms"
+        elif busy_frac is not None and busy_frac < 0.7:
+            why = f"; below 0.5 parallel efficiency: shard threads busy {busy_frac:.0%} of the wall (waiting to run)"
+        else:
+            why = (f"; below 0.5 parallel efficiency: each thread ran at {in_call:.2f} GiB/s inside its call against "
+                   f"{v_1:.2f} alone (contention in the per-unit allocation or memory system)")
+    return {"value": round(v_t, 4), "unit": "GiB/s", "cores": T, "kind": "port",
+            "sample": f"{desc} ({nbytes / 2**20:.0f} MiB), {reps_t} pass(es) on {T} threads (Go-faithful loop, "
+                      f"contiguous shards){why}",
             "seconds": round(dt_t, 2),
-            "single_thread": {"value": round(reps_1 * nbytes / dt_1 / GIB, 4), "unit": "GiB/s", "cores": 1,
+            "single_thread": {"value": round(v_1, 4), "unit": "GiB/s", "cores": 1,
                               "passes": reps_1, "seconds": round(dt_1, 2)},
+            "parallel_efficiency": None if eff is None else round(eff, 3), "threads_diagnostics": diag,
             "sample_parity_vs_gpu": bool(ok_t and ok_1), "host": cores, "extra": extra}
+
+
+def cgroup_throttling():
+    """(nr_throttled, throttled_usec) of this process's cgroup (cgroup v2 cpu.stat), or None."""
+    try:
+        st = dict(line.split() for line in open("/sys/fs/cgroup/cpu.stat"))
+        return int(st.get("nr_throttled", 0)), int(st.get("throttled_usec", 0))
+    except (OSError, ValueError):
+        return None
 
 
 def cpu_extra_lines(sample, S, L, m, want, seconds, threads, part=None):
@@ -802,12 +847,12 @@ def dry_run(args) -> int:
     dist = Dist("gloo")
     n, L = 256, 1500
     buf = O.c_splitmix64(0x1071 + dist.rank, n * L)
-    wall, launch_ms = timed_loop(lambda: O.c_batch(buf, n, stride=L, seg_len=L, threads=1), lambda: None,
-                                 dist.barrier, args.steps, args.warmup)
+    wall, launch_ms, own = timed_loop(lambda: O.c_batch(buf, n, stride=L, seg_len=L, threads=1), lambda: None,
+                                      dist.barrier, args.steps, args.warmup)
     wall_max = dist.max(wall)
     idents = dist.gather({"host": socket.gethostname(), "local_device": None, "pci": None, "uuid": None,
                           "key": None})
-    stats = dist.gather({"rank": dist.rank, "device": None, "wall_s": wall, "step_ms": None})
+    stats = dist.gather({"rank": dist.rank, "device": None, "wall_s": wall, "own_s": own, "step_ms": None})
     line = result_line(world=dist.world, steps=args.steps, warmup=args.warmup, wall_max=wall_max,
                        bytes_per_rank_step=n * L, units_total=n * dist.world, workload="dry run", cfg={"n": n, "seed": 0x1071},
                        launch_ms=launch_ms, alg_bytes_per_launch=n * L + 2 * n, cpu_baseline=None, traffic=None,
@@ -825,8 +870,11 @@ def dry_run(args) -> int:
 def build_library() -> None:
     """Bring libnsx_csum.so up to date before it is loaded (incremental make: a no-op when the pushed binary
     matches its sources; ~35 s for a full rebuild). A failed build is an error, never a stale library."""
-    r = subprocess.run(["make", "-s", "-j16", "-C", os.path.join(ROOT, "network-stack_amd")],
-                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    import fcntl
+    with open(os.path.join(ROOT, "network-stack_amd", ".build.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        r = subprocess.run(["make", "-s", "-j16", "-C", os.path.join(ROOT, "network-stack_amd")],
+                           stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     if r.returncode != 0:
         raise SystemExit(f"bench.py: building network-stack_amd failed:\n{r.stdout[-4000:]}")
 
@@ -834,8 +882,12 @@ def build_library() -> None:
 def main(argv=None) -> int:
     argv = sys.argv[1:] if argv is None else list(argv)
     args = parse_args(argv)
-    if not args.dry_run and not args.no_build and os.environ.get("NSX_BENCH_BUILT") != "1":
-        build_library()  # once, in the launching process, before any rank starts
+    # build once, in the launching process, before any rank starts: never in a rank a launcher started (WORLD_SIZE or
+    # LOCAL_RANK set — N ranks running make on one tree could load a half-written library), and under a lock, so two
+    # launching processes on one tree serialise
+    in_rank = "WORLD_SIZE" in os.environ or "LOCAL_RANK" in os.environ
+    if not args.dry_run and not args.no_build and not in_rank and os.environ.get("NSX_BENCH_BUILT") != "1":
+        build_library()
         os.environ["NSX_BENCH_BUILT"] = "1"
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return launch_ranks(args.gpus, argv)  # before anything touches a GPU
@@ -894,11 +946,11 @@ def main(argv=None) -> int:
     def ev_pair():
         return torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
-    wall, launch_ms = timed_loop(w["step"], torch.cuda.synchronize, lambda: dist.barrier(dev_id),
-                                 args.steps, args.warmup, ev_pair)
+    wall, launch_ms, own = timed_loop(w["step"], torch.cuda.synchronize, lambda: dist.barrier(dev_id),
+                                      args.steps, args.warmup, ev_pair)
     wall_max = dist.max(wall, device)
     stats = dist.gather({"rank": dist.rank, "device": "%s/%s" % (socket.gethostname(), devf["devices"][dist.rank]["pci"]),
-                         "wall_s": wall, "step_ms": launch_ms[0] if launch_ms else None})
+                         "wall_s": wall, "own_s": own, "step_ms": launch_ms[0] if launch_ms else None})
     cpu = None
     if dist.world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(cfg, w, args.cpu_seconds)

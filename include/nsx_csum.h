@@ -276,6 +276,26 @@ int nsx_rx_ipv4_tcp_verify_host(const uint8_t* h_base, const uint64_t* h_offsets
 int nsx_rx_ipv6_tcp_verify_host(const uint8_t* h_base, const uint64_t* h_offsets, uint64_t n, uint64_t* h_mask,
                                 int num_gpus);
 
+/* The fused sender pass (nsx_tcp_build_dev) over host-resident segments: the
+ * header fields (nsx_tcp_hdr_soa members here are HOST arrays of n entries;
+ * `offset` nullable as for the device call), options (h_opt_off nullable),
+ * payloads, partials (nullable) and the output are in host memory, pageable or
+ * pinned (nsx_alloc_pinned; pinned data and output are DMA'd directly). Writes
+ * each wire image to h_out + h_out_off[i] with the device call's layout rule
+ * (h_out_off[i] a multiple of 4, room for the image rounded up to 4 bytes, the
+ * up to 3 bytes after it zero-filled; nsx_tcp_layout_host makes such offsets;
+ * bytes between a padded image and the next offset are left as they are) and
+ * the raw sums to h_raw (nullable). Offsets must be non-decreasing and every
+ * image shorter than 2^31 bytes (NSX_EINVAL otherwise, checked before any copy).
+ * Sharded by image bytes over num_gpus devices like the calls above (0 = auto),
+ * chunks of <= 64 MiB of images double-buffered per device.
+ * Replaces a Go send loop over bytes() + computeChecksum + the field store
+ * (transport/tcp/tcp.go:98-128, :110, :68-71) whose images then go into the
+ * transport's pipe or socket buffers (transport/pipe/pipe.go:92-124). */
+int nsx_tcp_build_host(const nsx_tcp_hdr_soa* h_hdr, const uint8_t* h_opts, const uint64_t* h_opt_off,
+                       const uint8_t* h_data, const uint64_t* h_data_off, const uint32_t* h_prefix_partial,
+                       uint64_t n, uint8_t* h_out, const uint64_t* h_out_off, uint16_t* h_raw, int num_gpus);
+
 /* The host batch calls keep per-device streams and grow-only device/pinned
  * staging buffers across calls (a transport calls them once per batch). This
  * frees the cached buffers; the next call re-allocates. Safe to call at any

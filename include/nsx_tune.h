@@ -106,6 +106,10 @@ int nsx_rx_ipv4_tcp_verify_host_tuned(const uint8_t* h_base, const uint64_t* h_o
                                       int num_gpus, const nsx_tune* tune);
 int nsx_rx_ipv6_tcp_verify_host_tuned(const uint8_t* h_base, const uint64_t* h_offsets, uint64_t n, uint64_t* h_mask,
                                       int num_gpus, const nsx_tune* tune);
+int nsx_tcp_build_host_tuned(const nsx_tcp_hdr_soa* h_hdr, const uint8_t* h_opts, const uint64_t* h_opt_off,
+                             const uint8_t* h_data, const uint64_t* h_data_off, const uint32_t* h_prefix_partial,
+                             uint64_t n, uint8_t* h_out, const uint64_t* h_out_off, uint16_t* h_raw, int num_gpus,
+                             const nsx_tune* tune);
 
 /* Kernel launches one nsx_csum_fixed_dev(_tuned) call makes for this batch on the current device (its
  * back-to-back windows; 1 for most batches), for per-launch timing in benchmarks. */

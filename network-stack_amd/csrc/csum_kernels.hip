@@ -3176,9 +3176,13 @@ bool ragged_tune_valid(const LaunchCfg& c) {
 }
 
 bool rx_tune_valid(const LaunchCfg& c) {
-    // segs_per_wave 5 / 6 / 7 force a mode of the default grid; they mean nothing on the shapes rows / blocks_per_cu
-    // select (silently running the auto shape there made fuzz cases test another form than they named)
-    const bool grid_mode = c.segs_per_wave == 5 || c.segs_per_wave == 6 || c.segs_per_wave == 7 || c.segs_per_wave == 8;
+    // segs_per_wave: 0 auto, 1 / 2 forced per-wave forms of the rows / blocks_per_cu shapes, 5 / 6 / 7 / 8 a mode of
+    // the default grid — which means nothing on the shapes rows / blocks_per_cu select (silently running
+    // the auto shape there made fuzz cases test another form than they named); any other value names no form
+    // (3, 4 or 9 used to run the automatic shape)
+    const int s = c.segs_per_wave;
+    if (!(s == 0 || s == 1 || s == 2 || (s >= 5 && s <= 8))) return false;
+    const bool grid_mode = s >= 5;
     return !grid_mode || ((c.rows == 0 || c.rows == 2) && c.blocks_per_cu == 0);
 }
 

@@ -103,6 +103,8 @@ def lib() -> ctypes.CDLL:
             "nsx_ipv4_hdr_verify_mask_dev_tuned": [vp, u64, u32, u64, vp, vp, vp],
             "nsx_csum_fixed_host_tuned": [vp, u64, u32, u64, vp, vp, i32, vp],
             "nsx_csum_ragged_host_tuned": [vp, vp, u64, vp, vp, i32, vp],
+            "nsx_tcp_build_host": [vp, vp, vp, vp, vp, vp, u64, vp, vp, vp, i32],
+            "nsx_tcp_build_host_tuned": [vp, vp, vp, vp, vp, vp, u64, vp, vp, vp, i32, vp],
             "nsx_fixed_launch_count": [u64, u32, u64, vp, ctypes.POINTER(u64)],
             "nsx_ipv4_hdr_launch_count": [vp, u64, u32, u64, vp, ctypes.POINTER(u64)],
         }
@@ -502,6 +504,58 @@ def tcp_build_dev(fields: dict, data, data_off, out, out_off, opts=None, opt_off
                                          _dev_ptr(out_off), _dev_ptr(raw), _stream(stream), _tune(tune)),
            "nsx_tcp_build_dev")
     return out
+
+
+_BUILD_NP = {"src_port": np.uint16, "dst_port": np.uint16, "seq_num": np.uint32, "ack_num": np.uint32,
+             "offset": np.uint8, "control": np.uint8, "window": np.uint16, "urgent_ptr": np.uint16}
+
+
+def tcp_build_host(fields: dict, data: np.ndarray, data_off: np.ndarray, out_off: np.ndarray | None = None,
+                   opts: np.ndarray | None = None, opt_off: np.ndarray | None = None,
+                   partial: np.ndarray | None = None, out: np.ndarray | None = None, want_raw: bool = True,
+                   num_gpus: int = 0, tune=None):
+    """The fused sender pass over host-resident segments (nsx_tcp_build_host): fields = dict of host arrays (a
+    missing or None "offset" is computed on the device, tcp.go:59-66); out_off defaults to nsx_tcp_layout_host;
+    out (host uint8, e.g. a PinnedBuffer's array) is allocated when not given. Returns (out, raw or None)."""
+    data = np.ascontiguousarray(data, np.uint8)
+    data_off = np.ascontiguousarray(data_off, np.uint64)
+    n = data_off.size - 1
+    cols = {}
+    for k, _ in BUILD_FIELDS:
+        v = fields.get(k)
+        if v is None:
+            if k != "offset":
+                raise ValueError(f"tcp_build_host: header field {k!r} missing")
+            continue
+        v = np.ascontiguousarray(v).view(_BUILD_NP[k]) if np.asarray(v).dtype.itemsize == np.dtype(_BUILD_NP[k]).itemsize \
+            else np.ascontiguousarray(v, _BUILD_NP[k])
+        if v.size < n:
+            raise ValueError(f"tcp_build_host {k}: {v.size} entries for {n} segments")
+        cols[k] = v
+    oo = None if opt_off is None else np.ascontiguousarray(opt_off, np.uint64)
+    if oo is not None and opts is None:
+        raise ValueError("tcp_build_host: opt_off given without opts")
+    ob = None if opts is None else (np.ascontiguousarray(opts, np.uint8) if len(opts) else np.zeros(1, np.uint8))
+    if out_off is None:
+        out_off = tcp_layout_host(data_off, oo)
+    out_off = np.ascontiguousarray(out_off, np.uint64)
+    if n > 0 and data.size < int(data_off[-1]):
+        raise ValueError(f"tcp_build_host data: {data.size} B given, data_off ends at {int(data_off[-1])}")
+    if oo is not None and n > 0 and ob.size < int(oo[-1]):
+        raise ValueError(f"tcp_build_host opts: {ob.size} B given, opt_off ends at {int(oo[-1])}")
+    if out is None:
+        out = np.zeros(int(out_off[-1]) if n > 0 else 0, np.uint8)
+    if n > 0 and out.size < int(out_off[-1]):
+        raise ValueError(f"tcp_build_host out: {out.size} B given, out_off ends at {int(out_off[-1])}")
+    part = None if partial is None else np.ascontiguousarray(partial, np.uint32)
+    if part is not None and part.size < n:
+        raise ValueError(f"tcp_build_host partial: {part.size} entries for {n} segments")
+    raw = np.empty(max(n, 0), np.uint16) if want_raw else None
+    soa = TcpHdrSoA(*[_np_ptr(cols.get(k)) for k, _ in BUILD_FIELDS])
+    _check(lib().nsx_tcp_build_host_tuned(ctypes.byref(soa), _np_ptr(ob), _np_ptr(oo), _np_ptr(data),
+                                          _np_ptr(data_off), _np_ptr(part), n, _np_ptr(out), _np_ptr(out_off),
+                                          _np_ptr(raw), num_gpus, _tune(tune)), "nsx_tcp_build_host")
+    return out, raw
 
 
 def fill_splitmix64_dev(buf, seed: int, byte_off: int = 0, stream=None):

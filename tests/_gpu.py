@@ -48,3 +48,12 @@ def mask_words(valid):
     pad = np.zeros((valid.size + 63) // 64 * 64, np.uint8)
     pad[:valid.size] = valid
     return np.packbits(pad, bitorder="little").view(np.uint64)
+
+
+def pseudo_headers(addrs, tcp_len):
+    """(n, 12) IPv4 pseudo-header bytes src(4) dst(4) 0 6 len(2) (RFC 9293 §3.1; ip.Addr.Raw(),
+    network/ip/v4/ipv4.go:15; ip.NextProtoTCP, protocols.go:8) from (2, n, 4) address bytes, as a Go caller
+    would pass ipPseudoHeader (tcp.go:72-73)."""
+    n = addrs.shape[1]
+    return np.ascontiguousarray(np.concatenate(
+        [addrs[0], addrs[1], np.tile(np.array([0, 6, tcp_len >> 8, tcp_len & 0xFF], np.uint8), (n, 1))], 1))

@@ -38,7 +38,7 @@ def test_header_declares_the_boundary():
 def test_library_exports_every_declared_symbol():
     L = nsx.lib()
     declared = declared_functions() + declared_functions(TUNE_HEADER)
-    assert len(declared_functions(TUNE_HEADER)) == 14
+    assert len(declared_functions(TUNE_HEADER)) == 15
     missing = [n for n in declared if not hasattr(L, n)]
     assert not missing, missing
     out = subprocess.run(["nm", "-D", "--defined-only", nsx.LIB_PATH], capture_output=True, text=True).stdout
@@ -359,3 +359,63 @@ def test_receive_grid_modes_off_the_default_grid_are_einval():
                 with pytest.raises(nsx.NsxError) as e:
                     fn(buf, offs, tune=dict(bad, segs_per_wave=mode))
                 assert e.value.code == nsx.NSX_EINVAL, (mode, bad)
+    # values that name no receive form at all are refused on every grid, not run as the auto shape
+    for bad in (3, 4, 9, -1):
+        for extra in ({}, dict(rows=4), dict(blocks_per_cu=2)):
+            for fn in (nsx.rx_ipv4_tcp_verify_host, nsx.rx_ipv6_tcp_verify_host):
+                with pytest.raises(nsx.NsxError) as e:
+                    fn(buf, offs, tune=dict(extra, segs_per_wave=bad))
+                assert e.value.code == nsx.NSX_EINVAL, (bad, extra)
+
+
+def _build_host_case(n=3, pay=10):
+    fields = {k: np.arange(n).astype({1: np.uint8, 2: np.uint16, 4: np.uint32}[s]) for k, s in nsx.BUILD_FIELDS}
+    data_off = np.arange(n + 1, dtype=np.uint64) * np.uint64(pay)
+    return fields, np.zeros(n * pay, np.uint8), data_off
+
+
+def test_tcp_build_host_validates_before_any_device():
+    """nsx_tcp_build_host (the sender pass over host memory) checks every span it will copy before
+    touching a device — on a GPU-less host a well-formed call is NSX_ENODEV and a malformed one NSX_EINVAL: offsets
+    that decrease, image slots that are not 4-aligned or too short for image + padding (nsx_tcp_layout_host's rule),
+    opt_off without opts, a missing header field."""
+    fields, data, data_off = _build_host_case()
+    if nsx.device_count() == 0:
+        with pytest.raises(nsx.NsxError) as e:
+            nsx.tcp_build_host(fields, data, data_off)
+        assert e.value.code == nsx.NSX_ENODEV
+    lay = nsx.tcp_layout_host(data_off)  # 32 B slots: 30 B images + 2 B padding
+    bad_layouts = [lay + np.uint64(2),                                            # not 4-aligned
+                   np.array([0, 32, 60, 96], np.uint64),                          # slot 1 too short
+                   np.array([0, 32, 64, 64], np.uint64)]                          # last slot empty
+    for oo in bad_layouts:
+        with pytest.raises(nsx.NsxError) as e:
+            nsx.tcp_build_host(fields, data, data_off, out_off=oo, out=np.zeros(200, np.uint8))
+        assert e.value.code == nsx.NSX_EINVAL, oo
+    with pytest.raises(nsx.NsxError) as e:  # decreasing data offsets
+        nsx.tcp_build_host(fields, data, np.array([0, 10, 5, 30], np.uint64), out_off=lay, out=np.zeros(200, np.uint8))
+    assert e.value.code == nsx.NSX_EINVAL
+    L = nsx.lib()
+    soa = nsx.TcpHdrSoA(*[None if k == "window" else c.ctypes.data for k, c in
+                          ((k, fields[k]) for k, _ in nsx.BUILD_FIELDS)])
+    out = np.zeros(200, np.uint8)
+    ptr = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    assert L.nsx_tcp_build_host(ctypes.byref(soa), None, None, ptr(data), ptr(data_off), None, 3, ptr(out), ptr(lay),
+                                None, 0) == nsx.NSX_EINVAL  # window missing
+    soa.window = fields["window"].ctypes.data
+    assert L.nsx_tcp_build_host(ctypes.byref(soa), None, ptr(data_off), ptr(data), ptr(data_off), None, 3, ptr(out),
+                                ptr(lay), None, 0) == nsx.NSX_EINVAL  # opt_off without opts
+    assert L.nsx_tcp_build_host(ctypes.byref(soa), None, None, ptr(data), ptr(data_off), None, 0, ptr(out), ptr(lay),
+                                None, 0) == 0  # n == 0: nothing to do
+    # binding extent checks (ValueError before the C call)
+    for kw, msg in ((dict(data=np.zeros(29, np.uint8)), "data_off ends at 30"),
+                    (dict(out=np.zeros(95, np.uint8)), "out_off ends at 96"),
+                    (dict(partial=np.zeros(2, np.uint32)), "partial"),
+                    (dict(opt_off=np.zeros(4, np.uint64)), "opt_off given without opts")):
+        args = dict(fields=fields, data=data, data_off=data_off)
+        args.update(kw)
+        with pytest.raises(ValueError) as e:
+            nsx.tcp_build_host(**args)
+        assert msg in str(e.value), (msg, str(e.value))
+    with pytest.raises(ValueError):
+        nsx.tcp_build_host(dict(fields, seq_num=None), data, data_off)

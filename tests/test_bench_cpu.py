@@ -40,10 +40,22 @@ def test_gpus_2_launches_two_ranks_itself():
     per = line["per_gpu"]
     assert [p["rank"] for p in per] == [0, 1]
     for p in per:
-        assert set(p) == {"rank", "device", "gib_s", "wall_s", "kernel_ms", "roofline_frac"}
-        assert p["gib_s"] > 0 and p["wall_s"] > 0
+        assert set(p) == {"rank", "device", "gib_s", "own_s", "wall_s", "kernel_ms", "roofline_frac"}
+        assert p["gib_s"] > 0 and 0 < p["own_s"] <= p["wall_s"]
     assert line["value_per_gpu_mean"] == pytest.approx(line["value"] / 2, abs=1e-3)
     assert min(p["gib_s"] for p in per) >= line["value"] / 2 - 1e-3  # the aggregate uses the slowest wall
+
+
+def test_per_gpu_rate_uses_each_ranks_own_clock():
+    """the barrier-closed wall is the slowest rank's time on every rank, so a per-GPU rate from it
+    cannot show a slow GPU; per_gpu uses each rank's own clock (own_s, closed before the closing barrier)."""
+    stats = [{"rank": r, "device": f"h/{r}", "wall_s": 1.25, "own_s": 1.0 if r != 1 else 1.25, "step_ms": 0.2}
+             for r in range(2)]
+    line = bench.result_line(world=2, steps=10, warmup=1, wall_max=1.25, bytes_per_rank_step=1 << 30,
+                             units_total=2, workload="w", cfg={"n": 1, "seed": 1}, launch_ms=[0.2],
+                             alg_bytes_per_launch=1 << 30, cpu_baseline=None, traffic=None, rank_stats=stats)
+    assert [p["gib_s"] for p in line["per_gpu"]] == [10.0, 8.0]
+    assert line["value"] == pytest.approx(16.0)
 
 
 def test_per_gpu_entries_show_a_slow_gpu():

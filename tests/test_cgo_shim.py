@@ -23,7 +23,7 @@ from conftest import ROOT
 
 GO_DIR = os.path.join(ROOT, "network-stack_amd", "go", "transport", "tcp")
 HEADER = os.path.join(ROOT, "include", "nsx_csum.h")
-SHIM_FILES = ("checksum_nsx.go", "batch_nsx.go", "rx_nsx.go")
+SHIM_FILES = ("checksum_nsx.go", "batch_nsx.go", "rx_nsx.go", "build_nsx.go")
 
 
 def _norm(t: str) -> str:
@@ -48,6 +48,12 @@ def header_prototypes() -> dict:
                 types.append(_norm(pm.group(1)))
         protos[name] = (_norm(ret), types)
     return protos
+
+
+def header_typedefs() -> set:
+    """The struct typedef names include/nsx_csum.h declares (cgo's C.<name>)."""
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    return set(re.findall(r"typedef\s+struct\s*\{[^}]*\}\s*(\w+)\s*;", src))
 
 
 def header_constants() -> set:
@@ -183,7 +189,29 @@ def test_every_c_call_matches_the_header(shim):
             seen.add(fn)
     # the shim's surface: single-segment host sum, pinned staging, the host batch and receive passes
     assert seen >= {"nsx_csum16", "nsx_strerror", "nsx_alloc_pinned", "nsx_free_pinned", "nsx_csum_ragged_host",
-                    "nsx_rx_ipv4_tcp_verify_host", "nsx_rx_ipv6_tcp_verify_host"}, seen
+                    "nsx_rx_ipv4_tcp_verify_host", "nsx_rx_ipv6_tcp_verify_host", "nsx_tcp_build_host",
+                    "nsx_tcp_wire_len"}, seen
+
+
+def test_struct_fields_the_shim_sets_exist(shim):
+    """Every `h.<field> = (*C.<type>)(...)` the sender shim writes into a C struct names a member the header's
+    struct declares, with the member's type (const stripped) — what cgo checks for struct field assignments."""
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    members = {}
+    for body, name in re.findall(r"typedef\s+struct\s*\{([^}]*)\}\s*(\w+)\s*;", src):
+        for t, m in re.findall(r"((?:const\s+)?\w+\s*\*?)\s*(\w+)\s*;", body):
+            members[(name, m)] = _norm(t)
+    checked = 0
+    for gf in shim:
+        for var, typ in gf.vars.items():
+            tm = re.fullmatch(r"C\.(\w+)", typ)
+            if not tm or tm.group(1) not in header_typedefs():
+                continue
+            for fld, rhs in re.findall(rf"\b{var}\.(\w+)\s*=\s*([^\n]+)", gf.src):
+                assert (tm.group(1), fld) in members, f"{gf.path}: {tm.group(1)} has no member {fld}"
+                assert go_to_c(gf.expr_type(rhs)) == members[(tm.group(1), fld)], (gf.path, fld, rhs)
+                checked += 1
+    assert checked == 8  # build_nsx.go fills all eight nsx_tcp_hdr_soa members
 
 
 def test_constants_types_and_preamble(shim):
@@ -193,7 +221,8 @@ def test_constants_types_and_preamble(shim):
         for c in set(re.findall(r"\bC\.(NSX_\w+)", gf.src)):
             assert c in consts, f"{gf.path}: C.{c} is not #defined in include/nsx_csum.h"
         for t in set(re.findall(r"\bC\.(\w+)", gf.src)) - {c for c in consts} - set(protos) - {"GoString"}:
-            assert t in ("uint8_t", "uint16_t", "uint32_t", "uint64_t", "size_t", "int"), (gf.path, t)
+            assert t in ("uint8_t", "uint16_t", "uint32_t", "uint64_t", "size_t", "int") or t in header_typedefs(), \
+                (gf.path, t)
         assert '#include "nsx_csum.h"' in open(gf.path).read(), gf.path
         assert open(gf.path).read().startswith("//go:build nsx"), gf.path
     assert "#cgo LDFLAGS: -lnsx_csum" in open(os.path.join(GO_DIR, "checksum_nsx.go")).read()

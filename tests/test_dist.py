@@ -8,6 +8,7 @@ import json
 import multiprocessing as mp
 import os
 import socket
+import time
 
 import numpy as np
 import pytest
@@ -44,10 +45,12 @@ def _worker(rank, world, port, q):
 
         def step():
             res["out"] = O.c_batch(buf, n, stride=L, seg_len=L, threads=1)
+            if rank == 1:  # a slow GPU: its own rate must show it
+                time.sleep(0.05)
 
-        wall, launch_ms = bench.timed_loop(step, lambda: None, d.barrier, steps=4, warmup=1)
+        wall, launch_ms, own = bench.timed_loop(step, lambda: None, d.barrier, steps=4, warmup=1)
         wmax = d.max(wall)
-        stats = d.gather({"rank": rank, "device": f"cpu{rank}", "wall_s": wall, "step_ms": 0.5 + rank})
+        stats = d.gather({"rank": rank, "device": f"cpu{rank}", "wall_s": wall, "own_s": own, "step_ms": 0.5 + rank})
         line = bench.result_line(world=world, steps=4, warmup=1, wall_max=wmax, bytes_per_rank_step=n * L,
                                  units_total=n * world, workload="gloo-test", cfg={"n": n, "seed": 0x1071},
                                  launch_ms=launch_ms, alg_bytes_per_launch=n * L + 2 * n, cpu_baseline=None,
@@ -66,7 +69,7 @@ def _worker(rank, world, port, q):
         dist.all_gather_object(gathered, (lo, hi, mine.tolist()))
         full = O.c_batch(rb, lens.size, offsets=offs)
         stitched = [x for _, _, part in sorted(gathered) for x in part]
-        q.put(json.dumps({"rank": rank, "wall": wall, "wmax": wmax, "value": line["value"],
+        q.put(json.dumps({"rank": rank, "wall": wall, "own": own, "wmax": wmax, "value": line["value"],
                           "value_per_gpu_mean": line["value_per_gpu_mean"], "per_gpu": line["per_gpu"],
                           "n_gpus": line["n_gpus"], "stitched_ok": stitched == full.tolist(),
                           "sizes": [int(offs[b2] - offs[b1]) for b1, b2 in zip(bounds[:-1], bounds[1:])]}))
@@ -100,8 +103,10 @@ def test_bench_dist_logic_gloo_ws2():
         assert [p["rank"] for p in per] == [0, 1] and [p["device"] for p in per] == ["cpu0", "cpu1"]
         for p in per:
             # (gib_s is rounded to 3 decimals: at ~0.3 GiB/s that is up to 0.2%, so compare absolutely too)
-            assert p["gib_s"] == pytest.approx(512 * 1500 * 4 / by[p["rank"]]["wall"] / GIB, rel=1e-3, abs=6e-4)
+            assert p["gib_s"] == pytest.approx(512 * 1500 * 4 / by[p["rank"]]["own"] / GIB, rel=1e-3, abs=6e-4)
             assert p["gib_s"] >= r["value"] / 2 - 1e-3                               # no rank slower than the max
+            assert by[p["rank"]]["own"] <= by[p["rank"]]["wall"] + 1e-9                # own clock closes first
+        assert per[1]["gib_s"] < 0.8 * per[0]["gib_s"]  # the slow rank shows in its own rate
         assert per[0]["kernel_ms"] == 0.5 and per[1]["kernel_ms"] == 1.5
         assert per[0]["roofline_frac"] == pytest.approx((512 * 1502) / 0.5e-3 / 1e9 / 8000, abs=1e-4)
         assert r["stitched_ok"]                      # shards cover the batch exactly once

@@ -13,7 +13,7 @@ import os
 import numpy as np
 import pytest
 
-from _gpu import dev, host, run_fixed, run_ragged, setup_gpu, torch, u16
+from _gpu import dev, host, pseudo_headers, run_fixed, run_ragged, setup_gpu, torch, u16
 from conftest import GOLDEN
 from oracle import csum_oracle as O
 
@@ -181,13 +181,6 @@ def ipv4_pseudo_partials(addrs: np.ndarray, tcp_len: int) -> np.ndarray:
     ip.Addr.Raw(), network/ip/v4/ipv4.go:15; ip.NextProtoTCP, protocols.go:8), from (2, n, 4) address bytes."""
     a = addrs.astype(np.uint32)
     return ((a[..., 0] << 8) + a[..., 1] + (a[..., 2] << 8) + a[..., 3]).sum(0).astype(np.uint32) + 6 + tcp_len
-
-
-def pseudo_headers(addrs: np.ndarray, tcp_len: int) -> np.ndarray:
-    """(n, 12) pseudo-header bytes, as a Go caller would pass ipPseudoHeader (tcp.go:72-73)."""
-    n = addrs.shape[1]
-    return np.ascontiguousarray(np.concatenate(
-        [addrs[0], addrs[1], np.tile(np.array([0, 6, tcp_len >> 8, tcp_len & 0xFF], np.uint8), (n, 1))], 1))
 
 
 def test_config2_1M_x_1500_full():

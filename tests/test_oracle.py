@@ -182,6 +182,10 @@ def test_c_go_tcp_build_matches_segment_model():
         assert raw[i] == r
         s.checksum = O.field_value(r)
         assert wire[int(out_off[i]):int(out_off[i + 1])].tobytes() == s.bytes()
+    # the threaded form (full-size GPU checks of workloads 6 and 12) is the same loop over index shards
+    for t in (1, 3, 16):
+        w2, r2 = O.c_go_tcp_build_mt(fields, data, data_off, out_off, pseudo, threads=t)
+        assert np.array_equal(w2, wire) and np.array_equal(r2, raw), t
 
 
 def test_c_go_tcp_build_opts_matches_segment_model():
@@ -228,6 +232,9 @@ def test_c_go_tcp_build_opts_matches_segment_model():
         assert raw[i] == r, i
         sg.checksum = O.field_value(r)
         assert wire[int(out_off[i]):int(out_off[i + 1])].tobytes() == sg.bytes(), i
+    for t in (1, 7):  # the threaded form (full-size GPU check of workload 8)
+        w2, r2 = O.c_go_tcp_build_mt(fields, data, data_off, out_off, pseudo, opts=opts, opt_off=opt_off, threads=t)
+        assert np.array_equal(w2, wire) and np.array_equal(r2, raw), t
 
 
 def test_cpu_fast_line_matches_go_checksum():

@@ -5,6 +5,7 @@
 set -u
 n=${1:-2}
 mkdir -p gpurun_out
+make -s -j16 -C network-stack_amd || exit 1  # ranks under a launcher never build (bench.py)
 NSX_BENCH_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" \
   --master-addr 127.0.0.1 --master-port 29561 bench.py --gpus "$n" --steps 50 --warmup 5 \
   > gpurun_out/dist_rehearsal_n$n.log 2>&1

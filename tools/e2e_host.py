@@ -5,7 +5,8 @@ nsx_csum_ragged_host — pinned H2D → kernel → D2H, double-buffered over two
 streams per GPU — on config 2 (1M x 1500 B) and config 3 (1M ragged) batches
 held in pinned memory (nsx_alloc_pinned) and in pageable numpy memory, and the
 fused receive pass from host memory (nsx_rx_ipv4_tcp_verify_host) over ~770 MB of
-received datagrams (a mixed batch of tests/_rx.py tiled 200 times).
+received datagrams (a mixed batch of tests/_rx.py tiled 200 times), and the fused
+sender pass from host memory (nsx_tcp_build_host) on bench workload 6's shape.
 Results are spot-checked against the oracle (tools are test infrastructure).
 
     python tools/e2e_host.py [--reps 5] [--gpus 0]
@@ -104,6 +105,41 @@ def main():
                      "frames": int(yoffs.size - 1)}
         print(name, json.dumps(res[name]), flush=True)
     ypin.free()
+    # the sender pass from host memory (nsx_tcp_build_host): bench workload 6's shape — 1M option-less segments,
+    # 1480 B payloads, IPv4 pseudo-header partials — fields, payloads and partials in host memory, the 1500 B wire
+    # images and raw sums back into host memory. Rate by wire bytes; PCIe bytes = H2D (payload + 18 B fields + 16 B
+    # offsets + 4 B partial) + D2H (image + 2 B raw) per segment.
+    P, W = 1480, 1500
+    brng = np.random.default_rng(0x1074)
+    fields = {k: brng.integers(0, 1 << (8 * np.dtype(dt).itemsize), n, dtype=np.uint64).astype(dt)
+              for k, dt in zip(O.TCP_FIELDS, O.TCP_FIELD_DTYPES)}
+    fields["offset"][:] = 5
+    pseudo = np.concatenate([brng.integers(0, 256, (n, 8), dtype=np.uint8),
+                             np.tile(np.array([0, 6, W >> 8, W & 0xFF], np.uint8), (n, 1))], 1)
+    pw = pseudo.reshape(n, 6, 2).astype(np.uint32)
+    part = ((pw[..., 0] << 8) | pw[..., 1]).sum(1).astype(np.uint32)
+    data_off = np.arange(n + 1, dtype=np.uint64) * np.uint64(P)
+    out_off = nsx.tcp_layout_host(data_off)
+    dpage = O.c_splitmix64(0x1074, n * P)
+    dpin, opin = nsx.PinnedBuffer(n * P), nsx.PinnedBuffer(n * W)
+    dpin.array[:] = dpage
+    opage = np.zeros(n * W, np.uint8)
+    sel = np.arange(0, n, 4099)
+    sfields = {k: v[sel] for k, v in fields.items()}
+    sdata = np.concatenate([dpage[i * P:(i + 1) * P] for i in sel])
+    want, wraw = O.c_go_tcp_build(sfields, sdata, np.arange(sel.size + 1, dtype=np.uint64) * np.uint64(P),
+                                  np.arange(sel.size + 1, dtype=np.uint64) * np.uint64(W), pseudo[sel])
+    pcie = n * (P + 18 + 16 + 4) + n * (W + 2)
+    for name, d, o in (("build_pinned", dpin.array, opin.array), ("build_pageable", dpage, opage)):
+        t, (img, raw) = timed(lambda: nsx.tcp_build_host(fields, d, data_off, out_off=out_off, partial=part, out=o,
+                                                         num_gpus=a.gpus), a.reps)
+        assert np.array_equal(raw[sel], wraw), name
+        assert np.array_equal(np.concatenate([img[i * W:(i + 1) * W] for i in sel]), want), name
+        res[name] = {"seconds": t, "GB_per_s": n * W / t / 1e9, "GiB_per_s": n * W / t / (1 << 30),
+                     "pcie_GB_per_s_both_directions": pcie / t / 1e9, "segments": n}
+        print(name, json.dumps(res[name]), flush=True)
+    dpin.free()
+    opin.free()
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "e2e_host.json"), "w") as f:
         json.dump(res, f, indent=1)
