@@ -557,11 +557,13 @@ def test_tcp_build_host_gaps_offset_none_no_raw_and_the_device_call():
     assert np.array_equal(host(out), img_h) and np.array_equal(u16(rawd), raw_h)
     # many chunks: 60K workload-6-shaped segments (~90 MB of images), two shards
     m, P, W = 60_000, 1480, 1500
-    fw = {k: v[:m] for k, v in fields.items()}
+    fw = {k: rng.integers(0, 1 << (8 * np.dtype(dt).itemsize), m, dtype=np.uint64).astype(dt)
+          for k, dt in zip(O.TCP_FIELDS, O.TCP_FIELD_DTYPES)}
     fw["offset"] = np.full(m, 5, np.uint8)
     dw = O.c_splitmix64(0x1074, m * P)
     doff = np.arange(m + 1, dtype=np.uint64) * np.uint64(P)
-    ps = np.concatenate([pseudo[:m, :8], np.tile(np.array([0, 6, W >> 8, W & 0xFF], np.uint8), (m, 1))], 1)
+    ps = np.concatenate([rng.integers(0, 256, (m, 8), dtype=np.uint8),
+                         np.tile(np.array([0, 6, W >> 8, W & 0xFF], np.uint8), (m, 1))], 1)
     pw = ps.reshape(m, 6, 2).astype(np.uint32)
     pp = ((pw[..., 0] << 8) | pw[..., 1]).sum(1).astype(np.uint32)
     wwant, wwraw = O.c_go_tcp_build_mt(fw, dw, doff, np.arange(m + 1, dtype=np.uint64) * np.uint64(W), ps)
