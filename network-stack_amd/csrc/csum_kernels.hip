@@ -966,7 +966,9 @@ __device__ __forceinline__ uint32_t lds_range_sum(const lds16* slot, uint32_t p,
     // nearly every wave. A lane whose range has ended (j0 ≥ nch) reads its block from c0 again instead of c0 + j0,
     // so no lane reads more than 3 chunks past its range: in a run that mixes a several-KB unit with small ones, j0
     // runs up to the long unit's chunk count, and c0 + j0 would leave the slot.
-    const uint32_t nmax = wave_max(nch);
+    // Only a wave with a range past the first block pays for the wave maximum (round 5: 4 DPP + 4 v_readlane per run
+    // on every run of small units before; one compare and a scalar test now).
+    const bool more = __builtin_amdgcn_ballot_w64(nch > 8u) != 0;
     uint32_t acc;
     {
         u32x4 x[8];
@@ -990,15 +992,18 @@ __device__ __forceinline__ uint32_t lds_range_sum(const lds16* slot, uint32_t p,
             acc += j < nch ? s4 : 0u;
         }
     }
-    for (uint32_t j0 = 8; j0 < nmax; j0 += 4u) {
-        u32x4 x[4];
-        const lds16* blk = slot + c0 + (j0 < nch ? j0 : 0u);
+    if (more) {
+        const uint32_t nmax = wave_max(nch);
+        for (uint32_t j0 = 8; j0 < nmax; j0 += 4u) {
+            u32x4 x[4];
+            const lds16* blk = slot + c0 + (j0 < nch ? j0 : 0u);
 #pragma unroll
-        for (uint32_t j = 0; j < 4u; ++j) x[j] = lds_get(blk, j);
+            for (uint32_t j = 0; j < 4u; ++j) x[j] = lds_get(blk, j);
 #pragma unroll
-        for (uint32_t j = 0; j < 4u; ++j) {
-            const uint32_t s4 = sad4(x[j], 0u);
-            acc += j0 + j < nch ? s4 : 0u;
+            for (uint32_t j = 0; j < 4u; ++j) {
+                const uint32_t s4 = sad4(x[j], 0u);
+                acc += j0 + j < nch ? s4 : 0u;
+            }
         }
     }
     return acc;
@@ -1205,7 +1210,8 @@ __device__ __forceinline__ uint32_t pfx_stage(lds16* slot, u32x4 (&V)[VR], uint3
 // prefix sums and summed lane by lane (lds_range_sum, the LDS form, 3-6% faster on runs of ACKs alone: no per-row
 // scans); the slot (PfxSlot<7>, 9040 B) holds either layout.
 //   out(F, p, d0, live, a, s, cnt, off, end)  the results of units [a + s, a + s + cnt) (lane l = unit a + l):
-//                                      F = the unit's weighted sum, p its slot position, d0 = the slot dword at p/4;
+//                                      F = the unit's weighted sum (32-bit), p its slot position, d0 = the slot dword
+//                                      at p/4;
 //   stream(a, s, rem, off, end)        units [a + s, a + s + rem) of the run at a in the streaming form (lane l of
 //                                      off / end = unit a + l).
 template <uint32_t ROWS, bool HYB, uint32_t ALIGN, typename Out, typename Stream>
@@ -1302,7 +1308,7 @@ __device__ __forceinline__ void pfx_runs(const uint8_t* __restrict__ base, __amd
             const bool live = live_of(cur);
             const uint32_t p = live ? (uint32_t)((base + c_off) - cur.rbase) : 0u;
             const uint32_t d0 = sdw[p >> 2];
-            uint64_t F;
+            uint32_t F;  // < 2^32: a slot's bytes
             if (HYB && cur.direct) {
                 const uint32_t e = live ? (uint32_t)((base + c_end) - cur.rbase) : 0u;
                 F = lds_range_sum(slot, p, e, d0, live);
@@ -1315,7 +1321,7 @@ __device__ __forceinline__ void pfx_runs(const uint8_t* __restrict__ base, __amd
                 const uint32_t pq = q == 0u ? 0u : q == 1u ? pre1 : q == 2u ? pre2 : pre3;
                 const uint32_t sp = I[p >> 4] + __builtin_amdgcn_sad_u16(d0 & ((1u << (8u * (p & 3u))) - 1u), 0u, pq);
                 const uint32_t sn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sp, 0x130, 0xF, 0xF, false);  // wave_shl:1
-                F = (uint32_t)((lane == cur.s + cur.cnt - 1u ? total : sn) - sp);
+                F = (lane == cur.s + cur.cnt - 1u ? total : sn) - sp;
             }
             out(F, p, d0, live, a, cur.s, cur.cnt, c_off, c_end);
         }
@@ -1479,26 +1485,40 @@ constexpr uint32_t kRxBigMean = 640;
 // weighted byte sum F (exact; weights 1 / 256 at even / odd addresses, the LE half-sum rule) and writes the run's
 // mask bytes and the raw sums. d[0..5] = the dwords from the frame's start rounded down to 4 B (hd = start & 3;
 // IPv6 reads d[0..2]); opt(o) fills the IPv4 option dwords 6..15, called only when some lane has IHL > 5.
+//
+// Everything is summed in F's own domain (round 5): F is the BE one's-complement sum for an
+// odd start and its byte swap for an even one, and a byte swap is a multiplication by 256 modulo 0xFFFF (256·256 ≡ 1),
+// so the pseudo-header words are added in that domain too — rotated by the frame's start parity like the header
+// dwords, the length term shifted up a byte for an even start — and the receiver rule (raw == 0xFFFF, tcp.go:70)
+// is checked on fold(F − header + pseudo) directly: 0xFFFF is its own byte swap and every sum here is nonzero (the
+// pseudo part alone is ≥ 6), so the verdict equals the BE raw sum's. Only a caller asking for raw sums pays the
+// swap back to BE (round 4 swapped and folded both sums per frame on every call). The IPv4 header check is
+// fold(hs) == 0xFFFF, likewise swap-free.
 struct RxHdr {
     uint32_t hs;   // the header's weighted sum (IPv6: bytes 0-7), subtracted from F when hdr_ok
-    uint32_t aux;  // the pseudo-header's words not in F: IPv4 src + dst + 6 + TCP length; IPv6 payload length + 6
-    uint32_t ipr;  // IPv4 header raw sum (0 unless hdr_ok)
+    uint32_t aux;  // the pseudo-header's words not in F, in F's domain: IPv4 src + dst + 6 + TCP length; IPv6 payload
+                   // length + 6
     bool hdr_ok, well;
 };
 
-template <bool V6, typename OptFn>
-__device__ __forceinline__ RxHdr rx_hdr(const uint32_t (&d)[6], uint32_t hd, uint64_t flen, bool even, bool live,
-                                        OptFn&& opt) {
+// 16-bit byte swap of a value ≤ 0xFFFF: one v_perm_b32 (bytes 1, 0 of x; zeros above)
+__device__ __forceinline__ uint32_t swap16(uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x0C0C0001u); }
+
+// Frame lengths as the form has them: 64-bit in the streamed form (frames of any length), 32-bit where a frame lies
+// in a wave's slot (the LDS, hybrid and prefix forms: e − p < 2^15), which keeps the parse's compares single-word.
+template <bool V6, typename Len, typename OptFn>
+__device__ __forceinline__ RxHdr rx_hdr(const uint32_t (&d)[6], uint32_t hd, Len flen, bool live, OptFn&& opt) {
+    const uint32_t rot = hd & 1u;         // F's domain: the frame-relative dwords rotated one byte for an odd start
+    const uint32_t sh = (rot ^ 1u) << 3;  // ... and a BE term shifted up a byte for an even one
     if constexpr (V6) {
         const uint32_t H0 = __builtin_amdgcn_alignbyte(d[1], d[0], hd);  // version, class, flow label
         const uint32_t H1 = __builtin_amdgcn_alignbyte(d[2], d[1], hd);  // payload length, next header
-        const uint32_t plen = bswap16u(H1 & 0xFFFFu);
-        const bool well = live && flen >= 40u && (H0 & 0xF0u) == 0x60u && plen + 40u == flen &&
+        const uint32_t plen = swap16(H1 & 0xFFFFu);
+        const bool well = live && flen >= (Len)40 && (H0 & 0xF0u) == 0x60u && (Len)(plen + 40u) == flen &&
                           ((H1 >> 16) & 0xFFu) == 6u && plen >= 20u;  // tcp.go:131
-        const uint32_t rot = hd & 1u;  // see the IPv4 header sum below
         const uint32_t h8 = __builtin_amdgcn_sad_u16(__builtin_amdgcn_alignbyte(H1, H1, rot), 0u,
                                                      __builtin_amdgcn_sad_u16(__builtin_amdgcn_alignbyte(H0, H0, rot), 0u, 0u));
-        return RxHdr{h8, plen + 6u, 0u, true, well};  // F − h8 = addresses ‖ segment
+        return RxHdr{h8, (plen + 6u) << sh, true, well};  // F − h8 = addresses ‖ segment
     } else {
         // IPv4 header fields (RFC 791 §3.1): header dword m = bytes 4m..4m+3, little-endian view.
         const uint32_t H0 = __builtin_amdgcn_alignbyte(d[1], d[0], hd);
@@ -1507,17 +1527,16 @@ __device__ __forceinline__ RxHdr rx_hdr(const uint32_t (&d)[6], uint32_t hd, uin
         const uint32_t H3 = __builtin_amdgcn_alignbyte(d[4], d[3], hd);
         const uint32_t H4 = __builtin_amdgcn_alignbyte(d[5], d[4], hd);
         const uint32_t ihl = H0 & 15u, hlen = ihl * 4u;
-        const uint32_t total = bswap16u(H0 >> 16);
-        const uint32_t frag = bswap16u(H1 >> 16);  // flags + fragment offset
+        const uint32_t total = swap16(H0 >> 16);
+        const uint32_t frag = H1 >> 16;  // flags + fragment offset, byte-swapped: the 0x3FFF field is 0xFF3F here
         const uint32_t proto = (H2 >> 8) & 0xFFu;
-        const bool hdr_ok = live && flen >= 20u && ihl >= 5u && hlen <= flen;
-        const bool well = hdr_ok && (H0 & 0xF0u) == 0x40u && total == flen && (frag & 0x3FFFu) == 0u &&
+        const bool hdr_ok = live && flen >= (Len)20 && ihl >= 5u && (Len)hlen <= flen;
+        const bool well = hdr_ok && (H0 & 0xF0u) == 0x40u && (Len)total == flen && (frag & 0xFF3Fu) == 0u &&
                           proto == 6u && total - hlen >= 20u;  // tcp.go:131: a segment is at least 20 bytes
         // Header sum over bytes [start, start + hlen), hlen = 4·IHL: the frame-relative dwords H_j, j < IHL, whole.
         // F weights bytes by address parity (the LE half-sum rule), so for an odd start each H_j is rotated one
         // byte before its v_sad_u16 (the halves then pair byte 1 with 2 and 3 with 0): no byte masks (round 2's
         // keep_mask per window dword cost ~45 VALU per frame set).
-        const uint32_t rot = hd & 1u;
         auto hsum = [&](uint32_t h, uint32_t acc) {
             return __builtin_amdgcn_sad_u16(__builtin_amdgcn_alignbyte(h, h, rot), 0u, acc);
         };
@@ -1533,41 +1552,44 @@ __device__ __forceinline__ RxHdr rx_hdr(const uint32_t (&d)[6], uint32_t hd, uin
                 lo = o[j - 5];
             }
         }
-        const uint32_t ipr = hdr_ok ? finish(hs, even, 0u) : 0u;
-        // Pseudo-header source and destination (header dwords 3-4) as BE words: Σ bswap16(half) = the v_sad_u16
-        // of the dword rotated one byte.
-        const uint32_t pseudo = __builtin_amdgcn_sad_u16(
-            __builtin_amdgcn_alignbyte(H4, H4, 1u), 0u,
-            __builtin_amdgcn_sad_u16(__builtin_amdgcn_alignbyte(H3, H3, 1u), 0u, 6u + ((total - hlen) & 0xFFFFu)));
-        return RxHdr{hs, pseudo, ipr, hdr_ok, well};
+        // Pseudo-header source and destination (header dwords 3-4) and 0, 6, TCP length, in F's domain: the
+        // address dwords rotated like the header's (BE words for an odd start, LE half-sums — the swapped words — for
+        // an even one), the constant words shifted up a byte for an even start.
+        const uint32_t pseudo = hsum(H4, hsum(H3, (6u + ((total - hlen) & 0xFFFFu)) << sh));
+        return RxHdr{hs, pseudo, hdr_ok, well};
     }
 }
 
-template <bool V6>
-__device__ __forceinline__ void rx_verdict(uint64_t F, const RxHdr& h, bool even, bool live, uint32_t ak, uint32_t cnt,
+template <bool V6, typename Sum>
+__device__ __forceinline__ void rx_verdict(Sum F, const RxHdr& h, bool even, bool live, uint32_t ak, uint32_t cnt,
                                            uint32_t n, uint32_t lane, const RxOuts& ro, uint32_t s) {
-    const uint64_t T = F - (h.hdr_ok ? h.hs : 0u);  // the TCP segment's weighted sum (IPv6: addresses ‖ segment)
-    const uint32_t tle = fold32((uint32_t)T) + fold32((uint32_t)(T >> 32));
-    const uint32_t tcpr = h.well ? finish(tle, even, h.aux) : 0u;
-    const uint64_t bits = __builtin_amdgcn_ballot_w64(h.well && (V6 || h.ipr == 0xFFFFu) && tcpr == 0xFFFFu);
+    const Sum T = F - (Sum)(h.hdr_ok ? h.hs : 0u);  // the TCP segment's weighted sum (IPv6: addresses ‖ segment)
+    uint32_t tle;
+    if constexpr (sizeof(Sum) == 8) tle = fold32((uint32_t)T) + fold32((uint32_t)(T >> 32));
+    else tle = fold32(T);
+    const uint32_t tf = fold32(tle + h.aux);  // ≡ the raw TCP sum, in F's domain (≥ 1)
+    const uint32_t ipf = fold32(h.hs);        // ≡ the IPv4 header's raw sum, in F's domain
+    const uint64_t bits = __builtin_amdgcn_ballot_w64(h.well && (V6 || ipf == 0xFFFFu) && tf == 0xFFFFu);
     rx_store_mask(ro.mrs, bits, ak, cnt, n, lane, s);
-    if (ro.raw) {
+    if (ro.raw) {  // the raw sums in BE (tcp.go:94): back out of F's domain
+        const uint32_t tcpr = h.well ? (even ? swap16(tf) : tf) : 0u;
+        const uint32_t ipr = h.hdr_ok ? (even ? swap16(ipf) : ipf) : 0u;
         if (ro.tpk.buf) {  // parked (the streamed form: frames [ak, ak + cnt), live = lane < cnt)
-            if constexpr (!V6) park_put(ro.ipk, ak, cnt, lane, h.ipr);
+            if constexpr (!V6) park_put(ro.ipk, ak, cnt, lane, ipr);
             park_put(ro.tpk, ak, cnt, lane, tcpr);
         } else {
             if constexpr (!V6)
-                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)h.ipr, ro.irs, live ? (ak + lane) * 2u : kOOB, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ipr, ro.irs, live ? (ak + lane) * 2u : kOOB, 0, 0);
             __builtin_amdgcn_raw_buffer_store_b16((uint16_t)tcpr, ro.trs, live ? (ak + lane) * 2u : kOOB, 0, 0);
         }
     }
 }
 
-template <bool V6, typename OptFn>
-__device__ __forceinline__ void rx_frame_out(uint64_t F, const uint32_t (&d)[6], uint32_t hd, uint64_t flen, bool even,
+template <bool V6, typename Sum, typename Len, typename OptFn>
+__device__ __forceinline__ void rx_frame_out(Sum F, const uint32_t (&d)[6], uint32_t hd, Len flen, bool even,
                                              bool live, uint32_t ak, uint32_t cnt, uint32_t n, uint32_t lane,
                                              const RxOuts& ro, OptFn&& opt, uint32_t s = 0) {
-    rx_verdict<V6>(F, rx_hdr<V6>(d, hd, flen, even, live, opt), even, live, ak, cnt, n, lane, ro, s);
+    rx_verdict<V6>(F, rx_hdr<V6>(d, hd, flen, live, opt), even, live, ak, cnt, n, lane, ro, s);
 }
 
 // One run of NS sets of ≤ 64 frames in the streaming form: frame a + 64k + lane = [my_off[k], my_end[k]) for
@@ -1713,7 +1735,7 @@ __device__ __forceinline__ void rx_runs_pfx(const uint8_t* __restrict__ base, __
                                             const RxOuts& ro) {
     static_assert(kPfxRun == kRxRun && kPfxDirectSlot == kRxSlot, "the receive pass's runs and direct slot");
     const uint32_t* sdw = reinterpret_cast<const uint32_t*>(slot);
-    auto out = [&](uint64_t F, uint32_t p, uint32_t d0, bool live, uint32_t a, uint32_t s, uint32_t cnt, uint64_t off,
+    auto out = [&](uint32_t F, uint32_t p, uint32_t d0, bool live, uint32_t a, uint32_t s, uint32_t cnt, uint64_t off,
                    uint64_t end) {
         const uint32_t w0 = p >> 2;
         uint32_t d[6];
@@ -1725,7 +1747,8 @@ __device__ __forceinline__ void rx_runs_pfx(const uint8_t* __restrict__ base, __
 #pragma unroll
             for (int j = 6; j < 16; ++j) o[j - 6] = sdw[w0 + j];
         };
-        rx_frame_out<V6>(F, d, p & 3u, end - off, (p & 1u) == 0, live, a, cnt, n, lane, ro, opt, s);
+        // a live frame lies in the slot (< 2^15 bytes): its length from the offsets' low words
+        rx_frame_out<V6>(F, d, p & 3u, (uint32_t)end - (uint32_t)off, (p & 1u) == 0, live, a, cnt, n, lane, ro, opt, s);
     };
     auto stream = [&](uint32_t a, uint32_t s, uint32_t rem, uint64_t off, uint64_t end) {  // lanes shifted by s
         uint32_t cnt1[1] = {rem};
@@ -1750,12 +1773,12 @@ __device__ __forceinline__ void rx_run_lds(const uint8_t* __restrict__ base, con
 #pragma unroll
     for (int j = 0; j < (V6 ? 3 : 6); ++j) d[j] = sdw[w0 + j];
     if constexpr (V6) d[3] = d[4] = d[5] = 0u;
-    const uint64_t F = lds_range_sum(slot, p, e, d[0], live);  // the frame's weighted sum
+    const uint32_t F = lds_range_sum(slot, p, e, d[0], live);  // the frame's weighted sum (< 2^32: ≤ 8 KiB)
     auto opt = [&](uint32_t (&o)[10]) {
 #pragma unroll
         for (int j = 6; j < 16; ++j) o[j - 6] = sdw[w0 + j];
     };
-    rx_frame_out<V6>(F, d, hd, my_end - my_off, (p & 1u) == 0, live, a, cnt, n, lane, ro, opt);
+    rx_frame_out<V6>(F, d, hd, e - p, (p & 1u) == 0, live, a, cnt, n, lane, ro, opt);
 }
 
 // A wave's runs [a0, a_end) in the LDS form (runs of 64 frames from a multiple of 8, as rx_runs).
