@@ -1293,7 +1293,11 @@ __device__ __forceinline__ void pfx_runs(const uint8_t* __restrict__ base, __amd
             lds_stage<VR>(slot, V, cur.span, lane);
             lds_zero_tail(slot, cur.span, lane);
         } else {
+#if defined(NSX_RX_DIAG) && NSX_RX_DIAG == 4
+            lds_stage<VR>(slot, V, cur.span, lane);  // diagnostic build only: rows staged, no chunk prefix sums
+#else
             total = pfx_stage<ROWS, VR>(slot, V, cur.span, lane);
+#endif
         }
         // The next piece: the rest of this run, or the next run (whose offsets are already loaded).
         const bool adv = cur.cnt == cur.rem;
@@ -1738,6 +1742,11 @@ __device__ __forceinline__ void rx_runs_pfx(const uint8_t* __restrict__ base, __
     auto out = [&](uint32_t F, uint32_t p, uint32_t d0, bool live, uint32_t a, uint32_t s, uint32_t cnt, uint64_t off,
                    uint64_t end) {
         const uint32_t w0 = p >> 2;
+#if defined(NSX_RX_DIAG) && (NSX_RX_DIAG == 3 || NSX_RX_DIAG == 4)
+        // diagnostic build only: the prefix form's loads, staging and mask stores with no per-frame work
+        rx_store_mask(ro.mrs, __builtin_amdgcn_ballot_w64(live && F == 0x12345678u + d0), a, cnt, n, lane, s);
+        return;
+#endif
         uint32_t d[6];
         d[0] = d0;
 #pragma unroll
@@ -1769,11 +1778,21 @@ __device__ __forceinline__ void rx_run_lds(const uint8_t* __restrict__ base, con
     const uint32_t p = live ? (uint32_t)((base + my_off) - rbase) : 0u;
     const uint32_t e = live ? (uint32_t)((base + my_end) - rbase) : 0u;
     const uint32_t hd = p & 3u, w0 = p >> 2;
+#if defined(NSX_RX_DIAG) && NSX_RX_DIAG == 1
+    // diagnostic build only (make exp): the loop's loads, staging and mask stores with no per-frame work
+    rx_store_mask(ro.mrs, __builtin_amdgcn_ballot_w64(live && sdw[w0] == 0x12345678u), a, cnt, n, lane);
+    return;
+#endif
     uint32_t d[6];
 #pragma unroll
     for (int j = 0; j < (V6 ? 3 : 6); ++j) d[j] = sdw[w0 + j];
     if constexpr (V6) d[3] = d[4] = d[5] = 0u;
     const uint32_t F = lds_range_sum(slot, p, e, d[0], live);  // the frame's weighted sum (< 2^32: ≤ 8 KiB)
+#if defined(NSX_RX_DIAG) && NSX_RX_DIAG == 2
+    // diagnostic build only: the frame sums without the header parse and verdict
+    rx_store_mask(ro.mrs, __builtin_amdgcn_ballot_w64(live && fold32(F + d[1]) == 0xFFFFu), a, cnt, n, lane);
+    return;
+#endif
     auto opt = [&](uint32_t (&o)[10]) {
 #pragma unroll
         for (int j = 6; j < 16; ++j) o[j - 6] = sdw[w0 + j];
@@ -1872,6 +1891,86 @@ __device__ __forceinline__ void rx_runs_lds(const uint8_t* __restrict__ base, __
 }
 
 
+// The small-frame mode's LDS loop with TWO runs of rows in flight (round 5): rx_runs_lds<·, ·,
+// true> keeps one run in flight while it sums another, so a wave's loads stop at every run — its next run's rows are
+// issued only once this run's have landed and been staged. Here two register sets alternate: run j's rows (set A) are
+// staged, set A is refilled at once with run j + 2, and run j is summed while runs j + 1 (set B) and j + 2 load. Each
+// iteration issues the offsets of run j + 3 BEFORE the rows of run j + 2, so that reading run j + 2's geometry next
+// iteration never waits on younger row loads (vmcnt counts in issue order). The first run that is not a direct run
+// hands the rest of the range to the hybrid loop, as in rx_runs_lds.
+template <int R, bool V6>
+__device__ __forceinline__ void rx_runs_lds2(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
+                                             uint32_t a0, uint32_t a_end, uint32_t lane, lds16* slot,
+                                             const RxOuts& ro) {
+    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+    auto load_off = [&](uint32_t i, bool live) -> uint64_t {
+        const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, live ? i * 8 : kOOB, 0, 0);
+        return ((uint64_t)x.y << 32) | x.x;
+    };
+    struct Run {
+        const uint8_t* rbase;
+        uint64_t span;
+        uint32_t cnt;
+        bool lds;
+    };
+    auto geo = [&](uint32_t a, uint64_t off, uint64_t end) {  // wave-uniform geometry of run a (a direct run?)
+        Run g{base, 0, a < a_end ? min(kRxRun, a_end - a) : 0u, false};
+        if (g.cnt) {
+            const uint64_t lo = readlane64(off, 0), hi = readlane64(end, g.cnt - 1u);
+            g.rbase = reinterpret_cast<const uint8_t*>(((uintptr_t)(base + lo)) & ~(uintptr_t)127);
+            g.span = (uint64_t)((base + hi) - g.rbase);
+            g.lds = g.span <= (uint64_t)kRxSlotRows * kRow &&
+                    !__builtin_amdgcn_ballot_w64(lane < g.cnt && end - off > kPfxDirectMax);
+        }
+        return g;
+    };
+    auto issue = [&](u32x4 (&V)[kRxSlotRows], const Run& g, bool on) {  // rows past the run: empty loads
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(g.rbase, on ? (g.span + 3) & ~3ull : 0ull);
+#pragma unroll
+        for (uint32_t r = 0; r < kRxSlotRows; ++r) V[r] = bld16<true>(rs, r * kRow + lane * 16u);
+    };
+    auto offs_of = [&](uint32_t a, uint64_t& off, uint64_t& end) {
+        off = load_off(a + lane, a < a_end && a + lane <= n);
+        end = load_off(a + lane + 1u, a < a_end && a + lane + 1u <= n);
+    };
+    uint32_t a = a0;
+    uint64_t o0, e0, o1, e1, o2, e2;
+    offs_of(a, o0, e0);
+    offs_of(a + kRxRun, o1, e1);
+    Run g0 = geo(a, o0, e0);
+    if (!g0.lds) {
+        if (g0.cnt) rx_runs_pfx<R, V6, 7, true>(base, ofs, n, a, a_end, lane, slot, ro);
+        return;
+    }
+    u32x4 VA[kRxSlotRows], VB[kRxSlotRows];
+    issue(VA, g0, true);
+    Run g1 = geo(a + kRxRun, o1, e1);
+    offs_of(a + 2u * kRxRun, o2, e2);  // offsets of run j + 2 before the rows of run j + 1
+    issue(VB, g1, g1.lds);
+    // One iteration: run a's rows in V are staged, V is refilled with run a + 128, run a is summed. Returns whether
+    // the next run (a + 64 after the rotation) is a staged direct run.
+    auto step = [&](u32x4 (&V)[kRxSlotRows]) -> bool {
+        lds_stage<kRxSlotRows>(slot, V, g0.span, lane);
+        lds_zero_tail(slot, g0.span, lane);
+        const Run g2 = geo(a + 2u * kRxRun, o2, e2);
+        uint64_t o3, e3;
+        offs_of(a + 3u * kRxRun, o3, e3);
+        issue(V, g2, g1.lds && g2.lds);
+        rx_run_lds<V6>(base, g0.rbase, a, g0.cnt, o0, e0, n, lane, slot, ro);
+        a += kRxRun;
+        g0 = g1, o0 = o1, e0 = e1;
+        g1 = g2, o1 = o2, e1 = e2;
+        o2 = o3, e2 = e3;
+        return g0.lds;
+    };
+    for (;;) {
+        if (!step(VA)) break;
+        if (!step(VB)) break;
+    }
+    if (a < a_end) rx_runs_pfx<R, V6, 7, true>(base, ofs, n, a, a_end, lane, slot, ro);
+}
+
+
 // The receive pass's grids by the batch's mean frame m: m <
 // kRxPfxMean: two waves per block (§7 step 68), the LDS loop for runs of small frames that fit 8 KiB, handing over at the first
 // other run to the hybrid loop (direct pieces for such runs, prefix pieces of ≤ 7 KiB otherwise; §7 step 59);
@@ -1897,8 +1996,13 @@ constexpr uint32_t kRxStreamBigN = 5u << 19;       // 2.5M frames
 // 30-40% on every small-frame mix, §7 step 43.)
 // WPS: waves per SIMD the registers must allow (__launch_bounds__'s second argument): 1 = no constraint (158 VGPRs,
 // 3 waves per SIMD at the default 3 blocks/CU); 4 = the 4-blocks/CU instantiations (≤ 128 VGPRs).
+#if defined(NSX_RX_DIAG) && NSX_RX_DIAG == 5
+#define NSX_RX_WPS(w) 2  // diagnostic build only: registers for two run sets in flight
+#else
+#define NSX_RX_WPS(w) (w)
+#endif
 template <int R, bool V6, int WPS, int PF = 0>
-__global__ __launch_bounds__(kBlock, WPS) void rx_tcp_kernel(const uint8_t* __restrict__ base,
+__global__ __launch_bounds__(kBlock, NSX_RX_WPS(WPS)) void rx_tcp_kernel(const uint8_t* __restrict__ base,
                                                              const uint64_t* __restrict__ offsets, uint32_t n,
                                                              uint64_t* __restrict__ mask,
                                                              uint16_t* __restrict__ ip_raw,
@@ -1939,7 +2043,11 @@ __global__ __launch_bounds__(kBlock, WPS) void rx_tcp_kernel(const uint8_t* __re
             if (wave >= 2u) return;
             const WaveRange wr = range(gridDim.x, 2u, wave);
             lds16* slot = lds_rx + wave * (PfxSlot<7>::kBytes / 16u);
+#if defined(NSX_RX_DIAG) && NSX_RX_DIAG == 5
+            if (mode == 5) rx_runs_lds2<R, V6>(base, ofs, n, wr.a0, wr.a_end, lane, slot, ro);
+#else
             if (mode == 5) rx_runs_lds<R, V6, true>(base, ofs, n, wr.a0, wr.a_end, lane, slot, ro);
+#endif
             else rx_runs_pfx<R, V6, 7, true>(base, ofs, n, wr.a0, wr.a_end, lane, slot, ro);
         } else {  // streamed runs on 3 of the 4 blocks per CU (the auto choice and mode 8, which forces it); mode 1:
                   // on every block
