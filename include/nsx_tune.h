@@ -55,8 +55,9 @@ typedef struct nsx_tune {
                                   the hybrid loop (such runs as prefix-form pieces of <= 7 KiB); below the
                                   streaming threshold (448 B in batches of < 2.5M frames, 768 B from 2.5M)
                                   the prefix form with 15 KiB slots on two waves per block, else streamed
-                                  runs on 3 blocks/CU; 5 / 6 / 7 / 8 force the small-frame mode / the two-wave prefix
-                                  form / the hybrid loop throughout / the streamed runs (3 blocks/CU) on that grid (NSX_EINVAL with rows
+                                  runs on 3 blocks/CU; 5 / 6 / 7 / 8 / 9 force the small-frame mode / the two-wave prefix
+                                  form / the hybrid loop throughout / the streamed runs (3 blocks/CU) / the small-frame
+                                  mode fed by LDS-DMA through a ring on that grid (NSX_EINVAL with rows
                                   other than 0 / 2 or with blocks_per_cu set). With rows or blocks_per_cu set (the
                                   pre-prefix shapes): 0 = per wave the LDS form (mean < 128 B) or streamed
                                   runs, 1 = streamed runs, 2 = the LDS form. (A run that does not fit the

@@ -38,7 +38,7 @@ hipError_t launch_ragged(const LaunchCfg& c, const void* d_base, const uint64_t*
                          const uint32_t* partial, uint16_t* out, uint8_t* ok, hipStream_t st);
 // Fused receive pass: IPv4 (ipver 4: header + pseudo-header + TCP checksum) or IPv6 (ipver 6: pseudo-header +
 // TCP checksum) per frame into a validity bitmask (ceil(n/64) words); ip_raw (IPv4 only) / tcp_raw nullable.
-// false for overrides that name no shape of the receive kernels (segs_per_wave outside {0, 1, 2, 5-8}, or 5-8 off the
+// false for overrides that name no shape of the receive kernels (segs_per_wave outside {0, 1, 2, 5-9}, or 5-9 off the
 // default grid): NSX_EINVAL
 bool rx_tune_valid(const LaunchCfg& c);
 bool ragged_tune_valid(const LaunchCfg& c);

@@ -1971,6 +1971,146 @@ __device__ __forceinline__ void rx_runs_lds2(const uint8_t* __restrict__ base, _
 }
 
 
+// ---- LDS-DMA: loads that write LDS directly (buffer_load_dwordx4 … lds), no VGPR destination ----
+// Issued as inline asm, so that hipcc neither reorders other memory operations across them nor waits for them on its
+// own: a wave that uses them counts its vector-memory operations itself and waits with an explicit vmcnt. M0 (the
+// LDS destination base, wave-uniform) is set and restored inside the one statement (MI355X guides: M0 is
+// compiler-reserved). One wave instruction writes 16 B per active lane at lds_byte + 16·lane.
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t lds_byte) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen nt lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(rs), "s"(lds_byte) : "memory");
+}
+
+// Wait until at most n of this wave's vector-memory operations are outstanding (n wave-uniform; s_waitcnt takes an
+// immediate, so n is rounded DOWN to one of the listed counts — waiting for more than asked is always safe).
+__device__ __forceinline__ void wait_vm_le(uint32_t n) {
+#define NSX_VMW(k) asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory")
+    n = __builtin_amdgcn_readfirstlane(n);
+    if (n >= 16u) {
+        if (n >= 40u) {
+            if (n >= 63u) NSX_VMW(63); else if (n >= 56u) NSX_VMW(56); else if (n >= 48u) NSX_VMW(48); else NSX_VMW(40);
+        } else if (n >= 28u) {
+            if (n >= 34u) NSX_VMW(34); else if (n >= 31u) NSX_VMW(31); else NSX_VMW(28);
+        } else {
+            if (n >= 25u) NSX_VMW(25); else if (n >= 22u) NSX_VMW(22); else if (n >= 19u) NSX_VMW(19); else NSX_VMW(16);
+        }
+    } else if (n >= 8u) {
+        if (n >= 14u) NSX_VMW(14); else if (n >= 12u) NSX_VMW(12); else if (n >= 10u) NSX_VMW(10); else NSX_VMW(8);
+    } else if (n >= 4u) {
+        if (n >= 7u) NSX_VMW(7); else if (n >= 6u) NSX_VMW(6); else if (n >= 5u) NSX_VMW(5); else NSX_VMW(4);
+    } else {
+        if (n >= 3u) NSX_VMW(3); else if (n >= 2u) NSX_VMW(2); else if (n >= 1u) NSX_VMW(1); else NSX_VMW(0);
+    }
+#undef NSX_VMW
+}
+
+// The small-frame mode's LDS loop fed by LDS-DMA through a ring (round 5): rx_runs_lds keeps
+// one run's rows in flight (in VGPRs) while it sums another, so its loads stop at every run. Here each run's rows go
+// straight from HBM into a ring of LDS run regions packed back to back (a region is the run's span rounded up to 16 B;
+// the last row's lanes past the span are masked off, so no region is written past its end), and a wave keeps up to
+// two runs in flight beyond the one it sums, as many as the ring holds. Each run's 66 offsets come the same way,
+// four runs ahead of the sum, into one of four 528 B areas; the run's geometry and each lane's frame bounds are read
+// from there. The wave counts its own vector-memory operations (the DMAs and rx_run_lds's stores) and waits for a
+// group with vmcnt(younger operations). The first run that is not a direct run (too wide for 8 rows, or holding a
+// frame over kPfxDirectMax bytes) hands the rest of the range to the hybrid loop, after the ring has drained.
+// region: the wave's LDS (kRingWave bytes); offsets areas first, then the ring, then a 128 B pad that the chunk and
+// header-window reads of a run's last frames may reach.
+constexpr uint32_t kRingOffArea = 528;  // 33 lanes × 16 B: offsets[a .. a + 65]
+constexpr uint32_t kRingWave = 20480;   // per wave: the default grid's 40 KB blocks hold two
+constexpr uint32_t kRingBegin = 4u * kRingOffArea, kRingEnd = kRingWave - 128u;
+template <int R, bool V6>
+__device__ __forceinline__ void rx_runs_ring(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
+                                             uint32_t a0, uint32_t a_end, uint32_t lane, lds16* region,
+                                             const RxOuts& ro) {
+    const uint32_t reg = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)region);
+    const uint8_t* rb8 = reinterpret_cast<const uint8_t*>(region);
+    const uint32_t stores_per_run = 1u + (ro.raw ? (V6 ? 1u : 2u) : 0u);  // rx_run_lds: the mask byte (+ raw sums)
+    uint32_t vmc = 0;      // this wave's vector-memory operations issued in this loop
+    uint32_t om[4];        // vmc right after the offsets DMA of run k (slot k & 3)
+    auto om_get = [&](uint32_t k) { k &= 3u; return k == 0 ? om[0] : k == 1 ? om[1] : k == 2 ? om[2] : om[3]; };
+    auto om_set = [&](uint32_t k, uint32_t v) {
+        k &= 3u;
+        om[0] = k == 0 ? v : om[0], om[1] = k == 1 ? v : om[1], om[2] = k == 2 ? v : om[2], om[3] = k == 3 ? v : om[3];
+    };
+    auto issue_offs = [&](uint32_t r) {  // run index r (a = a0 + 64 r): offsets[a .. a + 65] into area r & 3
+        const uint32_t a = a0 + r * kRxRun;
+        if (lane < 33u) dma16(ofs, a < a_end ? (a + 2u * lane) * 8u : kOOB, reg + (r & 3u) * kRingOffArea);
+        om_set(r, ++vmc);
+    };
+    auto area_off = [&](uint32_t r, uint32_t l) {  // offsets[a + l] of run r from its area
+        return *reinterpret_cast<const uint64_t*>(rb8 + (r & 3u) * kRingOffArea + l * 8u);
+    };
+    struct Q {
+        uint32_t r, cnt, pos, span, mark;
+        const uint8_t* rbase;
+    };
+    const uint32_t nruns = (a_end - a0 + kRxRun - 1u) / kRxRun;
+    for (uint32_t r = 0; r < 4u && r < nruns; ++r) issue_offs(r);
+    Q q0{}, q1{}, q2{};
+    uint32_t qlen = 0, u = 0, last_end = kRingBegin;
+    bool stop = false;
+    for (;;) {
+        // fill: up to two runs in flight beyond the one to be summed, while the ring has room
+        while (qlen < 3u && u < nruns && !stop) {
+            wait_vm_le(vmc - om_get(u));
+            const uint32_t a = a0 + u * kRxRun, cnt = min(kRxRun, a_end - a);
+            const uint64_t off = area_off(u, lane), end = area_off(u, lane + 1u);
+            const uint64_t lo = readlane64(off, 0), hi = readlane64(end, cnt - 1u);
+            const uint8_t* rbase = reinterpret_cast<const uint8_t*>(((uintptr_t)(base + lo)) & ~(uintptr_t)127);
+            const uint64_t span = (uint64_t)((base + hi) - rbase);
+            if (span > (uint64_t)kRxSlotRows * kRow || __builtin_amdgcn_ballot_w64(lane < cnt && end - off > kPfxDirectMax)) {
+                stop = true;  // not a direct run: the hybrid loop takes over from run u
+                break;
+            }
+            const uint32_t f = ((uint32_t)span + 15u) & ~15u;
+            uint32_t pos;
+            if (qlen == 0u) {
+                pos = last_end + f <= kRingEnd ? last_end : kRingBegin;
+            } else if (last_end >= q0.pos) {
+                if (last_end + f <= kRingEnd) pos = last_end;
+                else if (kRingBegin + f <= q0.pos) pos = kRingBegin;
+                else break;  // no room until the oldest run is summed
+            } else {
+                if (last_end + f <= q0.pos) pos = last_end;
+                else break;
+            }
+            // the rows: whole 1 KiB rows, the last one's lanes past the span masked off
+            const __amdgpu_buffer_rsrc_t rs = make_rsrc(rbase, (span + 3) & ~3ull);
+            const uint32_t rows = __builtin_amdgcn_readfirstlane(((uint32_t)span + kRow - 1u) / kRow);
+            for (uint32_t rr = 0; rr + 1u < rows; ++rr) dma16(rs, rr * kRow + lane * 16u, reg + pos + rr * kRow);
+            if (rows) {
+                const uint32_t lr = rows - 1u;
+                if (lr * kRow + lane * 16u < (uint32_t)span) dma16(rs, lr * kRow + lane * 16u, reg + pos + lr * kRow);
+            }
+            vmc += rows;
+            const Q e{u, cnt, pos, (uint32_t)span, vmc, rbase};
+            if (qlen == 0u) q0 = e; else if (qlen == 1u) q1 = e; else q2 = e;
+            ++qlen;
+            last_end = pos + f;
+            ++u;
+        }
+        if (qlen == 0u) break;
+        // sum the oldest run
+        wait_vm_le(vmc - q0.mark);
+        lds16* slot = reinterpret_cast<lds16*>(const_cast<uint8_t*>(rb8) + q0.pos);
+        lds_zero_tail(slot, q0.span, lane);
+        const uint64_t my_off = area_off(q0.r, lane), my_end = area_off(q0.r, lane + 1u);
+        rx_run_lds<V6>(base, q0.rbase, a0 + q0.r * kRxRun, q0.cnt, my_off, my_end, n, lane, slot, ro);
+        vmc += stores_per_run;
+        // its offsets area is free: the offsets of the run four ahead
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this run's LDS reads are done before the area is refilled
+        if (q0.r + 4u < nruns) issue_offs(q0.r + 4u);
+        q0 = q1, q1 = q2;
+        --qlen;
+    }
+    wait_vm_le(0u);  // nothing may still be landing in the region the hybrid loop stages into
+    const uint32_t a_sw = a0 + u * kRxRun;
+    if (stop && a_sw < a_end) rx_runs_pfx<R, V6, 7, true>(base, ofs, n, a_sw, a_end, lane, region, ro);
+}
+
+
 // The receive pass's grids by the batch's mean frame m: m <
 // kRxPfxMean: two waves per block (§7 step 68), the LDS loop for runs of small frames that fit 8 KiB, handing over at the first
 // other run to the hybrid loop (direct pieces for such runs, prefix pieces of ≤ 7 KiB otherwise; §7 step 59);
@@ -2035,6 +2175,10 @@ __global__ __launch_bounds__(kBlock, NSX_RX_WPS(WPS)) void rx_tcp_kernel(const u
             const WaveRange wr = range(gridDim.x, 2u, wave);
             rx_runs_pfx<R, V6, 15, false>(base, ofs, n, wr.a0, wr.a_end, lane,
                                           lds_rx + wave * (PfxSlot<15>::kBytes / 16u), ro);
+        } else if (mode == 9) {  // two waves per block: the LDS loop fed by LDS-DMA through a ring (§7 step 70)
+            if (wave >= 2u) return;
+            const WaveRange wr = range(gridDim.x, 2u, wave);
+            rx_runs_ring<R, V6>(base, ofs, n, wr.a0, wr.a_end, lane, lds_rx + wave * (kRingWave / 16u), ro);
         } else if (mode == 5 || mode == 7) {  // two waves per block: the LDS loop until a run needs the hybrid loop
                                               // (5), or the hybrid loop throughout (7). Four waves per block ran
                                               // 2.5-4.4% slower on 40-120 B frames (workloads 13, 16; 17 −0.3%):
@@ -3307,12 +3451,12 @@ bool ragged_tune_valid(const LaunchCfg& c) {
 }
 
 bool rx_tune_valid(const LaunchCfg& c) {
-    // segs_per_wave: 0 auto, 1 / 2 forced per-wave forms of the rows / blocks_per_cu shapes, 5 / 6 / 7 / 8 a mode of
+    // segs_per_wave: 0 auto, 1 / 2 forced per-wave forms of the rows / blocks_per_cu shapes, 5 / 6 / 7 / 8 / 9 a mode of
     // the default grid — which means nothing on the shapes rows / blocks_per_cu select (silently running
     // the auto shape there made fuzz cases test another form than they named); any other value names no form
     // (3, 4 or 9 used to run the automatic shape)
     const int s = c.segs_per_wave;
-    if (!(s == 0 || s == 1 || s == 2 || (s >= 5 && s <= 8))) return false;
+    if (!(s == 0 || s == 1 || s == 2 || (s >= 5 && s <= 9))) return false;
     const bool grid_mode = s >= 5;
     return !grid_mode || ((c.rows == 0 || c.rows == 2) && c.blocks_per_cu == 0);
 }
@@ -3338,11 +3482,14 @@ hipError_t launch_rx_tcp(const LaunchCfg& c, int ipver, const void* d_base, cons
     // PF = -1 kernel at 4 blocks/CU, each block with two 15-row prefix slots of LDS (its four 7-row slots fit the
     // same 38.5 KB), the mode chosen in-kernel by the batch's mean frame.
     const bool auto_grid = rows == 2 && c.blocks_per_cu == 0 &&
-                           (c.segs_per_wave == 0 || c.segs_per_wave == 5 || c.segs_per_wave == 6 ||
-                            c.segs_per_wave == 7 || c.segs_per_wave == 8);
+                           (c.segs_per_wave == 0 || (c.segs_per_wave >= 5 && c.segs_per_wave <= 9));
     if (auto_grid) {
-        constexpr size_t la = (size_t)PfxSlot<15>::kBytes * 2;
-        static_assert(la >= (size_t)PfxSlot<7>::kBytes * kWavesPerBlock && la * 4 <= 163840, "4 blocks per CU");
+        // per block: two 15-row prefix slots or four 7-row slots (38.5 KB); forced mode 9, two DMA rings (kRingWave
+        // each: 40 KB, 4 blocks per CU taking the CU's whole 160 KB)
+        constexpr size_t la_def = (size_t)PfxSlot<15>::kBytes * 2, la_ring = (size_t)kRingWave * 2;
+        static_assert(la_def >= (size_t)PfxSlot<7>::kBytes * kWavesPerBlock && la_def * 4 <= 163840 &&
+                          la_ring * 4 <= 163840, "4 blocks per CU");
+        const size_t la = c.segs_per_wave == 9 ? la_ring : la_def;
         for (uint64_t c0 = 0; c0 < n; c0 += kRaggedChunk) {
             const uint32_t cn = (uint32_t)(n - c0 < kRaggedChunk ? n - c0 : kRaggedChunk);
             const uint32_t grid = grid_for((cn + kRxRun - 1) / kRxRun, (uint32_t)c.cus * 4u);

@@ -353,14 +353,14 @@ def test_receive_grid_modes_off_the_default_grid_are_einval():
     The host entry points check before touching a device, so this runs on any host."""
     offs = np.array([0, 40], np.uint64)
     buf = np.zeros(40, np.uint8)
-    for mode in (5, 6, 7, 8):
+    for mode in (5, 6, 7, 8, 9):
         for bad in (dict(blocks_per_cu=2), dict(rows=4), dict(rows=16, blocks_per_cu=1)):
             for fn in (nsx.rx_ipv4_tcp_verify_host, nsx.rx_ipv6_tcp_verify_host):
                 with pytest.raises(nsx.NsxError) as e:
                     fn(buf, offs, tune=dict(bad, segs_per_wave=mode))
                 assert e.value.code == nsx.NSX_EINVAL, (mode, bad)
     # ADVICE r4: values that name no receive form at all are refused on every grid, not run as the auto shape
-    for bad in (3, 4, 9, -1):
+    for bad in (3, 4, 10, -1):
         for extra in ({}, dict(rows=4), dict(blocks_per_cu=2)):
             for fn in (nsx.rx_ipv4_tcp_verify_host, nsx.rx_ipv6_tcp_verify_host):
                 with pytest.raises(nsx.NsxError) as e:

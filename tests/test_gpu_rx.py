@@ -58,10 +58,12 @@ TUNES = [dict(rows=2), dict(rows=4), dict(rows=16), dict(blocks_per_cu=1), dict(
          dict(segs_per_wave=1), dict(segs_per_wave=1, rows=4), dict(segs_per_wave=1, blocks_per_cu=4),  # streamed runs
          dict(segs_per_wave=2), dict(segs_per_wave=2, blocks_per_cu=1), dict(segs_per_wave=2, blocks_per_cu=4),
          dict(segs_per_wave=2, blocks_per_cu=8), dict(blocks_per_cu=4),  # LDS form; 4 blocks/CU = the capped kernel
-         dict(segs_per_wave=5), dict(segs_per_wave=6), dict(segs_per_wave=7), dict(segs_per_wave=8)]  # the default grid's modes
+         dict(segs_per_wave=5), dict(segs_per_wave=6), dict(segs_per_wave=7), dict(segs_per_wave=8),
+         dict(segs_per_wave=9)]  # the default grid's modes
 # the default grid's modes forced (5 the LDS loop handing over to the hybrid loop, 7 the hybrid loop throughout, both
-# on two waves per block; 6 the 15-row prefix form on two waves per block)
-PFX = [dict(segs_per_wave=5), dict(segs_per_wave=6), dict(segs_per_wave=7), dict(segs_per_wave=8)]
+# on two waves per block; 6 the 15-row prefix form on two waves per block; 9 the LDS loop fed by LDS-DMA through a ring,
+# handing over to the hybrid loop like 5)
+PFX = [dict(segs_per_wave=5), dict(segs_per_wave=6), dict(segs_per_wave=7), dict(segs_per_wave=8), dict(segs_per_wave=9)]
 
 
 @pytest.mark.parametrize("n", [1, 255, 256, 257, 1000, 30_001])

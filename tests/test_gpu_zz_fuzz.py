@@ -214,10 +214,10 @@ def test_fuzz_tcp_build_options(case):
 
 def rx_fuzz_tune(rng) -> dict:
     """A random receive-pass launch shape: one of the default grid's modes (segs_per_wave 0 auto, 5 small-frame,
-    6 two-wave prefix, 7 hybrid, 8 streamed; rows 0 or 2, no blocks_per_cu), or one of the older shapes rows / blocks_per_cu
+    6 two-wave prefix, 7 hybrid, 8 streamed, 9 small-frame through the LDS-DMA ring; rows 0 or 2, no blocks_per_cu), or one of the older shapes rows / blocks_per_cu
     select (segs_per_wave 0 auto, 1 streamed, 2 LDS) — never a mode on a grid it does not exist on."""
     if rng.random() < 0.5:
-        return dict(rows=int(rng.choice([0, 2])), segs_per_wave=int(rng.choice([0, 5, 6, 7, 8])))
+        return dict(rows=int(rng.choice([0, 2])), segs_per_wave=int(rng.choice([0, 5, 6, 7, 8, 9])))
     return dict(rows=int(rng.choice([0, 2, 4, 8, 16])), blocks_per_cu=int(rng.choice([1, 2, 4, 8])),
                 segs_per_wave=int(rng.choice([0, 1, 2])))
 
