@@ -235,7 +235,13 @@ int nsx_ipv4_hdr_verify_mask_dev(const void* d_base, uint64_t stride, uint32_t h
  * Bits past n in the last word are 0; d_mask holds ceil(n/64) words.
  * d_ip_raw (nullable): the header's raw sum (0 when IHL < 5 or IHL*4 exceeds the
  * frame). d_tcp_raw (nullable): the raw sum over pseudo-header ‖ segment (0
- * unless the frame is well-formed as above). One pass over the frame bytes. */
+ * unless the frame is well-formed as above). One pass over the frame bytes.
+ * Work split: batches whose mean frame is under the streaming threshold deal
+ * their last eighth of frames to the GPU's waves as they finish, from counters
+ * the library keeps per stream (64 streams per device, in the library's own
+ * device memory; every launch leaves them at zero for the stream's next). A
+ * launch on a stream being captured into a graph, or on a stream past the 64th,
+ * splits the batch statically instead; results are the same either way. */
 int nsx_rx_ipv4_tcp_verify_dev(const void* d_base, const uint64_t* d_offsets, uint64_t n, uint64_t* d_mask,
                                uint16_t* d_ip_raw, uint16_t* d_tcp_raw, nsx_stream_t stream);
 
@@ -251,7 +257,8 @@ int nsx_rx_ipv4_tcp_verify_dev(const void* d_base, const uint64_t* d_offsets, ui
  *     src(16) dst(16) payload length(4) 0 0 0 6 from the header's own addresses
  *     ‖ the segment is 0xFFFF (tcp.go:70 over computeChecksum, tcp.go:72-95).
  * IPv6 has no header checksum. d_tcp_raw (nullable): that raw sum, 0 unless the
- * frame is well-formed. Layout rules as nsx_rx_ipv4_tcp_verify_dev. */
+ * frame is well-formed. Layout rules and work split as
+ * nsx_rx_ipv4_tcp_verify_dev. */
 int nsx_rx_ipv6_tcp_verify_dev(const void* d_base, const uint64_t* d_offsets, uint64_t n, uint64_t* d_mask,
                                uint16_t* d_tcp_raw, nsx_stream_t stream);
 

@@ -27,6 +27,8 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
 #include <type_traits>
 
 #include "csum_kernels.h"
@@ -1173,6 +1175,80 @@ constexpr uint32_t kPfxDirectSlot = kPfxDirectRows * kRow + 256;
 // Units up to this long may be summed lane by lane in direct pieces: 17 chunks.
 constexpr uint32_t kPfxDirectMax = 256;
 
+// Run sequences (round 5): the runs of kPfxRun units a wave takes, in order, named by their
+// first unit. The run loops (pfx_runs, rx_runs_lds) read them two runs ahead — the next run's rows and the offsets of
+// the run after it are loaded while one run is summed — and call next() exactly once per run, in order: a dealt
+// sequence pulls from a shared counter there. cnt(a) = the units of run a; a value a with !live(a) ends the
+// sequence (cnt 0).
+
+// The units [a0, a_end) in runs from a0 (end: a_end).
+struct StaticRuns {
+    uint32_t a0, a_end;
+    __device__ __forceinline__ bool live(uint32_t a) const { return a < a_end; }
+    __device__ __forceinline__ uint32_t first() const { return a0; }
+    __device__ __forceinline__ uint32_t next(uint32_t a) const { return a + kPfxRun < a_end ? a + kPfxRun : a_end; }
+    __device__ __forceinline__ uint32_t cnt(uint32_t a) const { return min(kPfxRun, a_end - a); }
+    __device__ __forceinline__ void refill() const {}
+};
+
+// A wave's static runs [a0, e_st), then runs dealt from a pool: the batch's last units [S, n), as runs from S, split
+// into one share per counter ("head") — the share's runs pb + 64 t, t < q, go to the waves of this head in the order
+// they ask (end: n). A wave always holds one ticket ahead (pulled one run before it is needed, so that the counter's
+// round trip, ~1-3 µs under load, overlaps a run's work): the pull is a returning device-scope atomic add from lane
+// 0, its value read (readfirstlane) only when the ticket is taken. Every wave of the head takes tickets until one is
+// past its share, so the head sees exactly q + (its waves) pulls per launch: the wave that draws the last of them,
+// `last`, resets the counter to 0 for the next launch that uses it — launches on one stream run one after another,
+// and the host gives each stream its own heads (rx_deal_heads).
+struct DealtRuns {
+    uint32_t a0, e_st, n;
+    uint32_t pb, q, last;
+    uint32_t* head;
+    uint32_t lane;
+    uint32_t tk;    // the reserved ticket (lane 0's VGPR until taken)
+    bool dealing;   // false once a ticket past the share was taken (or without a head)
+    bool want;      // a ticket was taken and the next is not yet pulled (refill)
+    __device__ __forceinline__ uint32_t pull() const {
+        uint32_t t = 0u;
+        if (lane == 0u) t = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return t;
+    }
+    __device__ __forceinline__ void init() {
+        tk = pull();
+        dealing = true;
+        want = false;
+    }
+    // The pull for the next ticket, issued by the run loops after a run's loads: vmcnt retires in issue order, so
+    // loads issued behind the atomic would wait for its round trip too.
+    __device__ __forceinline__ void refill() {
+        if (want) tk = pull();
+        want = false;
+    }
+    __device__ __forceinline__ uint32_t take() {
+        if (!dealing) return n;
+        refill();
+        const uint32_t t = __builtin_amdgcn_readfirstlane(tk);
+        if (t < q) {
+            want = true;
+            return pb + t * kPfxRun;
+        }
+        dealing = false;
+        if (t == last && lane == 0u) __hip_atomic_store(head, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return n;
+    }
+    __device__ __forceinline__ bool live(uint32_t a) const { return a < n; }
+    __device__ __forceinline__ uint32_t first() { return a0 < e_st ? a0 : take(); }
+    // a static run's successor, else a dealt run (a pool run, or the end n: both ≥ e_st)
+    __device__ __forceinline__ uint32_t next(uint32_t a) { return a + kPfxRun < e_st ? a + kPfxRun : take(); }
+    __device__ __forceinline__ uint32_t cnt(uint32_t a) const { return min(kPfxRun, (a < e_st ? e_st : n) - a); }
+};
+
+// A run loop's state at a run boundary, handed from one loop to another (rx_runs_lds → the hybrid loop): run a with
+// its offsets (lane l = unit a + l; c_end: a + l + 1), the next run an with its offsets.
+struct RunHead {
+    uint32_t a, an;
+    uint64_t c_off, c_end, n_off, n_end;
+};
+
 // Stage a piece's rows [0, span) into the slot (the rows already in V, all loaded) with their chunk prefix sums;
 // returns S(span), the weighted sum of the staged bytes. The chunk holding byte `span` keeps only its bytes below
 // it (the row loads read whole dwords up to 4·ceil(span/4): up to 3 bytes of the next unit). I[0] = 0 is written
@@ -1204,8 +1280,8 @@ __device__ __forceinline__ uint32_t pfx_stage(lds16* slot, u32x4 (&V)[VR], uint3
     return carry;
 }
 
-// A wave's units [a0, a_end) in runs of 64 (from a0), as pieces of the prefix form with ROWS-row slots. Unit a + l =
-// bytes [offsets[a + l], offsets[a + l + 1]), lanes holding both ends. HYB (the hybrid loop, §7 step 55): a whole run
+// A wave's runs (the sequence q; h: the state a loop handed over, else q's first run), as pieces of the prefix form
+// with ROWS-row slots. Unit a + l = bytes [offsets[a + l], offsets[a + l + 1]), lanes holding both ends. HYB (the hybrid loop, §7 step 55): a whole run
 // whose bytes fit 8 rows and whose units are all ≤ kPfxDirectMax bytes is a DIRECT piece instead — staged without
 // prefix sums and summed lane by lane (lds_range_sum, the LDS form, 3-6% faster on runs of ACKs alone: no per-row
 // scans); the slot (PfxSlot<7>, 9040 B) holds either layout.
@@ -1214,10 +1290,10 @@ __device__ __forceinline__ uint32_t pfx_stage(lds16* slot, u32x4 (&V)[VR], uint3
 //                                      at p/4;
 //   stream(a, s, rem, off, end)        units [a + s, a + s + rem) of the run at a in the streaming form (lane l of
 //                                      off / end = unit a + l).
-template <uint32_t ROWS, bool HYB, uint32_t ALIGN, typename Out, typename Stream>
+template <uint32_t ROWS, bool HYB, uint32_t ALIGN, typename Seq, typename Out, typename Stream>
 __device__ __forceinline__ void pfx_runs(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
-                                         uint32_t a0, uint32_t a_end, uint32_t lane, lds16* slot, Out&& out,
-                                         Stream&& stream) {
+                                         Seq& q, uint32_t lane, lds16* slot, Out&& out, Stream&& stream,
+                                         const RunHead* h = nullptr) {
     typedef uint32_t v2u __attribute__((ext_vector_type(2)));
     constexpr uint32_t kCap = ROWS * kRow;
     constexpr uint32_t VR = HYB && ROWS < kPfxDirectRows ? kPfxDirectRows : ROWS;  // rows in flight per piece
@@ -1237,7 +1313,7 @@ __device__ __forceinline__ void pfx_runs(const uint8_t* __restrict__ base, __amd
     // Wave-uniform geometry of the piece of run a from lane s (off/end: that run's offsets, lane l = unit a + l).
     auto geo = [&](uint32_t a, uint32_t s, uint64_t off, uint64_t end) {
         Piece g{a, s, 0u, 0u, base, 0u, false};
-        const uint32_t rc = a < a_end ? min(kPfxRun, a_end - a) : 0u;
+        const uint32_t rc = q.cnt(a);
         if (s < rc) {
             g.rem = rc - s;
             g.rbase = reinterpret_cast<const uint8_t*>(((uintptr_t)(base + readlane64(off, s))) & ~(uintptr_t)127);
@@ -1267,11 +1343,19 @@ __device__ __forceinline__ void pfx_runs(const uint8_t* __restrict__ base, __amd
         for (uint32_t r = 0; r < VR; ++r) V[r] = bld16<true>(rs, r * kRow + lane * 16u);
     };
     auto live_of = [&](const Piece& g) { return lane >= g.s && lane < g.s + g.cnt; };
-    uint32_t a = a0;
-    uint64_t c_off = load_off(a + lane, a < a_end && a + lane <= n);
-    uint64_t c_end = load_off(a + lane + 1u, a < a_end && a + lane + 1u <= n);
-    uint64_t n_off = load_off(a + kPfxRun + lane, a + kPfxRun < a_end && a + kPfxRun + lane <= n);
-    uint64_t n_end = load_off(a + kPfxRun + lane + 1u, a + kPfxRun < a_end && a + kPfxRun + lane + 1u <= n);
+    auto offs = [&](uint32_t a, uint32_t k) { return load_off(a + lane + k, q.live(a) && a + lane + k <= n); };
+    uint32_t a, an;
+    uint64_t c_off, c_end, n_off, n_end;
+    if (h) {
+        a = h->a, an = h->an;
+        c_off = h->c_off, c_end = h->c_end, n_off = h->n_off, n_end = h->n_end;
+    } else {
+        a = q.first();
+        c_off = offs(a, 0u), c_end = offs(a, 1u);
+        an = q.next(a);
+        n_off = offs(an, 0u), n_end = offs(an, 1u);
+        q.refill();
+    }
     Piece cur = geo(a, 0u, c_off, c_end);
     issue(cur);
     __builtin_amdgcn_s_waitcnt(kWaitVm0);  // nothing in flight at the loop's entry (rx_runs_lds, §7 step 50)
@@ -1279,10 +1363,11 @@ __device__ __forceinline__ void pfx_runs(const uint8_t* __restrict__ base, __amd
         if (!cur.cnt) {
             // The first ALIGN units from s exceed the slot: stream the run's units from s on.
             stream(a, cur.s, cur.rem, c_off, c_end);
-            a += kPfxRun;
+            a = an;
             c_off = n_off, c_end = n_end;
-            n_off = load_off(a + kPfxRun + lane, a + kPfxRun < a_end && a + kPfxRun + lane <= n);
-            n_end = load_off(a + kPfxRun + lane + 1u, a + kPfxRun < a_end && a + kPfxRun + lane + 1u <= n);
+            an = q.next(a);
+            n_off = offs(an, 0u), n_end = offs(an, 1u);
+            q.refill();
             cur = geo(a, 0u, c_off, c_end);
             issue(cur);
             __builtin_amdgcn_s_waitcnt(kWaitVm0);
@@ -1302,12 +1387,12 @@ __device__ __forceinline__ void pfx_runs(const uint8_t* __restrict__ base, __amd
         // The next piece: the rest of this run, or the next run (whose offsets are already loaded).
         const bool adv = cur.cnt == cur.rem;
         Piece nxt;
-        if (adv) nxt = geo(a + kPfxRun, 0u, n_off, n_end);
+        if (adv) nxt = geo(an, 0u, n_off, n_end);
         else nxt = geo(a, cur.s + cur.cnt, c_off, c_end);
         issue(nxt);
-        const uint32_t ap = a + 2u * kPfxRun;
-        const uint64_t p_off = load_off(ap + lane, adv && ap < a_end && ap + lane <= n);
-        const uint64_t p_end = load_off(ap + lane + 1u, adv && ap < a_end && ap + lane + 1u <= n);
+        const uint32_t an2 = adv ? q.next(an) : an;  // the run after the next, once this run is done (else unused)
+        const uint64_t p_off = offs(adv ? an2 : n, 0u), p_end = offs(adv ? an2 : n, 1u);
+        q.refill();
         {
             const bool live = live_of(cur);
             const uint32_t p = live ? (uint32_t)((base + c_off) - cur.rbase) : 0u;
@@ -1330,7 +1415,7 @@ __device__ __forceinline__ void pfx_runs(const uint8_t* __restrict__ base, __amd
             out(F, p, d0, live, a, cur.s, cur.cnt, c_off, c_end);
         }
         if (adv) {
-            a += kPfxRun;
+            a = an, an = an2;
             c_off = n_off, c_end = n_end;
             n_off = p_off, n_end = p_end;
         }
@@ -1733,10 +1818,10 @@ constexpr uint32_t kRxSlotRows = 8;
 constexpr uint32_t kRxSlot = kRxSlotRows * kRow + 256;  // + pad: a header window or chunk block read past the end
 
 // The receive pass in the prefix form (pfx_runs: pieces cut at whole mask bytes; the header window from the slot).
-template <int R, bool V6, uint32_t ROWS, bool HYB>
+template <int R, bool V6, uint32_t ROWS, bool HYB, typename Seq>
 __device__ __forceinline__ void rx_runs_pfx(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
-                                            uint32_t a0, uint32_t a_end, uint32_t lane, lds16* slot,
-                                            const RxOuts& ro) {
+                                            Seq& q, uint32_t lane, lds16* slot, const RxOuts& ro,
+                                            const RunHead* h = nullptr) {
     static_assert(kPfxRun == kRxRun && kPfxDirectSlot == kRxSlot, "the receive pass's runs and direct slot");
     const uint32_t* sdw = reinterpret_cast<const uint32_t*>(slot);
     auto out = [&](uint32_t F, uint32_t p, uint32_t d0, bool live, uint32_t a, uint32_t s, uint32_t cnt, uint64_t off,
@@ -1765,7 +1850,7 @@ __device__ __forceinline__ void rx_runs_pfx(const uint8_t* __restrict__ base, __
         uint64_t e1[1] = {(uint64_t)__shfl_down((unsigned long long)end, s)};
         rx_run_stream<R, V6, 1>(base, a + s, cnt1, o1, e1, 0u, n, lane, ro);
     };
-    pfx_runs<ROWS, HYB, 8u>(base, ofs, n, a0, a_end, lane, slot, out, stream);
+    pfx_runs<ROWS, HYB, 8u>(base, ofs, n, q, lane, slot, out, stream, h);
 }
 
 template <bool V6>
@@ -1804,15 +1889,15 @@ __device__ __forceinline__ void rx_run_lds(const uint8_t* __restrict__ base, con
 // SW (the default grid's small-frame mode, §7 step 59): a run that is not a direct run — too wide for the slot, or
 // holding a frame over kPfxDirectMax bytes, which one lane would sum alone — hands the rest of the wave's range to the
 // hybrid loop (rx_runs_pfx<·, 7, true>) instead of being streamed; waves of ACKs alone stay in this tighter loop.
-template <int R, bool V6, bool SW = false>
+template <int R, bool V6, bool SW = false, typename Seq>
 __device__ __forceinline__ void rx_runs_lds(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
-                                            uint32_t a0, uint32_t a_end, uint32_t lane, lds16* slot,
-                                            const RxOuts& ro) {
+                                            Seq& q, uint32_t lane, lds16* slot, const RxOuts& ro) {
     typedef uint32_t v2u __attribute__((ext_vector_type(2)));
     auto load_off = [&](uint32_t i, bool live) -> uint64_t {
         const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, live ? i * 8 : kOOB, 0, 0);
         return ((uint64_t)x.y << 32) | x.x;
     };
+    auto offs = [&](uint32_t a, uint32_t k) { return load_off(a + lane + k, q.live(a) && a + lane + k <= n); };
     struct Run {
         const uint8_t* rbase;
         uint64_t span;
@@ -1820,7 +1905,7 @@ __device__ __forceinline__ void rx_runs_lds(const uint8_t* __restrict__ base, __
         bool lds;
     };
     auto geo = [&](uint32_t a, uint64_t off, uint64_t end) {  // wave-uniform geometry of run a
-        Run g{base, 0, a < a_end ? min(kRxRun, a_end - a) : 0u, false};
+        Run g{base, 0, q.cnt(a), false};
         if (g.cnt) {
             const uint64_t lo = readlane64(off, 0), hi = readlane64(end, g.cnt - 1u);
             g.rbase = reinterpret_cast<const uint8_t*>(((uintptr_t)(base + lo)) & ~(uintptr_t)127);
@@ -1840,31 +1925,31 @@ __device__ __forceinline__ void rx_runs_lds(const uint8_t* __restrict__ base, __
     // outer loop. (Kept apart so that the streaming form's loads still in flight at its end — its pipeline issues
     // one empty batch past the run — never merge into the LDS loop's wait counts: at a merge hipcc waits
     // vmcnt(0) before reusing such a register, which drained the next run's rows right after their issue.)
-    // The offsets of the outer loop's next run are always loaded one run ahead (before a streamed run, or by the LDS
-    // loop), so that a switch between the forms does not wait for them (§7 step 53).
-    uint32_t a = a0;
-    uint64_t c_off = load_off(a + lane, a < a_end && a + lane <= n);
-    uint64_t c_end = load_off(a + lane + 1u, a < a_end && a + lane + 1u <= n);
-    while (a < a_end) {
+    // The next run and its offsets are always known one run ahead (before a streamed run, or by the LDS loop), so
+    // that a switch between the forms does not wait for them (§7 step 53); they are carried across the switch.
+    uint32_t a = q.first();
+    uint64_t c_off = offs(a, 0u), c_end = offs(a, 1u);
+    uint32_t an = q.next(a);
+    uint64_t n_off = offs(an, 0u), n_end = offs(an, 1u);
+    q.refill();
+    while (q.live(a)) {
         Run cur = geo(a, c_off, c_end);
         if (SW && !cur.lds) {
-            rx_runs_pfx<R, V6, 7, true>(base, ofs, n, a, a_end, lane, slot, ro);
+            const RunHead h{a, an, c_off, c_end, n_off, n_end};
+            rx_runs_pfx<R, V6, 7, true>(base, ofs, n, q, lane, slot, ro, &h);
             return;
         }
         if (!cur.lds) {  // a run too wide for the slot: the streaming form
-            const uint32_t as = a + kRxRun;
-            const uint64_t s_off = load_off(as + lane, as < a_end && as + lane <= n);
-            const uint64_t s_end = load_off(as + lane + 1u, as < a_end && as + lane + 1u <= n);
             uint32_t cnt1[1] = {cur.cnt};
             uint64_t o1[1] = {c_off}, e1[1] = {c_end};
             rx_run_stream<R, V6, 1>(base, a, cnt1, o1, e1, 0u, n, lane, ro);
-            a = as, c_off = s_off, c_end = s_end;
+            a = an, c_off = n_off, c_end = n_end;
+            an = q.next(a);
+            n_off = offs(an, 0u), n_end = offs(an, 1u);
+            q.refill();
             continue;
         }
         issue(cur);
-        uint32_t an = a + kRxRun;
-        uint64_t n_off = load_off(an + lane, an < a_end && an + lane <= n);
-        uint64_t n_end = load_off(an + lane + 1u, an < a_end && an + lane + 1u <= n);
         // Enter the loop with nothing in flight (the first run's rows and offsets are read at its head anyway). With
         // them pending, hipcc's wait-count pass merged the entry edge into the loop head and waited vmcnt(0) in
         // every iteration before reading the next run's offsets — a wait on the previous run's result stores,
@@ -1876,16 +1961,15 @@ __device__ __forceinline__ void rx_runs_lds(const uint8_t* __restrict__ base, __
             Run nxt = geo(an, n_off, n_end);
             if (!nxt.lds) nxt.span = 0;  // the rows of a run that will be streamed are not staged: empty loads
             issue(nxt);
-            const uint32_t an2 = an + kRxRun;
-            const uint64_t p_off = load_off(an2 + lane, an2 < a_end && an2 + lane <= n);
-            const uint64_t p_end = load_off(an2 + lane + 1u, an2 < a_end && an2 + lane + 1u <= n);
+            const uint32_t an2 = q.next(an);
+            const uint64_t p_off = offs(an2, 0u), p_end = offs(an2, 1u);
+            q.refill();
             rx_run_lds<V6>(base, cur.rbase, a, cur.cnt, c_off, c_end, n, lane, slot, ro);
-            a = an;
+            a = an, an = an2;
             c_off = n_off, c_end = n_end;
-            if (!nxt.lds) break;  // the end of the wave's range, or a run for the outer loop
-            cur = nxt;
             n_off = p_off, n_end = p_end;
-            an = an2;
+            if (!nxt.lds) break;  // the end of the wave's runs, or a run for the outer loop
+            cur = nxt;
         }
     }
 }
@@ -1939,7 +2023,10 @@ __device__ __forceinline__ void rx_runs_lds2(const uint8_t* __restrict__ base, _
     offs_of(a + kRxRun, o1, e1);
     Run g0 = geo(a, o0, e0);
     if (!g0.lds) {
-        if (g0.cnt) rx_runs_pfx<R, V6, 7, true>(base, ofs, n, a, a_end, lane, slot, ro);
+        if (g0.cnt) {
+            StaticRuns rest{a, a_end};
+            rx_runs_pfx<R, V6, 7, true>(base, ofs, n, rest, lane, slot, ro);
+        }
         return;
     }
     u32x4 VA[kRxSlotRows], VB[kRxSlotRows];
@@ -1967,7 +2054,8 @@ __device__ __forceinline__ void rx_runs_lds2(const uint8_t* __restrict__ base, _
         if (!step(VA)) break;
         if (!step(VB)) break;
     }
-    if (a < a_end) rx_runs_pfx<R, V6, 7, true>(base, ofs, n, a, a_end, lane, slot, ro);
+    StaticRuns rest{a, a_end};
+    if (a < a_end) rx_runs_pfx<R, V6, 7, true>(base, ofs, n, rest, lane, slot, ro);
 }
 
 
@@ -2107,7 +2195,8 @@ __device__ __forceinline__ void rx_runs_ring(const uint8_t* __restrict__ base, _
     }
     wait_vm_le(0u);  // nothing may still be landing in the region the hybrid loop stages into
     const uint32_t a_sw = a0 + u * kRxRun;
-    if (stop && a_sw < a_end) rx_runs_pfx<R, V6, 7, true>(base, ofs, n, a_sw, a_end, lane, region, ro);
+    StaticRuns rest{a_sw, a_end};
+    if (stop && a_sw < a_end) rx_runs_pfx<R, V6, 7, true>(base, ofs, n, rest, lane, region, ro);
 }
 
 
@@ -2125,6 +2214,18 @@ constexpr uint32_t kRxPfxMean = 112;
 constexpr uint32_t kRxStreamMeanSmallN = 448;      // the streaming threshold below kRxStreamBigN frames
 constexpr uint32_t kRxStreamMeanBigN = 768;        // ... and from kRxStreamBigN frames
 constexpr uint32_t kRxStreamBigN = 5u << 19;       // 2.5M frames
+// The two-wave modes' dealt runs (§7 step 72): the pool is the batch's last 1/2^kRxPoolShift, dealt from
+// kRxDealHeads counters, each on its own 64 B line; kRxDealSlots streams per device hold heads at once.
+#ifndef NSX_RX_POOL_SHIFT
+#define NSX_RX_POOL_SHIFT 3
+#endif
+constexpr uint32_t kRxPoolShift = NSX_RX_POOL_SHIFT;
+#ifndef NSX_RX_DEAL_SPREAD
+#define NSX_RX_DEAL_SPREAD 1
+#endif
+constexpr uint32_t kRxDealHeads = 32;
+constexpr uint32_t kRxDealStride = 16;  // dwords
+constexpr uint32_t kRxDealSlots = 64;
 
 // PF = -1: the default grid's kernel (4 blocks/CU, PfxSlot<15> × 2 of LDS per block): sets 0 = by the batch's mean
 // frame and frame count (above), 1 = streamed runs on every block, 8 = streamed runs on 3 blocks per CU, 5 = the small-frame mode (LDS loop, then the hybrid
@@ -2147,11 +2248,40 @@ __global__ __launch_bounds__(kBlock, NSX_RX_WPS(WPS)) void rx_tcp_kernel(const u
                                                              uint64_t* __restrict__ mask,
                                                              uint16_t* __restrict__ ip_raw,
                                                              uint16_t* __restrict__ tcp_raw, int sets,
-                                                             uint32_t big_keep) {
+                                                             uint32_t big_keep, uint32_t* __restrict__ deal) {
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+#if defined(NSX_RX_DIAG) && NSX_RX_DIAG == 7
+    const uint64_t t_k = __builtin_amdgcn_s_memrealtime();  // diagnostic build only: kernel entry
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+#endif
     const __amdgpu_buffer_rsrc_t ofs = make_rsrc(offsets, ((uint64_t)n + 1) * 8);
+#if defined(NSX_RX_DIAG) && NSX_RX_DIAG == 7
+    // diagnostic build only (tools/probes/rx_wave_times.py): the two-wave modes' per-wave s_memrealtime stamps
+    // (100 MHz) of entry, range ready and end, the wave's bytes and where it ran (HW_ID's low half: wave, SIMD, CU,
+    // SH, SE; XCC_ID), written over the tcp_raw buffer (no raw sums in this build): [g] = {t_entry, t_range, t_end,
+    // bytes | id << 32}
+    auto timed = [&](const WaveRange& wr, uint32_t nb, uint32_t wpb, RxOuts& rq, auto&& body) {
+        rq.raw = false;
+        const uint64_t t_rg = __builtin_amdgcn_s_memrealtime();
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        body();
+        const uint64_t t_out = __builtin_amdgcn_s_memrealtime();
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        const uint32_t b = blockIdx.x;
+        const uint32_t g = (nb >= 16 && (nb & 7) == 0) ? ((b & 7) * (nb >> 3) + (b >> 3)) * wpb + wave : b * wpb + wave;
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        const uint64_t id = (uint64_t)((xcc & 0xFu) << 16 | (hw & 0xFFFFu)) << 32;
+        const uint64_t v = lane == 0 ? t_k : lane == 1 ? t_rg : lane == 2 ? t_out : (wr.bytes & 0xFFFFFFFFu) | id;
+        uint64_t* ts = reinterpret_cast<uint64_t*>(tcp_raw);
+        if (ts && lane < 4u) ts[(uint64_t)g * 4u + lane] = v;
+    };
+    RxOuts ro = rx_outs(mask, ip_raw, tcp_raw, n);
+#else
     const RxOuts ro = rx_outs(mask, ip_raw, tcp_raw, n);
+#endif
     extern __shared__ lds16 lds_rx[];
     // Byte-balanced wave ranges (as csum_ragged_scan_kernel), cut at multiples of 8 frames. Cut at whole mask
     // words (64 frames, ~50 KB) instead, a wave streamed up to one run more than the mean, and the launch
@@ -2169,30 +2299,62 @@ __global__ __launch_bounds__(kBlock, NSX_RX_WPS(WPS)) void rx_tcp_kernel(const u
             const uint64_t stream_mean = n >= kRxStreamBigN ? kRxStreamMeanBigN : kRxStreamMeanSmallN;
             mode = tot >= stream_mean * n ? 1 : tot >= (uint64_t)kRxPfxMean * n ? 6 : 5;
         }
-        if (mode == 6) {  // two waves per block, 15-row slots (waves 0-1: as fast as 0-1 / 2-3 by block parity
-                          // and as 2 blocks/CU of four waves)
-            if (wave >= 2u) return;
-            const WaveRange wr = range(gridDim.x, 2u, wave);
-            rx_runs_pfx<R, V6, 15, false>(base, ofs, n, wr.a0, wr.a_end, lane,
-                                          lds_rx + wave * (PfxSlot<15>::kBytes / 16u), ro);
-        } else if (mode == 9) {  // two waves per block: the LDS loop fed by LDS-DMA through a ring (§7 step 70)
+        if (mode == 9) {  // two waves per block: the LDS loop fed by LDS-DMA through a ring (§7 step 70)
             if (wave >= 2u) return;
             const WaveRange wr = range(gridDim.x, 2u, wave);
             rx_runs_ring<R, V6>(base, ofs, n, wr.a0, wr.a_end, lane, lds_rx + wave * (kRingWave / 16u), ro);
-        } else if (mode == 5 || mode == 7) {  // two waves per block: the LDS loop until a run needs the hybrid loop
-                                              // (5), or the hybrid loop throughout (7). Four waves per block ran
-                                              // 2.5-4.4% slower on 40-120 B frames (workloads 13, 16; 17 −0.3%):
-                                              // with 8 waves per CU the VALU-heavy LDS loop queues less for issue
-                                              // 
+        } else if (mode == 5 || mode == 6 || mode == 7) {
+            // Two waves per block. 5: the LDS loop until a run needs the hybrid loop; 7: the hybrid loop throughout
+            // (four waves per block ran 2.5-4.4% slower on 40-120 B frames, workloads 13, 16; 17 −0.3%: with 8 waves
+            // per CU the VALU-heavy LDS loop queues less for issue); 6: the prefix form with
+            // 15-row slots (waves 0-1: as fast as 0-1 / 2-3 by block parity and as 2 blocks/CU of four waves, §7 step
+            // 55).
+            // The runs (§7 step 72): with heads for this launch (deal), each wave's equal share of the batch's first
+            // n − n/2^kRxPoolShift frames, then runs dealt to the waves as they ask, from kRxDealHeads counters
+            // (waves and pool in that many contiguous groups, so a head's waves share an XCD); without, each wave's
+            // share of the whole batch. Waves ran their equal shares at ±4% speeds, and a launch waited 6-9 µs (7%)
+            // for its last waves (tools/probes/rx_wave_times.py, profiles/r05_rx_wave_times.txt).
             if (wave >= 2u) return;
-            const WaveRange wr = range(gridDim.x, 2u, wave);
-            lds16* slot = lds_rx + wave * (PfxSlot<7>::kBytes / 16u);
-#if defined(NSX_RX_DIAG) && NSX_RX_DIAG == 5
-            if (mode == 5) rx_runs_lds2<R, V6>(base, ofs, n, wr.a0, wr.a_end, lane, slot, ro);
+            const uint32_t nb = gridDim.x, W2 = nb * 2u, b = blockIdx.x;
+            const uint32_t g = (nb >= 16 && (nb & 7) == 0) ? ((b & 7) * (nb >> 3) + (b >> 3)) * 2u + wave : b * 2u + wave;
+            const uint32_t S = deal ? (n - (n >> kRxPoolShift)) & ~(kPfxRun - 1u) : n;
+            DealtRuns q{0u, 0u, n, 0u, 0u, 0u, nullptr, lane, 0u, false, false};
+            WaveRange wr{0u, 0u, 0u};
+            if (S > 0u) wr = wave_range(ofs, S, g, W2, lane, kRxSmallFrame, 8u);
+            q.a0 = wr.a0, q.e_st = wr.a_end;
+            if (deal) {
+#if NSX_RX_DEAL_SPREAD
+                const uint32_t H = min(kRxDealHeads, W2), h = g % H;
+                const uint32_t g0 = 0u, g1 = (W2 - h + H - 1u) / H;  // waves g ≡ h mod H
 #else
-            if (mode == 5) rx_runs_lds<R, V6, true>(base, ofs, n, wr.a0, wr.a_end, lane, slot, ro);
+                const uint32_t H = min(kRxDealHeads, W2), h = (uint32_t)((uint64_t)g * H / W2);
+                const uint32_t g0 = (uint32_t)(((uint64_t)h * W2 + H - 1u) / H);
+                const uint32_t g1 = (uint32_t)(((uint64_t)(h + 1u) * W2 + H - 1u) / H);
 #endif
-            else rx_runs_pfx<R, V6, 7, true>(base, ofs, n, wr.a0, wr.a_end, lane, slot, ro);
+                const uint32_t Q = (n - S + kPfxRun - 1u) / kPfxRun;  // the pool's runs
+                const uint32_t r0 = (uint32_t)((uint64_t)Q * h / H);
+                const uint32_t qh = (uint32_t)((uint64_t)Q * (h + 1u) / H) - r0;
+                q.pb = S + r0 * kPfxRun, q.q = qh, q.last = qh + (g1 - g0) - 1u;
+                q.head = deal + h * kRxDealStride;
+                q.init();
+            }
+#if defined(NSX_RX_DIAG) && NSX_RX_DIAG == 7
+            timed(wr, gridDim.x, 2u, ro, [&] {
+#endif
+            if (mode == 6) {
+                rx_runs_pfx<R, V6, 15, false>(base, ofs, n, q, lane, lds_rx + wave * (PfxSlot<15>::kBytes / 16u), ro);
+            } else {
+                lds16* slot = lds_rx + wave * (PfxSlot<7>::kBytes / 16u);
+#if defined(NSX_RX_DIAG) && NSX_RX_DIAG == 5
+                if (mode == 5) rx_runs_lds2<R, V6>(base, ofs, n, wr.a0, wr.a_end, lane, slot, ro);
+#else
+                if (mode == 5) rx_runs_lds<R, V6, true>(base, ofs, n, q, lane, slot, ro);
+#endif
+                else rx_runs_pfx<R, V6, 7, true>(base, ofs, n, q, lane, slot, ro);
+            }
+#if defined(NSX_RX_DIAG) && NSX_RX_DIAG == 7
+            });
+#endif
         } else {  // streamed runs on 3 of the 4 blocks per CU (the auto choice and mode 8, which forces it); mode 1:
                   // on every block
             const uint32_t nb = active_blocks(ofs, n, 0u, sets == 0 || sets == 8 ? 3u : 0u);
@@ -2221,7 +2383,8 @@ __global__ __launch_bounds__(kBlock, NSX_RX_WPS(WPS)) void rx_tcp_kernel(const u
     const uint32_t a0 = wr.a0, a_end = wr.a_end;
     const bool small = sets == 2 || (sets == 0 && wr.bytes < (uint64_t)kRxSmallFrame * (a_end - a0));
     if (small) {
-        rx_runs_lds<R, V6>(base, ofs, n, a0, a_end, lane, lds_rx + wave * (kRxSlot / 16u), ro);
+        StaticRuns q{a0, a_end};
+        rx_runs_lds<R, V6>(base, ofs, n, q, lane, lds_rx + wave * (kRxSlot / 16u), ro);
     } else {
         rx_runs<R, V6, 1>(base, ofs, n, a0, a_end, lane, ro);
     }
@@ -3461,6 +3624,55 @@ bool rx_tune_valid(const LaunchCfg& c) {
     return !grid_mode || ((c.rows == 0 || c.rows == 2) && c.blocks_per_cu == 0);
 }
 
+// The receive pass's deal counters (§7 step 72): kRxDealSlots sets of kRxDealHeads heads per device, zero at load;
+// every launch leaves its heads at 0 (DealtRuns), so a set can serve one stream's launches one after another.
+__device__ uint32_t g_rx_deal[kRxDealSlots * kRxDealHeads * kRxDealStride];
+
+// The heads for a launch on stream st of the current device: the stream's own set (given on first use, kept for the
+// process), or nullptr — equal static shares — when the stream is being captured into a graph (a graph's launches
+// could replay on several streams at once), when every set is given out, or in builds without dealing.
+static uint32_t* rx_deal_heads(hipStream_t st) {
+#if defined(NSX_RX_NO_DEAL) || (defined(NSX_RX_DIAG) && NSX_RX_DIAG == 5)
+    (void)st;
+    return nullptr;
+#else
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess) {
+        (void)hipGetLastError();  // a refused query (e.g. the legacy stream while another captures) is not the launch's error
+        return nullptr;
+    }
+    if (cs != hipStreamCaptureStatusNone) return nullptr;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    static std::mutex mu;
+    static std::map<std::pair<int, hipStream_t>, uint32_t> slot_of;
+    static std::map<int, std::pair<uint32_t*, uint32_t>> dev_sets;  // device → (its g_rx_deal, sets given)
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = slot_of.find({dev, st});
+    auto& ds = dev_sets[dev];
+    if (!ds.first) {
+        void* p = nullptr;
+        if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_rx_deal)) != hipSuccess || !p) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        ds.first = static_cast<uint32_t*>(p);
+    }
+    uint32_t slot;
+    if (it != slot_of.end()) {
+        slot = it->second;
+    } else {
+        if (ds.second >= kRxDealSlots) return nullptr;
+        slot = ds.second++;
+        slot_of[{dev, st}] = slot;
+    }
+    return ds.first + (size_t)slot * kRxDealHeads * kRxDealStride;
+#endif
+}
+
 hipError_t launch_rx_tcp(const LaunchCfg& c, int ipver, const void* d_base, const uint64_t* d_offsets, uint64_t n,
                          uint64_t* mask, uint16_t* ip_raw, uint16_t* tcp_raw, hipStream_t st) {
     if (!rx_tune_valid(c)) return hipErrorInvalidValue;
@@ -3490,6 +3702,7 @@ hipError_t launch_rx_tcp(const LaunchCfg& c, int ipver, const void* d_base, cons
         static_assert(la_def >= (size_t)PfxSlot<7>::kBytes * kWavesPerBlock && la_def * 4 <= 163840 &&
                           la_ring * 4 <= 163840, "4 blocks per CU");
         const size_t la = c.segs_per_wave == 9 ? la_ring : la_def;
+        uint32_t* deal = rx_deal_heads(st);
         for (uint64_t c0 = 0; c0 < n; c0 += kRaggedChunk) {
             const uint32_t cn = (uint32_t)(n - c0 < kRaggedChunk ? n - c0 : kRaggedChunk);
             const uint32_t grid = grid_for((cn + kRxRun - 1) / kRxRun, (uint32_t)c.cus * 4u);
@@ -3497,10 +3710,10 @@ hipError_t launch_rx_tcp(const LaunchCfg& c, int ipver, const void* d_base, cons
             uint16_t* tc = tcp_raw ? tcp_raw + c0 : nullptr;
             if (ipver == 6)
                 hipLaunchKernelGGL((rx_tcp_kernel<2, true, 4, -1>), dim3(grid), dim3(kBlock), la, st, base, d_offsets + c0,
-                                   cn, mask + c0 / 64, nullptr, tc, c.segs_per_wave, 0u);
+                                   cn, mask + c0 / 64, nullptr, tc, c.segs_per_wave, 0u, deal);
             else
                 hipLaunchKernelGGL((rx_tcp_kernel<2, false, 4, -1>), dim3(grid), dim3(kBlock), la, st, base,
-                                   d_offsets + c0, cn, mask + c0 / 64, ic, tc, c.segs_per_wave, 0u);
+                                   d_offsets + c0, cn, mask + c0 / 64, ic, tc, c.segs_per_wave, 0u, deal);
             const hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
@@ -3514,10 +3727,10 @@ hipError_t launch_rx_tcp(const LaunchCfg& c, int ipver, const void* d_base, cons
 #define NSX_RX(R_, W_)                                                                                            \
         if (rows == R_ && w4 == (W_ == 4) && ipver == 6)                                                           \
             hipLaunchKernelGGL((rx_tcp_kernel<R_, true, W_>), dim3(grid), dim3(kBlock), lds, st, base, d_offsets + c0, \
-                               cn, mask + c0 / 64, nullptr, tc, sets, keep);                                             \
+                               cn, mask + c0 / 64, nullptr, tc, sets, keep, nullptr);                                    \
         if (rows == R_ && w4 == (W_ == 4) && ipver != 6)                                                           \
             hipLaunchKernelGGL((rx_tcp_kernel<R_, false, W_>), dim3(grid), dim3(kBlock), lds, st, base,                \
-                               d_offsets + c0, cn, mask + c0 / 64, ic, tc, sets, keep);
+                               d_offsets + c0, cn, mask + c0 / 64, ic, tc, sets, keep, nullptr);
         NSX_RX(2, 1) NSX_RX(4, 1) NSX_RX(8, 1) NSX_RX(16, 1) NSX_RX(2, 4)
 #undef NSX_RX
         const hipError_t e = hipGetLastError();

@@ -251,6 +251,53 @@ def test_rx_bench_workload_full_size():
     assert np.array_equal(got, np.packbits(pad, bitorder="little").view(np.uint64))
 
 
+def test_rx_dealt_runs_back_to_back_and_on_many_streams():
+    """The two-wave modes deal each launch's last runs from counters of the launch's stream, which the launch leaves
+    at zero for the next: launches back to back on one stream with no sync between them —
+    batches of different sizes (3 frames to 200k) and modes (auto, 5, 6, 7) — and launches on 70 HIP streams at once,
+    more than the 64 counter sets a device gives out (the rest run equal static shares), all equal the oracle."""
+    import ctypes
+    rng = np.random.default_rng(0x8A)
+    cases = []
+    for n, mp in ((200_000, 40), (150_001, 120), (3, 40), (70_000, 1460), (129, 40), (64 * 1000, 80)):
+        buf, offs, _ = _rx.batch(rng, n, lead=int(rng.integers(4)), max_payload=mp)
+        cases.append((dev(buf), dev(offs.view(np.int64)), O.c_rx_ipv4_tcp(buf, offs)))
+    modes = [None, dict(segs_per_wave=5), dict(segs_per_wave=6), dict(segs_per_wave=7)]
+
+    def launch(k, tune, stream=None):
+        dbuf, doffs, _ = cases[k]
+        n = doffs.numel() - 1
+        with torch.cuda.stream(stream or torch.cuda.current_stream()):  # the outputs' fill ordered before the launch
+            mask = torch.full(((n + 63) // 64,), 0x5A5A5A5A5A5A5A5A, dtype=torch.int64, device="cuda")
+            ipr = torch.empty(n, dtype=torch.int16, device="cuda")
+            tcpr = torch.empty(n, dtype=torch.int16, device="cuda")
+            nsx.rx_ipv4_tcp_verify_dev(dbuf, doffs, mask=mask, ip_raw=ipr, tcp_raw=tcpr, tune=tune)
+        return k, tune, (mask, ipr, tcpr)
+
+    def check(results):
+        torch.cuda.synchronize()
+        for k, tune, (mask, ipr, tcpr) in results:
+            got = (host(mask).view(np.uint64), u16(ipr), u16(tcpr))
+            for w, g, what in zip(cases[k][2], got, ("mask", "ip_raw", "tcp_raw")):
+                assert np.array_equal(w, g), (what, k, tune)
+
+    check([launch(k, modes[(r + k) % 4]) for r in range(4) for k in range(len(cases))])
+    torch.cuda.synchronize()
+    hip = ctypes.CDLL("libamdhip64.so")
+    handles = []
+    for _ in range(70):
+        h = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(h)) == 0
+        handles.append(h)
+    try:
+        streams = [torch.cuda.ExternalStream(h.value) for h in handles]
+        check([launch((i + r) % len(cases), modes[i % 4], streams[i]) for r in range(2) for i in range(len(streams))])
+    finally:
+        torch.cuda.synchronize()
+        for h in handles:
+            hip.hipStreamDestroy(h)
+
+
 @pytest.mark.parametrize("shards", [1, 2, 3, 8])
 def test_rx_host_batches_sharded(shards):
     """nsx_rx_ipv4_tcp_verify_host: the receive pass from host memory (pinned staging, H2D → kernel → D2H of

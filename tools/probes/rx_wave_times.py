@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""Per-wave timeline of the receive pass's small-frame mode (diagnostic build only: make exp X=diag7
+EXTRA_KFLAGS=-DNSX_RX_DIAG=7, whose kernel writes each wave's s_memrealtime stamps over the tcp_raw buffer instead of
+raw sums). Loads network-stack_amd/lib_diag7, builds a bench workload, runs it many times back to back, and prints
+the distribution of wave start (relative to the launch's first wave), range-ready and end times, in µs, and how
+the end times split over the hardware (the kernel also records each wave's HW_ID and XCC_ID): per XCD, per CU and
+within a block — with the tail each level of balancing would leave (every CU's, or every block's, waves ending at
+their mean).
+
+    python tools/probes/rx_wave_times.py [--config 13] [--launches 20]
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "network-stack_amd")]
+
+import numpy as np  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=13)
+    ap.add_argument("--launches", type=int, default=20)
+    ap.add_argument("--mode", type=int, default=5)
+    ap.add_argument("--lib", default="diag7", help="network-stack_amd/lib_<name>: a build with NSX_RX_DIAG=7")
+    a = ap.parse_args()
+    import nsx
+    nsx.LIB_PATH = os.path.join(ROOT, "network-stack_amd", f"lib_{a.lib}", "libnsx_csum.so")
+    import torch
+    import bench
+    torch.cuda.set_device(0)
+    cfg = dict(bench.WORKLOADS[a.config])
+    w = bench.build_workload(cfg, 0, torch.device("cuda", 0))
+    n = cfg["n"]
+    ts = torch.zeros(max(n, 4096 * 16), dtype=torch.int16, device="cuda")
+    rx = nsx.rx_ipv6_tcp_verify_dev if cfg.get("ipver") == 6 else nsx.rx_ipv4_tcp_verify_dev
+    tune = dict(segs_per_wave=a.mode)
+    for _ in range(200):
+        rx(w["buf"], w["d_offs"], mask=w["out"], tcp_raw=ts, tune=tune)
+    torch.cuda.synchronize()
+    rows = []
+    for _ in range(a.launches):
+        ts.zero_()
+        for _ in range(3):
+            rx(w["buf"], w["d_offs"], mask=w["out"], tcp_raw=ts, tune=tune)
+        torch.cuda.synchronize()
+        t = ts.view(torch.int64).cpu().numpy().view(np.uint64)
+        nw = int(np.count_nonzero(t[2::4]))
+        t = t[: nw * 4].reshape(nw, 4).astype(np.int64)
+        t0 = t[:, 0].min()
+        rows.append(((t[:, 0] - t0) / 100.0, (t[:, 1] - t0) / 100.0, (t[:, 2] - t0) / 100.0, t[:, 3] & 0xFFFFFFFF,
+                     t[:, 3] >> 32))
+    for name, k in (("start", 0), ("range", 1), ("end", 2)):
+        v = np.concatenate([r[k] for r in rows])
+        print(f"{name:6s} us: min {v.min():7.2f} p10 {np.percentile(v, 10):7.2f} p50 {np.percentile(v, 50):7.2f} "
+              f"p90 {np.percentile(v, 90):7.2f} p99 {np.percentile(v, 99):7.2f} max {v.max():7.2f}")
+    # by XCD: waves are numbered XCD-major (g = xcd * W/8 + i), so the end time's mean per eighth of g
+    nw = len(rows[0][0])
+    for k, nm in ((2, "end"),):
+        per = np.mean([[r[k][x * nw // 8:(x + 1) * nw // 8].mean() - np.median(r[k]) for x in range(8)] for r in rows], 0)
+        print(f"{nm} minus median, mean per XCD (us): " + " ".join(f"{v:+.2f}" for v in per))
+    # does a wave's end follow its frame bytes? (correlation over waves, median over launches)
+    if rows[0][3].max() != rows[0][3].min():
+        print(f"corr(end, bytes) {np.median([np.corrcoef(r[2], r[3])[0, 1] for r in rows]):.3f}; bytes per wave "
+              f"p1 {np.percentile(rows[0][3], 1):.0f} p50 {np.median(rows[0][3]):.0f} p99 {np.percentile(rows[0][3], 99):.0f}")
+    # where the spread lives: CU = (XCC_ID, HW_ID's SE/SH/CU bits); block = the wave pair g // 2
+    def grouped_tail(r, key):
+        end, med = r[2], np.median(r[2])
+        _, inv = np.unique(key, return_inverse=True)
+        means = np.bincount(inv, weights=end) / np.bincount(inv)
+        within = end - means[inv]
+        return means.max() - med, means.std(), within.std(), int(np.bincount(inv).mean())
+    for nm, keyf in (("CU", lambda r: ((r[4] >> 16) << 8) | ((r[4] >> 8) & 0xFF)),
+                     ("SIMD", lambda r: ((r[4] >> 16) << 10) | ((r[4] >> 4) & 0xFFF)),
+                     ("block", lambda r: np.arange(len(r[2])) // 2)):
+        v = np.array([grouped_tail(r, keyf(r)) for r in rows])
+        print(f"by {nm:5s}: waves per group {int(v[0, 3])}; std of group means {np.median(v[:, 1]):.2f} us, std within "
+              f"groups {np.median(v[:, 2]):.2f} us; tail if each group's waves ended at their mean "
+              f"{np.median(v[:, 0]):.2f} us")
+    print(f"end std over waves {np.median([r[2].std() for r in rows]):.2f} us")
+    ends = np.array([r[2].max() for r in rows])
+    med_end = np.array([np.median(r[2]) for r in rows])
+    print(f"launch span (first start -> last end) us: median {np.median(ends):.2f}; median wave end {np.median(med_end):.2f}; "
+          f"tail (last end - median end) {np.median(ends - med_end):.2f}; waves {len(rows[0][0])}")
+
+
+if __name__ == "__main__":
+    main()

@@ -10,7 +10,7 @@ mkdir -p "$out"
 export TMPDIR=/tmp
 # the library is built here, before rocprofv3 starts (its preloaded library initialises the GPU first), and bench.py
 # loads it as it is (--no-build): no compiler runs as a child of a profiled process
-make -s -j16 -C network-stack_amd || exit 1
+[ -n "${NO_MAKE:-}" ] || make -s -j16 -C network-stack_amd || exit 1  # NO_MAKE: a library swapped in by tools/valu_ab.sh
 B="bench.py --config $cfg --steps 50 --warmup 5 --cpu-seconds 0 --no-build ${BENCH_EXTRA:-}"
 run() {  # run <name> <timeout> rocprofv3-args...
   local name=$1 t=$2; shift 2
