@@ -2279,6 +2279,7 @@ __global__ __launch_bounds__(kBlock, NSX_RX_WPS(WPS)) void rx_tcp_kernel(const u
         if (ts && lane < 4u) ts[(uint64_t)g * 4u + lane] = v;
     };
     RxOuts ro = rx_outs(mask, ip_raw, tcp_raw, n);
+    ro.raw = false;  // tcp_raw holds the stamps
 #else
     const RxOuts ro = rx_outs(mask, ip_raw, tcp_raw, n);
 #endif
@@ -2368,7 +2369,13 @@ __global__ __launch_bounds__(kBlock, NSX_RX_WPS(WPS)) void rx_tcp_kernel(const u
                 rp.tpk = make_park<uint16_t>(pb, ro.trs, tcp_raw, wr.a0, V6 ? 4096u : 2048u);
                 if constexpr (!V6) rp.ipk = make_park<uint16_t>(pb + 2048, ro.irs, ip_raw, wr.a0, 2048u);
             }
+#if defined(NSX_RX_DIAG) && NSX_RX_DIAG == 7
+            timed(wr, nb, kWavesPerBlock, ro, [&] {
+#endif
             rx_runs<R, V6, 1>(base, ofs, n, wr.a0, wr.a_end, lane, rp);
+#if defined(NSX_RX_DIAG) && NSX_RX_DIAG == 7
+            });
+#endif
             if (ro.raw) {
                 park_flush(rp.tpk, lane);
                 if constexpr (!V6) park_flush(rp.ipk, lane);

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--config", type=int, default=13)
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--mode", type=int, default=5)
+    ap.add_argument("--wpb", type=int, default=2, help="waves per block taking ranges (streamed modes: 4)")
     ap.add_argument("--lib", default="diag7", help="network-stack_amd/lib_<name>: a build with NSX_RX_DIAG=7")
     a = ap.parse_args()
     import nsx
@@ -74,7 +75,7 @@ def main():
         return means.max() - med, means.std(), within.std(), int(np.bincount(inv).mean())
     for nm, keyf in (("CU", lambda r: ((r[4] >> 16) << 8) | ((r[4] >> 8) & 0xFF)),
                      ("SIMD", lambda r: ((r[4] >> 16) << 10) | ((r[4] >> 4) & 0xFFF)),
-                     ("block", lambda r: np.arange(len(r[2])) // 2)):
+                     ("block", lambda r: np.arange(len(r[2])) // a.wpb)):
         v = np.array([grouped_tail(r, keyf(r)) for r in rows])
         print(f"by {nm:5s}: waves per group {int(v[0, 3])}; std of group means {np.median(v[:, 1]):.2f} us, std within "
               f"groups {np.median(v[:, 2]):.2f} us; tail if each group's waves ended at their mean "
