@@ -1035,6 +1035,116 @@ __device__ __forceinline__ void lds_stage(lds16* slot, u32x4 (&V)[ROWS], uint64_
     __builtin_amdgcn_wave_barrier();
 }
 
+constexpr uint32_t kSeqRun = 64;
+// Run sequences (round 5): the runs of kSeqRun units a wave takes, in order, named by their
+// first unit. The run loops (pfx_runs, rx_runs_lds) read them two runs ahead — the next run's rows and the offsets of
+// the run after it are loaded while one run is summed — and call next() exactly once per run, in order: a dealt
+// sequence pulls from a shared counter there. cnt(a) = the units of run a; a value a with !live(a) ends the
+// sequence (cnt 0).
+
+// The units [a0, a_end) in runs of `run` from a0 (end: a_end).
+struct StaticRuns {
+    uint32_t a0, a_end, run = kSeqRun;
+    __device__ __forceinline__ bool live(uint32_t a) const { return a < a_end; }
+    __device__ __forceinline__ uint32_t first() const { return a0; }
+    __device__ __forceinline__ uint32_t next(uint32_t a) const { return a + run < a_end ? a + run : a_end; }
+    __device__ __forceinline__ uint32_t cnt(uint32_t a) const { return min(run, a_end - a); }
+    __device__ __forceinline__ void refill() const {}
+};
+
+// A wave's static runs [a0, e_st), then runs dealt from a pool: the batch's last units [S, n), as runs from S, split
+// into one share per counter ("head") — the share's runs pb + 64 t, t < q, go to the waves of this head in the order
+// they ask (end: n). A wave always holds one ticket ahead (pulled one run before it is needed, so that the counter's
+// round trip, ~1-3 µs under load, overlaps a run's work): the pull is a returning device-scope atomic add from lane
+// 0, its value read (readfirstlane) only when the ticket is taken. Every wave of the head takes tickets until one is
+// past its share, so the head sees exactly q + (its waves) pulls per launch: the wave that draws the last of them,
+// `last`, resets the counter to 0 for the next launch that uses it — launches on one stream run one after another,
+// and the host gives each stream its own heads (deal_heads).
+struct DealtRuns {
+    uint32_t a0, e_st, n;
+    uint32_t pb, q, last;
+    uint32_t* head;
+    uint32_t lane;
+    uint32_t tk;    // the reserved ticket (lane 0's VGPR until taken)
+    bool dealing;   // false once a ticket past the share was taken (or without a head)
+    bool want;      // a ticket was taken and the next is not yet pulled (refill)
+    __device__ __forceinline__ uint32_t pull() const {
+        uint32_t t = 0u;
+        if (lane == 0u) t = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return t;
+    }
+    __device__ __forceinline__ void init() {
+        tk = pull();
+        dealing = true;
+        want = false;
+    }
+    // The pull for the next ticket, issued by the run loops after a run's loads: vmcnt retires in issue order, so
+    // loads issued behind the atomic would wait for its round trip too.
+    __device__ __forceinline__ void refill() {
+        if (want) tk = pull();
+        want = false;
+    }
+    __device__ __forceinline__ uint32_t take() {
+        if (!dealing) return n;
+        refill();
+        const uint32_t t = __builtin_amdgcn_readfirstlane(tk);
+        if (t < q) {
+            want = true;
+            return pb + t * kSeqRun;
+        }
+        dealing = false;
+        if (t == last && lane == 0u) __hip_atomic_store(head, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return n;
+    }
+    __device__ __forceinline__ bool live(uint32_t a) const { return a < n; }
+    __device__ __forceinline__ uint32_t first() { return a0 < e_st ? a0 : take(); }
+    // a static run's successor, else a dealt run (a pool run, or the end n: both ≥ e_st)
+    __device__ __forceinline__ uint32_t next(uint32_t a) { return a + kSeqRun < e_st ? a + kSeqRun : take(); }
+    __device__ __forceinline__ uint32_t cnt(uint32_t a) const { return min(kSeqRun, (a < e_st ? e_st : n) - a); }
+};
+
+// The deal's shape: the pool is a batch's last 1/2^kDealPoolShift, dealt from kDealHeads counters, each on its own
+// 64 B line (kDealStride dwords); kDealSlots streams per device hold a set of heads at once (deal_heads).
+#ifndef NSX_DEAL_POOL_SHIFT
+#define NSX_DEAL_POOL_SHIFT 3
+#endif
+constexpr uint32_t kDealPoolShift = NSX_DEAL_POOL_SHIFT;
+constexpr uint32_t kDealHeads = 32;
+constexpr uint32_t kDealStride = 16;
+constexpr uint32_t kDealSlots = 64;
+
+// Wave g of W's runs: with heads for this launch (deal), its equal share (wave_range: small_mean, align,
+// count_align) of the batch's first n − n/2^kDealPoolShift units (S, a multiple of kSeqRun), then runs of the pool
+// [S, n) dealt from head g mod kDealHeads — the waves of a head spread over every XCD (heads per XCD left the XCDs'
+// speed differences in place, §7 step 72); without, its equal share of the whole batch. wr_out: the static share.
+__device__ __forceinline__ DealtRuns deal_runs(__amdgpu_buffer_rsrc_t ofs, uint32_t n, uint32_t g, uint32_t W,
+                                               uint32_t lane, uint32_t small_mean, uint32_t align,
+                                               uint32_t count_align, uint32_t* deal, WaveRange* wr_out = nullptr) {
+    const uint32_t S = deal ? (n - (n >> kDealPoolShift)) & ~(kSeqRun - 1u) : n;
+    DealtRuns q{0u, 0u, n, 0u, 0u, 0u, nullptr, lane, 0u, false, false};
+    WaveRange wr{0u, 0u, 0u};
+    if (S > 0u) wr = wave_range(ofs, S, g, W, lane, small_mean, align, count_align);
+    q.a0 = wr.a0, q.e_st = wr.a_end;
+    if (wr_out) *wr_out = wr;
+    if (deal) {
+        const uint32_t H = min(kDealHeads, W), h = g % H;
+        const uint32_t Q = (n - S + kSeqRun - 1u) / kSeqRun;  // the pool's runs
+        const uint32_t r0 = (uint32_t)((uint64_t)Q * h / H);
+        const uint32_t qh = (uint32_t)((uint64_t)Q * (h + 1u) / H) - r0;
+        q.pb = S + r0 * kSeqRun, q.q = qh, q.last = qh + (W - h + H - 1u) / H - 1u;  // + the head's waves g ≡ h
+        q.head = deal + h * kDealStride;
+        q.init();
+    }
+    return q;
+}
+
+// A run loop's state at a run boundary, handed from one loop to another (rx_runs_lds → the hybrid loop): run a with
+// its offsets (lane l = unit a + l; c_end: a + l + 1), the next run an with its offsets.
+struct RunHead {
+    uint32_t a, an;
+    uint64_t c_off, c_end, n_off, n_end;
+};
+
 // The LDS form of the ragged checksum for small segments, the receive pass's
 // (rx_runs_lds) applied to runs of ≤ run segments: lane l sums segment a + l out of the wave's slot, both of its
 // offsets loaded by the lane itself. A run too wide for the slot is streamed (as ≤ 63 + the rest).
@@ -1050,19 +1160,19 @@ __device__ __forceinline__ void lds_stage(lds16* slot, u32x4 (&V)[ROWS], uint64_
 constexpr uint32_t kScanSlotRows = 8;
 constexpr uint32_t kScanSlot = kScanSlotRows * kRow + 256;  // + pad: lds_range_sum's first chunk block reads past the end
 
-template <int R, bool VERIFY, bool PIPE, bool PARK>
+template <int R, bool VERIFY, bool PIPE, bool PARK, typename Seq>
 __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
                                                 __amdgpu_buffer_rsrc_t prs, __amdgpu_buffer_rsrc_t ors,
-                                                __amdgpu_buffer_rsrc_t oks, uint32_t run, uint32_t a0, uint32_t a_end,
-                                                uint32_t lane, lds16* slot, bool has_part, const void* out, bool raw) {
+                                                __amdgpu_buffer_rsrc_t oks, uint32_t run, Seq& q, uint32_t lane,
+                                                lds16* slot, bool has_part, const void* out, bool raw) {
     typedef uint32_t v2u __attribute__((ext_vector_type(2)));
     auto ld64 = [&](uint32_t i, bool live) -> uint64_t {
         const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, live ? i * 8 : kOOB, 0, 0);
         return ((uint64_t)x.y << 32) | x.x;
     };
     // lane l < run length: segment a + l = [offsets[a + l], offsets[a + l + 1])
-    auto load_offs = [&](uint32_t a) { return ld64(a + lane, a < a_end && lane < run && a + lane <= n); };
-    auto load_ends = [&](uint32_t a) { return ld64(a + lane + 1u, a < a_end && lane < run && a + lane + 1u <= n); };
+    auto load_offs = [&](uint32_t a) { return ld64(a + lane, q.live(a) && lane < run && a + lane <= n); };
+    auto load_ends = [&](uint32_t a) { return ld64(a + lane + 1u, q.live(a) && lane < run && a + lane + 1u <= n); };
     struct Run {
         const uint8_t* rbase;
         uint64_t span;
@@ -1070,7 +1180,7 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
         bool lds;
     };
     auto geo = [&](uint32_t a, uint64_t off, uint64_t end) {  // wave-uniform geometry of run a
-        Run g{base, 0, a < a_end ? min(run, a_end - a) : 0u, false};
+        Run g{base, 0, q.cnt(a), false};
         if (g.cnt) {
             const uint64_t lo = readlane64(off, 0), hi = readlane64(end, g.cnt - 1u);
             g.rbase = reinterpret_cast<const uint8_t*>(((uintptr_t)(base + lo)) & ~(uintptr_t)127);
@@ -1088,16 +1198,21 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
 #pragma unroll
         for (uint32_t r = 0; r < kScanSlotRows; ++r) V[r] = bld16<true>(rs, r * kRow + lane * 16u);
     };
-    // PARK: the results parked in the slot after the run's (the small-segment mode gives each wave two)
-    using T = typename std::conditional<VERIFY, uint8_t, uint16_t>::type;
-    ScanPark<VERIFY> pk = make_park<T>(PARK ? reinterpret_cast<T*>(reinterpret_cast<uint8_t*>(slot) + kScanSlot) : nullptr,
-                                       VERIFY ? oks : ors, out, a0);
     // As rx_runs_lds: the LDS loop runs while consecutive runs fit the slot; a run that does not is streamed on
     // its own in the outer loop, so the streaming form's loads in flight at its end never merge into the LDS
-    // loop's wait counts.
-    uint32_t a = a0;
-    while (a < a_end) {
-        uint64_t c_off = load_offs(a), c_end = load_ends(a);
+    // loop's wait counts. The next run and its offsets are carried across (a dealt sequence's next() is called once
+    // per run).
+    uint32_t a = q.first();
+    uint64_t c_off = load_offs(a), c_end = load_ends(a);
+    uint32_t an = q.next(a);
+    uint64_t n_off = load_offs(an), n_end = load_ends(an);
+    q.refill();
+    // PARK: the results parked in the slot after the run's (the small-segment mode gives each wave two); a dealt run
+    // that does not follow the parked ones flushes them (park_put)
+    using T = typename std::conditional<VERIFY, uint8_t, uint16_t>::type;
+    ScanPark<VERIFY> pk = make_park<T>(PARK ? reinterpret_cast<T*>(reinterpret_cast<uint8_t*>(slot) + kScanSlot) : nullptr,
+                                       VERIFY ? oks : ors, out, q.live(a) ? a : 0u);
+    while (q.live(a)) {
         Run cur = geo(a, c_off, c_end);
         if (!cur.lds) {  // too wide for the slot: streamed (boundaries in lanes 0..cnt: ≤ 63 segments, then the rest)
             const uint32_t part = load_part(a, cur.cnt);
@@ -1110,31 +1225,35 @@ __device__ __forceinline__ void ragged_runs_lds(const uint8_t* __restrict__ base
                 const uint64_t o2[1] = {lane == 0 ? readlane64(c_off, c1) : readlane64(c_end, c1)};
                 ragged_run_stream<R, VERIFY, PIPE, 1>(base, a + c1, kScanRun, cnt2, o2, part2, ors, raw, lane, pk);
             }
-            a += run;
+            a = an, c_off = n_off, c_end = n_end;
+            an = q.next(a);
+            n_off = load_offs(an), n_end = load_ends(an);
+            q.refill();
             continue;
         }
         issue(cur);
-        uint64_t n_off = load_offs(a + run), n_end = load_ends(a + run);
         __builtin_amdgcn_s_waitcnt(kWaitVm0);  // as in rx_runs_lds: nothing in flight at the loop's entry
         for (;;) {
             const uint32_t part = load_part(a, cur.cnt);
             lds_stage<kScanSlotRows>(slot, V, cur.span, lane);
             lds_zero_tail(slot, cur.span, lane);
-            Run nxt = geo(a + run, n_off, n_end);
+            Run nxt = geo(an, n_off, n_end);
             if (!nxt.lds) nxt.span = 0;  // a run that will be streamed is not staged: empty loads
             issue(nxt);
-            const uint64_t p_off = load_offs(a + 2u * run), p_end = load_ends(a + 2u * run);
+            const uint32_t an2 = q.next(an);
+            const uint64_t p_off = load_offs(an2), p_end = load_ends(an2);
+            q.refill();
             const bool mine = lane < cur.cnt;
             const uint32_t p = mine ? (uint32_t)((base + c_off) - cur.rbase) : 0u;
             const uint32_t e = mine ? (uint32_t)((base + c_end) - cur.rbase) : 0u;
             const uint32_t dq = reinterpret_cast<const uint32_t*>(slot)[p >> 2];
             const uint32_t res = finish(fold32(lds_range_sum(slot, p, e, dq, mine)), (p & 1u) == 0, part);
             put_results<VERIFY>(pk, ors, raw, a, cur.cnt, lane, res);
-            a += run;
-            if (!nxt.lds) break;  // the end of the wave's range, or a run for the outer loop
+            a = an, an = an2;
+            c_off = n_off, c_end = n_end;
+            n_off = p_off, n_end = p_end;
+            if (!nxt.lds) break;  // the end of the wave's runs, or a run for the outer loop
             cur = nxt;
-            c_off = n_off, n_off = p_off;
-            c_end = n_end, n_end = p_end;
         }
     }
     park_flush(pk, lane);
@@ -1175,79 +1294,6 @@ constexpr uint32_t kPfxDirectSlot = kPfxDirectRows * kRow + 256;
 // Units up to this long may be summed lane by lane in direct pieces: 17 chunks.
 constexpr uint32_t kPfxDirectMax = 256;
 
-// Run sequences (round 5): the runs of kPfxRun units a wave takes, in order, named by their
-// first unit. The run loops (pfx_runs, rx_runs_lds) read them two runs ahead — the next run's rows and the offsets of
-// the run after it are loaded while one run is summed — and call next() exactly once per run, in order: a dealt
-// sequence pulls from a shared counter there. cnt(a) = the units of run a; a value a with !live(a) ends the
-// sequence (cnt 0).
-
-// The units [a0, a_end) in runs from a0 (end: a_end).
-struct StaticRuns {
-    uint32_t a0, a_end;
-    __device__ __forceinline__ bool live(uint32_t a) const { return a < a_end; }
-    __device__ __forceinline__ uint32_t first() const { return a0; }
-    __device__ __forceinline__ uint32_t next(uint32_t a) const { return a + kPfxRun < a_end ? a + kPfxRun : a_end; }
-    __device__ __forceinline__ uint32_t cnt(uint32_t a) const { return min(kPfxRun, a_end - a); }
-    __device__ __forceinline__ void refill() const {}
-};
-
-// A wave's static runs [a0, e_st), then runs dealt from a pool: the batch's last units [S, n), as runs from S, split
-// into one share per counter ("head") — the share's runs pb + 64 t, t < q, go to the waves of this head in the order
-// they ask (end: n). A wave always holds one ticket ahead (pulled one run before it is needed, so that the counter's
-// round trip, ~1-3 µs under load, overlaps a run's work): the pull is a returning device-scope atomic add from lane
-// 0, its value read (readfirstlane) only when the ticket is taken. Every wave of the head takes tickets until one is
-// past its share, so the head sees exactly q + (its waves) pulls per launch: the wave that draws the last of them,
-// `last`, resets the counter to 0 for the next launch that uses it — launches on one stream run one after another,
-// and the host gives each stream its own heads (rx_deal_heads).
-struct DealtRuns {
-    uint32_t a0, e_st, n;
-    uint32_t pb, q, last;
-    uint32_t* head;
-    uint32_t lane;
-    uint32_t tk;    // the reserved ticket (lane 0's VGPR until taken)
-    bool dealing;   // false once a ticket past the share was taken (or without a head)
-    bool want;      // a ticket was taken and the next is not yet pulled (refill)
-    __device__ __forceinline__ uint32_t pull() const {
-        uint32_t t = 0u;
-        if (lane == 0u) t = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return t;
-    }
-    __device__ __forceinline__ void init() {
-        tk = pull();
-        dealing = true;
-        want = false;
-    }
-    // The pull for the next ticket, issued by the run loops after a run's loads: vmcnt retires in issue order, so
-    // loads issued behind the atomic would wait for its round trip too.
-    __device__ __forceinline__ void refill() {
-        if (want) tk = pull();
-        want = false;
-    }
-    __device__ __forceinline__ uint32_t take() {
-        if (!dealing) return n;
-        refill();
-        const uint32_t t = __builtin_amdgcn_readfirstlane(tk);
-        if (t < q) {
-            want = true;
-            return pb + t * kPfxRun;
-        }
-        dealing = false;
-        if (t == last && lane == 0u) __hip_atomic_store(head, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return n;
-    }
-    __device__ __forceinline__ bool live(uint32_t a) const { return a < n; }
-    __device__ __forceinline__ uint32_t first() { return a0 < e_st ? a0 : take(); }
-    // a static run's successor, else a dealt run (a pool run, or the end n: both ≥ e_st)
-    __device__ __forceinline__ uint32_t next(uint32_t a) { return a + kPfxRun < e_st ? a + kPfxRun : take(); }
-    __device__ __forceinline__ uint32_t cnt(uint32_t a) const { return min(kPfxRun, (a < e_st ? e_st : n) - a); }
-};
-
-// A run loop's state at a run boundary, handed from one loop to another (rx_runs_lds → the hybrid loop): run a with
-// its offsets (lane l = unit a + l; c_end: a + l + 1), the next run an with its offsets.
-struct RunHead {
-    uint32_t a, an;
-    uint64_t c_off, c_end, n_off, n_end;
-};
 
 // Stage a piece's rows [0, span) into the slot (the rows already in V, all loaded) with their chunk prefix sums;
 // returns S(span), the weighted sum of the staged bytes. The chunk holding byte `span` keeps only its bytes below
@@ -1435,7 +1481,7 @@ template <int R, bool VERIFY, bool PIPE, int NS>
 __global__ __launch_bounds__(kBlock, NS == 2 ? 4 : 1) void csum_ragged_scan_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, uint32_t n,
     const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t run, int sets,
-    uint32_t big_keep, bool park) {
+    uint32_t big_keep, bool park, uint32_t* __restrict__ deal) {
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const __amdgpu_buffer_rsrc_t ofs = make_rsrc(offsets, ((uint64_t)n + 1) * 8);
@@ -1458,14 +1504,20 @@ __global__ __launch_bounds__(kBlock, NS == 2 ? 4 : 1) void csum_ragged_scan_kern
     if (sets == 2 || (NS == 2 && sets == 0 && run == 0 &&
                       ld_off(ofs, n) - ld_off(ofs, 0) < (uint64_t)kScanLdsSeg * n)) {
         if (wave >= 2u) return;
-        const uint32_t nb = gridDim.x, W = nb * 2u;
-        const WaveRange wr = wave_range(ofs, n, wave_no(nb, 2u), W, lane, kScanLdsSeg, 1u, kWave);
-        if (lds_run == kWave)
-            ragged_runs_lds<R, VERIFY, PIPE, true>(base, ofs, n, prs, ors, oks, kWave, wr.a0, wr.a_end, lane,
-                                                   lds_scan + wave * (2u * kScanSlot / 16u), partial != nullptr, pout, raw);
-        else  // tune.run_segs (tests): shorter runs, stored run by run
-            ragged_runs_lds<R, VERIFY, PIPE, false>(base, ofs, n, prs, ors, oks, lds_run, wr.a0, wr.a_end, lane,
-                                                    lds_scan + wave * (2u * kScanSlot / 16u), partial != nullptr, pout, raw);
+        const uint32_t nb = gridDim.x, W = nb * 2u, g = wave_no(nb, 2u);
+        lds16* slot = lds_scan + wave * (2u * kScanSlot / 16u);
+        if (lds_run == kWave) {
+            // runs of 64, results parked: the batch's last eighth dealt to the waves as they finish (the receive
+            // pass's DealtRuns), with heads for this launch
+            DealtRuns q = deal_runs(ofs, n, g, W, lane, kScanLdsSeg, 1u, kWave, deal);
+            ragged_runs_lds<R, VERIFY, PIPE, true>(base, ofs, n, prs, ors, oks, kWave, q, lane, slot,
+                                                   partial != nullptr, pout, raw);
+        } else {  // tune.run_segs (tests): shorter runs, stored run by run
+            const WaveRange wr = wave_range(ofs, n, g, W, lane, kScanLdsSeg, 1u, kWave);
+            StaticRuns q{wr.a0, wr.a_end, lds_run};
+            ragged_runs_lds<R, VERIFY, PIPE, false>(base, ofs, n, prs, ors, oks, lds_run, q, lane, slot,
+                                                    partial != nullptr, pout, raw);
+        }
         return;
     }
     // The grid is sized for small segments (4 blocks/CU); on the default grid (big_keep ≠ 0) streamed batches take
@@ -1486,7 +1538,8 @@ __global__ __launch_bounds__(kBlock, NS == 2 ? 4 : 1) void csum_ragged_scan_kern
     // 160 B mean). The streamed forms park their results in the wave's unused LDS slot when the launch has one.
     void* pbuf = park ? static_cast<void*>(lds_scan + wave * (kScanSlot / 16u)) : nullptr;
     if (sets == 3 || (NS == 2 && sets == 0 && wave_bytes < (uint64_t)kScanLdsSeg * (a_end - a0))) {
-        ragged_runs_lds<R, VERIFY, PIPE, false>(base, ofs, n, prs, ors, oks, lds_run, a0, a_end, lane,
+        StaticRuns q{a0, a_end, lds_run};
+        ragged_runs_lds<R, VERIFY, PIPE, false>(base, ofs, n, prs, ors, oks, lds_run, q, lane,
                                                 lds_scan + wave * (kScanSlot / 16u), partial != nullptr, pout, raw);
     } else if (NS == 2 && (sets == 5 || (sets == 0 && wave_bytes < (uint64_t)kScanTwoSetSeg * (a_end - a0)))) {
         ragged_runs<R, VERIFY, PIPE, 2>(base, ofs, n, prs, ors, oks, scan_run, a0, a_end, lane, pbuf, pout, raw);
@@ -2214,18 +2267,6 @@ constexpr uint32_t kRxPfxMean = 112;
 constexpr uint32_t kRxStreamMeanSmallN = 448;      // the streaming threshold below kRxStreamBigN frames
 constexpr uint32_t kRxStreamMeanBigN = 768;        // ... and from kRxStreamBigN frames
 constexpr uint32_t kRxStreamBigN = 5u << 19;       // 2.5M frames
-// The two-wave modes' dealt runs (§7 step 72): the pool is the batch's last 1/2^kRxPoolShift, dealt from
-// kRxDealHeads counters, each on its own 64 B line; kRxDealSlots streams per device hold heads at once.
-#ifndef NSX_RX_POOL_SHIFT
-#define NSX_RX_POOL_SHIFT 3
-#endif
-constexpr uint32_t kRxPoolShift = NSX_RX_POOL_SHIFT;
-#ifndef NSX_RX_DEAL_SPREAD
-#define NSX_RX_DEAL_SPREAD 1
-#endif
-constexpr uint32_t kRxDealHeads = 32;
-constexpr uint32_t kRxDealStride = 16;  // dwords
-constexpr uint32_t kRxDealSlots = 64;
 
 // PF = -1: the default grid's kernel (4 blocks/CU, PfxSlot<15> × 2 of LDS per block): sets 0 = by the batch's mean
 // frame and frame count (above), 1 = streamed runs on every block, 8 = streamed runs on 3 blocks per CU, 5 = the small-frame mode (LDS loop, then the hybrid
@@ -2310,35 +2351,15 @@ __global__ __launch_bounds__(kBlock, NSX_RX_WPS(WPS)) void rx_tcp_kernel(const u
             // per CU the VALU-heavy LDS loop queues less for issue); 6: the prefix form with
             // 15-row slots (waves 0-1: as fast as 0-1 / 2-3 by block parity and as 2 blocks/CU of four waves, §7 step
             // 55).
-            // The runs (§7 step 72): with heads for this launch (deal), each wave's equal share of the batch's first
-            // n − n/2^kRxPoolShift frames, then runs dealt to the waves as they ask, from kRxDealHeads counters
-            // (waves and pool in that many contiguous groups, so a head's waves share an XCD); without, each wave's
-            // share of the whole batch. Waves ran their equal shares at ±4% speeds, and a launch waited 6-9 µs (7%)
-            // for its last waves (tools/probes/rx_wave_times.py, profiles/r05_rx_wave_times.txt).
+            // The runs (§7 step 72, deal_runs): with heads for this launch (deal), each wave's equal share of the
+            // batch's first 7/8, then runs of the last 1/8 dealt to the waves as they finish. With equal shares of the
+            // whole batch the waves ran at speeds ±4% apart (by CU and XCD, not by data), and a launch waited 5-29 µs
+            // for its last waves (tools/probes/rx_wave_times.py, profiles/r05_rx_wave_times_by_cu.txt).
             if (wave >= 2u) return;
             const uint32_t nb = gridDim.x, W2 = nb * 2u, b = blockIdx.x;
             const uint32_t g = (nb >= 16 && (nb & 7) == 0) ? ((b & 7) * (nb >> 3) + (b >> 3)) * 2u + wave : b * 2u + wave;
-            const uint32_t S = deal ? (n - (n >> kRxPoolShift)) & ~(kPfxRun - 1u) : n;
-            DealtRuns q{0u, 0u, n, 0u, 0u, 0u, nullptr, lane, 0u, false, false};
-            WaveRange wr{0u, 0u, 0u};
-            if (S > 0u) wr = wave_range(ofs, S, g, W2, lane, kRxSmallFrame, 8u);
-            q.a0 = wr.a0, q.e_st = wr.a_end;
-            if (deal) {
-#if NSX_RX_DEAL_SPREAD
-                const uint32_t H = min(kRxDealHeads, W2), h = g % H;
-                const uint32_t g0 = 0u, g1 = (W2 - h + H - 1u) / H;  // waves g ≡ h mod H
-#else
-                const uint32_t H = min(kRxDealHeads, W2), h = (uint32_t)((uint64_t)g * H / W2);
-                const uint32_t g0 = (uint32_t)(((uint64_t)h * W2 + H - 1u) / H);
-                const uint32_t g1 = (uint32_t)(((uint64_t)(h + 1u) * W2 + H - 1u) / H);
-#endif
-                const uint32_t Q = (n - S + kPfxRun - 1u) / kPfxRun;  // the pool's runs
-                const uint32_t r0 = (uint32_t)((uint64_t)Q * h / H);
-                const uint32_t qh = (uint32_t)((uint64_t)Q * (h + 1u) / H) - r0;
-                q.pb = S + r0 * kPfxRun, q.q = qh, q.last = qh + (g1 - g0) - 1u;
-                q.head = deal + h * kRxDealStride;
-                q.init();
-            }
+            WaveRange wr;
+            DealtRuns q = deal_runs(ofs, n, g, W2, lane, kRxSmallFrame, 8u, 0u, deal, &wr);
 #if defined(NSX_RX_DIAG) && NSX_RX_DIAG == 7
             timed(wr, gridDim.x, 2u, ro, [&] {
 #endif
@@ -3544,6 +3565,56 @@ hipError_t launch_fixed(const LaunchCfg& c, const void* d_base, uint64_t stride,
     return hipGetLastError();
 }
 
+// The deal counters (§7 step 72) of the receive pass and the ragged checksum's small-segment mode: kDealSlots sets
+// of kDealHeads heads per device, zero at load; every launch leaves its heads at 0 (DealtRuns), so a set can serve
+// one stream's launches one after another, whichever kernel they are.
+__device__ uint32_t g_deal_heads[kDealSlots * kDealHeads * kDealStride];
+
+// The heads for a launch on stream st of the current device: the stream's own set (given on first use, kept for the
+// process), or nullptr — equal static shares — when the stream is being captured into a graph (a graph's launches
+// could replay on several streams at once), when every set is given out, or in builds without dealing.
+static uint32_t* deal_heads(hipStream_t st) {
+#if defined(NSX_NO_DEAL) || (defined(NSX_RX_DIAG) && NSX_RX_DIAG == 5)
+    (void)st;
+    return nullptr;
+#else
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess) {
+        (void)hipGetLastError();  // a refused query (e.g. the legacy stream while another captures) is not the launch's error
+        return nullptr;
+    }
+    if (cs != hipStreamCaptureStatusNone) return nullptr;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    static std::mutex mu;
+    static std::map<std::pair<int, hipStream_t>, uint32_t> slot_of;
+    static std::map<int, std::pair<uint32_t*, uint32_t>> dev_sets;  // device → (its g_deal_heads, sets given)
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = slot_of.find({dev, st});
+    auto& ds = dev_sets[dev];
+    if (!ds.first) {
+        void* p = nullptr;
+        if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_deal_heads)) != hipSuccess || !p) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        ds.first = static_cast<uint32_t*>(p);
+    }
+    uint32_t slot;
+    if (it != slot_of.end()) {
+        slot = it->second;
+    } else {
+        if (ds.second >= kDealSlots) return nullptr;
+        slot = ds.second++;
+        slot_of[{dev, st}] = slot;
+    }
+    return ds.first + (size_t)slot * kDealHeads * kDealStride;
+#endif
+}
+
 template <bool VERIFY>
 static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, const uint64_t* offsets, uint64_t n,
                                      const uint32_t* partial, uint16_t* out, uint8_t* ok, hipStream_t st) {
@@ -3575,6 +3646,7 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
     const bool pick = c.blocks_per_cu == 0 && pipe && rows == 2;
     const uint32_t mb = pick ? (uint32_t)c.cus * 4u : max_blocks_of(c, 2);
     const uint32_t keep = pick ? 2u : 0u;
+    uint32_t* deal = deal_heads(st);  // the small-segment mode's dealt runs
     for (uint64_t c0 = 0; c0 < n; c0 += kRaggedChunk) {
         const uint32_t cn = (uint32_t)(n - c0 < kRaggedChunk ? n - c0 : kRaggedChunk);
         const uint32_t grid = grid_for((cn + task * ns - 1) / (task * ns), mb);
@@ -3584,7 +3656,7 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
 #define NSX_RSCAN(R_, P_, NS_)                                                                                 \
         if (rows == R_ && pipe == P_ && ns == NS_)                                                              \
             hipLaunchKernelGGL((csum_ragged_scan_kernel<R_, VERIFY, P_, NS_>), dim3(grid), dim3(kBlock), lds, st,\
-                               base, offsets + c0, cn, pc, oc, kc, run, sets, keep, lds_form);
+                               base, offsets + c0, cn, pc, oc, kc, run, sets, keep, lds_form, deal);
         NSX_RSCAN(2, true, 1) NSX_RSCAN(4, true, 1) NSX_RSCAN(8, true, 1)
         NSX_RSCAN(4, false, 1) NSX_RSCAN(8, false, 1) NSX_RSCAN(16, false, 1)
         NSX_RSCAN(2, true, 2)
@@ -3631,55 +3703,6 @@ bool rx_tune_valid(const LaunchCfg& c) {
     return !grid_mode || ((c.rows == 0 || c.rows == 2) && c.blocks_per_cu == 0);
 }
 
-// The receive pass's deal counters (§7 step 72): kRxDealSlots sets of kRxDealHeads heads per device, zero at load;
-// every launch leaves its heads at 0 (DealtRuns), so a set can serve one stream's launches one after another.
-__device__ uint32_t g_rx_deal[kRxDealSlots * kRxDealHeads * kRxDealStride];
-
-// The heads for a launch on stream st of the current device: the stream's own set (given on first use, kept for the
-// process), or nullptr — equal static shares — when the stream is being captured into a graph (a graph's launches
-// could replay on several streams at once), when every set is given out, or in builds without dealing.
-static uint32_t* rx_deal_heads(hipStream_t st) {
-#if defined(NSX_RX_NO_DEAL) || (defined(NSX_RX_DIAG) && NSX_RX_DIAG == 5)
-    (void)st;
-    return nullptr;
-#else
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cs) != hipSuccess) {
-        (void)hipGetLastError();  // a refused query (e.g. the legacy stream while another captures) is not the launch's error
-        return nullptr;
-    }
-    if (cs != hipStreamCaptureStatusNone) return nullptr;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) {
-        (void)hipGetLastError();
-        return nullptr;
-    }
-    static std::mutex mu;
-    static std::map<std::pair<int, hipStream_t>, uint32_t> slot_of;
-    static std::map<int, std::pair<uint32_t*, uint32_t>> dev_sets;  // device → (its g_rx_deal, sets given)
-    std::lock_guard<std::mutex> lock(mu);
-    auto it = slot_of.find({dev, st});
-    auto& ds = dev_sets[dev];
-    if (!ds.first) {
-        void* p = nullptr;
-        if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_rx_deal)) != hipSuccess || !p) {
-            (void)hipGetLastError();
-            return nullptr;
-        }
-        ds.first = static_cast<uint32_t*>(p);
-    }
-    uint32_t slot;
-    if (it != slot_of.end()) {
-        slot = it->second;
-    } else {
-        if (ds.second >= kRxDealSlots) return nullptr;
-        slot = ds.second++;
-        slot_of[{dev, st}] = slot;
-    }
-    return ds.first + (size_t)slot * kRxDealHeads * kRxDealStride;
-#endif
-}
-
 hipError_t launch_rx_tcp(const LaunchCfg& c, int ipver, const void* d_base, const uint64_t* d_offsets, uint64_t n,
                          uint64_t* mask, uint16_t* ip_raw, uint16_t* tcp_raw, hipStream_t st) {
     if (!rx_tune_valid(c)) return hipErrorInvalidValue;
@@ -3709,7 +3732,7 @@ hipError_t launch_rx_tcp(const LaunchCfg& c, int ipver, const void* d_base, cons
         static_assert(la_def >= (size_t)PfxSlot<7>::kBytes * kWavesPerBlock && la_def * 4 <= 163840 &&
                           la_ring * 4 <= 163840, "4 blocks per CU");
         const size_t la = c.segs_per_wave == 9 ? la_ring : la_def;
-        uint32_t* deal = rx_deal_heads(st);
+        uint32_t* deal = deal_heads(st);
         for (uint64_t c0 = 0; c0 < n; c0 += kRaggedChunk) {
             const uint32_t cn = (uint32_t)(n - c0 < kRaggedChunk ? n - c0 : kRaggedChunk);
             const uint32_t grid = grid_for((cn + kRxRun - 1) / kRxRun, (uint32_t)c.cus * 4u);

@@ -146,6 +146,67 @@ def test_ragged_small_segment_bench_workload_full_size():
     assert np.array_equal(u16(out), want_p)
 
 
+def test_ragged_dealt_runs_back_to_back_and_on_many_streams():
+    """The small-segment mode deals each launch's last runs from the stream's counters, shared with the receive pass
+    and left at zero by every launch: checksum and batch-verify launches of 3 to 300k
+    segments, with and without partials, back to back on one stream with no sync between them and interleaved with
+    receive launches on the same counters, then on 70 HIP streams at once (past the 64 counter sets a device gives
+    out), all equal the oracle; a dealt run that does not follow the parked ones flushes them (outputs at odd
+    offsets)."""
+    import ctypes
+    import _rx
+    rng = np.random.default_rng(0x8B)
+    cases = []
+    for n in (300_001, 3, 64 * 700, 129, 100_000):
+        lens = rng.integers(0, 160, n).astype(np.uint64)
+        offs = np.zeros(n + 1, np.uint64)
+        offs[1:] = np.cumsum(lens)
+        offs += np.uint64(int(rng.integers(4)))
+        buf = O.c_splitmix64(0x8B + n, int(offs[-1]) + 3)
+        part = rng.integers(0, 1 << 31, n, dtype=np.uint32)
+        cases.append((dev(buf), dev(offs.view(np.int64)), dev(part.view(np.int32)),
+                      O.c_batch(buf, n, offsets=offs, threads=16), O.c_batch(buf, n, offsets=offs, partial=part, threads=16)))
+    rbuf, roffs, _ = _rx.batch(rng, 50_000, max_payload=40)
+    rx = (dev(rbuf), dev(roffs.view(np.int64)), O.c_rx_ipv4_tcp(rbuf, roffs)[0])
+
+    def launch(k, stream=None):
+        d, o, p, want, want_p = cases[k % len(cases)]
+        n = o.numel() - 1
+        with torch.cuda.stream(stream or torch.cuda.current_stream()):
+            out = torch.empty(n + 1, dtype=torch.int16, device="cuda")[1:]  # 2 B past a 16 B boundary
+            nsx.ragged_dev(d, o, partial=p if k & 1 else None, out=out)
+            raw = torch.empty(n, dtype=torch.int16, device="cuda")
+            ok = nsx.verify_ragged_dev(d, o, partial=p if k & 1 else None, raw=raw)
+            mask = torch.empty((rx[1].numel() + 62) // 64, dtype=torch.int64, device="cuda")
+            nsx.rx_ipv4_tcp_verify_dev(rx[0], rx[1], mask=mask)
+        return k, out, raw, ok, mask
+
+    def check(results):
+        torch.cuda.synchronize()
+        for k, out, raw, ok, mask in results:
+            want = cases[k % len(cases)][4 if k & 1 else 3]
+            assert np.array_equal(u16(out), want), k
+            assert np.array_equal(u16(raw), want), k
+            assert np.array_equal(host(ok).astype(bool), want == 0xFFFF), k
+            assert np.array_equal(host(mask).view(np.uint64), rx[2]), k
+
+    check([launch(k) for k in range(3 * len(cases))])
+    torch.cuda.synchronize()
+    hip = ctypes.CDLL("libamdhip64.so")
+    handles = []
+    for _ in range(70):
+        h = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(h)) == 0
+        handles.append(h)
+    try:
+        streams = [torch.cuda.ExternalStream(h.value) for h in handles]
+        check([launch(i + r, streams[i]) for r in range(2) for i in range(len(streams))])
+    finally:
+        torch.cuda.synchronize()
+        for h in handles:
+            hip.hipStreamDestroy(h)
+
+
 @pytest.mark.parametrize("n", [1, 126, 252, 253, 30_001, 400_003])
 def test_ragged_small_segments_every_form(n):
     """Segments of 0-200 B (mean ~100): the small-segment mode (2), the four-wave LDS form (3), the streamed runs
@@ -267,19 +328,23 @@ def test_ragged_byte_balanced_partition_edges():
                                            np.zeros(1500, np.uint64)]),
         "all_empty": np.zeros(4000, np.uint64),
         "few": rng.integers(0, 5000, 1030).astype(np.uint64),
+        # large skewed batches on the default grid (round 5): every wave's byte slice far from its equal-count
+        # share, and a dealt pool of large units behind a long run of empties
+        "sorted_big": np.sort(rng.integers(0, 3000, 300_000)).astype(np.uint64),
+        "empties_then_big": np.concatenate([np.zeros(200_000, np.uint64),
+                                            rng.integers(500, 9000, 60_000).astype(np.uint64)]),
     }
     for name, lens in cases.items():
         offs = np.zeros(lens.size + 1, np.uint64)
         offs[1:] = np.cumsum(lens)
         offs += np.uint64(3)
         buf = O.c_splitmix64(0x1099, int(offs[-1]) + 8)
-        want = O.c_batch(buf, lens.size, offsets=offs)
+        want = O.c_batch(buf, lens.size, offsets=offs, threads=16)
         d, o = dev(buf), dev(offs.view(np.int64))
-        for b in (1, 8):
-            for rs in (1, 16, 63):
-                out = torch.empty(lens.size, dtype=torch.int16, device="cuda")
-                nsx.ragged_dev(d, o, out=out, tune=dict(blocks_per_cu=b, run_segs=rs, block_mode=1))
-                assert np.array_equal(u16(out), want), (name, b, rs)
+        for tune in [None] + [dict(blocks_per_cu=b, run_segs=rs, block_mode=1) for b in (1, 8) for rs in (1, 16, 63)]:
+            out = torch.empty(lens.size, dtype=torch.int16, device="cuda")
+            nsx.ragged_dev(d, o, out=out, tune=tune)
+            assert np.array_equal(u16(out), want), (name, tune)
 
 
 # ------------------------------------------------------------------ verify / pseudo-header

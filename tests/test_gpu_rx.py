@@ -251,6 +251,24 @@ def test_rx_bench_workload_full_size():
     assert np.array_equal(got, np.packbits(pad, bitorder="little").view(np.uint64))
 
 
+def test_rx_skewed_batches_every_mode():
+    """Skewed batches — 100k ACK-size frames then 20k large ones, and the reverse — where equal-count and byte-balanced
+    wave ranges differ most and the dealt pool holds only large (or only small) frames, in
+    the automatic mode and every forced two-wave and streamed mode, equal the oracle."""
+    rng = np.random.default_rng(0x8C)
+    small, so, _ = _rx.batch(rng, 100_000, max_payload=40)
+    big, bo, _ = _rx.batch(rng, 20_000, max_payload=1460)
+    for first, fo, second, sec_o in ((small, so, big, bo), (big, bo, small, so)):
+        cut = int(fo[-1])
+        buf = np.concatenate([first[:cut], second])
+        offs = np.concatenate([fo[:-1], sec_o + np.uint64(cut)])
+        want = O.c_rx_ipv4_tcp(buf, offs)
+        for tune in [None, dict(segs_per_wave=1)] + PFX:
+            got = run_rx(buf, offs, tune)
+            for w, g, what in zip(want, got, ("mask", "ip_raw", "tcp_raw")):
+                assert np.array_equal(w, g), (what, tune)
+
+
 def test_rx_dealt_runs_back_to_back_and_on_many_streams():
     """The two-wave modes deal each launch's last runs from counters of the launch's stream, which the launch leaves
     at zero for the next: launches back to back on one stream with no sync between them —
