@@ -3132,11 +3132,21 @@ constexpr uint32_t kHdr20Lds = kHdr20Task * 20u;  // bytes of LDS per wave
 // Software-pipelined: two register sets of U tasks; the loads of the next set are issued before the
 // current set goes through LDS, so every wave keeps loads in flight while it computes and stores (one wave
 // per SIMD at 1 block/CU has no other wave to cover those phases).
+#if defined(NSX_F3_DIAG)
+// diagnostic build only (tools/probes/f3_wave_times.py): per wave {entry, end, tasks, XCC_ID << 16 | HW_ID's low
+// half} of the last ipv4_hdr20_kernel launch, read back with nsx_diag_stamps
+__device__ uint64_t g_f3_stamps[4096 * 4];
+#endif
 template <int MODE, int U>
 __global__ __launch_bounds__(kBlock) void ipv4_hdr20_kernel(uint8_t* __restrict__ base, uint32_t n,
                                                             uint16_t* __restrict__ out, uint32_t clog,
                                                             uint64_t* __restrict__ mask) {
     typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+#if defined(NSX_F3_DIAG)
+    const uint64_t t_k = __builtin_amdgcn_s_memrealtime();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    uint32_t ntk = 0;
+#endif
     extern __shared__ u32x4 lds20[];
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -3241,11 +3251,30 @@ __global__ __launch_bounds__(kBlock) void ipv4_hdr20_kernel(uint8_t* __restrict_
         const uint32_t t1 = t0 + step * U;
         issue(t1, B);
         consume(A);
+#if defined(NSX_F3_DIAG)
+        ntk += U;
+#endif
         if (!live(t1)) break;
         t0 = t1 + step * U;
         issue(t0, A);
         consume(B);
+#if defined(NSX_F3_DIAG)
+        ntk += U;
+#endif
     }
+#if defined(NSX_F3_DIAG)
+    {
+        const uint64_t t_out = __builtin_amdgcn_s_memrealtime();
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        const uint32_t g = blockIdx.x * kWavesPerBlock + wave;
+        const uint64_t v = lane == 0 ? t_k : lane == 1 ? t_out : lane == 2 ? (uint64_t)ntk
+                                                                             : (uint64_t)((xcc & 0xFu) << 16 | (hw & 0xFFFFu));
+        if (lane < 4u && g < 4096u) g_f3_stamps[g * 4u + lane] = v;
+    }
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -3869,6 +3898,13 @@ uint64_t ipv4_hdr_launch_count(const LaunchCfg& c, uintptr_t base, uint64_t stri
     return (n + win - 1) / win;
 }
 
+#if defined(NSX_F3_DIAG)
+hipError_t diag_f3_stamps(uint64_t* dst, uint64_t count) {
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_f3_stamps), std::min<uint64_t>(count, 4096 * 4) * 8, 0,
+                               hipMemcpyDeviceToHost);
+}
+#endif
+
 hipError_t launch_ipv4_hdr(const LaunchCfg& c, uint8_t* base, uint64_t stride, uint32_t hdr_off, uint64_t n,
                            int mode, uint16_t* out, uint64_t* mask, hipStream_t st) {
     // Kernel by layout: packed 20 B headers (stride 20, hdr_off 0, 4-aligned base) → the pipelined flat
@@ -3960,3 +3996,10 @@ hipError_t launch_fill_splitmix64(void* d_buf, uint64_t byte_off, uint64_t nbyte
 }
 
 }  // namespace nsx
+
+#if defined(NSX_F3_DIAG)
+// diagnostic build only: the per-wave stamps of the last packed-header launch (tools/probes/f3_wave_times.py)
+extern "C" __attribute__((visibility("default"))) int nsx_diag_f3_stamps(uint64_t* dst, uint64_t count) {
+    return nsx::diag_f3_stamps(dst, count) == hipSuccess ? 0 : -5;
+}
+#endif

@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Per-wave timeline of the packed-header kernel (ipv4_hdr20_kernel, workloads 7 and 9; diagnostic build only:
+make exp X=f3diag EXTRA_KFLAGS=-DNSX_F3_DIAG, whose kernel records each wave's s_memrealtime stamps at entry and
+end, its task count and where it ran, read back with nsx_diag_f3_stamps). Prints the end-time spread over the
+launch's waves, by XCD and CU, and the tail (last end − median end), in µs.
+
+    python tools/probes/f3_wave_times.py [--config 7] [--launches 20]
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "network-stack_amd")]
+
+import numpy as np  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=7)
+    ap.add_argument("--launches", type=int, default=20)
+    a = ap.parse_args()
+    import nsx
+    nsx.LIB_PATH = os.path.join(ROOT, "network-stack_amd", "lib_f3diag", "libnsx_csum.so")
+    import torch
+    import bench
+    torch.cuda.set_device(0)
+    cfg = dict(bench.WORKLOADS[a.config])
+    w = bench.build_workload(cfg, 0, torch.device("cuda", 0))
+    L = nsx.lib()
+    L.nsx_diag_f3_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+    st = np.zeros(4096 * 4, np.uint64)
+    for _ in range(100):
+        w["step"]()
+    torch.cuda.synchronize()
+    rows = []
+    for _ in range(a.launches):
+        w["step"]()
+        torch.cuda.synchronize()
+        assert L.nsx_diag_f3_stamps(st.ctypes.data, st.size) == 0
+        t = st.reshape(-1, 4).astype(np.int64)
+        t = t[t[:, 1] > 0]
+        t0 = t[:, 0].min()
+        rows.append(((t[:, 0] - t0) / 100.0, (t[:, 1] - t0) / 100.0, t[:, 2], t[:, 3]))
+        st[:] = 0
+    end = np.concatenate([r[1] for r in rows])
+    print(f"waves {len(rows[0][0])}; tasks per wave p1 {np.percentile(rows[0][2], 1):.0f} p50 {np.median(rows[0][2]):.0f} "
+          f"p99 {np.percentile(rows[0][2], 99):.0f}")
+    print(f"start us: max {max(r[0].max() for r in rows):.2f}")
+    print(f"end   us: min {end.min():.2f} p10 {np.percentile(end, 10):.2f} p50 {np.median(end):.2f} "
+          f"p90 {np.percentile(end, 90):.2f} p99 {np.percentile(end, 99):.2f} max {end.max():.2f}")
+    for nm, keyf in (("XCD", lambda r: r[3] >> 16), ("CU", lambda r: ((r[3] >> 16) << 8) | ((r[3] >> 8) & 0xFF))):
+        v = []
+        for r in rows:
+            _, inv = np.unique(keyf(r), return_inverse=True)
+            means = np.bincount(inv, weights=r[1]) / np.bincount(inv)
+            v.append((means.max() - np.median(r[1]), means.std()))
+        v = np.array(v)
+        print(f"by {nm}: std of group means {np.median(v[:, 1]):.2f} us; tail if each group's waves ended at their "
+              f"mean {np.median(v[:, 0]):.2f} us")
+    tails = [r[1].max() - np.median(r[1]) for r in rows]
+    spans = [r[1].max() for r in rows]
+    print(f"launch span (first start -> last end) us: median {np.median(spans):.2f}; tail (last end - median end) "
+          f"{np.median(tails):.2f}")
+
+
+if __name__ == "__main__":
+    main()
