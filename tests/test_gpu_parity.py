@@ -150,9 +150,9 @@ def test_ragged_dealt_runs_back_to_back_and_on_many_streams():
     """The small-segment mode deals each launch's last runs from the stream's counters, shared with the receive pass
     and left at zero by every launch: checksum and batch-verify launches of 3 to 300k
     segments, with and without partials, back to back on one stream with no sync between them and interleaved with
-    receive launches on the same counters, then on 70 HIP streams at once (past the 64 counter sets a device gives
-    out), all equal the oracle; a dealt run that does not follow the parked ones flushes them (outputs at odd
-    offsets)."""
+    receive launches on the same counters (and packed-header launches), then on 70 HIP streams at once (past the 64
+    counter sets a device gives out), all equal the oracle; a dealt run that does not follow the parked ones flushes
+    them (outputs at odd offsets)."""
     import ctypes
     import _rx
     rng = np.random.default_rng(0x8B)
@@ -168,6 +168,11 @@ def test_ragged_dealt_runs_back_to_back_and_on_many_streams():
                       O.c_batch(buf, n, offsets=offs, threads=16), O.c_batch(buf, n, offsets=offs, partial=part, threads=16)))
     rbuf, roffs, _ = _rx.batch(rng, 50_000, max_payload=40)
     rx = (dev(rbuf), dev(roffs.view(np.int64)), O.c_rx_ipv4_tcp(rbuf, roffs)[0])
+    # packed 20 B headers between them (IHL 5 everywhere, so every raw sum is the plain sum of the 20 bytes)
+    nh = 300_001
+    hbuf = rng.integers(0, 256, nh * 20 + 4, dtype=np.uint8)
+    hbuf[0:nh * 20:20] = 0x45
+    hdr = (dev(hbuf), O.c_batch(hbuf, nh, stride=20, seg_len=20, threads=16))
 
     def launch(k, stream=None):
         d, o, p, want, want_p = cases[k % len(cases)]
@@ -179,11 +184,13 @@ def test_ragged_dealt_runs_back_to_back_and_on_many_streams():
             ok = nsx.verify_ragged_dev(d, o, partial=p if k & 1 else None, raw=raw)
             mask = torch.empty((rx[1].numel() + 62) // 64, dtype=torch.int64, device="cuda")
             nsx.rx_ipv4_tcp_verify_dev(rx[0], rx[1], mask=mask)
-        return k, out, raw, ok, mask
+            hraw = nsx.ipv4_hdr_csum_dev(hdr[0], 20, nh, mode=0)
+        return k, out, raw, ok, mask, hraw
 
     def check(results):
         torch.cuda.synchronize()
-        for k, out, raw, ok, mask in results:
+        for k, out, raw, ok, mask, hraw in results:
+            assert np.array_equal(u16(hraw), hdr[1]), k
             want = cases[k % len(cases)][4 if k & 1 else 3]
             assert np.array_equal(u16(out), want), k
             assert np.array_equal(u16(raw), want), k
