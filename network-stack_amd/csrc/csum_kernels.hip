@@ -1109,7 +1109,10 @@ struct DealtRuns {
 #define NSX_DEAL_POOL_SHIFT 3
 #endif
 constexpr uint32_t kDealPoolShift = NSX_DEAL_POOL_SHIFT;
-constexpr uint32_t kDealHeads = 32;
+#ifndef NSX_DEAL_HEADS
+#define NSX_DEAL_HEADS 32
+#endif
+constexpr uint32_t kDealHeads = NSX_DEAL_HEADS;
 constexpr uint32_t kDealStride = 16;
 constexpr uint32_t kDealSlots = 64;
 
