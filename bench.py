@@ -58,7 +58,9 @@ Printed by rank 0: one JSON line with the contract fields plus
                  the line itself; value_per_gpu_mean = value / ranks.
 
 The product library is brought up to date (`make -C network-stack_amd`, a no-op
-when nothing changed) before it is loaded, so a stale pushed binary never runs.
+when nothing changed, under a file lock) before it is loaded — by the launching
+process, or by each rank an outside launcher started — so a stale pushed binary
+never runs.
 """
 from __future__ import annotations
 
@@ -748,16 +750,20 @@ def cpu_baseline(cfg, w, seconds: float) -> dict:
             lib.oracle_go_batch_ragged(_ptr(sample), _ptr(offs, lo), hi - lo, None, 0, _ptr(out, lo))
         nbytes, desc = hi_b, f"first {m} ragged segments of rank 0's batch"
         check["segments"] = lambda: np.array_equal(out, gpu)
-    busy = []  # (thread, seconds) of every shard call in the all-threads leg
+    busy = []  # seconds of every shard call in the all-threads leg
+    passes = []  # per pass: [(shard start − pass start, shard duration)] over its T shard calls
 
     def timed_go(t):
         t0 = time.perf_counter()
         go(bounds[t], bounds[t + 1])
-        busy.append(time.perf_counter() - t0)
+        t1 = time.perf_counter()
+        busy.append(t1 - t0)
+        return t0, t1
     thr0 = cgroup_throttling()
     with ThreadPoolExecutor(T) as ex:
         def all_cores():
-            list(ex.map(timed_go, range(T)))
+            p0 = time.perf_counter()
+            passes.append([(a - p0, b - a) for a, b in ex.map(timed_go, range(T))])
         reps_t, dt_t = _run_for(all_cores, seconds / 2)
         ok_t = all(f() for f in check.values())
     thr1 = cgroup_throttling()
@@ -772,19 +778,38 @@ def cpu_baseline(cfg, w, seconds: float) -> dict:
     # than alone: allocator or memory contention), plus any CPU-quota throttling the cgroup recorded meanwhile
     busy_frac = sum(busy) / (T * dt_t) if dt_t else None
     in_call = (nbytes * reps_t / T) / (sum(busy) / T) / GIB if busy else None
+    # per pass: the shard calls' durations, max / min over the T shards (imbalance: one shard
+    # doing more work, or running slower, than the others), the latest shard's start after the pass began (a thread
+    # that was not running when its shard was handed out), and the slowest shard's duration against the 1-thread
+    # time of its share (every shard running slow: contention); medians over the passes
+    shard_max_min = [max(d for _, d in p) / max(min(d for _, d in p), 1e-9) for p in passes]
+    late_start_ms = [max(a for a, _ in p) * 1e3 for p in passes]
+    slowest_ms = [max(d for _, d in p) * 1e3 for p in passes]
+    alone_ms = dt_1 / max(reps_1, 1) / T * 1e3  # one shard's share of the 1-thread pass
+    med = (lambda v: round(float(np.median(v)), 3) if v else None)
     diag = {"busy_fraction": None if busy_frac is None else round(busy_frac, 3),
             "per_thread_gib_s_in_call": None if in_call is None else round(in_call, 4),
             "cgroup_throttled_ms": None if thr0 is None or thr1 is None else round((thr1[1] - thr0[1]) / 1e3, 1),
-            "cgroup_throttled_periods": None if thr0 is None or thr1 is None else thr1[0] - thr0[0]}
+            "cgroup_throttled_periods": None if thr0 is None or thr1 is None else thr1[0] - thr0[0],
+            "shard_duration_max_over_min": med(shard_max_min), "shard_latest_start_ms": med(late_start_ms),
+            "slowest_shard_ms": med(slowest_ms), "shard_alone_ms": round(alone_ms, 3),
+            "pass_wall_ms": round(dt_t / max(reps_t, 1) * 1e3, 3)}
     why = ""
     if eff is not None and eff < 0.5:
+        imbalanced = diag["shard_duration_max_over_min"] is not None and diag["shard_duration_max_over_min"] > 1.5
+        late = diag["shard_latest_start_ms"] is not None and diag["shard_latest_start_ms"] > 0.25 * diag["pass_wall_ms"]
         if diag["cgroup_throttled_ms"]:
             why = f"; below 0.5 parallel efficiency: the cgroup's CPU quota throttled the process {diag['cgroup_throttled_ms']} ms"
-        elif busy_frac is not None and busy_frac < 0.7:
-            why = f"; below 0.5 parallel efficiency: shard threads busy {busy_frac:.0%} of the wall (waiting to run)"
+        elif late:
+            why = (f"; below 0.5 parallel efficiency: shards started up to {diag['shard_latest_start_ms']:.1f} ms into a "
+                   f"{diag['pass_wall_ms']:.1f} ms pass (threads not running when handed a shard: descheduled)")
+        elif imbalanced:
+            why = (f"; below 0.5 parallel efficiency: the shards are imbalanced — the slowest call took "
+                   f"{diag['shard_duration_max_over_min']:.1f}x the fastest within a pass")
         else:
-            why = (f"; below 0.5 parallel efficiency: each thread ran at {in_call:.2f} GiB/s inside its call against "
-                   f"{v_1:.2f} alone (contention in the per-unit allocation or memory system)")
+            why = (f"; below 0.5 parallel efficiency: every shard runs slow — the slowest took {diag['slowest_shard_ms']:.1f} "
+                   f"ms against {alone_ms:.1f} ms for its share on one thread alone, {in_call:.2f} GiB/s per thread in "
+                   f"the calls against {v_1:.2f} alone (contention in the per-unit allocation or memory system)")
     return {"value": round(v_t, 4), "unit": "GiB/s", "cores": T, "kind": "port",
             "sample": f"{desc} ({nbytes / 2**20:.0f} MiB), {reps_t} pass(es) on {T} threads (Go-faithful loop, "
                       f"contiguous shards){why}",
@@ -882,11 +907,11 @@ def build_library() -> None:
 def main(argv=None) -> int:
     argv = sys.argv[1:] if argv is None else list(argv)
     args = parse_args(argv)
-    # build once, in the launching process, before any rank starts: never in a rank a launcher started (WORLD_SIZE or
-    # LOCAL_RANK set — N ranks running make on one tree could load a half-written library), and under a lock, so two
-    # launching processes on one tree serialise
-    in_rank = "WORLD_SIZE" in os.environ or "LOCAL_RANK" in os.environ
-    if not args.dry_run and not args.no_build and not in_rank and os.environ.get("NSX_BENCH_BUILT") != "1":
+    # bring the library up to date before anything loads it, under a file lock: in the launching process before any
+    # rank starts (its ranks inherit NSX_BENCH_BUILT and skip it), and in every rank an outside launcher started
+    # (torchrun … bench.py: WORLD_SIZE set, NSX_BENCH_BUILT not) — there the first rank to take the lock builds and
+    # the others, waiting on it, find nothing to do, so no rank loads a stale or half-written library
+    if not args.dry_run and not args.no_build and os.environ.get("NSX_BENCH_BUILT") != "1":
         build_library()
         os.environ["NSX_BENCH_BUILT"] = "1"
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:

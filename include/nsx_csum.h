@@ -236,12 +236,16 @@ int nsx_ipv4_hdr_verify_mask_dev(const void* d_base, uint64_t stride, uint32_t h
  * d_ip_raw (nullable): the header's raw sum (0 when IHL < 5 or IHL*4 exceeds the
  * frame). d_tcp_raw (nullable): the raw sum over pseudo-header ‖ segment (0
  * unless the frame is well-formed as above). One pass over the frame bytes.
- * Work split: batches whose mean frame is under the streaming threshold deal
- * their last eighth of frames to the GPU's waves as they finish, from counters
- * the library keeps per stream (64 streams per device, in the library's own
- * device memory; every launch leaves them at zero for the stream's next). A
- * launch on a stream being captured into a graph, or on a stream past the 64th,
- * splits the batch statically instead; results are the same either way. */
+ * Work split: the batch's last eighth of frames is dealt to the GPU's waves as
+ * they finish, from counters the library keeps per stream (64 streams per
+ * device, in the library's own device memory; every launch leaves them at zero
+ * for the stream's next, so launches sharing them must run one after another).
+ * Only a handle that is one ordered queue of the current device gets counters:
+ * a stream the caller created, or the null stream. hipStreamPerThread (one
+ * handle, a different stream per host thread), a stream of another device, a
+ * stream being captured into a graph, and streams past the 64th split the
+ * batch statically instead; results are the same either way. See
+ * nsx_stream_release. */
 int nsx_rx_ipv4_tcp_verify_dev(const void* d_base, const uint64_t* d_offsets, uint64_t n, uint64_t* d_mask,
                                uint16_t* d_ip_raw, uint16_t* d_tcp_raw, nsx_stream_t stream);
 
@@ -308,6 +312,14 @@ int nsx_tcp_build_host(const nsx_tcp_hdr_soa* h_hdr, const uint8_t* h_opts, cons
  * frees the cached buffers; the next call re-allocates. Safe to call at any
  * time; concurrent host batch calls on a device wait for each other. */
 int nsx_host_cache_release(void);
+
+/* Return the per-stream work-deal counters the device calls above gave
+ * `stream` (nsx_rx_ipv4_tcp_verify_dev and friends) before the caller destroys
+ * it: call after the stream has drained (hipStreamSynchronize) and before
+ * hipStreamDestroy. The counters go to the next new stream; without this, a
+ * process that creates and destroys streams in a loop keeps the first 64 on the
+ * dealt path and splits every later one statically (correct, ~2% slower). */
+int nsx_stream_release(nsx_stream_t stream);
 
 /* Pinned (DMA-registered) host memory for zero-copy staging from Go via
  * unsafe.Slice (cgo forbids C retaining Go pointers; runtime.Pinner does not

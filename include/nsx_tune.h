@@ -72,7 +72,11 @@ typedef struct nsx_tune {
     int32_t kernel;            /* NSX_TUNE_KERNEL_* */
     int32_t shards_per_device; /* host batch calls: contiguous shards per GPU, each with its own host thread,
                                   streams and staging (default 1) */
-    int32_t reserved[6];
+    int32_t deal;              /* the ragged small-segment mode and the receive passes: 0 = the batch's last
+                                  eighth dealt to the waves from the stream's counters where the stream allows
+                                  it (nsx_csum.h, nsx_rx_ipv4_tcp_verify_dev), -1 = equal static shares
+                                  throughout (A/B; replaces round 5's NSX_NO_DEAL build) */
+    int32_t reserved[5];
 } nsx_tune;
 
 int nsx_csum_fixed_dev_tuned(const void* d_base, uint64_t stride, uint32_t seg_len, uint64_t n,
@@ -119,6 +123,10 @@ int nsx_fixed_launch_count(uint64_t stride, uint32_t seg_len, uint64_t n, const 
  * packed 20 B headers of at least 2^26 go out as back-to-back windows of about 2^25. */
 int nsx_ipv4_hdr_launch_count(const void* d_base, uint64_t stride, uint32_t hdr_off, uint64_t n, const nsx_tune* tune,
                               uint64_t* out_count);
+
+/* Per-stream deal counter sets currently given out on the current device (tests: a stream returned with
+ * nsx_stream_release gives its set to the next stream instead of taking a fresh one). */
+int nsx_deal_sets_in_use(uint32_t* out_count);
 
 #ifdef __cplusplus
 }

@@ -82,6 +82,7 @@ LaunchCfg launch_cfg(int cus, const nsx_tune* t) {
         c.xcd_chunk = t->xcd_chunk;
         c.window_bytes = t->window_bytes;
         c.kernel = t->kernel;
+        c.deal = t->deal;
     }
     return c;
 }
@@ -383,6 +384,20 @@ int nsx_fill_splitmix64_dev(void* d_buf, uint64_t byte_off, uint64_t nbytes, uin
 int nsx_shard_plan(const uint64_t* h_offsets, uint64_t n, int parts, uint64_t* out_bounds) {
     if (parts < 1 || !out_bounds) return NSX_EINVAL;
     nsx::shard_plan(h_offsets, n, parts, out_bounds);
+    return NSX_OK;
+}
+
+// ------------------------------------------------------------ per-stream deal counters
+int nsx_stream_release(nsx_stream_t stream) {
+    nsx::deal_release(static_cast<hipStream_t>(stream));
+    return NSX_OK;
+}
+
+int nsx_deal_sets_in_use(uint32_t* out_count) {
+    if (!out_count) return NSX_EINVAL;
+    const int dev = current_device();
+    if (dev < 0) return NSX_ENODEV;
+    *out_count = nsx::deal_sets_in_use(dev);
     return NSX_OK;
 }
 

@@ -22,6 +22,7 @@ struct LaunchCfg {
     int xcd_chunk = 0;        // XCD deal: 0 auto, 1..20 = chunks of 2^k tasks, else contiguous eighths
     int64_t window_bytes = 0; // fixed short-segment path: back-to-back launches of ≤ this many bytes (0 auto, -1 one)
     int kernel = 0;           // force an alternative code path (nsx_tune.h NSX_TUNE_KERNEL_*); 0 = by layout
+    int deal = 0;             // -1: equal static shares (no dealt runs) for this call
 };
 
 // The LaunchCfg of one call on a device with `cus` compute units; t nullable (csum_api.cpp).
@@ -84,6 +85,9 @@ hipError_t launch_tcp_parse(const LaunchCfg& c, const void* d_base, const uint64
 // mode 0 verify (out), 1 fill (out nullable), 2 verify into the bitmask `mask` (ceil(n/64) words)
 hipError_t launch_ipv4_hdr(const LaunchCfg& c, uint8_t* base, uint64_t stride, uint32_t hdr_off, uint64_t n,
                            int mode, uint16_t* out, uint64_t* mask, hipStream_t st);
+// The per-stream deal counter sets (csum_kernels.hip deal_heads): return stream st's for reuse; sets given out.
+void deal_release(hipStream_t st);
+uint32_t deal_sets_in_use(int dev);
 hipError_t launch_fill_splitmix64(void* d_buf, uint64_t byte_off, uint64_t nbytes, uint64_t seed,
                                   uint32_t max_blocks, hipStream_t st);
 

@@ -30,6 +30,7 @@
 #include <map>
 #include <mutex>
 #include <type_traits>
+#include <vector>
 
 #include "csum_kernels.h"
 
@@ -1427,11 +1428,7 @@ __device__ __forceinline__ void pfx_runs(const uint8_t* __restrict__ base, __amd
             lds_stage<VR>(slot, V, cur.span, lane);
             lds_zero_tail(slot, cur.span, lane);
         } else {
-#if defined(NSX_RX_DIAG) && NSX_RX_DIAG == 4
-            lds_stage<VR>(slot, V, cur.span, lane);  // diagnostic build only: rows staged, no chunk prefix sums
-#else
             total = pfx_stage<ROWS, VR>(slot, V, cur.span, lane);
-#endif
         }
         // The next piece: the rest of this run, or the next run (whose offsets are already loaded).
         const bool adv = cur.cnt == cur.rem;
@@ -1863,6 +1860,158 @@ __device__ __forceinline__ void rx_runs(const uint8_t* __restrict__ base, __amdg
     }
 }
 
+// ---- The streamed modes' tail, dealt through the block's LDS (round 6) ----
+// With equal static shares the streamed receive pass (workloads 10, 11, 14: 12 waves per CU, ~5 runs of 64 frames
+// each, ~20 µs a run) waited 9-16 µs for its last waves — whole blocks run 3-4 µs apart (the waves of one block end
+// within ~1 µs of each other, profiles/r05_rx_wave_times_streamed.txt) — and dealing whole runs from the per-stream
+// heads (DealtRuns) would leave a tail of up to a run. Here the batch's last 1/2^kStreamPoolShift of frames is dealt
+// in pieces of kStreamPiece frames (~12 KB, ~5 µs), and the ticket round trip (a device-scope atomic, 1-3 µs) is
+// kept off the streaming waves altogether: each block runs three streaming waves and one dealer wave (4 blocks × 3
+// streaming waves per CU = the 12 of the static layout). The dealer pulls tickets from the stream's heads for the
+// pieces its waves have claimed and posts them in an LDS ring; a streaming wave claims its next piece one unit ahead
+// (an LDS atomic) and reads it from the ring when it moves on, so no vector-memory wait of a streaming wave ever
+// covers a ticket (vmcnt retires in issue order: loads issued behind an atomic wait for it too, §7 step 72).
+constexpr uint32_t kStreamPiece = 16;      // frames per dealt piece (a multiple of 8: whole mask bytes)
+constexpr uint32_t kStreamPoolShift = 3;   // the pool: the batch's last eighth of frames
+constexpr uint32_t kPieceRing = 64;        // ring entries per block
+constexpr uint32_t kPieceFree = ~0u;       // an entry read by its consumer (or never written)
+constexpr uint32_t kStreamWaves = 3;       // streaming waves per block (wave 3 deals)
+
+struct PieceRing {
+    uint32_t claim;     // entries claimed by the streaming waves (LDS atomic add)
+    uint32_t produced;  // entries the dealer has written, in order
+    uint32_t end_at;    // the dealer's final entry count once its head's share ran out (~0 until then)
+    uint32_t pad;
+    uint32_t e[kPieceRing];  // entry p at e[p % kPieceRing]: a piece's first frame; kPieceFree once read
+};
+
+// A streaming wave's units: its static runs [a0, e_st) of kRxRun frames, then dealt pieces until the share ends
+// (n). The entry for the unit after next is claimed when next() hands out a unit whose successor is a piece, and
+// read (waiting for the dealer only if it has not posted it yet) when next() moves on to it.
+struct RingRuns {
+    uint32_t a0, e_st, n;
+    PieceRing* rg;
+    uint32_t lane;
+    uint32_t pend;  // the claimed entry not yet read (kPieceFree: none)
+    __device__ __forceinline__ uint32_t claim() const {
+        uint32_t v = 0u;
+        if (lane == 0u) v = __hip_atomic_fetch_add(&rg->claim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return __builtin_amdgcn_readfirstlane(v);
+    }
+    __device__ __forceinline__ uint32_t read(uint32_t idx) const {  // entry idx: a piece's first frame, or n
+        for (;;) {
+            const uint32_t p = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(&rg->produced, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+            if (idx < p) {
+                uint32_t* slot = &rg->e[idx % kPieceRing];
+                const uint32_t v = __builtin_amdgcn_readfirstlane(
+                    __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+                if (lane == 0u) __hip_atomic_store(slot, kPieceFree, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                return v;
+            }
+            const uint32_t e = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(&rg->end_at, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+            if (idx >= e) return n;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    // after handing out unit r: is its successor a piece? then claim that piece's entry now
+    __device__ __forceinline__ uint32_t ahead(uint32_t r) {
+        if (r < n && (r >= e_st || r + kRxRun >= e_st)) pend = claim();
+        return r;
+    }
+    __device__ __forceinline__ uint32_t first() {
+        if (a0 < e_st) return ahead(a0);
+        return ahead(read(claim()));
+    }
+    __device__ __forceinline__ uint32_t next(uint32_t a) {
+        uint32_t r;
+        if (a + kRxRun < e_st) {
+            r = a + kRxRun;
+        } else {
+            r = pend == kPieceFree ? n : read(pend);
+            pend = kPieceFree;
+        }
+        return ahead(r);
+    }
+    __device__ __forceinline__ uint32_t cnt(uint32_t a) const {
+        return a < e_st ? min(kRxRun, e_st - a) : min(kStreamPiece, n - a);
+    }
+};
+
+// The dealer wave of a block: for every entry its streaming waves claim, a ticket from the block's head (at most 4
+// pulls in flight), posted to the ring; past the head's share it posts the end. The head's dword 0 is the ticket
+// counter (shared with DealtRuns, which leaves it at 0), dword 1 counts the head's dealers that have finished: the
+// last one to finish resets both to 0 for the stream's next launch (a dealer may pull up to 4 tickets past the
+// share, so the pull count cannot mark the last pull as in DealtRuns).
+__device__ __forceinline__ void stream_dealer(PieceRing* rg, uint32_t* head, uint32_t pb, uint32_t qh, uint32_t dealers,
+                                              uint32_t lane) {
+    uint32_t p = 0u;
+    bool live = true;
+    while (live) {
+        const uint32_t c = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(&rg->claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        const uint32_t k = min(c - p, 4u);
+        if (k == 0u) {
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+        uint32_t t[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (uint32_t j = 0; j < 4u; ++j)
+            if (j < k && lane == 0u) t[j] = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (uint32_t j = 0; j < 4u; ++j) {
+            const uint32_t tj = __builtin_amdgcn_readfirstlane(t[j]);
+            if (j < k) {
+                if (tj < qh) {
+                    uint32_t* slot = &rg->e[p % kPieceRing];
+                    // the entry's previous use must have been read (its consumer frees it): rarely waits
+                    while ((uint32_t)__builtin_amdgcn_readfirstlane(
+                               __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != kPieceFree)
+                        __builtin_amdgcn_s_sleep(1);
+                    if (lane == 0u)
+                        __hip_atomic_store(slot, pb + tj * kStreamPiece, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    ++p;
+                } else {
+                    live = false;
+                }
+            }
+        }
+        if (lane == 0u) __hip_atomic_store(&rg->produced, p, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (lane == 0u) {
+        __hip_atomic_store(&rg->end_at, p, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint32_t done = __hip_atomic_fetch_add(head + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (done + 1u == dealers) {
+            __hip_atomic_store(head, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(head + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// A streaming wave's units (RingRuns) in the streaming form, the offsets of the next unit loaded one unit ahead.
+template <int R, bool V6>
+__device__ __forceinline__ void rx_runs_ring(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
+                                             RingRuns& q, uint32_t lane, const RxOuts& ro) {
+    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+    auto load_off = [&](uint32_t i, bool live) -> uint64_t {
+        const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, live ? i * 8 : kOOB, 0, 0);
+        return ((uint64_t)x.y << 32) | x.x;
+    };
+    uint32_t a = q.first();
+    uint64_t no = load_off(a + lane, a < n && a + lane <= n), ne = load_off(a + lane + 1, a < n && a + lane + 1 <= n);
+    while (a < n) {
+        uint32_t cnt[1] = {q.cnt(a)};
+        uint64_t my_off[1] = {no}, my_end[1] = {ne};
+        const uint32_t an = q.next(a);
+        no = load_off(an + lane, an < n && an + lane <= n);
+        ne = load_off(an + lane + 1, an < n && an + lane + 1 <= n);
+        rx_run_stream<R, V6, 1>(base, a, cnt, my_off, my_end, 0u, n, lane, ro);
+        a = an;
+    }
+}
+
 // The LDS form of the receive pass, for waves of small frames. A run of 64 frames whose
 // bytes fit kRxSlotRows rows is staged whole into the wave's LDS slot — coalesced 16 B-per-lane row loads, issued
 // one run ahead (the next run's rows are in flight while this one is summed), then ds_write_b128 — and each lane
@@ -1883,11 +2032,6 @@ __device__ __forceinline__ void rx_runs_pfx(const uint8_t* __restrict__ base, __
     auto out = [&](uint32_t F, uint32_t p, uint32_t d0, bool live, uint32_t a, uint32_t s, uint32_t cnt, uint64_t off,
                    uint64_t end) {
         const uint32_t w0 = p >> 2;
-#if defined(NSX_RX_DIAG) && (NSX_RX_DIAG == 3 || NSX_RX_DIAG == 4)
-        // diagnostic build only: the prefix form's loads, staging and mask stores with no per-frame work
-        rx_store_mask(ro.mrs, __builtin_amdgcn_ballot_w64(live && F == 0x12345678u + d0), a, cnt, n, lane, s);
-        return;
-#endif
         uint32_t d[6];
         d[0] = d0;
 #pragma unroll
@@ -1919,21 +2063,11 @@ __device__ __forceinline__ void rx_run_lds(const uint8_t* __restrict__ base, con
     const uint32_t p = live ? (uint32_t)((base + my_off) - rbase) : 0u;
     const uint32_t e = live ? (uint32_t)((base + my_end) - rbase) : 0u;
     const uint32_t hd = p & 3u, w0 = p >> 2;
-#if defined(NSX_RX_DIAG) && NSX_RX_DIAG == 1
-    // diagnostic build only (make exp): the loop's loads, staging and mask stores with no per-frame work
-    rx_store_mask(ro.mrs, __builtin_amdgcn_ballot_w64(live && sdw[w0] == 0x12345678u), a, cnt, n, lane);
-    return;
-#endif
     uint32_t d[6];
 #pragma unroll
     for (int j = 0; j < (V6 ? 3 : 6); ++j) d[j] = sdw[w0 + j];
     if constexpr (V6) d[3] = d[4] = d[5] = 0u;
     const uint32_t F = lds_range_sum(slot, p, e, d[0], live);  // the frame's weighted sum (< 2^32: ≤ 8 KiB)
-#if defined(NSX_RX_DIAG) && NSX_RX_DIAG == 2
-    // diagnostic build only: the frame sums without the header parse and verdict
-    rx_store_mask(ro.mrs, __builtin_amdgcn_ballot_w64(live && fold32(F + d[1]) == 0xFFFFu), a, cnt, n, lane);
-    return;
-#endif
     auto opt = [&](uint32_t (&o)[10]) {
 #pragma unroll
         for (int j = 6; j < 16; ++j) o[j - 6] = sdw[w0 + j];
@@ -2028,90 +2162,6 @@ __device__ __forceinline__ void rx_runs_lds(const uint8_t* __restrict__ base, __
             cur = nxt;
         }
     }
-}
-
-
-// The small-frame mode's LDS loop with TWO runs of rows in flight (round 5): rx_runs_lds<·, ·,
-// true> keeps one run in flight while it sums another, so a wave's loads stop at every run — its next run's rows are
-// issued only once this run's have landed and been staged. Here two register sets alternate: run j's rows (set A) are
-// staged, set A is refilled at once with run j + 2, and run j is summed while runs j + 1 (set B) and j + 2 load. Each
-// iteration issues the offsets of run j + 3 BEFORE the rows of run j + 2, so that reading run j + 2's geometry next
-// iteration never waits on younger row loads (vmcnt counts in issue order). The first run that is not a direct run
-// hands the rest of the range to the hybrid loop, as in rx_runs_lds.
-template <int R, bool V6>
-__device__ __forceinline__ void rx_runs_lds2(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t ofs, uint32_t n,
-                                             uint32_t a0, uint32_t a_end, uint32_t lane, lds16* slot,
-                                             const RxOuts& ro) {
-    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
-    auto load_off = [&](uint32_t i, bool live) -> uint64_t {
-        const v2u x = __builtin_amdgcn_raw_buffer_load_b64(ofs, live ? i * 8 : kOOB, 0, 0);
-        return ((uint64_t)x.y << 32) | x.x;
-    };
-    struct Run {
-        const uint8_t* rbase;
-        uint64_t span;
-        uint32_t cnt;
-        bool lds;
-    };
-    auto geo = [&](uint32_t a, uint64_t off, uint64_t end) {  // wave-uniform geometry of run a (a direct run?)
-        Run g{base, 0, a < a_end ? min(kRxRun, a_end - a) : 0u, false};
-        if (g.cnt) {
-            const uint64_t lo = readlane64(off, 0), hi = readlane64(end, g.cnt - 1u);
-            g.rbase = reinterpret_cast<const uint8_t*>(((uintptr_t)(base + lo)) & ~(uintptr_t)127);
-            g.span = (uint64_t)((base + hi) - g.rbase);
-            g.lds = g.span <= (uint64_t)kRxSlotRows * kRow &&
-                    !__builtin_amdgcn_ballot_w64(lane < g.cnt && end - off > kPfxDirectMax);
-        }
-        return g;
-    };
-    auto issue = [&](u32x4 (&V)[kRxSlotRows], const Run& g, bool on) {  // rows past the run: empty loads
-        const __amdgpu_buffer_rsrc_t rs = make_rsrc(g.rbase, on ? (g.span + 3) & ~3ull : 0ull);
-#pragma unroll
-        for (uint32_t r = 0; r < kRxSlotRows; ++r) V[r] = bld16<true>(rs, r * kRow + lane * 16u);
-    };
-    auto offs_of = [&](uint32_t a, uint64_t& off, uint64_t& end) {
-        off = load_off(a + lane, a < a_end && a + lane <= n);
-        end = load_off(a + lane + 1u, a < a_end && a + lane + 1u <= n);
-    };
-    uint32_t a = a0;
-    uint64_t o0, e0, o1, e1, o2, e2;
-    offs_of(a, o0, e0);
-    offs_of(a + kRxRun, o1, e1);
-    Run g0 = geo(a, o0, e0);
-    if (!g0.lds) {
-        if (g0.cnt) {
-            StaticRuns rest{a, a_end};
-            rx_runs_pfx<R, V6, 7, true>(base, ofs, n, rest, lane, slot, ro);
-        }
-        return;
-    }
-    u32x4 VA[kRxSlotRows], VB[kRxSlotRows];
-    issue(VA, g0, true);
-    Run g1 = geo(a + kRxRun, o1, e1);
-    offs_of(a + 2u * kRxRun, o2, e2);  // offsets of run j + 2 before the rows of run j + 1
-    issue(VB, g1, g1.lds);
-    // One iteration: run a's rows in V are staged, V is refilled with run a + 128, run a is summed. Returns whether
-    // the next run (a + 64 after the rotation) is a staged direct run.
-    auto step = [&](u32x4 (&V)[kRxSlotRows]) -> bool {
-        lds_stage<kRxSlotRows>(slot, V, g0.span, lane);
-        lds_zero_tail(slot, g0.span, lane);
-        const Run g2 = geo(a + 2u * kRxRun, o2, e2);
-        uint64_t o3, e3;
-        offs_of(a + 3u * kRxRun, o3, e3);
-        issue(V, g2, g1.lds && g2.lds);
-        rx_run_lds<V6>(base, g0.rbase, a, g0.cnt, o0, e0, n, lane, slot, ro);
-        a += kRxRun;
-        g0 = g1, o0 = o1, e0 = e1;
-        g1 = g2, o1 = o2, e1 = e2;
-        o2 = o3, e2 = e3;
-        return g0.lds;
-    };
-    for (;;) {
-        if (!step(VA)) break;
-        if (!step(VB)) break;
-    }
-    StaticRuns rest{a, a_end};
-    if (a < a_end) rx_runs_pfx<R, V6, 7, true>(base, ofs, n, rest, lane, slot, ro);
 }
 
 
@@ -2281,13 +2331,30 @@ constexpr uint32_t kRxStreamBigN = 5u << 19;       // 2.5M frames
 // 30-40% on every small-frame mix, §7 step 43.)
 // WPS: waves per SIMD the registers must allow (__launch_bounds__'s second argument): 1 = no constraint (158 VGPRs,
 // 3 waves per SIMD at the default 3 blocks/CU); 4 = the 4-blocks/CU instantiations (≤ 128 VGPRs).
-#if defined(NSX_RX_DIAG) && NSX_RX_DIAG == 5
-#define NSX_RX_WPS(w) 2  // diagnostic build only: registers for two run sets in flight
+
+// Wave w of this block's wpb in a grid of nb blocks, numbered XCD by XCD (blocks b, b + 8, ... run on one XCD).
+__device__ __forceinline__ uint32_t wave_number(uint32_t nb, uint32_t wpb, uint32_t w) {
+    const uint32_t b = blockIdx.x;
+    return (nb >= 16 && (nb & 7) == 0) ? ((b & 7) * (nb >> 3) + (b >> 3)) * wpb + w : b * wpb + w;
+}
+
+// Per-wave timing stamps, the one diagnostic hook in the product kernels (the receive pass and the packed-header
+// kernel): entry(), ready() once the wave's range is known, done(wave number, work) at its end. The product build's
+// WaveStamps records nothing and every call compiles away (the code object is byte-identical to one without the
+// calls). `make stamps` builds lib_stamps/ with the recording policy of tools/probes/wave_stamps.h instead, read back
+// by tools/probes/rx_wave_times.py and f3_wave_times.py.
+#ifdef NSX_WAVE_STAMPS
+#include "../../tools/probes/wave_stamps.h"
 #else
-#define NSX_RX_WPS(w) (w)
+struct WaveStamps {
+    __device__ __forceinline__ void entry() {}
+    __device__ __forceinline__ void ready() {}
+    __device__ __forceinline__ void done(uint32_t g, uint64_t work, uint32_t lane) {}
+};
 #endif
+
 template <int R, bool V6, int WPS, int PF = 0>
-__global__ __launch_bounds__(kBlock, NSX_RX_WPS(WPS)) void rx_tcp_kernel(const uint8_t* __restrict__ base,
+__global__ __launch_bounds__(kBlock, WPS) void rx_tcp_kernel(const uint8_t* __restrict__ base,
                                                              const uint64_t* __restrict__ offsets, uint32_t n,
                                                              uint64_t* __restrict__ mask,
                                                              uint16_t* __restrict__ ip_raw,
@@ -2295,47 +2362,17 @@ __global__ __launch_bounds__(kBlock, NSX_RX_WPS(WPS)) void rx_tcp_kernel(const u
                                                              uint32_t big_keep, uint32_t* __restrict__ deal) {
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-#if defined(NSX_RX_DIAG) && NSX_RX_DIAG == 7
-    const uint64_t t_k = __builtin_amdgcn_s_memrealtime();  // diagnostic build only: kernel entry
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-#endif
+    WaveStamps ws;
+    ws.entry();
     const __amdgpu_buffer_rsrc_t ofs = make_rsrc(offsets, ((uint64_t)n + 1) * 8);
-#if defined(NSX_RX_DIAG) && NSX_RX_DIAG == 7
-    // diagnostic build only (tools/probes/rx_wave_times.py): the two-wave modes' per-wave s_memrealtime stamps
-    // (100 MHz) of entry, range ready and end, the wave's bytes and where it ran (HW_ID's low half: wave, SIMD, CU,
-    // SH, SE; XCC_ID), written over the tcp_raw buffer (no raw sums in this build): [g] = {t_entry, t_range, t_end,
-    // bytes | id << 32}
-    auto timed = [&](const WaveRange& wr, uint32_t nb, uint32_t wpb, RxOuts& rq, auto&& body) {
-        rq.raw = false;
-        const uint64_t t_rg = __builtin_amdgcn_s_memrealtime();
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        body();
-        const uint64_t t_out = __builtin_amdgcn_s_memrealtime();
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        const uint32_t b = blockIdx.x;
-        const uint32_t g = (nb >= 16 && (nb & 7) == 0) ? ((b & 7) * (nb >> 3) + (b >> 3)) * wpb + wave : b * wpb + wave;
-        uint32_t hw, xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        const uint64_t id = (uint64_t)((xcc & 0xFu) << 16 | (hw & 0xFFFFu)) << 32;
-        const uint64_t v = lane == 0 ? t_k : lane == 1 ? t_rg : lane == 2 ? t_out : (wr.bytes & 0xFFFFFFFFu) | id;
-        uint64_t* ts = reinterpret_cast<uint64_t*>(tcp_raw);
-        if (ts && lane < 4u) ts[(uint64_t)g * 4u + lane] = v;
-    };
-    RxOuts ro = rx_outs(mask, ip_raw, tcp_raw, n);
-    ro.raw = false;  // tcp_raw holds the stamps
-#else
     const RxOuts ro = rx_outs(mask, ip_raw, tcp_raw, n);
-#endif
     extern __shared__ lds16 lds_rx[];
     // Byte-balanced wave ranges (as csum_ragged_scan_kernel), cut at multiples of 8 frames. Cut at whole mask
     // words (64 frames, ~50 KB) instead, a wave streamed up to one run more than the mean, and the launch
     // waited ~20 µs for those waves at any batch size.
     // XCD-contiguous numbering of the blocks; wpb of each block's waves take ranges.
     auto range = [&](uint32_t nb, uint32_t wpb, uint32_t w) {
-        const uint32_t b = blockIdx.x, W = nb * wpb;
-        const uint32_t g = (nb >= 16 && (nb & 7) == 0) ? ((b & 7) * (nb >> 3) + (b >> 3)) * wpb + w : b * wpb + w;
-        return wave_range(ofs, n, g, W, lane, kRxSmallFrame, 8u);
+        return wave_range(ofs, n, wave_number(nb, wpb, w), nb * wpb, lane, kRxSmallFrame, 8u);
     };
     if constexpr (PF < 0) {
         int mode = sets;
@@ -2359,29 +2396,58 @@ __global__ __launch_bounds__(kBlock, NSX_RX_WPS(WPS)) void rx_tcp_kernel(const u
             // whole batch the waves ran at speeds ±4% apart (by CU and XCD, not by data), and a launch waited 5-29 µs
             // for its last waves (tools/probes/rx_wave_times.py, profiles/r05_rx_wave_times_by_cu.txt).
             if (wave >= 2u) return;
-            const uint32_t nb = gridDim.x, W2 = nb * 2u, b = blockIdx.x;
-            const uint32_t g = (nb >= 16 && (nb & 7) == 0) ? ((b & 7) * (nb >> 3) + (b >> 3)) * 2u + wave : b * 2u + wave;
+            const uint32_t W2 = gridDim.x * 2u, g = wave_number(gridDim.x, 2u, wave);
             WaveRange wr;
             DealtRuns q = deal_runs(ofs, n, g, W2, lane, kRxSmallFrame, 8u, 0u, deal, &wr);
-#if defined(NSX_RX_DIAG) && NSX_RX_DIAG == 7
-            timed(wr, gridDim.x, 2u, ro, [&] {
-#endif
+            ws.ready();
             if (mode == 6) {
                 rx_runs_pfx<R, V6, 15, false>(base, ofs, n, q, lane, lds_rx + wave * (PfxSlot<15>::kBytes / 16u), ro);
             } else {
                 lds16* slot = lds_rx + wave * (PfxSlot<7>::kBytes / 16u);
-#if defined(NSX_RX_DIAG) && NSX_RX_DIAG == 5
-                if (mode == 5) rx_runs_lds2<R, V6>(base, ofs, n, wr.a0, wr.a_end, lane, slot, ro);
-#else
                 if (mode == 5) rx_runs_lds<R, V6, true>(base, ofs, n, q, lane, slot, ro);
-#endif
                 else rx_runs_pfx<R, V6, 7, true>(base, ofs, n, q, lane, slot, ro);
             }
-#if defined(NSX_RX_DIAG) && NSX_RX_DIAG == 7
-            });
-#endif
-        } else {  // streamed runs on 3 of the 4 blocks per CU (the auto choice and mode 8, which forces it); mode 1:
-                  // on every block
+            ws.done(g, wr.bytes, lane);
+        } else if (deal && (sets == 0 || sets == 8)) {
+            // Streamed runs with the batch's last eighth dealt in pieces through the block's LDS ring (the auto
+            // choice and mode 8 when the stream has heads; §7 step 75): waves 0-2 of every block stream, wave 3 deals.
+            PieceRing* rg = reinterpret_cast<PieceRing*>(lds_rx + kStreamWaves * (PfxSlot<7>::kBytes / 16u));
+            static_assert(sizeof(PieceRing) <= PfxSlot<7>::kBytes && kPieceRing <= kWave, "the ring in wave 3's slot");
+            if (wave == kStreamWaves) {
+                if (lane < kPieceRing) rg->e[lane] = kPieceFree;
+                if (lane == 0u) rg->claim = 0u, rg->produced = 0u, rg->end_at = ~0u;
+            }
+            __syncthreads();
+            const uint32_t nb = gridDim.x;
+            const uint32_t S = (n - (n >> kStreamPoolShift)) & ~(kRxRun - 1u);  // the static shares: frames [0, S)
+            if (wave == kStreamWaves) {
+                // head h of the block (numbered XCD by XCD, so every head has blocks on all 8 XCDs), its share of the
+                // pool's pieces and its dealers
+                const uint32_t H = min(kDealHeads, nb), h = wave_number(nb, 1u, 0u) % H;
+                const uint32_t Q = (n - S + kStreamPiece - 1u) / kStreamPiece;
+                const uint32_t r0 = (uint32_t)((uint64_t)Q * h / H), qh = (uint32_t)((uint64_t)Q * (h + 1u) / H) - r0;
+                stream_dealer(rg, deal + h * kDealStride, S + r0 * kStreamPiece, qh, (nb - h + H - 1u) / H, lane);
+                return;
+            }
+            const uint32_t g = wave_number(nb, kStreamWaves, wave);
+            WaveRange wr{0u, 0u, 0u};
+            if (S > 0u) wr = wave_range(ofs, S, g, nb * kStreamWaves, lane, kRxSmallFrame, 8u);
+            RxOuts rp = ro;
+            if (ro.raw) {  // parked in the wave's 7-row slot, as below
+                uint16_t* pb = reinterpret_cast<uint16_t*>(lds_rx + wave * (PfxSlot<7>::kBytes / 16u));
+                rp.tpk = make_park<uint16_t>(pb, ro.trs, tcp_raw, wr.a0, V6 ? 4096u : 2048u);
+                if constexpr (!V6) rp.ipk = make_park<uint16_t>(pb + 2048, ro.irs, ip_raw, wr.a0, 2048u);
+            }
+            ws.ready();
+            RingRuns q{wr.a0, wr.a_end, n, rg, lane, kPieceFree};
+            rx_runs_ring<R, V6>(base, ofs, n, q, lane, rp);
+            if (ro.raw) {
+                park_flush(rp.tpk, lane);
+                if constexpr (!V6) park_flush(rp.ipk, lane);
+            }
+            ws.done(g, wr.bytes, lane);
+        } else {  // streamed runs on 3 of the 4 blocks per CU (the auto choice and mode 8, which forces it, on a
+                  // stream without heads); mode 1: on every block
             const uint32_t nb = active_blocks(ofs, n, 0u, sets == 0 || sets == 8 ? 3u : 0u);
             if (blockIdx.x >= nb) return;
             const WaveRange wr = range(nb, kWavesPerBlock, wave);
@@ -2393,17 +2459,13 @@ __global__ __launch_bounds__(kBlock, NSX_RX_WPS(WPS)) void rx_tcp_kernel(const u
                 rp.tpk = make_park<uint16_t>(pb, ro.trs, tcp_raw, wr.a0, V6 ? 4096u : 2048u);
                 if constexpr (!V6) rp.ipk = make_park<uint16_t>(pb + 2048, ro.irs, ip_raw, wr.a0, 2048u);
             }
-#if defined(NSX_RX_DIAG) && NSX_RX_DIAG == 7
-            timed(wr, nb, kWavesPerBlock, ro, [&] {
-#endif
+            ws.ready();
             rx_runs<R, V6, 1>(base, ofs, n, wr.a0, wr.a_end, lane, rp);
-#if defined(NSX_RX_DIAG) && NSX_RX_DIAG == 7
-            });
-#endif
             if (ro.raw) {
                 park_flush(rp.tpk, lane);
                 if constexpr (!V6) park_flush(rp.ipk, lane);
             }
+            ws.done(wave_number(nb, kWavesPerBlock, wave), wr.bytes, lane);
         }
         return;
     }
@@ -3135,21 +3197,14 @@ constexpr uint32_t kHdr20Lds = kHdr20Task * 20u;  // bytes of LDS per wave
 // Software-pipelined: two register sets of U tasks; the loads of the next set are issued before the
 // current set goes through LDS, so every wave keeps loads in flight while it computes and stores (one wave
 // per SIMD at 1 block/CU has no other wave to cover those phases).
-#if defined(NSX_F3_DIAG)
-// diagnostic build only (tools/probes/f3_wave_times.py): per wave {entry, end, tasks, XCC_ID << 16 | HW_ID's low
-// half} of the last ipv4_hdr20_kernel launch, read back with nsx_diag_stamps
-__device__ uint64_t g_f3_stamps[4096 * 4];
-#endif
 template <int MODE, int U>
 __global__ __launch_bounds__(kBlock) void ipv4_hdr20_kernel(uint8_t* __restrict__ base, uint32_t n,
                                                             uint16_t* __restrict__ out, uint32_t clog,
                                                             uint64_t* __restrict__ mask) {
     typedef uint32_t v2u __attribute__((ext_vector_type(2)));
-#if defined(NSX_F3_DIAG)
-    const uint64_t t_k = __builtin_amdgcn_s_memrealtime();
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    uint32_t ntk = 0;
-#endif
+    WaveStamps ws;
+    ws.entry();
+    uint32_t ntk = 0;  // tasks done (for the stamps)
     extern __shared__ u32x4 lds20[];
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -3254,30 +3309,14 @@ __global__ __launch_bounds__(kBlock) void ipv4_hdr20_kernel(uint8_t* __restrict_
         const uint32_t t1 = t0 + step * U;
         issue(t1, B);
         consume(A);
-#if defined(NSX_F3_DIAG)
         ntk += U;
-#endif
         if (!live(t1)) break;
         t0 = t1 + step * U;
         issue(t0, A);
         consume(B);
-#if defined(NSX_F3_DIAG)
         ntk += U;
-#endif
     }
-#if defined(NSX_F3_DIAG)
-    {
-        const uint64_t t_out = __builtin_amdgcn_s_memrealtime();
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        uint32_t hw, xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        const uint32_t g = blockIdx.x * kWavesPerBlock + wave;
-        const uint64_t v = lane == 0 ? t_k : lane == 1 ? t_out : lane == 2 ? (uint64_t)ntk
-                                                                             : (uint64_t)((xcc & 0xFu) << 16 | (hw & 0xFFFFu));
-        if (lane < 4u && g < 4096u) g_f3_stamps[g * 4u + lane] = v;
-    }
-#endif
+    ws.done(blockIdx.x * kWavesPerBlock + wave, ntk, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -3602,49 +3641,91 @@ hipError_t launch_fixed(const LaunchCfg& c, const void* d_base, uint64_t stride,
 // one stream's launches one after another, whichever kernel they are.
 __device__ uint32_t g_deal_heads[kDealSlots * kDealHeads * kDealStride];
 
-// The heads for a launch on stream st of the current device: the stream's own set (given on first use, kept for the
-// process), or nullptr — equal static shares — when the stream is being captured into a graph (a graph's launches
-// could replay on several streams at once), when every set is given out, or in builds without dealing.
-static uint32_t* deal_heads(hipStream_t st) {
-#if defined(NSX_NO_DEAL) || (defined(NSX_RX_DIAG) && NSX_RX_DIAG == 5)
-    (void)st;
-    return nullptr;
-#else
+// Which streams get a set. The deal is correct only if the launches sharing a set run one after another: the wave
+// that draws a head's last pull resets it for the next launch (DealtRuns). So a set is given only to a handle that
+// names ONE ordered queue of the current device:
+// - a stream the caller created (hipStreamCreate*), on the current device;
+// - the device's null stream (nullptr, and hipStreamLegacy, its explicit name; keyed together).
+// Every other launch takes equal static shares (nullptr), bit-exact as well:
+// - hipStreamPerThread: one handle value that stands for a different stream on every host thread, so launches from
+//   two threads on it may run at once;
+// - a stream of another device (g_deal_heads is per device: the set would be device A's memory under a kernel on B);
+// - a stream being captured into a graph (a graph's launches could replay on several streams at once);
+// - tune.deal = -1 (the A/B switch that replaced round 5's NSX_NO_DEAL build), or every set given out.
+// A set stays with its stream for the process unless the stream is returned (nsx_stream_release, before the caller
+// destroys it): returned sets are given out again first, so streams created and destroyed in a loop do not use up
+// the 64 sets.
+struct DealSets {
+    uint32_t* base = nullptr;    // the device's g_deal_heads
+    uint32_t fresh = 0;          // sets never given out start here
+    std::vector<uint32_t> free;  // returned sets (their heads are 0: every launch that used them has completed)
+};
+static std::mutex g_deal_mu;
+static std::map<std::pair<int, hipStream_t>, uint32_t> g_deal_slot;  // (device, stream) → set
+static std::map<int, DealSets> g_deal_dev;
+
+static hipStream_t deal_key(hipStream_t st) { return st == hipStreamLegacy ? nullptr : st; }
+
+static uint32_t* deal_heads(const LaunchCfg& c, hipStream_t st) {
+    if (c.deal < 0 || st == hipStreamPerThread) return nullptr;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(st, &cs) != hipSuccess) {
         (void)hipGetLastError();  // a refused query (e.g. the legacy stream while another captures) is not the launch's error
         return nullptr;
     }
     if (cs != hipStreamCaptureStatusNone) return nullptr;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) {
+    int dev = 0, sdev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipStreamGetDevice(st, &sdev) != hipSuccess) {
         (void)hipGetLastError();
         return nullptr;
     }
-    static std::mutex mu;
-    static std::map<std::pair<int, hipStream_t>, uint32_t> slot_of;
-    static std::map<int, std::pair<uint32_t*, uint32_t>> dev_sets;  // device → (its g_deal_heads, sets given)
-    std::lock_guard<std::mutex> lock(mu);
-    auto it = slot_of.find({dev, st});
-    auto& ds = dev_sets[dev];
-    if (!ds.first) {
+    if (sdev != dev) return nullptr;
+    const hipStream_t key = deal_key(st);
+    std::lock_guard<std::mutex> lock(g_deal_mu);
+    DealSets& ds = g_deal_dev[dev];
+    if (!ds.base) {
         void* p = nullptr;
         if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_deal_heads)) != hipSuccess || !p) {
             (void)hipGetLastError();
             return nullptr;
         }
-        ds.first = static_cast<uint32_t*>(p);
+        ds.base = static_cast<uint32_t*>(p);
     }
     uint32_t slot;
-    if (it != slot_of.end()) {
+    auto it = g_deal_slot.find({dev, key});
+    if (it != g_deal_slot.end()) {
         slot = it->second;
+    } else if (!ds.free.empty()) {
+        slot = ds.free.back();
+        ds.free.pop_back();
+        g_deal_slot[{dev, key}] = slot;
     } else {
-        if (ds.second >= kDealSlots) return nullptr;
-        slot = ds.second++;
-        slot_of[{dev, st}] = slot;
+        if (ds.fresh >= kDealSlots) return nullptr;
+        slot = ds.fresh++;
+        g_deal_slot[{dev, key}] = slot;
     }
-    return ds.first + (size_t)slot * kDealHeads * kDealStride;
-#endif
+    return ds.base + (size_t)slot * kDealHeads * kDealStride;
+}
+
+// Return stream st's sets (on every device) for reuse: the caller has synchronised st and is about to destroy it.
+void deal_release(hipStream_t st) {
+    const hipStream_t key = deal_key(st);
+    std::lock_guard<std::mutex> lock(g_deal_mu);
+    for (auto it = g_deal_slot.begin(); it != g_deal_slot.end();) {
+        if (it->first.second == key) {
+            g_deal_dev[it->first.first].free.push_back(it->second);
+            it = g_deal_slot.erase(it);
+        } else {
+            ++it;
+        }
+    }
+}
+
+// Sets given out on the current device (tests: a released stream's set is reused, not a fresh one).
+uint32_t deal_sets_in_use(int dev) {
+    std::lock_guard<std::mutex> lock(g_deal_mu);
+    auto it = g_deal_dev.find(dev);
+    return it == g_deal_dev.end() ? 0u : it->second.fresh - (uint32_t)it->second.free.size();
 }
 
 template <bool VERIFY>
@@ -3678,7 +3759,7 @@ static hipError_t launch_ragged_scan(const LaunchCfg& c, const uint8_t* base, co
     const bool pick = c.blocks_per_cu == 0 && pipe && rows == 2;
     const uint32_t mb = pick ? (uint32_t)c.cus * 4u : max_blocks_of(c, 2);
     const uint32_t keep = pick ? 2u : 0u;
-    uint32_t* deal = deal_heads(st);  // the small-segment mode's dealt runs
+    uint32_t* deal = deal_heads(c, st);  // the small-segment mode's dealt runs
     for (uint64_t c0 = 0; c0 < n; c0 += kRaggedChunk) {
         const uint32_t cn = (uint32_t)(n - c0 < kRaggedChunk ? n - c0 : kRaggedChunk);
         const uint32_t grid = grid_for((cn + task * ns - 1) / (task * ns), mb);
@@ -3764,7 +3845,7 @@ hipError_t launch_rx_tcp(const LaunchCfg& c, int ipver, const void* d_base, cons
         static_assert(la_def >= (size_t)PfxSlot<7>::kBytes * kWavesPerBlock && la_def * 4 <= 163840 &&
                           la_ring * 4 <= 163840, "4 blocks per CU");
         const size_t la = c.segs_per_wave == 9 ? la_ring : la_def;
-        uint32_t* deal = deal_heads(st);
+        uint32_t* deal = deal_heads(c, st);
         for (uint64_t c0 = 0; c0 < n; c0 += kRaggedChunk) {
             const uint32_t cn = (uint32_t)(n - c0 < kRaggedChunk ? n - c0 : kRaggedChunk);
             const uint32_t grid = grid_for((cn + kRxRun - 1) / kRxRun, (uint32_t)c.cus * 4u);
@@ -3901,13 +3982,6 @@ uint64_t ipv4_hdr_launch_count(const LaunchCfg& c, uintptr_t base, uint64_t stri
     return (n + win - 1) / win;
 }
 
-#if defined(NSX_F3_DIAG)
-hipError_t diag_f3_stamps(uint64_t* dst, uint64_t count) {
-    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_f3_stamps), std::min<uint64_t>(count, 4096 * 4) * 8, 0,
-                               hipMemcpyDeviceToHost);
-}
-#endif
-
 hipError_t launch_ipv4_hdr(const LaunchCfg& c, uint8_t* base, uint64_t stride, uint32_t hdr_off, uint64_t n,
                            int mode, uint16_t* out, uint64_t* mask, hipStream_t st) {
     // Kernel by layout: packed 20 B headers (stride 20, hdr_off 0, 4-aligned base) → the pipelined flat
@@ -3999,10 +4073,3 @@ hipError_t launch_fill_splitmix64(void* d_buf, uint64_t byte_off, uint64_t nbyte
 }
 
 }  // namespace nsx
-
-#if defined(NSX_F3_DIAG)
-// diagnostic build only: the per-wave stamps of the last packed-header launch (tools/probes/f3_wave_times.py)
-extern "C" __attribute__((visibility("default"))) int nsx_diag_f3_stamps(uint64_t* dst, uint64_t count) {
-    return nsx::diag_f3_stamps(dst, count) == hipSuccess ? 0 : -5;
-}
-#endif

@@ -418,7 +418,9 @@ void run_build_job(BuildJob* j) {
     auto finish = [&](int s) {  // chunk pending[s] is complete on the device: hand its results to the caller
         const Chunk* c = pending[s];
         const uint64_t lead_o = c->byte_lo & 255;
-        if (!out_pinned) std::memcpy(j->out + c->byte_lo, ctx->h_ostage[s].as<uint8_t>() + lead_o, c->byte_hi - c->byte_lo);
+        // the images back into pageable caller memory: the same multi-threaded copy as the payloads' way in (one
+        // thread's memcpy held the pageable build at 31.7 GB/s of PCIe traffic against 54.3 pinned)
+        if (!out_pinned) stage_copy(j->out + c->byte_lo, ctx->h_ostage[s].as<uint8_t>() + lead_o, c->byte_hi - c->byte_lo);
         if (j->raw) std::memcpy(j->raw + c->c0, ctx->h_rawstage[s].p, (c->c1 - c->c0) * sizeof(uint16_t));
         pending[s] = nullptr;
     };
@@ -508,7 +510,7 @@ void run_build_job(BuildJob* j) {
         uint8_t* d_out = ctx->d_out[s].as<uint8_t>();
         uint8_t* out_dst = out_pinned ? j->out + c.byte_lo : ctx->h_ostage[s].as<uint8_t>() + lead_o;
         if (j->gaps && span_o) {  // the caller's bytes between images stay as they are
-            if (!out_pinned) std::memcpy(out_dst, j->out + c.byte_lo, span_o);
+            if (!out_pinned) stage_copy(out_dst, j->out + c.byte_lo, span_o);
             NSX_TRY(hipMemcpyAsync(d_out + lead_o, out_dst, span_o, hipMemcpyHostToDevice, st[s]));
         }
         const nsx::TcpHdrSoA h{(const uint16_t*)dev_f[0], (const uint16_t*)dev_f[1], (const uint32_t*)dev_f[2],

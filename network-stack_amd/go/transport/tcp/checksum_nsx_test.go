@@ -77,3 +77,56 @@ func TestBuildSegmentsMatchesReferenceSendLoop(t *testing.T) {
 		}
 	}
 }
+
+// The reuse forms a transport keeps across batches: one Sender building batch
+// after batch through its one pinned block (the results equal the one-shot
+// BuildSegments'), and one PinnedBatch reset and refilled past its first
+// capacity (it grows) whose checksums equal the single-segment path's.
+func TestReuseFormsMatchOneShot(t *testing.T) {
+	snd := NewSender()
+	defer snd.Close()
+	pb, err := NewPinnedBatch(16)
+	if err != nil {
+		t.Skipf("no GPU: %v", err)
+	}
+	defer pb.Free()
+	for round := 0; round < 4; round++ {
+		segs := make([]segment, 3+round*40)
+		pseudo := make([][]byte, len(segs))
+		for i := range segs {
+			segs[i] = segment{srcPort: uint16(i), seqNum: uint32(round<<20 | i), data: make([]byte, (i*37+round)%1500)}
+			for k := range segs[i].data {
+				segs[i].data[k] = byte(k*7 + i + round)
+			}
+			segs[i].offset = segs[i].computeOffset()
+			pseudo[i] = []byte{10, 0, 0, 1, 10, 0, byte(round), byte(i), 0, 6, 0, 0}
+		}
+		got, err := snd.Build(segs, pseudo, 0)
+		if err != nil {
+			t.Skipf("no GPU: %v", err)
+		}
+		one, err := BuildSegments(segs, pseudo, 0)
+		if err != nil {
+			t.Fatal(err)
+		}
+		pb.Reset()
+		for i := 0; i < got.Len(); i++ {
+			if got.Raw[i] != one.Raw[i] || string(got.Image(i)) != string(one.Image(i)) {
+				t.Fatalf("round %d segment %d: Sender.Build differs from BuildSegments", round, i)
+			}
+			if err := pb.Append(got.Image(i)); err != nil {
+				t.Fatal(err)
+			}
+		}
+		one.Free()
+		sums, err := pb.Checksum(pseudo, 0)
+		if err != nil {
+			t.Fatal(err)
+		}
+		for i := range sums {
+			if want := checksum16(pseudo[i], got.Image(i)); sums[i] != want || sums[i] != 0xFFFF {
+				t.Fatalf("round %d segment %d: %#x, want %#x = 0xffff (tcp.go:70)", round, i, sums[i], want)
+			}
+		}
+	}
+}

@@ -29,7 +29,8 @@ class Tune(ctypes.Structure):
     _fields_ = [("blocks_per_cu", ctypes.c_int32), ("segs_per_wave", ctypes.c_int32),
                 ("block_mode", ctypes.c_int32), ("rows", ctypes.c_int32), ("run_segs", ctypes.c_int32),
                 ("xcd_chunk", ctypes.c_int32), ("window_bytes", ctypes.c_int64), ("kernel", ctypes.c_int32),
-                ("shards_per_device", ctypes.c_int32), ("reserved", ctypes.c_int32 * 6)]
+                ("shards_per_device", ctypes.c_int32), ("deal", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 5)]
 
 
 TUNE_FIELDS = tuple(f for f, _ in Tune._fields_ if f != "reserved")
@@ -73,6 +74,8 @@ def lib() -> ctypes.CDLL:
             "nsx_pseudo_ipv6_partial_dev": [vp, vp, vp, u8, u64, vp, vp],
             "nsx_verify_mask_dev": [vp, u64, vp, vp],
             "nsx_host_cache_release": [],
+            "nsx_stream_release": [vp],
+            "nsx_deal_sets_in_use": [ctypes.POINTER(u32)],
             "nsx_csum_fixed_host": [vp, u64, u32, u64, vp, vp, i32],
             "nsx_csum_ragged_host": [vp, vp, u64, vp, vp, i32],
             "nsx_alloc_pinned": [sz, ctypes.POINTER(vp)],
@@ -202,6 +205,20 @@ def shard_plan(n: int, parts: int, offsets: np.ndarray | None = None) -> np.ndar
     off = None if offsets is None else np.ascontiguousarray(offsets, np.uint64)
     _check(lib().nsx_shard_plan(_np_ptr(off), n, parts, _np_ptr(b)), "nsx_shard_plan")
     return b
+
+
+def stream_release(stream) -> None:
+    """nsx_stream_release: return a stream's deal counters (call after it has drained, before destroying it).
+    `stream`: a torch stream, or a raw handle value (int)."""
+    h = stream if isinstance(stream, int) else stream.cuda_stream
+    _check(lib().nsx_stream_release(ctypes.c_void_p(h)), "nsx_stream_release")
+
+
+def deal_sets_in_use() -> int:
+    """Per-stream deal counter sets given out on the current device (nsx_deal_sets_in_use)."""
+    c = ctypes.c_uint32(0)
+    _check(lib().nsx_deal_sets_in_use(ctypes.byref(c)), "nsx_deal_sets_in_use")
+    return c.value
 
 
 def ipv4_hdr_launch_count(buf, stride: int, n: int, hdr_off: int = 0, tune=None) -> int:
@@ -545,6 +562,10 @@ def tcp_build_host(fields: dict, data: np.ndarray, data_off: np.ndarray, out_off
         raise ValueError(f"tcp_build_host opts: {ob.size} B given, opt_off ends at {int(oo[-1])}")
     if out is None:
         out = np.zeros(int(out_off[-1]) if n > 0 else 0, np.uint8)
+    # the C call writes the images contiguously from out's first byte: a strided view, or a view of wider elements,
+    # would be written past
+    if not isinstance(out, np.ndarray) or out.dtype != np.uint8 or not out.flags.c_contiguous:
+        raise ValueError("tcp_build_host out: needs a C-contiguous uint8 array")
     if n > 0 and out.size < int(out_off[-1]):
         raise ValueError(f"tcp_build_host out: {out.size} B given, out_off ends at {int(out_off[-1])}")
     part = None if partial is None else np.ascontiguousarray(partial, np.uint32)

@@ -38,7 +38,7 @@ def test_header_declares_the_boundary():
 def test_library_exports_every_declared_symbol():
     L = nsx.lib()
     declared = declared_functions() + declared_functions(TUNE_HEADER)
-    assert len(declared_functions(TUNE_HEADER)) == 15
+    assert len(declared_functions(TUNE_HEADER)) == 16
     missing = [n for n in declared if not hasattr(L, n)]
     assert not missing, missing
     out = subprocess.run(["nm", "-D", "--defined-only", nsx.LIB_PATH], capture_output=True, text=True).stdout
@@ -64,8 +64,9 @@ def test_tune_struct_layout_matches_header():
 #include <stdio.h>
 #include "nsx_tune.h"
 int main(void) {
-    printf("%zu %zu %zu %zu %zu\n", sizeof(nsx_tune), offsetof(nsx_tune, window_bytes),
-           offsetof(nsx_tune, kernel), offsetof(nsx_tune, shards_per_device), offsetof(nsx_tune, reserved));
+    printf("%zu %zu %zu %zu %zu %zu\n", sizeof(nsx_tune), offsetof(nsx_tune, window_bytes),
+           offsetof(nsx_tune, kernel), offsetof(nsx_tune, shards_per_device), offsetof(nsx_tune, deal),
+           offsetof(nsx_tune, reserved));
     return 0;
 }
 ''')
@@ -74,7 +75,7 @@ int main(void) {
         got = [int(x) for x in subprocess.run([exe], capture_output=True, text=True).stdout.split()]
     T = nsx.Tune
     assert got == [ctypes.sizeof(T), T.window_bytes.offset, T.kernel.offset, T.shards_per_device.offset,
-                   T.reserved.offset]
+                   T.deal.offset, T.reserved.offset]
     with pytest.raises(ValueError):
         nsx._tune(dict(no_such_knob=1))
 
@@ -411,7 +412,10 @@ def test_tcp_build_host_validates_before_any_device():
     for kw, msg in ((dict(data=np.zeros(29, np.uint8)), "data_off ends at 30"),
                     (dict(out=np.zeros(95, np.uint8)), "out_off ends at 96"),
                     (dict(partial=np.zeros(2, np.uint32)), "partial"),
-                    (dict(opt_off=np.zeros(4, np.uint64)), "opt_off given without opts")):
+                    (dict(opt_off=np.zeros(4, np.uint64)), "opt_off given without opts"),
+                    # the images are written contiguously from out's first byte
+                    (dict(out=np.zeros(400, np.uint8)[::2]), "C-contiguous uint8"),
+                    (dict(out=np.zeros(100, np.uint16)), "C-contiguous uint8")):
         args = dict(fields=fields, data=data, data_off=data_off)
         args.update(kw)
         with pytest.raises(ValueError) as e:

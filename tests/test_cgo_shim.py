@@ -256,3 +256,52 @@ def test_checker_catches_a_mismatch():
     assert go_to_c(gf.expr_type("C.int(n)")) == "int" != header_prototypes()["nsx_csum_ragged_host"][1][2]
     with pytest.raises(AssertionError):
         gf.expr_type("someUntypedThing")
+
+
+def _go_funcs(src: str) -> dict:
+    """name (receiver type prefixed: 'PinnedBatch.Verify') -> body text, for every func in a Go source."""
+    out = {}
+    for m in re.finditer(r"^func\s+(?:\(\s*\w+\s+\*?(\w+)\s*\)\s*)?(\w+)(?:\[[^\]]*\])?\s*\(", src, re.M):
+        i = src.index("{", _close(src, m.end() - 1))
+        depth = 0
+        for j in range(i, len(src)):
+            depth += {"{": 1, "}": -1}.get(src[j], 0)
+            if depth == 0:
+                break
+        out[(m.group(1) + "." if m.group(1) else "") + m.group(2)] = src[i:j + 1]
+    return out
+
+
+def test_go_entry_points_pin_memory_only_when_a_batch_outgrows_the_block(shim):
+    """the Go side must not pin (hipHostMalloc) and unpin per call — page registration costs
+    milliseconds against a small batch's tens of microseconds. Checked on the shim's source:
+      - nsx_alloc_pinned is called in exactly one place, pinnedArena.reserve, after its early return for a block
+        that is already large enough (grow-only, at least doubling), and nsx_free_pinned only in pinnedArena.free;
+      - the reuse forms a transport keeps across batches — PinnedBatch.Checksum, PinnedBatch.Verify (rx),
+        Sender.Build — reach the library with no allocation or free of pinned memory of their own;
+      - the one-shot forms (ChecksumSegments, VerifyDatagrams/VerifyPackets6, BuildSegments) are wrappers over
+        them."""
+    funcs = {}
+    for gf in shim:
+        funcs.update(_go_funcs(gf.src))
+    where_alloc = [k for k, b in funcs.items() if "C.nsx_alloc_pinned" in b]
+    where_free = [k for k, b in funcs.items() if "C.nsx_free_pinned" in b]
+    assert where_alloc == ["pinnedArena.reserve"], where_alloc
+    assert where_free == ["pinnedArena.free"], where_free
+    res = funcs["pinnedArena.reserve"]
+    assert re.search(r"if n <= uint64\(len\(a\.buf\)\) \{\s*return nil", res)
+    assert res.index("return nil") < res.index("C.nsx_alloc_pinned") and "c *= 2" in res
+    for k, call in (("PinnedBatch.Checksum", "C.nsx_csum_ragged_host"), ("PinnedBatch.Verify", "C.nsx_rx_ipv4_tcp_verify_host"),
+                    ("PinnedBatch.Verify", "C.nsx_rx_ipv6_tcp_verify_host"), ("build", "C.nsx_tcp_build_host")):
+        assert call in funcs[k], (k, call)
+        assert "NewPinnedBatch" not in funcs[k] and ".free()" not in funcs[k] and ".Free()" not in funcs[k], k
+    assert "build(&s.arena" in funcs["Sender.Build"] and "arena.reserve(" in funcs["build"]
+    assert "b.Checksum(" in funcs["ChecksumSegments"] and "b.Verify(" in funcs["verifyFrames"]
+    assert "verifyFrames(" in funcs["VerifyDatagrams"] and "verifyFrames(" in funcs["VerifyPackets6"]
+    assert "build(a, b" in funcs["BuildSegments"]
+    # the sender's C call sees only pinned memory: every pointer argument is a region of the arena
+    gf = next(g for g in shim if g.path.endswith("build_nsx.go"))
+    (fn, args), = [c for c in gf.c_calls() if c[0] == "nsx_tcp_build_host"]
+    for a in args:
+        assert a.startswith(("&h", "(*C.uint8_t)(region(", "(*C.uint64_t)(region(", "(*C.uint16_t)(region(",
+                             "optOffs", "partial", "C.uint64_t(n)", "C.int(")), a

@@ -205,13 +205,104 @@ def test_ragged_dealt_runs_back_to_back_and_on_many_streams():
         h = ctypes.c_void_p()
         assert hip.hipStreamCreate(ctypes.byref(h)) == 0
         handles.append(h)
+    used0 = nsx.deal_sets_in_use()
     try:
         streams = [torch.cuda.ExternalStream(h.value) for h in handles]
         check([launch(i + r, streams[i]) for r in range(2) for i in range(len(streams))])
     finally:
         torch.cuda.synchronize()
         for h in handles:
+            nsx.stream_release(h.value)  # the sets go back before the stream is destroyed
             hip.hipStreamDestroy(h)
+    assert nsx.deal_sets_in_use() <= used0
+    # a released set is given to the next new stream, not a fresh one: creating and destroying streams in a loop
+    # does not use the 64 sets up
+    for r in range(80):
+        h = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(h)) == 0
+        try:
+            res = [launch(r, torch.cuda.ExternalStream(h.value))]
+            check(res)
+            assert nsx.deal_sets_in_use() <= used0 + 1
+        finally:
+            torch.cuda.synchronize()
+            nsx.stream_release(h.value)
+            hip.hipStreamDestroy(h)
+
+
+def test_dealt_runs_on_hipStreamPerThread_from_concurrent_threads():
+    """hipStreamPerThread (handle 2) is ONE handle value that names a different stream on every host thread, so
+    launches from several threads on it run at the same time: sharing one deal-counter set between them would
+    interleave their tickets. The library gives that handle no set (equal static
+    shares, deal_heads in csum_kernels.hip). Four host threads each make 20 launches of the ragged checksum's
+    small-segment mode and of the IPv4 receive pass's small-frame mode through the C ABI on hipStreamPerThread,
+    concurrently, into their own outputs; every output equals the oracle, no set was given out for them, and fresh
+    launches on the null stream and on a new stream afterwards equal the oracle too (no counter left non-zero)."""
+    import ctypes
+    import threading
+    import _rx
+    L = nsx.lib()
+    hip = ctypes.CDLL("libamdhip64.so")
+    per_thread = ctypes.c_void_p(2)  # hipStreamPerThread (hip_runtime_api.h)
+    rng = np.random.default_rng(0x5A7)
+    n = 200_001
+    lens = rng.integers(0, 160, n).astype(np.uint64)  # mean < 128 B: the small-segment mode (dealt runs)
+    offs = np.zeros(n + 1, np.uint64)
+    offs[1:] = np.cumsum(lens)
+    buf = O.c_splitmix64(0x5A7, int(offs[-1]) + 3)
+    want = O.c_batch(buf, n, offsets=offs, threads=16)
+    rbuf, roffs, _ = _rx.batch(rng, 120_000, max_payload=40)  # small frames: the two-wave LDS mode (dealt runs)
+    rwant = O.c_rx_ipv4_tcp(rbuf, roffs)[0]
+    d, o, rd, ro = dev(buf), dev(offs.view(np.int64)), dev(rbuf), dev(roffs.view(np.int64))
+    nr = roffs.size - 1
+    T, K = 4, 20
+    outs = [[torch.full((n,), -1, dtype=torch.int16, device="cuda") for _ in range(K)] for _ in range(T)]
+    masks = [[torch.full(((nr + 63) // 64,), -1, dtype=torch.int64, device="cuda") for _ in range(K)] for _ in range(T)]
+    torch.cuda.synchronize()
+    used0 = nsx.deal_sets_in_use()
+    errs = []
+    go = threading.Barrier(T)
+
+    def worker(t):
+        try:
+            assert hip.hipSetDevice(0) == 0
+            go.wait()
+            for k in range(K):
+                rc = L.nsx_csum_ragged_dev(ctypes.c_void_p(d.data_ptr()), ctypes.c_void_p(o.data_ptr()), n, None,
+                                           ctypes.c_void_p(outs[t][k].data_ptr()), per_thread)
+                assert rc == 0, rc
+                rc = L.nsx_rx_ipv4_tcp_verify_dev(ctypes.c_void_p(rd.data_ptr()), ctypes.c_void_p(ro.data_ptr()), nr,
+                                                  ctypes.c_void_p(masks[t][k].data_ptr()), None, None, per_thread)
+                assert rc == 0, rc
+            assert hip.hipStreamSynchronize(per_thread) == 0
+        except BaseException as e:  # noqa: BLE001 — reported below
+            errs.append((t, e))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    torch.cuda.synchronize()
+    assert not errs, errs
+    assert nsx.deal_sets_in_use() == used0  # hipStreamPerThread took no set
+    for t in range(T):
+        for k in range(K):
+            assert np.array_equal(u16(outs[t][k]), want), (t, k)
+            assert np.array_equal(host(masks[t][k]).view(np.uint64), rwant), (t, k)
+    # afterwards: the null stream and a new stream (each with its own set) still get exact results
+    null = torch.cuda.default_stream()
+    s = torch.cuda.Stream()
+    for st in (null, s, null):
+        out = nsx.ragged_dev(d, o, out=torch.empty(n, dtype=torch.int16, device="cuda"), stream=st)
+        mask = nsx.rx_ipv4_tcp_verify_dev(rd, ro, stream=st)
+        st.synchronize()
+        assert np.array_equal(u16(out), want)
+        assert np.array_equal(host(mask).view(np.uint64), rwant)
+    # and the A/B switch: equal static shares on a stream that has a set
+    out = nsx.ragged_dev(d, o, tune=dict(deal=-1))
+    assert np.array_equal(u16(out), want)
+    assert np.array_equal(host(nsx.rx_ipv4_tcp_verify_dev(rd, ro, tune=dict(deal=-1))).view(np.uint64), rwant)
 
 
 @pytest.mark.parametrize("n", [1, 126, 252, 253, 30_001, 400_003])

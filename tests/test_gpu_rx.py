@@ -313,6 +313,74 @@ def test_rx_dealt_runs_back_to_back_and_on_many_streams():
     finally:
         torch.cuda.synchronize()
         for h in handles:
+            nsx.stream_release(h.value)  # later tests' streams get these sets again
+            hip.hipStreamDestroy(h)
+
+
+def test_rx_streamed_dealt_pieces_back_to_back_and_on_many_streams():
+    """The streamed modes deal the batch's last eighth in 16-frame pieces through each block's LDS ring: waves 0-2
+    stream, wave 3 pulls tickets from the stream's heads for the pieces they claim, and the last dealer of a head
+    resets it. IPv4 and IPv6 batches of 1 to 250k frames of full-size payloads (the streamed
+    choice), launched back to back on one stream with no sync between them — auto, forced mode 8, the static split
+    (deal -1) — interleaved with small-frame launches (mode 5, DealtRuns on the same heads), raw outputs 2 B past a
+    16 B boundary; then on 70 streams at once; every mask bit and raw sum equals the oracle."""
+    import ctypes
+    rng = np.random.default_rng(0x8C)
+    cases = []
+    for n, mp, ip in ((250_001, 1460, 4), (1, 1460, 4), (3, 1400, 6), (129, 1460, 4), (1000, 1460, 6),
+                      (70_001, 1460, 4), (64 * 700, 1440, 6), (50_000, 40, 4)):
+        kinds = _rx.KINDS6 if ip == 6 else _rx.KINDS
+        buf, offs, _ = _rx.batch(rng, n, kinds=kinds, lead=int(rng.integers(4)), max_payload=mp, ip=ip)
+        want = O.c_rx_ipv6_tcp(buf, offs) if ip == 6 else O.c_rx_ipv4_tcp(buf, offs)
+        cases.append((dev(buf), dev(offs.view(np.int64)), ip, want))
+    modes = [None, dict(segs_per_wave=8), dict(deal=-1), dict(segs_per_wave=5)]
+
+    def launch(k, tune, stream=None):
+        dbuf, doffs, ip, _ = cases[k]
+        n = doffs.numel() - 1
+        with torch.cuda.stream(stream or torch.cuda.current_stream()):
+            mask = torch.full(((n + 63) // 64,), 0x5A5A5A5A5A5A5A5A, dtype=torch.int64, device="cuda")
+            ipr = torch.empty(n + 1, dtype=torch.int16, device="cuda")[1:]
+            tcpr = torch.empty(n + 1, dtype=torch.int16, device="cuda")[1:]
+            if ip == 6:
+                nsx.rx_ipv6_tcp_verify_dev(dbuf, doffs, mask=mask, tcp_raw=tcpr, tune=tune)
+            else:
+                nsx.rx_ipv4_tcp_verify_dev(dbuf, doffs, mask=mask, ip_raw=ipr, tcp_raw=tcpr, tune=tune)
+        return k, tune, (mask, ipr, tcpr)
+
+    def check(results):
+        torch.cuda.synchronize()
+        for k, tune, (mask, ipr, tcpr) in results:
+            ip, want = cases[k][2], cases[k][3]
+            assert np.array_equal(host(mask).view(np.uint64), want[0]), ("mask", k, tune)
+            if ip == 6:
+                assert np.array_equal(u16(tcpr), want[1]), ("tcp_raw", k, tune)
+            else:
+                assert np.array_equal(u16(ipr), want[1]), ("ip_raw", k, tune)
+                assert np.array_equal(u16(tcpr), want[2]), ("tcp_raw", k, tune)
+
+    check([launch(k, modes[(r + k) % 4]) for r in range(6) for k in range(len(cases))])
+    # the mask alone (no raw outputs: the bench's call) on the default stream, back to back
+    for k in range(len(cases)):
+        dbuf, doffs, ip, want = cases[k]
+        f = nsx.rx_ipv6_tcp_verify_dev if ip == 6 else nsx.rx_ipv4_tcp_verify_dev
+        masks = [f(dbuf, doffs) for _ in range(3)]
+        for m in masks:
+            assert np.array_equal(host(m).view(np.uint64), want[0]), k
+    hip = ctypes.CDLL("libamdhip64.so")
+    handles = []
+    for _ in range(70):
+        h = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(h)) == 0
+        handles.append(h)
+    try:
+        streams = [torch.cuda.ExternalStream(h.value) for h in handles]
+        check([launch((i + r) % len(cases), modes[(i + r) % 2], streams[i]) for r in range(2)
+               for i in range(len(streams))])
+    finally:
+        torch.cuda.synchronize()
+        for h in handles:
+            nsx.stream_release(h.value)
             hip.hipStreamDestroy(h)
 
 

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
-"""Per-wave timeline of the packed-header kernel (ipv4_hdr20_kernel, workloads 7 and 9; diagnostic build only:
-make exp X=f3diag EXTRA_KFLAGS=-DNSX_F3_DIAG, whose kernel records each wave's s_memrealtime stamps at entry and
-end, its task count and where it ran, read back with nsx_diag_f3_stamps). Prints the end-time spread over the
-launch's waves, by XCD and CU, and the tail (last end − median end), in µs.
+"""Per-wave timeline of the packed-header kernel (ipv4_hdr20_kernel, workloads 7 and 9; diagnostic library only:
+`make -C network-stack_amd stamps`, whose kernels' WaveStamps hook records each wave's s_memrealtime stamps at entry
+and end, its task count and where it ran, tools/probes/wave_stamps.h, read back with nsx_diag_wave_stamps). Prints
+the end-time spread over the launch's waves, by XCD and CU, and the tail (last end − median end), in µs.
 
     python tools/probes/f3_wave_times.py [--config 7] [--launches 20]
 """
@@ -23,28 +23,28 @@ def main():
     ap.add_argument("--launches", type=int, default=20)
     a = ap.parse_args()
     import nsx
-    nsx.LIB_PATH = os.path.join(ROOT, "network-stack_amd", "lib_f3diag", "libnsx_csum.so")
+    nsx.LIB_PATH = os.path.join(ROOT, "network-stack_amd", "lib_stamps", "libnsx_csum.so")
     import torch
     import bench
     torch.cuda.set_device(0)
     cfg = dict(bench.WORKLOADS[a.config])
     w = bench.build_workload(cfg, 0, torch.device("cuda", 0))
     L = nsx.lib()
-    L.nsx_diag_f3_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
-    st = np.zeros(4096 * 4, np.uint64)
+    L.nsx_diag_wave_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+    st = np.zeros(8192 * 4, np.uint64)
     for _ in range(100):
         w["step"]()
     torch.cuda.synchronize()
     rows = []
     for _ in range(a.launches):
+        assert L.nsx_diag_wave_stamps(st.ctypes.data, st.size) == 0  # clears
         w["step"]()
         torch.cuda.synchronize()
-        assert L.nsx_diag_f3_stamps(st.ctypes.data, st.size) == 0
+        assert L.nsx_diag_wave_stamps(st.ctypes.data, st.size) == 0
         t = st.reshape(-1, 4).astype(np.int64)
-        t = t[t[:, 1] > 0]
+        t = t[t[:, 2] > 0]  # {entry, ready (0), end, tasks | where << 32}
         t0 = t[:, 0].min()
-        rows.append(((t[:, 0] - t0) / 100.0, (t[:, 1] - t0) / 100.0, t[:, 2], t[:, 3]))
-        st[:] = 0
+        rows.append(((t[:, 0] - t0) / 100.0, (t[:, 2] - t0) / 100.0, t[:, 3] & 0xFFFFFFFF, t[:, 3] >> 32))
     end = np.concatenate([r[1] for r in rows])
     print(f"waves {len(rows[0][0])}; tasks per wave p1 {np.percentile(rows[0][2], 1):.0f} p50 {np.median(rows[0][2]):.0f} "
           f"p99 {np.percentile(rows[0][2], 99):.0f}")

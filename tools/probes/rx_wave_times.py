@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Per-wave timeline of the receive pass's small-frame mode (diagnostic build only: make exp X=diag7
-EXTRA_KFLAGS=-DNSX_RX_DIAG=7, whose kernel writes each wave's s_memrealtime stamps over the tcp_raw buffer instead of
-raw sums). Loads network-stack_amd/lib_diag7, builds a bench workload, runs it many times back to back, and prints
+"""Per-wave timeline of the receive pass (diagnostic library only: `make -C network-stack_amd stamps`, whose kernels'
+WaveStamps hook records each wave's s_memrealtime stamps, tools/probes/wave_stamps.h, read back with
+nsx_diag_wave_stamps). Loads network-stack_amd/lib_stamps, builds a bench workload, runs it many times back to back,
+and prints
 the distribution of wave start (relative to the launch's first wave), range-ready and end times, in µs, and how
 the end times split over the hardware (the kernel also records each wave's HW_ID and XCC_ID): per XCD, per CU and
 within a block — with the tail each level of balancing would leave (every CU's, or every block's, waves ending at
@@ -10,6 +11,7 @@ their mean).
     python tools/probes/rx_wave_times.py [--config 13] [--launches 20]
 """
 import argparse
+import ctypes
 import os
 import sys
 
@@ -25,7 +27,8 @@ def main():
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--mode", type=int, default=5)
     ap.add_argument("--wpb", type=int, default=2, help="waves per block taking ranges (streamed modes: 4)")
-    ap.add_argument("--lib", default="diag7", help="network-stack_amd/lib_<name>: a build with NSX_RX_DIAG=7")
+    ap.add_argument("--lib", default="stamps", help="network-stack_amd/lib_<name>: a build with NSX_WAVE_STAMPS")
+    ap.add_argument("--deal", type=int, default=0, help="nsx_tune.deal (-1: equal static shares)")
     a = ap.parse_args()
     import nsx
     nsx.LIB_PATH = os.path.join(ROOT, "network-stack_amd", f"lib_{a.lib}", "libnsx_csum.so")
@@ -34,20 +37,22 @@ def main():
     torch.cuda.set_device(0)
     cfg = dict(bench.WORKLOADS[a.config])
     w = bench.build_workload(cfg, 0, torch.device("cuda", 0))
-    n = cfg["n"]
-    ts = torch.zeros(max(n, 4096 * 16), dtype=torch.int16, device="cuda")
+    L = nsx.lib()
+    L.nsx_diag_wave_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+    st = np.zeros(8192 * 4, np.uint64)
     rx = nsx.rx_ipv6_tcp_verify_dev if cfg.get("ipver") == 6 else nsx.rx_ipv4_tcp_verify_dev
-    tune = dict(segs_per_wave=a.mode)
+    tune = dict(segs_per_wave=a.mode, deal=a.deal)
     for _ in range(200):
-        rx(w["buf"], w["d_offs"], mask=w["out"], tcp_raw=ts, tune=tune)
+        rx(w["buf"], w["d_offs"], mask=w["out"], tune=tune)
     torch.cuda.synchronize()
     rows = []
     for _ in range(a.launches):
-        ts.zero_()
+        assert L.nsx_diag_wave_stamps(st.ctypes.data, st.size) == 0  # clears
         for _ in range(3):
-            rx(w["buf"], w["d_offs"], mask=w["out"], tcp_raw=ts, tune=tune)
+            rx(w["buf"], w["d_offs"], mask=w["out"], tune=tune)
         torch.cuda.synchronize()
-        t = ts.view(torch.int64).cpu().numpy().view(np.uint64)
+        assert L.nsx_diag_wave_stamps(st.ctypes.data, st.size) == 0
+        t = st
         nw = int(np.count_nonzero(t[2::4]))
         t = t[: nw * 4].reshape(nw, 4).astype(np.int64)
         t0 = t[:, 0].min()
