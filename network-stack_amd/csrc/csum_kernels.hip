@@ -213,6 +213,140 @@ constexpr int kWaitVm0 = 0x0F70;
 // Cache-policy operand of a buffer store on gfx950: sc1 (bit 4) = write-through, the line leaves the XCD's L2.
 constexpr int kStoreSc1 = 16;
 
+// Wave w of this block's wpb in a grid of nb blocks, numbered XCD by XCD (blocks b, b + 8, ... run on one XCD).
+__device__ __forceinline__ uint32_t wave_number(uint32_t nb, uint32_t wpb, uint32_t w) {
+    const uint32_t b = blockIdx.x;
+    return (nb >= 16 && (nb & 7) == 0) ? ((b & 7) * (nb >> 3) + (b >> 3)) * wpb + w : b * wpb + w;
+}
+
+// Per-wave timing stamps, the one diagnostic hook in the product kernels (the fixed-stride, receive-pass and
+// packed-header kernels): entry(), ready() once the wave's range is known, done(wave number, work) at its end. The product build's
+// WaveStamps records nothing and every call compiles away (the code object is byte-identical to one without the
+// calls). `make stamps` builds lib_stamps/ with the recording policy of tools/probes/wave_stamps.h instead, read back
+// by tools/probes/rx_wave_times.py and f3_wave_times.py.
+#ifdef NSX_WAVE_STAMPS
+#include "../../tools/probes/wave_stamps.h"
+#else
+struct WaveStamps {
+    __device__ __forceinline__ void entry() {}
+    __device__ __forceinline__ void ready() {}
+    __device__ __forceinline__ void done(uint32_t g, uint64_t work, uint32_t lane) {}
+};
+#endif
+
+// The deal's shape: the pool is a batch's last 1/2^kDealPoolShift, dealt from kDealHeads counters, each on its own
+// 64 B line (kDealStride dwords); kDealSlots streams per device hold a set of heads at once (deal_heads).
+#ifndef NSX_DEAL_POOL_SHIFT
+#define NSX_DEAL_POOL_SHIFT 3
+#endif
+constexpr uint32_t kDealPoolShift = NSX_DEAL_POOL_SHIFT;
+#ifndef NSX_DEAL_HEADS
+#define NSX_DEAL_HEADS 32
+#endif
+constexpr uint32_t kDealHeads = NSX_DEAL_HEADS;
+constexpr uint32_t kDealStride = 16;
+constexpr uint32_t kDealSlots = 64;
+
+// ---- Work dealt through a block's LDS ring (round 6) ----
+// A batch's last units are dealt to the waves as they finish, without any streaming wave waiting on a ticket's round
+// trip: one dealer wave per block pulls tickets (device-scope atomics on the stream's heads, 1-3 µs each) for the
+// entries its block's streaming waves have claimed and posts them in an LDS ring; a streaming wave claims entries
+// ahead (an LDS atomic) and reads them from LDS when it gets there. vmcnt retires in issue order, so a ticket pulled
+// by a streaming wave itself would hold up every load issued after it (§7 step 72). The receive pass's streamed
+// modes (rx_runs_ring) and the fixed-stride kernel (csum_fixed_swp_kernel<·, ·, true>) use it.
+constexpr uint32_t kPieceRing = 64;        // ring entries per block
+constexpr uint32_t kPieceFree = ~0u;       // an entry read by its consumer (or never written)
+
+struct PieceRing {
+    uint32_t claim;     // entries claimed by the streaming waves (LDS atomic add)
+    uint32_t produced;  // entries the dealer has written, in order
+    uint32_t end_at;    // the dealer's final entry count once its head's share ran out (~0 until then)
+    uint32_t pad;
+    uint32_t e[kPieceRing];  // entry p at e[p % kPieceRing]: a piece's first frame; kPieceFree once read
+};
+
+// A streaming wave's side of the block's ring: claim an entry (an LDS atomic), read a claimed entry (waiting for the
+// dealer only if it has not posted it yet; `end` past the share) and free its slot for the dealer.
+struct RingClient {
+    PieceRing* rg;
+    uint32_t lane;
+    __device__ __forceinline__ uint32_t claim() const {
+        uint32_t v = 0u;
+        if (lane == 0u) v = __hip_atomic_fetch_add(&rg->claim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return __builtin_amdgcn_readfirstlane(v);
+    }
+    __device__ __forceinline__ uint32_t read(uint32_t idx, uint32_t end) const {  // entry idx's value, or end
+        for (;;) {
+            const uint32_t p = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(&rg->produced, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+            if (idx < p) {
+                uint32_t* slot = &rg->e[idx % kPieceRing];
+                const uint32_t v = __builtin_amdgcn_readfirstlane(
+                    __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+                if (lane == 0u) __hip_atomic_store(slot, kPieceFree, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                return v;
+            }
+            const uint32_t e = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(&rg->end_at, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+            if (idx >= e) return end;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+};
+
+// The dealer wave of a block: for every entry its streaming waves claim, a ticket t from the block's head (at most
+// 4 pulls in flight), posted to the ring as the piece's first unit pb + t·unit; past the head's share it posts the end. The head's dword 0 is the ticket
+// counter (shared with DealtRuns, which leaves it at 0), dword 1 counts the head's dealers that have finished: the
+// last one to finish resets both to 0 for the stream's next launch (a dealer may pull up to 4 tickets past the
+// share, so the pull count cannot mark the last pull as in DealtRuns).
+__device__ __forceinline__ void ring_dealer(PieceRing* rg, uint32_t* head, uint32_t pb, uint32_t unit, uint32_t qh,
+                                            uint32_t dealers, uint32_t lane) {
+    uint32_t p = 0u;
+    bool live = true;
+    while (live) {
+        const uint32_t c = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(&rg->claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        const uint32_t k = min(c - p, 4u);
+        if (k == 0u) {
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+        uint32_t t[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (uint32_t j = 0; j < 4u; ++j)
+            if (j < k && lane == 0u) t[j] = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (uint32_t j = 0; j < 4u; ++j) {
+            const uint32_t tj = __builtin_amdgcn_readfirstlane(t[j]);
+            if (j < k) {
+                if (tj < qh) {
+                    uint32_t* slot = &rg->e[p % kPieceRing];
+                    // the entry's previous use must have been read (its consumer frees it): rarely waits
+                    while ((uint32_t)__builtin_amdgcn_readfirstlane(
+                               __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != kPieceFree)
+                        __builtin_amdgcn_s_sleep(1);
+                    if (lane == 0u)
+                        __hip_atomic_store(slot, pb + tj * unit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    ++p;
+                } else {
+                    live = false;
+                }
+            }
+        }
+        if (lane == 0u) __hip_atomic_store(&rg->produced, p, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (lane == 0u) {
+        __hip_atomic_store(&rg->end_at, p, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint32_t done = __hip_atomic_fetch_add(head + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (done + 1u == dealers) {
+            __hip_atomic_store(head, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(head + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint64_t bytes) {
     // Wave-uniform inputs only, so no waterfall loop (guide T20); clamp without a
     // 64-bit unsigned compare (SALU has none: hipcc would borrow VGPRs for it).
@@ -343,14 +477,47 @@ __global__ __launch_bounds__(kBlock) void csum_fixed_buf_kernel(
 // pipelined: two register sets of one task each (U segments × NROWS rows); the next task's loads are issued
 // before the current task is reduced, so a wave keeps its loads in flight through its own reduce/park/flush
 // phases instead of leaving them to other waves.
-template <int U, int NROWS>
-__global__ __launch_bounds__(kBlock) void csum_fixed_swp_kernel(
+//
+// DEAL (round 6): the batch's last 1/2^kDealPoolShift of the tasks are not split statically
+// but dealt through the block's LDS ring (ring_dealer) to the four streaming waves as they finish: a fifth wave per
+// block pulls the tickets from the stream's heads. With equal static shares the launch waited ~12 µs (5%) for its
+// last waves — the XCDs and CUs run at different speeds (tools/probes/f3_wave_times.py --config 2,
+// profiles/r06_fixed_wave_times_c2.txt). A dealt task's 8 results are finished with their own partials and stored
+// at once (16 B).
+template <int U, int NROWS, bool DEAL = false>
+__global__ __launch_bounds__(DEAL ? kBlock + kWave : kBlock) void csum_fixed_swp_kernel(
     const uint8_t* __restrict__ base, uint64_t stride, uint32_t seg_len, uint32_t n,
-    const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, uint32_t chunk_log2) {
+    const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, uint32_t chunk_log2,
+    uint32_t* __restrict__ deal) {
     constexpr uint32_t G = kWave / U;
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const uint32_t ntasks = (n + U - 1) / U;
+    WaveStamps ws;
+    ws.entry();
+    uint32_t ntk = 0;  // tasks done (for the stamps)
+    const uint32_t all_tasks = (n + U - 1) / U;
+    uint32_t ntasks = all_tasks;  // the statically split tasks [0, ntasks)
+    [[maybe_unused]] RingClient rc{nullptr, lane};
+    [[maybe_unused]] uint32_t claim0 = 0, claim1 = 0;
+    if constexpr (DEAL) {
+        __shared__ PieceRing ring;
+        ntasks = all_tasks - (all_tasks >> kDealPoolShift);
+        if (wave == kWavesPerBlock) {
+            if (lane < kPieceRing) ring.e[lane] = kPieceFree;
+            if (lane == 0u) ring.claim = 0u, ring.produced = 0u, ring.end_at = ~0u;
+        }
+        __syncthreads();
+        if (wave == kWavesPerBlock) {  // the dealer: head h (blocks numbered XCD by XCD), its share of the pool
+            const uint32_t nb = gridDim.x, H = min(kDealHeads, nb), h = wave_number(nb, 1u, 0u) % H;
+            const uint32_t Q = all_tasks - ntasks;
+            const uint32_t r0 = (uint32_t)((uint64_t)Q * h / H), qh = (uint32_t)((uint64_t)Q * (h + 1u) / H) - r0;
+            ring_dealer(&ring, deal + h * kDealStride, ntasks + r0, 1u, qh, (nb - h + H - 1u) / H, lane);
+            return;
+        }
+        rc.rg = &ring;
+        claim0 = rc.claim();  // two pool entries claimed ahead from the start: posted by the time they are needed
+        claim1 = rc.claim();
+    }
     TaskIter it = task_iter(ntasks, wave);
     const ChunkDeal cd = chunk_deal(it, wave, chunk_log2, ntasks);
     const uint32_t end = (uint32_t)it.end, step = (uint32_t)it.step;
@@ -393,6 +560,7 @@ __global__ __launch_bounds__(kBlock) void csum_fixed_swp_kernel(
             const uint32_t tot = wave_sum(fold32(acc));
             res = lane == k * U + u ? tot : res;
         }
+        ++ntk;
         if (++k == G) {
             res = finish(res, true, gpart);
             fixed_flush<U>(res, first, step, k, n, ors, lane, cd);
@@ -418,6 +586,64 @@ __global__ __launch_bounds__(kBlock) void csum_fixed_swp_kernel(
         res = finish(res, true, gpart);
         fixed_flush<U>(res, first, step, k, n, ors, lane, cd);
     }
+    if constexpr (DEAL) {
+        // The pool: tasks read from the ring (each claimed two tasks ahead), software-pipelined like the static
+        // loop; a task's partials load with its rows, its results are finished and stored when it is summed.
+        struct PSet {
+            u32x4 v[U][NROWS];
+            uint32_t t, part;
+        };
+        auto take = [&]() {
+            const uint32_t t = rc.read(claim0, all_tasks);
+            claim0 = claim1;
+            if (t < all_tasks) claim1 = rc.claim();
+            return t;
+        };
+        auto pissue = [&](uint32_t t, PSet& S) {
+            S.t = t;
+            const bool ok = t < all_tasks;
+            const uint32_t s0 = (ok ? t : 0u) * U;
+            const uint8_t* p = base + (uint64_t)s0 * stride;
+#pragma unroll
+            for (int u = 0; u < U; ++u, p += stride) {
+                const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+                    const_cast<uint8_t*>(p), 0, (ok && s0 + u < n) ? (int)seg_len : 0, 0x00020000);
+#pragma unroll
+                for (int rr = 0; rr < NROWS; ++rr) S.v[u][rr] = bld16<true>(r, rr * kRow + lane * 16);
+            }
+            S.part = __builtin_amdgcn_raw_buffer_load_b32(prs, ok && lane < (uint32_t)U && s0 + lane < n ? (s0 + lane) * 4
+                                                                                                          : kOOB, 0, 0);
+        };
+        auto pconsume = [&](PSet& S) {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int rr = 0; rr < NROWS; ++rr) asm volatile("" : "+v"(S.v[u][rr]));
+            uint32_t r = 0;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                uint32_t acc = 0;
+#pragma unroll
+                for (int rr = 0; rr < NROWS; ++rr) acc = sad4(S.v[u][rr], acc);
+                const uint32_t tot = wave_sum(fold32(acc));
+                r = lane == (uint32_t)u ? tot : r;
+            }
+            r = finish(r, true, S.part);
+            const uint32_t seg = S.t * U + lane;
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)r, ors, lane < (uint32_t)U && seg < n ? seg * 2 : kOOB, 0, 0);
+            ++ntk;
+        };
+        PSet P0, P1;
+        pissue(take(), P0);
+        while (P0.t < all_tasks) {
+            pissue(take(), P1);
+            pconsume(P0);
+            if (P1.t >= all_tasks) break;
+            pissue(take(), P0);
+            pconsume(P1);
+        }
+    }
+    ws.done(blockIdx.x * kWavesPerBlock + wave, ntk, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -1104,18 +1330,6 @@ struct DealtRuns {
     __device__ __forceinline__ uint32_t cnt(uint32_t a) const { return min(kSeqRun, (a < e_st ? e_st : n) - a); }
 };
 
-// The deal's shape: the pool is a batch's last 1/2^kDealPoolShift, dealt from kDealHeads counters, each on its own
-// 64 B line (kDealStride dwords); kDealSlots streams per device hold a set of heads at once (deal_heads).
-#ifndef NSX_DEAL_POOL_SHIFT
-#define NSX_DEAL_POOL_SHIFT 3
-#endif
-constexpr uint32_t kDealPoolShift = NSX_DEAL_POOL_SHIFT;
-#ifndef NSX_DEAL_HEADS
-#define NSX_DEAL_HEADS 32
-#endif
-constexpr uint32_t kDealHeads = NSX_DEAL_HEADS;
-constexpr uint32_t kDealStride = 16;
-constexpr uint32_t kDealSlots = 64;
 
 // Wave g of W's runs: with heads for this launch (deal), its equal share (wave_range: small_mean, align,
 // count_align) of the batch's first n − n/2^kDealPoolShift units (S, a multiple of kSeqRun), then runs of the pool
@@ -1871,50 +2085,29 @@ __device__ __forceinline__ void rx_runs(const uint8_t* __restrict__ base, __amdg
 // pieces its waves have claimed and posts them in an LDS ring; a streaming wave claims its next piece one unit ahead
 // (an LDS atomic) and reads it from the ring when it moves on, so no vector-memory wait of a streaming wave ever
 // covers a ticket (vmcnt retires in issue order: loads issued behind an atomic wait for it too, §7 step 72).
-constexpr uint32_t kStreamPiece = 16;      // frames per dealt piece (a multiple of 8: whole mask bytes)
-constexpr uint32_t kStreamPoolShift = 3;   // the pool: the batch's last eighth of frames
-constexpr uint32_t kPieceRing = 64;        // ring entries per block
-constexpr uint32_t kPieceFree = ~0u;       // an entry read by its consumer (or never written)
+#ifndef NSX_STREAM_PIECE
+#define NSX_STREAM_PIECE 16
+#endif
+#ifndef NSX_STREAM_POOL_SHIFT
+#define NSX_STREAM_POOL_SHIFT 3
+#endif
+constexpr uint32_t kStreamPiece = NSX_STREAM_PIECE;          // frames per dealt piece (a multiple of 8: whole mask bytes)
+constexpr uint32_t kStreamPoolShift = NSX_STREAM_POOL_SHIFT;  // the pool: the batch's last eighth of frames
 constexpr uint32_t kStreamWaves = 3;       // streaming waves per block (wave 3 deals)
-
-struct PieceRing {
-    uint32_t claim;     // entries claimed by the streaming waves (LDS atomic add)
-    uint32_t produced;  // entries the dealer has written, in order
-    uint32_t end_at;    // the dealer's final entry count once its head's share ran out (~0 until then)
-    uint32_t pad;
-    uint32_t e[kPieceRing];  // entry p at e[p % kPieceRing]: a piece's first frame; kPieceFree once read
-};
+#ifndef NSX_STREAM_ROTATE
+#define NSX_STREAM_ROTATE 0
+#endif
+constexpr bool kStreamRotate = NSX_STREAM_ROTATE;
 
 // A streaming wave's units: its static runs [a0, e_st) of kRxRun frames, then dealt pieces until the share ends
 // (n). The entry for the unit after next is claimed when next() hands out a unit whose successor is a piece, and
-// read (waiting for the dealer only if it has not posted it yet) when next() moves on to it.
+// read when next() moves on to it.
 struct RingRuns {
     uint32_t a0, e_st, n;
-    PieceRing* rg;
-    uint32_t lane;
+    RingClient rc;
     uint32_t pend;  // the claimed entry not yet read (kPieceFree: none)
-    __device__ __forceinline__ uint32_t claim() const {
-        uint32_t v = 0u;
-        if (lane == 0u) v = __hip_atomic_fetch_add(&rg->claim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        return __builtin_amdgcn_readfirstlane(v);
-    }
-    __device__ __forceinline__ uint32_t read(uint32_t idx) const {  // entry idx: a piece's first frame, or n
-        for (;;) {
-            const uint32_t p = __builtin_amdgcn_readfirstlane(
-                __hip_atomic_load(&rg->produced, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
-            if (idx < p) {
-                uint32_t* slot = &rg->e[idx % kPieceRing];
-                const uint32_t v = __builtin_amdgcn_readfirstlane(
-                    __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-                if (lane == 0u) __hip_atomic_store(slot, kPieceFree, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                return v;
-            }
-            const uint32_t e = __builtin_amdgcn_readfirstlane(
-                __hip_atomic_load(&rg->end_at, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
-            if (idx >= e) return n;
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
+    __device__ __forceinline__ uint32_t claim() const { return rc.claim(); }
+    __device__ __forceinline__ uint32_t read(uint32_t idx) const { return rc.read(idx, n); }
     // after handing out unit r: is its successor a piece? then claim that piece's entry now
     __device__ __forceinline__ uint32_t ahead(uint32_t r) {
         if (r < n && (r >= e_st || r + kRxRun >= e_st)) pend = claim();
@@ -1938,57 +2131,6 @@ struct RingRuns {
         return a < e_st ? min(kRxRun, e_st - a) : min(kStreamPiece, n - a);
     }
 };
-
-// The dealer wave of a block: for every entry its streaming waves claim, a ticket from the block's head (at most 4
-// pulls in flight), posted to the ring; past the head's share it posts the end. The head's dword 0 is the ticket
-// counter (shared with DealtRuns, which leaves it at 0), dword 1 counts the head's dealers that have finished: the
-// last one to finish resets both to 0 for the stream's next launch (a dealer may pull up to 4 tickets past the
-// share, so the pull count cannot mark the last pull as in DealtRuns).
-__device__ __forceinline__ void stream_dealer(PieceRing* rg, uint32_t* head, uint32_t pb, uint32_t qh, uint32_t dealers,
-                                              uint32_t lane) {
-    uint32_t p = 0u;
-    bool live = true;
-    while (live) {
-        const uint32_t c = __builtin_amdgcn_readfirstlane(
-            __hip_atomic_load(&rg->claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-        const uint32_t k = min(c - p, 4u);
-        if (k == 0u) {
-            __builtin_amdgcn_s_sleep(2);
-            continue;
-        }
-        uint32_t t[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-        for (uint32_t j = 0; j < 4u; ++j)
-            if (j < k && lane == 0u) t[j] = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-        for (uint32_t j = 0; j < 4u; ++j) {
-            const uint32_t tj = __builtin_amdgcn_readfirstlane(t[j]);
-            if (j < k) {
-                if (tj < qh) {
-                    uint32_t* slot = &rg->e[p % kPieceRing];
-                    // the entry's previous use must have been read (its consumer frees it): rarely waits
-                    while ((uint32_t)__builtin_amdgcn_readfirstlane(
-                               __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != kPieceFree)
-                        __builtin_amdgcn_s_sleep(1);
-                    if (lane == 0u)
-                        __hip_atomic_store(slot, pb + tj * kStreamPiece, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    ++p;
-                } else {
-                    live = false;
-                }
-            }
-        }
-        if (lane == 0u) __hip_atomic_store(&rg->produced, p, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    if (lane == 0u) {
-        __hip_atomic_store(&rg->end_at, p, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const uint32_t done = __hip_atomic_fetch_add(head + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (done + 1u == dealers) {
-            __hip_atomic_store(head, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(head + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-}
 
 // A streaming wave's units (RingRuns) in the streaming form, the offsets of the next unit loaded one unit ahead.
 template <int R, bool V6>
@@ -2332,27 +2474,6 @@ constexpr uint32_t kRxStreamBigN = 5u << 19;       // 2.5M frames
 // WPS: waves per SIMD the registers must allow (__launch_bounds__'s second argument): 1 = no constraint (158 VGPRs,
 // 3 waves per SIMD at the default 3 blocks/CU); 4 = the 4-blocks/CU instantiations (≤ 128 VGPRs).
 
-// Wave w of this block's wpb in a grid of nb blocks, numbered XCD by XCD (blocks b, b + 8, ... run on one XCD).
-__device__ __forceinline__ uint32_t wave_number(uint32_t nb, uint32_t wpb, uint32_t w) {
-    const uint32_t b = blockIdx.x;
-    return (nb >= 16 && (nb & 7) == 0) ? ((b & 7) * (nb >> 3) + (b >> 3)) * wpb + w : b * wpb + w;
-}
-
-// Per-wave timing stamps, the one diagnostic hook in the product kernels (the receive pass and the packed-header
-// kernel): entry(), ready() once the wave's range is known, done(wave number, work) at its end. The product build's
-// WaveStamps records nothing and every call compiles away (the code object is byte-identical to one without the
-// calls). `make stamps` builds lib_stamps/ with the recording policy of tools/probes/wave_stamps.h instead, read back
-// by tools/probes/rx_wave_times.py and f3_wave_times.py.
-#ifdef NSX_WAVE_STAMPS
-#include "../../tools/probes/wave_stamps.h"
-#else
-struct WaveStamps {
-    __device__ __forceinline__ void entry() {}
-    __device__ __forceinline__ void ready() {}
-    __device__ __forceinline__ void done(uint32_t g, uint64_t work, uint32_t lane) {}
-};
-#endif
-
 template <int R, bool V6, int WPS, int PF = 0>
 __global__ __launch_bounds__(kBlock, WPS) void rx_tcp_kernel(const uint8_t* __restrict__ base,
                                                              const uint64_t* __restrict__ offsets, uint32_t n,
@@ -2411,25 +2532,28 @@ __global__ __launch_bounds__(kBlock, WPS) void rx_tcp_kernel(const uint8_t* __re
         } else if (deal && (sets == 0 || sets == 8)) {
             // Streamed runs with the batch's last eighth dealt in pieces through the block's LDS ring (the auto
             // choice and mode 8 when the stream has heads; §7 step 75): waves 0-2 of every block stream, wave 3 deals.
-            PieceRing* rg = reinterpret_cast<PieceRing*>(lds_rx + kStreamWaves * (PfxSlot<7>::kBytes / 16u));
-            static_assert(sizeof(PieceRing) <= PfxSlot<7>::kBytes && kPieceRing <= kWave, "the ring in wave 3's slot");
-            if (wave == kStreamWaves) {
+            // the dealer: wave 3, or (NSX_STREAM_ROTATE builds) the wave of the block's slot on its CU, so that the 4
+            // blocks of a CU put their dealers on different SIMDs
+            const uint32_t dw = kStreamRotate ? (uint32_t)((uint64_t)blockIdx.x * kWavesPerBlock / gridDim.x) : kStreamWaves;
+            PieceRing* rg = reinterpret_cast<PieceRing*>(lds_rx + dw * (PfxSlot<7>::kBytes / 16u));
+            static_assert(sizeof(PieceRing) <= PfxSlot<7>::kBytes && kPieceRing <= kWave, "the ring in the dealer's slot");
+            if (wave == dw) {
                 if (lane < kPieceRing) rg->e[lane] = kPieceFree;
                 if (lane == 0u) rg->claim = 0u, rg->produced = 0u, rg->end_at = ~0u;
             }
             __syncthreads();
             const uint32_t nb = gridDim.x;
             const uint32_t S = (n - (n >> kStreamPoolShift)) & ~(kRxRun - 1u);  // the static shares: frames [0, S)
-            if (wave == kStreamWaves) {
+            if (wave == dw) {
                 // head h of the block (numbered XCD by XCD, so every head has blocks on all 8 XCDs), its share of the
                 // pool's pieces and its dealers
                 const uint32_t H = min(kDealHeads, nb), h = wave_number(nb, 1u, 0u) % H;
                 const uint32_t Q = (n - S + kStreamPiece - 1u) / kStreamPiece;
                 const uint32_t r0 = (uint32_t)((uint64_t)Q * h / H), qh = (uint32_t)((uint64_t)Q * (h + 1u) / H) - r0;
-                stream_dealer(rg, deal + h * kDealStride, S + r0 * kStreamPiece, qh, (nb - h + H - 1u) / H, lane);
+                ring_dealer(rg, deal + h * kDealStride, S + r0 * kStreamPiece, kStreamPiece, qh, (nb - h + H - 1u) / H, lane);
                 return;
             }
-            const uint32_t g = wave_number(nb, kStreamWaves, wave);
+            const uint32_t g = wave_number(nb, kStreamWaves, wave < dw ? wave : wave - 1u);
             WaveRange wr{0u, 0u, 0u};
             if (S > 0u) wr = wave_range(ofs, S, g, nb * kStreamWaves, lane, kRxSmallFrame, 8u);
             RxOuts rp = ro;
@@ -2439,7 +2563,7 @@ __global__ __launch_bounds__(kBlock, WPS) void rx_tcp_kernel(const uint8_t* __re
                 if constexpr (!V6) rp.ipk = make_park<uint16_t>(pb + 2048, ro.irs, ip_raw, wr.a0, 2048u);
             }
             ws.ready();
-            RingRuns q{wr.a0, wr.a_end, n, rg, lane, kPieceFree};
+            RingRuns q{wr.a0, wr.a_end, n, RingClient{rg, lane}, kPieceFree};
             rx_runs_ring<R, V6>(base, ofs, n, q, lane, rp);
             if (ro.raw) {
                 park_flush(rp.tpk, lane);
@@ -3575,6 +3699,8 @@ uint64_t fixed_launch_count(const LaunchCfg& c, uintptr_t /*base*/, uint64_t str
 }
 
 // One launch of the short-segment fixed path: U segments per wave task, NR rows per segment.
+static uint32_t* deal_heads(const LaunchCfg& c, hipStream_t st);  // below: the stream's work-deal counters
+
 static hipError_t launch_fixed_short(const LaunchCfg& c, const uint8_t* base, uint64_t stride, uint32_t seg_len,
                                      uint64_t n, const uint32_t* partial, uint16_t* out, int nrows, bool aligned,
                                      hipStream_t st) {
@@ -3587,11 +3713,25 @@ static hipError_t launch_fixed_short(const LaunchCfg& c, const uint8_t* base, ui
     const uint64_t ntasks = (n + u - 1) / u;
     const uint32_t grid = grid_for(ntasks, max_blocks_of(c, aligned ? 1 : 2));
     const uint32_t clog = deal_clog(c.xcd_chunk, ntasks, (uint64_t)u * stride);
+    // The default aligned shapes deal their last tasks through each block's ring (a fifth, dealer wave per block;
+    // §7 step 77) when the stream has heads and the batch has at least 64 tasks per block.
+    if (aligned && c.segs_per_wave == 0 && ntasks >= 64ull * grid) {
+        if (uint32_t* deal = deal_heads(c, st)) {
+#define NSX_FIXED_DEAL(U_, NR_)                                                                                  \
+    if (u == U_ && nrows == NR_) {                                                                               \
+        hipLaunchKernelGGL((csum_fixed_swp_kernel<U_, NR_, true>), dim3(grid), dim3(kBlock + kWave), 0, st, base, \
+                           stride, seg_len, (uint32_t)n, partial, out, clog, deal);                              \
+        return hipGetLastError();                                                                                \
+    }
+            NSX_FIXED_DEAL(8, 1) NSX_FIXED_DEAL(8, 2) NSX_FIXED_DEAL(4, 4)
+#undef NSX_FIXED_DEAL
+        }
+    }
 #define NSX_FIXED(U_, NR_)                                                                                    \
     if (u == U_ && nrows == NR_) {                                                                             \
         if (aligned)                                                                                           \
             hipLaunchKernelGGL((csum_fixed_swp_kernel<U_, NR_>), dim3(grid), dim3(kBlock), 0, st, base, stride, \
-                               seg_len, (uint32_t)n, partial, out, clog);                                      \
+                               seg_len, (uint32_t)n, partial, out, clog, nullptr);                             \
         else                                                                                                   \
             hipLaunchKernelGGL((csum_fixed_buf_kernel<U_, NR_>), dim3(grid), dim3(kBlock), 0, st, base, stride, \
                                seg_len, (uint32_t)n, partial, out, clog);                                      \

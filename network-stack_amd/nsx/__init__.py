@@ -111,7 +111,11 @@ def lib() -> ctypes.CDLL:
             "nsx_fixed_launch_count": [u64, u32, u64, vp, ctypes.POINTER(u64)],
             "nsx_ipv4_hdr_launch_count": [vp, u64, u32, u64, vp, ctypes.POINTER(u64)],
         }
+        # present since ABI round 6; an older library (same-box A/B against a previous build) lacks them
+        optional = {"nsx_stream_release", "nsx_deal_sets_in_use"}
         for name, args in sig.items():
+            if name in optional and not hasattr(L, name):
+                continue
             f = getattr(L, name)
             f.argtypes = args
             f.restype = ctypes.c_int

@@ -146,6 +146,60 @@ def test_ragged_small_segment_bench_workload_full_size():
     assert np.array_equal(u16(out), want_p)
 
 
+def test_fixed_dealt_tasks_back_to_back_and_on_many_streams():
+    """The aligned fixed-stride kernel deals its last eighth of tasks through each block's LDS ring (a fifth, dealer
+    wave per block pulling from the stream's heads): the three default shapes (8 segments × 1
+    row, 8 × 2, 4 × 4), batch sizes from just over the dealing threshold (64 tasks per block) to 1M segments, with
+    and without partials, outputs 2 B past a 16 B boundary, launched back to back on one stream with no sync between
+    them — interleaved with the static split (deal -1) and with receive-pass launches that deal from the same heads —
+    then on 70 streams at once; every raw sum equals the oracle."""
+    import ctypes
+    import _rx
+    rng = np.random.default_rng(0x8D)
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    cases = []
+    for L, n in ((1500, 1 << 20), (1500, 64 * 8 * cus + 7), (1000, 300_001), (3000, 200_003), (1500, 64 * 8 * cus - 8),
+                 (3996, 150_001)):
+        buf = O.c_splitmix64(0x8D + n + L, n * L + 4)
+        part = rng.integers(0, 1 << 31, n, dtype=np.uint32)
+        cases.append((dev(buf), L, n, dev(part.view(np.int32)), O.c_batch(buf, n, stride=L, seg_len=L, threads=16),
+                      O.c_batch(buf, n, stride=L, seg_len=L, partial=part, threads=16)))
+    rbuf, roffs, _ = _rx.batch(rng, 20_000, max_payload=1460)
+    rx = (dev(rbuf), dev(roffs.view(np.int64)), O.c_rx_ipv4_tcp(rbuf, roffs)[0])
+
+    def launch(k, tune=None, stream=None):
+        d, L, n, p, _, _ = cases[k % len(cases)]
+        with torch.cuda.stream(stream or torch.cuda.current_stream()):
+            out = torch.empty(n + 1, dtype=torch.int16, device="cuda")[1:]
+            nsx.fixed_dev(d, L, L, n, partial=p if k & 1 else None, out=out, tune=tune)
+            mask = nsx.rx_ipv4_tcp_verify_dev(rx[0], rx[1])
+        return k, out, mask
+
+    def check(results):
+        torch.cuda.synchronize()
+        for k, out, mask in results:
+            c = cases[k % len(cases)]
+            assert np.array_equal(u16(out), c[5] if k & 1 else c[4]), k
+            assert np.array_equal(host(mask).view(np.uint64), rx[2]), k
+
+    check([launch(k, dict(deal=-1) if r == 1 else None) for r in range(3) for k in range(2 * len(cases))])
+    torch.cuda.synchronize()
+    hip = ctypes.CDLL("libamdhip64.so")
+    handles = []
+    for _ in range(70):
+        h = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(h)) == 0
+        handles.append(h)
+    try:
+        streams = [torch.cuda.ExternalStream(h.value) for h in handles]
+        check([launch(i + r, None, streams[i]) for r in range(2) for i in range(len(streams))])
+    finally:
+        torch.cuda.synchronize()
+        for h in handles:
+            nsx.stream_release(h.value)
+            hip.hipStreamDestroy(h)
+
+
 def test_ragged_dealt_runs_back_to_back_and_on_many_streams():
     """The small-segment mode deals each launch's last runs from the stream's counters, shared with the receive pass
     and left at zero by every launch: checksum and batch-verify launches of 3 to 300k

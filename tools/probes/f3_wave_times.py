@@ -1,5 +1,7 @@
 #!/usr/bin/env python3
-"""Per-wave timeline of the packed-header kernel (ipv4_hdr20_kernel, workloads 7 and 9; diagnostic library only:
+"""Per-wave timeline of a stamped kernel (diagnostic library only) under one bench workload's step: the packed-header
+kernel (ipv4_hdr20_kernel, workloads 7 and 9) or the fixed-stride kernel (csum_fixed_swp_kernel, configs 2 and 5; the
+same stamps, work = tasks of 8 segments). Diagnostic library:
 `make -C network-stack_amd stamps`, whose kernels' WaveStamps hook records each wave's s_memrealtime stamps at entry
 and end, its task count and where it ran, tools/probes/wave_stamps.h, read back with nsx_diag_wave_stamps). Prints
 the end-time spread over the launch's waves, by XCD and CU, and the tail (last end − median end), in µs.
