@@ -300,39 +300,31 @@ struct RingClient {
 // last one to finish resets both to 0 for the stream's next launch (a dealer may pull up to 4 tickets past the
 // share, so the pull count cannot mark the last pull as in DealtRuns).
 __device__ __forceinline__ void ring_dealer(PieceRing* rg, uint32_t* head, uint32_t pb, uint32_t unit, uint32_t qh,
-                                            uint32_t dealers, uint32_t lane) {
+                                            uint32_t dealers, uint32_t ahead, uint32_t lane) {
     uint32_t p = 0u;
     bool live = true;
     while (live) {
+        // entries to post: every claimed one, plus `ahead` more, up to 16 per round trip
         const uint32_t c = __builtin_amdgcn_readfirstlane(
             __hip_atomic_load(&rg->claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-        const uint32_t k = min(c - p, 4u);
-        if (k == 0u) {
+        const uint32_t k = min(c + ahead - p, 16u);
+        if (k == 0u || (int32_t)(c + ahead - p) <= 0) {
             __builtin_amdgcn_s_sleep(2);
             continue;
         }
-        uint32_t t[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-        for (uint32_t j = 0; j < 4u; ++j)
-            if (j < k && lane == 0u) t[j] = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-        for (uint32_t j = 0; j < 4u; ++j) {
-            const uint32_t tj = __builtin_amdgcn_readfirstlane(t[j]);
-            if (j < k) {
-                if (tj < qh) {
-                    uint32_t* slot = &rg->e[p % kPieceRing];
-                    // the entry's previous use must have been read (its consumer frees it): rarely waits
-                    while ((uint32_t)__builtin_amdgcn_readfirstlane(
-                               __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != kPieceFree)
-                        __builtin_amdgcn_s_sleep(1);
-                    if (lane == 0u)
-                        __hip_atomic_store(slot, pb + tj * unit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    ++p;
-                } else {
-                    live = false;
-                }
-            }
-        }
+        // k tickets in one pull: base .. base + k − 1, of which those below qh are the head's share
+        uint32_t t = 0u;
+        if (lane == 0u) t = __hip_atomic_fetch_add(head, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t base = __builtin_amdgcn_readfirstlane(t);
+        const uint32_t v = base < qh ? min(k, qh - base) : 0u;
+        // lane j < v posts entry p + j; its slot's previous entry must have been read (rarely waits)
+        uint32_t* slot = &rg->e[(p + lane) % kPieceRing];
+        while (__builtin_amdgcn_ballot_w64(lane < v && __hip_atomic_load(slot, __ATOMIC_RELAXED,
+                                                                        __HIP_MEMORY_SCOPE_WORKGROUP) != kPieceFree))
+            __builtin_amdgcn_s_sleep(1);
+        if (lane < v) __hip_atomic_store(slot, pb + (base + lane) * unit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        p += v;
+        live = v == k;
         if (lane == 0u) __hip_atomic_store(&rg->produced, p, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     if (lane == 0u) {
@@ -344,8 +336,6 @@ __device__ __forceinline__ void ring_dealer(PieceRing* rg, uint32_t* head, uint3
         }
     }
 }
-
-
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint64_t bytes) {
     // Wave-uniform inputs only, so no waterfall loop (guide T20); clamp without a
@@ -484,8 +474,23 @@ __global__ __launch_bounds__(kBlock) void csum_fixed_buf_kernel(
 // last waves — the XCDs and CUs run at different speeds (tools/probes/f3_wave_times.py --config 2,
 // profiles/r06_fixed_wave_times_c2.txt). A dealt task's 8 results are finished with their own partials and stored
 // at once (16 B).
-template <int U, int NROWS, bool DEAL = false>
-__global__ __launch_bounds__(DEAL ? kBlock + kWave : kBlock) void csum_fixed_swp_kernel(
+#ifndef NSX_FIXED_AHEAD
+#define NSX_FIXED_AHEAD 4
+#endif
+constexpr uint32_t kFixedAhead = NSX_FIXED_AHEAD;  // ring entries the dealer posts beyond the claimed ones
+#ifndef NSX_FIXED_POOL_SHIFT
+#define NSX_FIXED_POOL_SHIFT 3
+#endif
+constexpr uint32_t kFixedPoolShift = NSX_FIXED_POOL_SHIFT;  // the dealt pool: the last 1/2^k of the tasks
+#ifndef NSX_FIXED_DEAL_MODE
+#define NSX_FIXED_DEAL_MODE 0
+#endif
+constexpr int kFixedDealMode = NSX_FIXED_DEAL_MODE;  // the aligned default shapes' deal: 0 none, 1 dealer wave, 2 in-wave
+// DEAL 1: the dealer wave and ring above; DEAL 2: each wave pulls its own tickets from the heads, two tasks ahead
+// (two ticket registers alternating with the two register sets, so no ticket is ever copied or selected — reading one
+// waits only for its own pull, issued two task-loads earlier; round 6 A/B).
+template <int U, int NROWS, int DEAL = 0>
+__global__ __launch_bounds__(DEAL == 1 ? kBlock + kWave : kBlock) void csum_fixed_swp_kernel(
     const uint8_t* __restrict__ base, uint64_t stride, uint32_t seg_len, uint32_t n,
     const uint32_t* __restrict__ partial, uint16_t* __restrict__ out, uint32_t chunk_log2,
     uint32_t* __restrict__ deal) {
@@ -499,9 +504,29 @@ __global__ __launch_bounds__(DEAL ? kBlock + kWave : kBlock) void csum_fixed_swp
     uint32_t ntasks = all_tasks;  // the statically split tasks [0, ntasks)
     [[maybe_unused]] RingClient rc{nullptr, lane};
     [[maybe_unused]] uint32_t claim0 = 0, claim1 = 0;
-    if constexpr (DEAL) {
+    // DEAL 2: this wave's head (waves numbered XCD by XCD: every head has waves on all 8 XCDs), its share of the
+    // pool, and the two tickets pulled at entry (held through the static part)
+    [[maybe_unused]] uint32_t* shead = nullptr;
+    [[maybe_unused]] uint32_t spb = 0, sq = 0, swaves = 0, tkx = 0, tky = 0;
+    auto spull = [&]() {
+        uint32_t t = 0u;
+        if (lane == 0u) t = __hip_atomic_fetch_add(shead, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return t;
+    };
+    if constexpr (DEAL == 2) {
+        ntasks = all_tasks - (all_tasks >> kFixedPoolShift);
+        const uint32_t W = gridDim.x * kWavesPerBlock, H = min(kDealHeads, W);
+        const uint32_t h = wave_number(gridDim.x, kWavesPerBlock, wave) % H;
+        const uint32_t Q = all_tasks - ntasks;
+        const uint32_t r0 = (uint32_t)((uint64_t)Q * h / H);
+        sq = (uint32_t)((uint64_t)Q * (h + 1u) / H) - r0;
+        spb = ntasks + r0;
+        swaves = (W - h + H - 1u) / H;
+        shead = deal + h * kDealStride;
+    }
+    if constexpr (DEAL == 1) {
         __shared__ PieceRing ring;
-        ntasks = all_tasks - (all_tasks >> kDealPoolShift);
+        ntasks = all_tasks - (all_tasks >> kFixedPoolShift);
         if (wave == kWavesPerBlock) {
             if (lane < kPieceRing) ring.e[lane] = kPieceFree;
             if (lane == 0u) ring.claim = 0u, ring.produced = 0u, ring.end_at = ~0u;
@@ -511,7 +536,7 @@ __global__ __launch_bounds__(DEAL ? kBlock + kWave : kBlock) void csum_fixed_swp
             const uint32_t nb = gridDim.x, H = min(kDealHeads, nb), h = wave_number(nb, 1u, 0u) % H;
             const uint32_t Q = all_tasks - ntasks;
             const uint32_t r0 = (uint32_t)((uint64_t)Q * h / H), qh = (uint32_t)((uint64_t)Q * (h + 1u) / H) - r0;
-            ring_dealer(&ring, deal + h * kDealStride, ntasks + r0, 1u, qh, (nb - h + H - 1u) / H, lane);
+            ring_dealer(&ring, deal + h * kDealStride, ntasks + r0, 1u, qh, (nb - h + H - 1u) / H, kFixedAhead, lane);
             return;
         }
         rc.rg = &ring;
@@ -572,21 +597,39 @@ __global__ __launch_bounds__(DEAL ? kBlock + kWave : kBlock) void csum_fixed_swp
     };
     Set A, B;
     uint32_t i = (uint32_t)it.next;
+    // DEAL 2: the two first tickets are pulled when the static stream has at most two tasks left, so that they are
+    // in hand when the pool starts and the waves' pulls spread over their different end times (pulled at entry, the
+    // 2048 pulls of a launch queued on 32 counters at once)
+    [[maybe_unused]] bool pulled = false;
+    auto pull_late = [&](uint32_t inext) {
+        if constexpr (DEAL == 2) {
+            if (!pulled && !(inext < end && cd.task(inext) < ntasks)) {
+                tkx = spull();
+                tky = spull();
+                pulled = true;
+            }
+        }
+    };
     issue(i, A);
     while (A.ok) {
         const uint32_t i1 = i + step;
+        pull_late(i1 + step);
         issue(i1, B);
         consume(i, A);
         if (!B.ok) break;
         i = i1 + step;
+        pull_late(i + step);
         issue(i, A);
         consume(i1, B);
+    }
+    if constexpr (DEAL == 2) {
+        if (!pulled) tkx = spull(), tky = spull();
     }
     if (k) {
         res = finish(res, true, gpart);
         fixed_flush<U>(res, first, step, k, n, ors, lane, cd);
     }
-    if constexpr (DEAL) {
+    if constexpr (DEAL != 0) {
         // The pool: tasks read from the ring (each claimed two tasks ahead), software-pipelined like the static
         // loop; a task's partials load with its rows, its results are finished and stored when it is summed.
         struct PSet {
@@ -634,13 +677,57 @@ __global__ __launch_bounds__(DEAL ? kBlock + kWave : kBlock) void csum_fixed_swp
             ++ntk;
         };
         PSet P0, P1;
-        pissue(take(), P0);
-        while (P0.t < all_tasks) {
-            pissue(take(), P1);
-            pconsume(P0);
-            if (P1.t >= all_tasks) break;
+        if constexpr (DEAL == 1) {
             pissue(take(), P0);
-            pconsume(P1);
+            while (P0.t < all_tasks) {
+                pissue(take(), P1);
+                pconsume(P0);
+                if (P1.t >= all_tasks) break;
+                pissue(take(), P0);
+                pconsume(P1);
+            }
+        } else {
+            // ticket register X feeds set P0, Y feeds P1; each is read two task-loads after its pull and refilled at
+            // once while the share lasts. A wave stops at the first ticket past the share and then reads its other
+            // outstanding pull too (a ticket is never dropped, whatever order the pulls executed in); the last wave of
+            // the head to finish resets it (dword 0) and the finished count (dword 1) for the stream's next launch.
+            auto tk_task = [&](uint32_t v) { return v < sq ? spb + v : all_tasks; };
+            P1.t = all_tasks;
+            uint32_t tx = tk_task(__builtin_amdgcn_readfirstlane(tkx));
+            if (tx < all_tasks) tkx = spull();
+            pissue(tx, P0);
+            bool ymore = true;  // Y holds an unread pull
+            while (P0.t < all_tasks) {
+                const uint32_t ty = tk_task(__builtin_amdgcn_readfirstlane(tky));
+                ymore = false;
+                if (ty < all_tasks) tky = spull(), ymore = true;
+                pissue(ty, P1);
+                pconsume(P0);
+                if (P1.t >= all_tasks) break;
+                tx = tk_task(__builtin_amdgcn_readfirstlane(tkx));
+                if (tx < all_tasks) tkx = spull();
+                pissue(tx, P0);
+                pconsume(P1);
+            }
+            // drain: P0 or P1 ended the loop with the end marker; the other ticket register may hold an unread pull
+            // (X if the loop ended on P1, else Y) — a valid one is a task to do
+            uint32_t last = all_tasks;
+            if (P1.t >= all_tasks && P0.t < all_tasks) {  // ended on P1: X was refilled when P0 was issued
+                last = tk_task(__builtin_amdgcn_readfirstlane(tkx));
+            } else if (ymore) {
+                last = tk_task(__builtin_amdgcn_readfirstlane(tky));
+            }
+            if (last < all_tasks) {  // rare: a pull executed out of order and returned inside the share; every pull
+                pissue(last, P0);    // after the one already seen past it returns past it too (one counter)
+                pconsume(P0);
+            }
+            if (lane == 0u) {
+                const uint32_t done = __hip_atomic_fetch_add(shead + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (done + 1u == swaves) {
+                    __hip_atomic_store(shead, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(shead + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
         }
     }
     ws.done(blockIdx.x * kWavesPerBlock + wave, ntk, lane);
@@ -851,25 +938,63 @@ struct WaveRange {
     uint64_t bytes;
 };
 // count_align (nonzero): the alignment of equal-count ranges instead of `align`.
-__device__ __forceinline__ WaveRange wave_range(__amdgpu_buffer_rsrc_t ofs, uint32_t n, uint32_t g, uint32_t W,
-                                                uint32_t lane, uint32_t small_mean, uint32_t align,
-                                                uint32_t count_align = 0) {
+// Weighted form: the wave's share is the slice [lo, hi) of a total weight T (the unweighted form: g, g + 1, W).
+__device__ __forceinline__ WaveRange wave_range_w(__amdgpu_buffer_rsrc_t ofs, uint32_t n, uint64_t lo, uint64_t hi,
+                                                  uint64_t T, uint32_t lane, uint32_t small_mean, uint32_t align,
+                                                  uint32_t count_align = 0) {
     const uint64_t o_lo = ld_off(ofs, 0), o_hi = ld_off(ofs, n);
     const uint64_t tot = o_hi - o_lo;
     uint32_t s[2];
     const bool by_count = tot < (uint64_t)small_mean * n;
     if (by_count && count_align) align = count_align;
     if (by_count) {
-        s[0] = (uint32_t)((uint64_t)n * g / W);
-        s[1] = (uint32_t)((uint64_t)n * (g + 1) / W);
+        s[0] = (uint32_t)((uint64_t)n * lo / T);
+        s[1] = (uint32_t)((uint64_t)n * hi / T);
     } else {
-        seg_lower_bound2(ofs, n, o_lo + tot * g / W, o_lo + tot * (g + 1) / W, lane, s);
+        seg_lower_bound2(ofs, n, o_lo + tot * lo / T, o_lo + tot * hi / T, lane, s);
     }
     WaveRange r;
-    r.a0 = g == 0 ? 0u : min((s[0] + align - 1u) / align * align, n);
-    r.a_end = g + 1 == W ? n : min((s[1] + align - 1u) / align * align, n);
-    r.bytes = by_count ? ld_off(ofs, r.a_end) - ld_off(ofs, r.a0) : tot * (g + 1) / W - tot * g / W;
+    r.a0 = lo == 0 ? 0u : min((s[0] + align - 1u) / align * align, n);
+    r.a_end = hi == T ? n : min((s[1] + align - 1u) / align * align, n);
+    r.bytes = by_count ? ld_off(ofs, r.a_end) - ld_off(ofs, r.a0) : tot * hi / T - tot * lo / T;
     return r;
+}
+
+__device__ __forceinline__ WaveRange wave_range(__amdgpu_buffer_rsrc_t ofs, uint32_t n, uint32_t g, uint32_t W,
+                                                uint32_t lane, uint32_t small_mean, uint32_t align,
+                                                uint32_t count_align = 0) {
+    return wave_range_w(ofs, n, g, g + 1u, W, lane, small_mean, align, count_align);
+}
+
+// Byte shares by the block's slot on its CU (round 6). A CU's blocks are dispatched
+// breadth-first (the first CUs/8 blocks of an XCD each go to their own CU, the next CUs/8 take the second place on
+// the same CUs, ...), and the CU issues its oldest waves first: in the streamed receive pass (3 blocks of 4 waves
+// per CU) the waves of a CU's first block ended 4.1 µs before the launch's median wave and those of its third 4.6 µs
+// after (workload 10; 14: −6.7 / +6.8 µs, tools/probes/rx_wave_times.py, profiles/r06_rx_wave_times_slots.txt) —
+// the launch's tail. So a wave's byte share is weighted by its block's slot, by the rates measured there (1/1024s);
+// slots past the table weigh as the last. Wave g = XCD-major as wave_number(nb, wpb, w).
+#ifndef NSX_SLOT_WEIGHTS
+#define NSX_SLOT_WEIGHTS 1
+#endif
+constexpr bool kSlotWeights = NSX_SLOT_WEIGHTS;
+constexpr uint32_t kSlotW[3] = {1059u, 1024u, 989u};
+struct SlotShare {
+    uint64_t lo, hi, T;
+};
+__device__ __forceinline__ SlotShare slot_share(uint32_t nb, uint32_t wpb, uint32_t w, uint32_t cus_per_xcd) {
+    const uint32_t b = blockIdx.x, per = nb >> 3;  // blocks per XCD (nb a multiple of 8)
+    const uint32_t x = b & 7u, j = b >> 3;        // XCD, place in the XCD's dispatch order
+    const uint32_t slots = (per + cus_per_xcd - 1u) / cus_per_xcd;
+    auto wt = [](uint32_t sl) { return kSlotW[sl < 3u ? sl : 2u]; };
+    uint64_t xw = 0, cum = 0;  // an XCD's total weight; the weight of its blocks before block j
+    for (uint32_t sl = 0; sl < slots; ++sl) {
+        const uint32_t cnt = min(cus_per_xcd, per - sl * cus_per_xcd);
+        xw += (uint64_t)cnt * wt(sl);
+        if (j >= sl * cus_per_xcd) cum += (uint64_t)min(cnt, j - sl * cus_per_xcd) * wt(sl);
+    }
+    const uint32_t me = wt(j / cus_per_xcd);
+    const uint64_t lo = (uint64_t)x * xw * wpb + cum * wpb + (uint64_t)w * me;
+    return SlotShare{lo, lo + me, 8ull * xw * wpb};
 }
 
 // Stream the bytes [rbase + head, rbase + span) as 1 KiB rows of one wave (rbase 128-byte aligned, so a row
@@ -2094,10 +2219,18 @@ __device__ __forceinline__ void rx_runs(const uint8_t* __restrict__ base, __amdg
 constexpr uint32_t kStreamPiece = NSX_STREAM_PIECE;          // frames per dealt piece (a multiple of 8: whole mask bytes)
 constexpr uint32_t kStreamPoolShift = NSX_STREAM_POOL_SHIFT;  // the pool: the batch's last eighth of frames
 constexpr uint32_t kStreamWaves = 3;       // streaming waves per block (wave 3 deals)
+#ifndef NSX_STREAM_AHEAD
+#define NSX_STREAM_AHEAD 0
+#endif
+constexpr uint32_t kStreamAhead = NSX_STREAM_AHEAD;  // entries the dealer posts beyond the claimed ones
 #ifndef NSX_STREAM_ROTATE
 #define NSX_STREAM_ROTATE 0
 #endif
 constexpr bool kStreamRotate = NSX_STREAM_ROTATE;
+#ifndef NSX_STREAM_DEAL
+#define NSX_STREAM_DEAL 0
+#endif
+constexpr bool kStreamDeal = NSX_STREAM_DEAL;  // the dealt streamed layout (A/B builds; the default: slot shares)
 
 // A streaming wave's units: its static runs [a0, e_st) of kRxRun frames, then dealt pieces until the share ends
 // (n). The entry for the unit after next is claimed when next() hands out a unit whose successor is a piece, and
@@ -2529,7 +2662,7 @@ __global__ __launch_bounds__(kBlock, WPS) void rx_tcp_kernel(const uint8_t* __re
                 else rx_runs_pfx<R, V6, 7, true>(base, ofs, n, q, lane, slot, ro);
             }
             ws.done(g, wr.bytes, lane);
-        } else if (deal && (sets == 0 || sets == 8)) {
+        } else if (kStreamDeal && deal && (sets == 0 || sets == 8)) {
             // Streamed runs with the batch's last eighth dealt in pieces through the block's LDS ring (the auto
             // choice and mode 8 when the stream has heads; §7 step 75): waves 0-2 of every block stream, wave 3 deals.
             // the dealer: wave 3, or (NSX_STREAM_ROTATE builds) the wave of the block's slot on its CU, so that the 4
@@ -2550,7 +2683,8 @@ __global__ __launch_bounds__(kBlock, WPS) void rx_tcp_kernel(const uint8_t* __re
                 const uint32_t H = min(kDealHeads, nb), h = wave_number(nb, 1u, 0u) % H;
                 const uint32_t Q = (n - S + kStreamPiece - 1u) / kStreamPiece;
                 const uint32_t r0 = (uint32_t)((uint64_t)Q * h / H), qh = (uint32_t)((uint64_t)Q * (h + 1u) / H) - r0;
-                ring_dealer(rg, deal + h * kDealStride, S + r0 * kStreamPiece, kStreamPiece, qh, (nb - h + H - 1u) / H, lane);
+                ring_dealer(rg, deal + h * kDealStride, S + r0 * kStreamPiece, kStreamPiece, qh, (nb - h + H - 1u) / H,
+                            kStreamAhead, lane);
                 return;
             }
             const uint32_t g = wave_number(nb, kStreamWaves, wave < dw ? wave : wave - 1u);
@@ -2574,7 +2708,15 @@ __global__ __launch_bounds__(kBlock, WPS) void rx_tcp_kernel(const uint8_t* __re
                   // stream without heads); mode 1: on every block
             const uint32_t nb = active_blocks(ofs, n, 0u, sets == 0 || sets == 8 ? 3u : 0u);
             if (blockIdx.x >= nb) return;
-            const WaveRange wr = range(nb, kWavesPerBlock, wave);
+            // byte shares weighted by the block's slot on its CU (slot_share) on the default grid: 4 blocks per CU
+            // launched (gridDim = 32 × CUs per XCD), the first 3/4 active
+            WaveRange wr;
+            if (kSlotWeights && nb >= 64 && (gridDim.x & 31u) == 0 && nb == gridDim.x / 4u * 3u) {
+                const SlotShare sh = slot_share(nb, kWavesPerBlock, wave, gridDim.x >> 5);
+                wr = wave_range_w(ofs, n, sh.lo, sh.hi, sh.T, lane, kRxSmallFrame, 8u);
+            } else {
+                wr = range(nb, kWavesPerBlock, wave);
+            }
             // raw sums parked in the wave's (otherwise unused) 7-row slot, 8 KiB: IPv4 2 × 2048 results, IPv6 4096
             static_assert(PfxSlot<7>::kBytes >= 8192, "two 4 KiB parks per wave slot");
             RxOuts rp = ro;
@@ -3715,12 +3857,13 @@ static hipError_t launch_fixed_short(const LaunchCfg& c, const uint8_t* base, ui
     const uint32_t clog = deal_clog(c.xcd_chunk, ntasks, (uint64_t)u * stride);
     // The default aligned shapes deal their last tasks through each block's ring (a fifth, dealer wave per block;
     // §7 step 77) when the stream has heads and the batch has at least 64 tasks per block.
-    if (aligned && c.segs_per_wave == 0 && ntasks >= 64ull * grid) {
+    if (kFixedDealMode != 0 && aligned && c.segs_per_wave == 0 && ntasks >= 64ull * grid) {
         if (uint32_t* deal = deal_heads(c, st)) {
 #define NSX_FIXED_DEAL(U_, NR_)                                                                                  \
     if (u == U_ && nrows == NR_) {                                                                               \
-        hipLaunchKernelGGL((csum_fixed_swp_kernel<U_, NR_, true>), dim3(grid), dim3(kBlock + kWave), 0, st, base, \
-                           stride, seg_len, (uint32_t)n, partial, out, clog, deal);                              \
+        hipLaunchKernelGGL((csum_fixed_swp_kernel<U_, NR_, kFixedDealMode>), dim3(grid),                          \
+                           dim3(kFixedDealMode == 1 ? kBlock + kWave : kBlock), 0, st, base, stride, seg_len,     \
+                           (uint32_t)n, partial, out, clog, deal);                                               \
         return hipGetLastError();                                                                                \
     }
             NSX_FIXED_DEAL(8, 1) NSX_FIXED_DEAL(8, 2) NSX_FIXED_DEAL(4, 4)
@@ -3730,7 +3873,7 @@ static hipError_t launch_fixed_short(const LaunchCfg& c, const uint8_t* base, ui
 #define NSX_FIXED(U_, NR_)                                                                                    \
     if (u == U_ && nrows == NR_) {                                                                             \
         if (aligned)                                                                                           \
-            hipLaunchKernelGGL((csum_fixed_swp_kernel<U_, NR_>), dim3(grid), dim3(kBlock), 0, st, base, stride, \
+            hipLaunchKernelGGL((csum_fixed_swp_kernel<U_, NR_, 0>), dim3(grid), dim3(kBlock), 0, st, base, stride, \
                                seg_len, (uint32_t)n, partial, out, clog, nullptr);                             \
         else                                                                                                   \
             hipLaunchKernelGGL((csum_fixed_buf_kernel<U_, NR_>), dim3(grid), dim3(kBlock), 0, st, base, stride, \

@@ -23,9 +23,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=7)
     ap.add_argument("--launches", type=int, default=20)
+    ap.add_argument("--lib", default="stamps", help="network-stack_amd/lib_<name>: a build with NSX_WAVE_STAMPS")
     a = ap.parse_args()
     import nsx
-    nsx.LIB_PATH = os.path.join(ROOT, "network-stack_amd", "lib_stamps", "libnsx_csum.so")
+    nsx.LIB_PATH = os.path.join(ROOT, "network-stack_amd", f"lib_{a.lib}", "libnsx_csum.so")
     import torch
     import bench
     torch.cuda.set_device(0)

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--wpb", type=int, default=2, help="waves per block taking ranges (streamed modes: 4)")
     ap.add_argument("--lib", default="stamps", help="network-stack_amd/lib_<name>: a build with NSX_WAVE_STAMPS")
     ap.add_argument("--deal", type=int, default=0, help="nsx_tune.deal (-1: equal static shares)")
+    ap.add_argument("--cus", type=int, default=256, help="CUs of the device (slot grouping)")
     a = ap.parse_args()
     import nsx
     nsx.LIB_PATH = os.path.join(ROOT, "network-stack_amd", f"lib_{a.lib}", "libnsx_csum.so")
@@ -85,6 +86,16 @@ def main():
         print(f"by {nm:5s}: waves per group {int(v[0, 3])}; std of group means {np.median(v[:, 1]):.2f} us, std within "
               f"groups {np.median(v[:, 2]):.2f} us; tail if each group's waves ended at their mean "
               f"{np.median(v[:, 0]):.2f} us")
+    # by the block's slot on its CU: blocks are dealt to CUs breadth-first (block b on XCD b & 7; its CU's blocks
+    # in order b >> 3 = 0, 32, 64, ... for 32 CUs per XCD), so a wave's slot = (b >> 3) // (CUs per XCD); the
+    # waves are numbered XCD-major (g // wpb = (b & 7) * per + (b >> 3), per = active blocks / 8)
+    nw = len(rows[0][2])
+    per = nw // a.wpb // 8
+    cus_per_xcd = max(1, a.cus // 8)
+    slot = ((np.arange(nw) // a.wpb) % per) // cus_per_xcd
+    for k in range(int(slot.max()) + 1):
+        v = [np.median(r[2][slot == k]) - np.median(r[2]) for r in rows]
+        print(f"slot {k}: waves {int((slot == k).sum())}, median end minus launch median {np.median(v):+.2f} us")
     print(f"end std over waves {np.median([r[2].std() for r in rows]):.2f} us")
     ends = np.array([r[2].max() for r in rows])
     med_end = np.array([np.median(r[2]) for r in rows])
