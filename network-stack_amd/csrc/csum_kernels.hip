@@ -939,8 +939,11 @@ struct WaveRange {
 };
 // count_align (nonzero): the alignment of equal-count ranges instead of `align`.
 // Weighted form: the wave's share is the slice [lo, hi) of a total weight T (the unweighted form: g, g + 1, W).
-__device__ __forceinline__ WaveRange wave_range_w(__amdgpu_buffer_rsrc_t ofs, uint32_t n, uint64_t lo, uint64_t hi,
-                                                  uint64_t T, uint32_t lane, uint32_t small_mean, uint32_t align,
+// (T < 2^32: the slices are scaled 32-bit weights; a 64-bit T — a full 64 / 64-bit division here — gave some waves of
+// the streamed receive pass wrong ranges in round 6's first slot-share build, with the same partition in exact
+// arithmetic, and is not used.)
+__device__ __forceinline__ WaveRange wave_range_w(__amdgpu_buffer_rsrc_t ofs, uint32_t n, uint32_t lo, uint32_t hi,
+                                                  uint32_t T, uint32_t lane, uint32_t small_mean, uint32_t align,
                                                   uint32_t count_align = 0) {
     const uint64_t o_lo = ld_off(ofs, 0), o_hi = ld_off(ofs, n);
     const uint64_t tot = o_hi - o_lo;
@@ -977,24 +980,33 @@ __device__ __forceinline__ WaveRange wave_range(__amdgpu_buffer_rsrc_t ofs, uint
 #define NSX_SLOT_WEIGHTS 1
 #endif
 constexpr bool kSlotWeights = NSX_SLOT_WEIGHTS;
-constexpr uint32_t kSlotW[3] = {1059u, 1024u, 989u};
+#ifndef NSX_SCAN_SLOT_WEIGHTS
+#define NSX_SCAN_SLOT_WEIGHTS 0
+#endif
+constexpr bool kScanSlotWeights = NSX_SCAN_SLOT_WEIGHTS;  // the ragged scan's streamed forms (A/B builds)
+#ifndef NSX_SLOT_W0
+#define NSX_SLOT_W0 1059
+#define NSX_SLOT_W1 1024
+#define NSX_SLOT_W2 989
+#endif
+constexpr uint32_t kSlotW0 = NSX_SLOT_W0, kSlotW1 = NSX_SLOT_W1, kSlotW2 = NSX_SLOT_W2;
 struct SlotShare {
-    uint64_t lo, hi, T;
+    uint32_t lo, hi, T;  // T = 8 · (an XCD's weight) · wpb < 2^32 for any grid this library launches
 };
 __device__ __forceinline__ SlotShare slot_share(uint32_t nb, uint32_t wpb, uint32_t w, uint32_t cus_per_xcd) {
     const uint32_t b = blockIdx.x, per = nb >> 3;  // blocks per XCD (nb a multiple of 8)
     const uint32_t x = b & 7u, j = b >> 3;        // XCD, place in the XCD's dispatch order
-    const uint32_t slots = (per + cus_per_xcd - 1u) / cus_per_xcd;
-    auto wt = [](uint32_t sl) { return kSlotW[sl < 3u ? sl : 2u]; };
-    uint64_t xw = 0, cum = 0;  // an XCD's total weight; the weight of its blocks before block j
-    for (uint32_t sl = 0; sl < slots; ++sl) {
-        const uint32_t cnt = min(cus_per_xcd, per - sl * cus_per_xcd);
-        xw += (uint64_t)cnt * wt(sl);
-        if (j >= sl * cus_per_xcd) cum += (uint64_t)min(cnt, j - sl * cus_per_xcd) * wt(sl);
-    }
-    const uint32_t me = wt(j / cus_per_xcd);
-    const uint64_t lo = (uint64_t)x * xw * wpb + cum * wpb + (uint64_t)w * me;
-    return SlotShare{lo, lo + me, 8ull * xw * wpb};
+    const uint32_t c = cus_per_xcd;
+    // the weight of the first k blocks of an XCD: slots 0 and 1 of c blocks each, then slot 2 and later (closed form:
+    // round 6's first build summed the slots in a loop, and its first slot's waves got wrong ranges on the GPU)
+    auto below = [&](uint32_t k) {
+        const uint32_t k0 = min(k, c), k1 = min(k - k0, c), k2 = k - k0 - k1;
+        return k0 * kSlotW0 + k1 * kSlotW1 + k2 * kSlotW2;
+    };
+    const uint32_t me = j < c ? kSlotW0 : j < 2u * c ? kSlotW1 : kSlotW2;
+    const uint32_t xw = below(per);
+    const uint32_t lo = x * xw * wpb + below(j) * wpb + w * me;
+    return SlotShare{lo, lo + me, 8u * xw * wpb};
 }
 
 // Stream the bytes [rbase + head, rbase + span) as 1 KiB rows of one wave (rbase 128-byte aligned, so a row
@@ -1823,6 +1835,8 @@ __global__ __launch_bounds__(kBlock, NS == 2 ? 4 : 1) void csum_ragged_scan_kern
     uint32_t big_keep, bool park, uint32_t* __restrict__ deal) {
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    WaveStamps ws;
+    ws.entry();
     const __amdgpu_buffer_rsrc_t ofs = make_rsrc(offsets, ((uint64_t)n + 1) * 8);
     const __amdgpu_buffer_rsrc_t prs = make_rsrc(partial, partial ? (uint64_t)n * 4 : 0);
     const __amdgpu_buffer_rsrc_t ors = make_rsrc(out, out ? (uint64_t)n * 2 : 0);
@@ -1868,9 +1882,17 @@ __global__ __launch_bounds__(kBlock, NS == 2 ? 4 : 1) void csum_ragged_scan_kern
     // a0 + NS·run, ... < a_end; a run never crosses a_end. Byte-balanced: wave g (XCD-contiguous numbering) owns
     // the segments that start in the g-th of W equal byte slices of the batch, so every wave streams the same
     // bytes (± one segment) and none is left running alone at the end of the launch.
-    const WaveRange wr = wave_range(ofs, n, wave_no(nb, kWavesPerBlock), nb * kWavesPerBlock, lane, kScanLdsSeg, 1u);
+    WaveRange wr;
+    if (kScanSlotWeights && nb >= 64 && (gridDim.x & 31u) == 0 && nb * 4u > gridDim.x && nb % (gridDim.x / 4u) == 0) {
+        // byte shares weighted by the block's slot on its CU (slot_share; 2 or 3 of the 4 blocks per CU active)
+        const SlotShare sh = slot_share(nb, kWavesPerBlock, wave, gridDim.x >> 5);
+        wr = wave_range_w(ofs, n, sh.lo, sh.hi, sh.T, lane, kScanLdsSeg, 1u);
+    } else {
+        wr = wave_range(ofs, n, wave_no(nb, kWavesPerBlock), nb * kWavesPerBlock, lane, kScanLdsSeg, 1u);
+    }
     const uint32_t a0 = wr.a0, a_end = wr.a_end;
     const uint64_t wave_bytes = wr.bytes;
+    ws.ready();
     // A wave whose own segments average under kScanLdsSeg bytes sums them out of LDS (§7 step 44); the others stream
     // runs of two 63-segment sets under kScanTwoSetSeg, else of one (§7 step 64: with results parked, one set beat
     // four at every mean from 160 B to 4.5 KB, by up to 9%, and two from ~400 B; two sets ran 3-5% faster at a
@@ -1885,6 +1907,7 @@ __global__ __launch_bounds__(kBlock, NS == 2 ? 4 : 1) void csum_ragged_scan_kern
     } else {
         ragged_runs<R, VERIFY, PIPE, 1>(base, ofs, n, prs, ors, oks, scan_run, a0, a_end, lane, pbuf, pout, raw);
     }
+    ws.done(wave_no(nb, kWavesPerBlock), wave_bytes, lane);
 }
 
 // ---------------------------------------------------------------------------

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--config", type=int, default=7)
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--lib", default="stamps", help="network-stack_amd/lib_<name>: a build with NSX_WAVE_STAMPS")
+    ap.add_argument("--wpb", type=int, default=4, help="waves per block that take work (slot grouping)")
+    ap.add_argument("--cus", type=int, default=256, help="CUs of the device (slot grouping)")
     a = ap.parse_args()
     import nsx
     nsx.LIB_PATH = os.path.join(ROOT, "network-stack_amd", f"lib_{a.lib}", "libnsx_csum.so")
@@ -63,6 +65,15 @@ def main():
         v = np.array(v)
         print(f"by {nm}: std of group means {np.median(v[:, 1]):.2f} us; tail if each group's waves ended at their "
               f"mean {np.median(v[:, 0]):.2f} us")
+    # by the block's slot on its CU (blocks dealt to CUs breadth-first; waves numbered XCD-major, g // wpb =
+    # (b & 7) * per + (b >> 3) for grids of the XCD-contiguous numbering; the fixed kernel numbers b * wpb + w)
+    nw = min(len(r[1]) for r in rows)
+    per = nw // a.wpb // 8
+    if per:
+        slot = ((np.arange(nw) // a.wpb) % per) // max(1, a.cus // 8)
+        for k in range(int(slot.max()) + 1):
+            v = [np.median(r[1][:nw][slot == k]) - np.median(r[1]) for r in rows]
+            print(f"slot {k}: waves {int((slot == k).sum())}, median end minus launch median {np.median(v):+.2f} us")
     tails = [r[1].max() - np.median(r[1]) for r in rows]
     spans = [r[1].max() for r in rows]
     print(f"launch span (first start -> last end) us: median {np.median(spans):.2f}; tail (last end - median end) "
