@@ -981,7 +981,7 @@ __device__ __forceinline__ WaveRange wave_range(__amdgpu_buffer_rsrc_t ofs, uint
 #endif
 constexpr bool kSlotWeights = NSX_SLOT_WEIGHTS;
 #ifndef NSX_SCAN_SLOT_WEIGHTS
-#define NSX_SCAN_SLOT_WEIGHTS 0
+#define NSX_SCAN_SLOT_WEIGHTS 1
 #endif
 constexpr bool kScanSlotWeights = NSX_SCAN_SLOT_WEIGHTS;  // the ragged scan's streamed forms (A/B builds)
 #ifndef NSX_SLOT_W0
@@ -989,11 +989,21 @@ constexpr bool kScanSlotWeights = NSX_SCAN_SLOT_WEIGHTS;  // the ragged scan's s
 #define NSX_SLOT_W1 1024
 #define NSX_SLOT_W2 989
 #endif
-constexpr uint32_t kSlotW0 = NSX_SLOT_W0, kSlotW1 = NSX_SLOT_W1, kSlotW2 = NSX_SLOT_W2;
+#ifndef NSX_SCAN_W0
+#define NSX_SCAN_W0 1059
+#define NSX_SCAN_W1 1024
+#endif
+// the streamed receive pass (3 active blocks per CU) and the ragged scan's streamed forms (2 or 3)
+struct SlotWeights {
+    uint32_t w0, w1, w2;
+};
+constexpr SlotWeights kRxSlotW{NSX_SLOT_W0, NSX_SLOT_W1, NSX_SLOT_W2};
+constexpr SlotWeights kScanSlotW{NSX_SCAN_W0, NSX_SCAN_W1, NSX_SLOT_W2};
 struct SlotShare {
     uint32_t lo, hi, T;  // T = 8 · (an XCD's weight) · wpb < 2^32 for any grid this library launches
 };
-__device__ __forceinline__ SlotShare slot_share(uint32_t nb, uint32_t wpb, uint32_t w, uint32_t cus_per_xcd) {
+__device__ __forceinline__ SlotShare slot_share(uint32_t nb, uint32_t wpb, uint32_t w, uint32_t cus_per_xcd,
+                                                const SlotWeights sw) {
     const uint32_t b = blockIdx.x, per = nb >> 3;  // blocks per XCD (nb a multiple of 8)
     const uint32_t x = b & 7u, j = b >> 3;        // XCD, place in the XCD's dispatch order
     const uint32_t c = cus_per_xcd;
@@ -1001,9 +1011,9 @@ __device__ __forceinline__ SlotShare slot_share(uint32_t nb, uint32_t wpb, uint3
     // round 6's first build summed the slots in a loop, and its first slot's waves got wrong ranges on the GPU)
     auto below = [&](uint32_t k) {
         const uint32_t k0 = min(k, c), k1 = min(k - k0, c), k2 = k - k0 - k1;
-        return k0 * kSlotW0 + k1 * kSlotW1 + k2 * kSlotW2;
+        return k0 * sw.w0 + k1 * sw.w1 + k2 * sw.w2;
     };
-    const uint32_t me = j < c ? kSlotW0 : j < 2u * c ? kSlotW1 : kSlotW2;
+    const uint32_t me = j < c ? sw.w0 : j < 2u * c ? sw.w1 : sw.w2;
     const uint32_t xw = below(per);
     const uint32_t lo = x * xw * wpb + below(j) * wpb + w * me;
     return SlotShare{lo, lo + me, 8u * xw * wpb};
@@ -1885,7 +1895,7 @@ __global__ __launch_bounds__(kBlock, NS == 2 ? 4 : 1) void csum_ragged_scan_kern
     WaveRange wr;
     if (kScanSlotWeights && nb >= 64 && (gridDim.x & 31u) == 0 && nb * 4u > gridDim.x && nb % (gridDim.x / 4u) == 0) {
         // byte shares weighted by the block's slot on its CU (slot_share; 2 or 3 of the 4 blocks per CU active)
-        const SlotShare sh = slot_share(nb, kWavesPerBlock, wave, gridDim.x >> 5);
+        const SlotShare sh = slot_share(nb, kWavesPerBlock, wave, gridDim.x >> 5, kScanSlotW);
         wr = wave_range_w(ofs, n, sh.lo, sh.hi, sh.T, lane, kScanLdsSeg, 1u);
     } else {
         wr = wave_range(ofs, n, wave_no(nb, kWavesPerBlock), nb * kWavesPerBlock, lane, kScanLdsSeg, 1u);
@@ -2735,7 +2745,7 @@ __global__ __launch_bounds__(kBlock, WPS) void rx_tcp_kernel(const uint8_t* __re
             // launched (gridDim = 32 × CUs per XCD), the first 3/4 active
             WaveRange wr;
             if (kSlotWeights && nb >= 64 && (gridDim.x & 31u) == 0 && nb == gridDim.x / 4u * 3u) {
-                const SlotShare sh = slot_share(nb, kWavesPerBlock, wave, gridDim.x >> 5);
+                const SlotShare sh = slot_share(nb, kWavesPerBlock, wave, gridDim.x >> 5, kRxSlotW);
                 wr = wave_range_w(ofs, n, sh.lo, sh.hi, sh.T, lane, kRxSmallFrame, 8u);
             } else {
                 wr = range(nb, kWavesPerBlock, wave);

@@ -19,7 +19,7 @@ __global__ __launch_bounds__(kBlock) void slot_share_probe(const uint64_t* __res
     const __amdgpu_buffer_rsrc_t ofs = make_rsrc(offsets, ((uint64_t)n + 1) * 8);
     const uint32_t nb = gridDim.x / 4u * 3u;
     if (blockIdx.x >= nb) return;
-    const SlotShare sh = slot_share(nb, kWavesPerBlock, wave, gridDim.x >> 5);
+    const SlotShare sh = slot_share(nb, kWavesPerBlock, wave, gridDim.x >> 5, kRxSlotW);
     const WaveRange a = wave_range_w(ofs, n, sh.lo, sh.hi, sh.T, lane, kRxSmallFrame, 8u);
     const uint32_t g = wave_number(nb, kWavesPerBlock, wave);
     const WaveRange b = wave_range(ofs, n, g, nb * kWavesPerBlock, lane, kRxSmallFrame, 8u);
