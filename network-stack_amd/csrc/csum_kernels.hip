@@ -974,8 +974,11 @@ __device__ __forceinline__ WaveRange wave_range(__amdgpu_buffer_rsrc_t ofs, uint
 // the same CUs, ...), and the CU issues its oldest waves first: in the streamed receive pass (3 blocks of 4 waves
 // per CU) the waves of a CU's first block ended 4.1 µs before the launch's median wave and those of its third 4.6 µs
 // after (workload 10; 14: −6.7 / +6.8 µs, tools/probes/rx_wave_times.py, profiles/r06_rx_wave_times_slots.txt) —
-// the launch's tail. So a wave's byte share is weighted by its block's slot, by the rates measured there (1/1024s);
-// slots past the table weigh as the last. Wave g = XCD-major as wave_number(nb, wpb, w).
+// the launch's tail. So a wave's byte share is weighted by its block's slot (1/1024s; slots past the third weigh as
+// the third). The measured rates alone (1059 / 1024 / 989) halved the slots' spread; the weights were then tuned on
+// workloads 10, 11, 14 (1080 / 1024 / 968; 1100 / 1024 / 950 was better on 10 only) and, for the ragged scan's two
+// active slots, on config 3 (1059 / 1024; 1050 and 1070 slower) — profiles/r06_slot_tune_libab.txt,
+// r06_scan_slot_tune_libab.txt. Wave g = XCD-major as wave_number(nb, wpb, w).
 #ifndef NSX_SLOT_WEIGHTS
 #define NSX_SLOT_WEIGHTS 1
 #endif
@@ -985,9 +988,9 @@ constexpr bool kSlotWeights = NSX_SLOT_WEIGHTS;
 #endif
 constexpr bool kScanSlotWeights = NSX_SCAN_SLOT_WEIGHTS;  // the ragged scan's streamed forms (A/B builds)
 #ifndef NSX_SLOT_W0
-#define NSX_SLOT_W0 1059
+#define NSX_SLOT_W0 1080
 #define NSX_SLOT_W1 1024
-#define NSX_SLOT_W2 989
+#define NSX_SLOT_W2 968
 #endif
 #ifndef NSX_SCAN_W0
 #define NSX_SCAN_W0 1059
