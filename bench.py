@@ -619,6 +619,7 @@ def cpu_baseline(cfg, w, seconds: float) -> dict:
     balanced for ragged batches — one thread each; ctypes releases the GIL) and on one thread. Both
     legs' results are compared with the GPU's for the same segments (the checker role)."""
     from concurrent.futures import ThreadPoolExecutor
+    import threading
     import numpy as np
     import torch
     sys.path.insert(0, ROOT)
@@ -759,8 +760,21 @@ def cpu_baseline(cfg, w, seconds: float) -> dict:
         t1 = time.perf_counter()
         busy.append(t1 - t0)
         return t0, t1
+    # each worker thread pinned to a CPU of its own, on distinct physical cores (round 6): left to
+    # the scheduler, the packed-header legs' last two shards of each pass ran 3.3x slower than the rest, each alone on
+    # its CPU on a near-idle host, and pinned they ran within 1.2x (tools/probes/cpu_shards.py,
+    # profiles/r06_cpu_shards.txt). NSX_BENCH_CPU_PIN=0 leaves placement to the scheduler.
+    pin = shard_cpus(T) if os.environ.get("NSX_BENCH_CPU_PIN", "1") != "0" else None
+    pin_next = iter(pin or ())
+    pin_lock = threading.Lock()
+
+    def pin_worker():
+        with pin_lock:
+            c = next(pin_next, None)
+        if c is not None:
+            os.sched_setaffinity(0, {c})  # pid 0: the calling thread only (Linux)
     thr0 = cgroup_throttling()
-    with ThreadPoolExecutor(T) as ex:
+    with ThreadPoolExecutor(T, initializer=pin_worker if pin else None) as ex:
         def all_cores():
             p0 = time.perf_counter()
             passes.append([(a - p0, b - a) for a, b in ex.map(timed_go, range(T))])
@@ -793,7 +807,8 @@ def cpu_baseline(cfg, w, seconds: float) -> dict:
             "cgroup_throttled_periods": None if thr0 is None or thr1 is None else thr1[0] - thr0[0],
             "shard_duration_max_over_min": med(shard_max_min), "shard_latest_start_ms": med(late_start_ms),
             "slowest_shard_ms": med(slowest_ms), "shard_alone_ms": round(alone_ms, 3),
-            "pass_wall_ms": round(dt_t / max(reps_t, 1) * 1e3, 3)}
+            "pass_wall_ms": round(dt_t / max(reps_t, 1) * 1e3, 3),
+            "pinned_cpus": pin}
     why = ""
     if eff is not None and eff < 0.5:
         imbalanced = diag["shard_duration_max_over_min"] is not None and diag["shard_duration_max_over_min"] > 1.5
@@ -812,12 +827,41 @@ def cpu_baseline(cfg, w, seconds: float) -> dict:
                    f"the calls against {v_1:.2f} alone (contention in the per-unit allocation or memory system)")
     return {"value": round(v_t, 4), "unit": "GiB/s", "cores": T, "kind": "port",
             "sample": f"{desc} ({nbytes / 2**20:.0f} MiB), {reps_t} pass(es) on {T} threads (Go-faithful loop, "
-                      f"contiguous shards){why}",
+                      f"contiguous shards, {'each thread pinned to its own core' if pin else 'threads placed by the scheduler'})"
+                      f"{why}",
             "seconds": round(dt_t, 2),
             "single_thread": {"value": round(v_1, 4), "unit": "GiB/s", "cores": 1,
                               "passes": reps_1, "seconds": round(dt_1, 2)},
             "parallel_efficiency": None if eff is None else round(eff, 3), "threads_diagnostics": diag,
             "sample_parity_vs_gpu": bool(ok_t and ok_1), "host": cores, "extra": extra}
+
+
+def shard_cpus(T):
+    """T CPUs of this process's affinity set for the CPU leg's worker threads, one per physical core (sysfs
+    thread_siblings_list) as far as the set has cores, those of the package the calling thread runs on first; None
+    when there are fewer than T CPUs or no topology to read."""
+    import ctypes
+    cpus = sorted(os.sched_getaffinity(0))
+    if len(cpus) < T:
+        return None
+
+    def topo(c, leaf):
+        with open(f"/sys/devices/system/cpu/cpu{c}/topology/{leaf}") as f:
+            return f.read().strip()
+    try:
+        here = ctypes.CDLL(None).sched_getcpu()
+        pkg_here = topo(here, "physical_package_id") if here >= 0 else None
+        cores, seen = [], set()
+        for c in cpus:
+            sib = topo(c, "thread_siblings_list")
+            if sib not in seen:
+                seen.add(sib)
+                cores.append((topo(c, "physical_package_id") != pkg_here, c))
+    except (OSError, AttributeError):
+        return None
+    first = [c for _, c in sorted(cores)]
+    rest = [c for c in cpus if c not in set(first)]
+    return (first + rest)[:T]
 
 
 def cgroup_throttling():

@@ -120,6 +120,9 @@ def test_cpu_baseline_fixed_all_cores_and_single_thread():
     res = bench.cpu_baseline(cfg, w, 0.2)
     assert res["sample_parity_vs_gpu"] and res["value"] > 0 and res["cores"] == bench.host_cores()["threads"]
     assert res["single_thread"]["cores"] == 1 and res["single_thread"]["value"] > 0
+    pin = res["threads_diagnostics"]["pinned_cpus"]  # one CPU per worker, distinct, inside the affinity set
+    assert pin is None or (len(pin) == res["cores"] and len(set(pin)) == len(pin)
+                           and set(pin) <= os.sched_getaffinity(0))
     for k in ("optimized_1_thread", "optimized_threads"):
         assert res["extra"][k]["parity"] and res["extra"][k]["value"] > 0, k
     w["out"][5] ^= 1  # a wrong "GPU" result is caught

@@ -34,7 +34,8 @@ def order(path):
 
 def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else "r04"
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"{tag}_bench_config*.json")), key=order)
+    files = sorted((f for f in glob.glob(os.path.join(ROOT, "profiles", f"{tag}_bench_config*.json"))
+                    if order(f)[0] != 999), key=order)  # config<W>[n].json only (not e.g. *_unpinned.json)
     print("| workload | whole-job | kernel mean per launch | kernel rate | roofline frac | HBM traffic / alg "
           "| CPU, all threads | CPU, 1 thread |")
     print("|---|---|---|---|---|---|---|---|")
