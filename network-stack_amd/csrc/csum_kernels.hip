@@ -1895,14 +1895,16 @@ __global__ __launch_bounds__(kBlock, NS == 2 ? 4 : 1) void csum_ragged_scan_kern
     // a0 + NS·run, ... < a_end; a run never crosses a_end. Byte-balanced: wave g (XCD-contiguous numbering) owns
     // the segments that start in the g-th of W equal byte slices of the batch, so every wave streams the same
     // bytes (± one segment) and none is left running alone at the end of the launch.
-    WaveRange wr;
+    // byte shares weighted by the block's slot on its CU (slot_share; 2 or 3 of the 4 blocks per CU active), else
+    // equal; one range search either way (a second instance of it cost the kernel ~4% more code)
+    SlotShare sh;
     if (kScanSlotWeights && nb >= 64 && (gridDim.x & 31u) == 0 && nb * 4u > gridDim.x && nb % (gridDim.x / 4u) == 0) {
-        // byte shares weighted by the block's slot on its CU (slot_share; 2 or 3 of the 4 blocks per CU active)
-        const SlotShare sh = slot_share(nb, kWavesPerBlock, wave, gridDim.x >> 5, kScanSlotW);
-        wr = wave_range_w(ofs, n, sh.lo, sh.hi, sh.T, lane, kScanLdsSeg, 1u);
+        sh = slot_share(nb, kWavesPerBlock, wave, gridDim.x >> 5, kScanSlotW);
     } else {
-        wr = wave_range(ofs, n, wave_no(nb, kWavesPerBlock), nb * kWavesPerBlock, lane, kScanLdsSeg, 1u);
+        const uint32_t g = wave_no(nb, kWavesPerBlock);
+        sh = SlotShare{g, g + 1u, nb * kWavesPerBlock};
     }
+    const WaveRange wr = wave_range_w(ofs, n, sh.lo, sh.hi, sh.T, lane, kScanLdsSeg, 1u);
     const uint32_t a0 = wr.a0, a_end = wr.a_end;
     const uint64_t wave_bytes = wr.bytes;
     ws.ready();
@@ -2746,13 +2748,14 @@ __global__ __launch_bounds__(kBlock, WPS) void rx_tcp_kernel(const uint8_t* __re
             if (blockIdx.x >= nb) return;
             // byte shares weighted by the block's slot on its CU (slot_share) on the default grid: 4 blocks per CU
             // launched (gridDim = 32 × CUs per XCD), the first 3/4 active
-            WaveRange wr;
+            SlotShare sh;
             if (kSlotWeights && nb >= 64 && (gridDim.x & 31u) == 0 && nb == gridDim.x / 4u * 3u) {
-                const SlotShare sh = slot_share(nb, kWavesPerBlock, wave, gridDim.x >> 5, kRxSlotW);
-                wr = wave_range_w(ofs, n, sh.lo, sh.hi, sh.T, lane, kRxSmallFrame, 8u);
+                sh = slot_share(nb, kWavesPerBlock, wave, gridDim.x >> 5, kRxSlotW);
             } else {
-                wr = range(nb, kWavesPerBlock, wave);
+                const uint32_t g = wave_number(nb, kWavesPerBlock, wave);
+                sh = SlotShare{g, g + 1u, nb * kWavesPerBlock};
             }
+            const WaveRange wr = wave_range_w(ofs, n, sh.lo, sh.hi, sh.T, lane, kRxSmallFrame, 8u);
             // raw sums parked in the wave's (otherwise unused) 7-row slot, 8 KiB: IPv4 2 × 2048 results, IPv6 4096
             static_assert(PfxSlot<7>::kBytes >= 8192, "two 4 KiB parks per wave slot");
             RxOuts rp = ro;
