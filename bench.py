@@ -763,7 +763,9 @@ def cpu_baseline(cfg, w, seconds: float) -> dict:
     # each worker thread pinned to a CPU of its own, on distinct physical cores (round 6): left to
     # the scheduler, the packed-header legs' last two shards of each pass ran 3.3x slower than the rest, each alone on
     # its CPU on a near-idle host, and pinned they ran within 1.2x (tools/probes/cpu_shards.py,
-    # profiles/r06_cpu_shards.txt). NSX_BENCH_CPU_PIN=0 leaves placement to the scheduler.
+    # profiles/r06_cpu_shards.txt). Pinned to a fixed set of cores, one box's leg still ran 1.9x imbalanced (a core
+    # shared with other work), so the cores are the least busy ones at the time (shard_cpus). NSX_BENCH_CPU_PIN=0
+    # leaves placement to the scheduler.
     pin = shard_cpus(T) if os.environ.get("NSX_BENCH_CPU_PIN", "1") != "0" else None
     pin_next = iter(pin or ())
     pin_lock = threading.Lock()
@@ -836,10 +838,12 @@ def cpu_baseline(cfg, w, seconds: float) -> dict:
             "sample_parity_vs_gpu": bool(ok_t and ok_1), "host": cores, "extra": extra}
 
 
-def shard_cpus(T):
-    """T CPUs of this process's affinity set for the CPU leg's worker threads, one per physical core (sysfs
-    thread_siblings_list) as far as the set has cores, those of the package the calling thread runs on first; None
-    when there are fewer than T CPUs or no topology to read."""
+def shard_cpus(T, probe_s=0.2):
+    """T CPUs of this process's affinity set for the CPU leg's worker threads: one per physical core (sysfs
+    thread_siblings_list) as far as the set has cores, the least busy cores first — each core's busy fraction over
+    `probe_s` seconds (/proc/stat, the busier of its SMT threads, in steps of 5%), so that threads do not land on cores
+    that other work on a shared host keeps busy — then those of the calling thread's package; None when there are
+    fewer than T CPUs or no topology to read."""
     import ctypes
     cpus = sorted(os.sched_getaffinity(0))
     if len(cpus) < T:
@@ -848,18 +852,32 @@ def shard_cpus(T):
     def topo(c, leaf):
         with open(f"/sys/devices/system/cpu/cpu{c}/topology/{leaf}") as f:
             return f.read().strip()
+
+    def jiffies():
+        t = {}
+        with open("/proc/stat") as f:
+            for line in f:
+                if line.startswith("cpu") and line[3].isdigit():
+                    v = [int(x) for x in line.split()[1:9]]
+                    t[int(line.split()[0][3:])] = (sum(v) - v[3] - v[4], sum(v))
+        return t
     try:
         here = ctypes.CDLL(None).sched_getcpu()
         pkg_here = topo(here, "physical_package_id") if here >= 0 else None
-        cores, seen = [], set()
+        j0 = jiffies()
+        time.sleep(probe_s)
+        j1 = jiffies()
+        busy = {c: (j1[c][0] - j0[c][0]) / max(j1[c][1] - j0[c][1], 1) for c in j1 if c in j0}
+        groups = {}
         for c in cpus:
-            sib = topo(c, "thread_siblings_list")
-            if sib not in seen:
-                seen.add(sib)
-                cores.append((topo(c, "physical_package_id") != pkg_here, c))
-    except (OSError, AttributeError):
+            groups.setdefault(topo(c, "thread_siblings_list"), []).append(c)
+        cores = []
+        for sib, members in groups.items():
+            load = max(busy.get(int(x), 0.0) for x in sib.replace("-", ",").split(",") if x)
+            cores.append((round(load * 20), topo(members[0], "physical_package_id") != pkg_here, members[0]))
+    except (OSError, AttributeError, ValueError):
         return None
-    first = [c for _, c in sorted(cores)]
+    first = [c for _, _, c in sorted(cores)]
     rest = [c for c in cpus if c not in set(first)]
     return (first + rest)[:T]
 
